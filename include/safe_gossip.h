@@ -1,0 +1,137 @@
+/*
+ * safe_gossip.h -- C ABI of the MI355X-native safe_gossip push-pull engine.
+ *
+ * One handle (gs_engine) is one simulated full-mesh network of n Gossipers,
+ * each gossiping up to R rumors, resident in HBM on one MI355X.  Every entry
+ * point is population-level: a call replaces the per-node Rust call it cites
+ * for ALL nodes at once.  Plain C types only; caller owns every host buffer,
+ * the engine owns every device buffer.  Not thread-safe per handle.
+ *
+ * Reference interface replaced (paths relative to the reference crate):
+ *   gs_create          <- Gossiper::default + create_network's add_peer mesh
+ *                         (src/gossiper.rs:130-140, :45-52, :157-171) and the
+ *                         parameter derivation of Gossip::add_peer
+ *                         (src/gossip.rs:59-64)
+ *   gs_send_new        <- Gossiper::send_new      (src/gossiper.rs:55-61)
+ *   gs_next_round      <- Gossiper::next_round for every node + delivery of
+ *                         every Push/Pull through handle_received_message
+ *                         (src/gossiper.rs:70-99; harness loop :198-235)
+ *   gs_messages        <- Gossiper::messages      (src/gossiper.rs:102-104)
+ *   gs_statistics      <- Gossiper::statistics    (src/gossiper.rs:107-109)
+ *   gs_statistics_reduce <- Statistics::add/min/max (src/gossip.rs:225-263)
+ *   gs_clear           <- Gossiper::clear (cfg(test), src/gossiper.rs:111-115)
+ *   status codes       <- enum Error               (src/error.rs:23-51)
+ *
+ * Round schedule: "2P" -- SURVEY.md section 8, i.e. the reference harness with
+ * pull batches delivered after all push batches of the round.  Peer choice is
+ * the injected Philox4x32-10 stream (gs_peer).
+ */
+#ifndef SAFE_GOSSIP_H
+#define SAFE_GOSSIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Mirrors src/error.rs:23-51 (positive) + engine errors (negative). */
+typedef enum {
+    GS_OK = 0,
+    GS_ERR_NO_PEERS = 1,          /* Error::NoPeers         */
+    GS_ERR_ALREADY_STARTED = 2,   /* Error::AlreadyStarted  */
+    GS_ERR_SIG_FAILURE = 3,       /* Error::SigFailure (reserved: no wire format) */
+    GS_ERR_IO = 4,                /* Error::Io (reserved)   */
+    GS_ERR_SERIALISATION = 5,     /* Error::Serialisation (reserved) */
+    GS_ERR_INVALID_ARGUMENT = -1,
+    GS_ERR_UNSUPPORTED = -2,      /* parameters outside the packed state layout */
+    GS_ERR_HIP = -3,
+    GS_ERR_OUT_OF_MEMORY = -4,
+    GS_ERR_DEVICE_LIMIT = -5      /* a node's in-degree exceeded the packed
+                                     counter range (probability ~1e-34/node) */
+} gs_status;
+
+typedef struct {
+    uint32_t n_nodes;        /* network size n (full mesh)                   */
+    uint32_t n_rumors;       /* R: rumor slots per node (1..4096)            */
+    uint64_t seed;           /* Philox key                                   */
+    uint32_t epoch;          /* Philox counter word 3 (iteration index)      */
+    uint8_t counter_max;     /* 0 = derive from n (src/gossip.rs:61)         */
+    uint8_t max_c_rounds;    /* 0 = derive from n (src/gossip.rs:62)         */
+    uint8_t max_rounds;      /* 0 = derive from n (src/gossip.rs:63)         */
+    uint8_t reserved0;
+    int32_t device;          /* HIP device ordinal, -1 = current             */
+    uint32_t reserved1[7];
+} gs_config;
+
+/* src/gossip.rs:209-221, same field order. */
+typedef struct {
+    uint64_t rounds;
+    uint64_t empty_pull_sent;
+    uint64_t empty_push_sent;
+    uint64_t full_message_sent;
+    uint64_t full_message_received;
+} gs_statistics_t;
+
+typedef enum { GS_REDUCE_SUM = 0, GS_REDUCE_MIN = 1, GS_REDUCE_MAX = 2 } gs_reduce_op;
+
+typedef struct {
+    uint32_t round;          /* 1-based index of the round just run          */
+    uint32_t any_live;       /* some node pushed a live rumor this round
+                                (the harness's `processed`, src/gossiper.rs:209-212) */
+} gs_round_report;
+
+typedef struct gs_engine gs_engine;
+
+gs_status   gs_create(const gs_config *cfg, gs_engine **out);
+void        gs_destroy(gs_engine *e);
+gs_status   gs_get_params(const gs_engine *e, uint8_t out[3]);
+
+/* Queue Gossiper::send_new(rumor) on `node`; applied in the next round's phase
+ * 0 right before that node's next_round (src/gossiper.rs:203-208). */
+gs_status   gs_send_new(gs_engine *e, uint32_t node, uint32_t rumor);
+
+/* One round for the whole population.  `report` may be NULL (no host sync). */
+gs_status   gs_next_round(gs_engine *e, gs_round_report *report);
+
+/* Observers: state after the last round's deliveries. */
+gs_status   gs_statistics(gs_engine *e, uint32_t node, gs_statistics_t *out);
+gs_status   gs_statistics_all(gs_engine *e, uint64_t *out /* n*5 */);
+gs_status   gs_statistics_reduce(gs_engine *e, gs_reduce_op op, gs_statistics_t *out);
+gs_status   gs_messages(gs_engine *e, uint32_t node, uint64_t *words /* ceil(R/64) */);
+gs_status   gs_known_all(gs_engine *e, uint64_t *words /* n*ceil(R/64) */);
+gs_status   gs_known_counts(gs_engine *e, uint64_t *known_total, uint64_t *nodes_complete);
+
+/* Parity dumps (u16 codes identical to the oracle's):
+ *   state: tag<<14 | f2<<7 | f1  (B: f1 round, f2 our_counter; C: f1
+ *          rounds_in_state_b, f2 round; A/D: 0), n*R entries.
+ *   rec:   anyC<<15 | cnt2<<7 | cnt1 over B.peer_counters; psize: n. */
+gs_status   gs_dump_state(gs_engine *e, uint16_t *out);
+gs_status   gs_dump_records(gs_engine *e, uint16_t *rec, uint32_t *psize);
+
+gs_status   gs_clear(gs_engine *e, uint32_t epoch);
+gs_status   gs_sync(gs_engine *e);
+uint32_t    gs_round(const gs_engine *e);
+
+/* Device-time of the last `gs_next_round`'s round kernel (HIP events on the
+ * engine stream), ms; for bench.py's roofline.  Returns <0 if unavailable. */
+float       gs_last_round_kernel_ms(gs_engine *e);
+/* Enable/disable HIP-event timing of the round kernel (default off). */
+void        gs_set_timing(gs_engine *e, int enable);
+/* Algorithmic HBM bytes of one round kernel (DESIGN.md, section Roofline). */
+double      gs_round_kernel_bytes(const gs_engine *e);
+
+/* Injected peer schedule: the peer node `node` chooses in `round`. */
+uint32_t    gs_peer(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node, uint32_t n);
+/* Origin for rumor `rumor` in the benchmark / harness schedules. */
+uint32_t    gs_origin(uint64_t seed, uint32_t epoch, uint32_t rumor, uint32_t n);
+/* Harness coin (rng.gen::<bool>(), src/gossiper.rs:204). */
+uint32_t    gs_coin(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node);
+/* Parameter derivation of Gossip::add_peer for network_size = n. */
+void        gs_derive_params(uint32_t n, uint8_t out[3]);
+const char *gs_status_string(gs_status s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SAFE_GOSSIP_H */

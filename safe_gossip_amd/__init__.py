@@ -1,0 +1,413 @@
+"""safe_gossip_amd -- MI355X-native engine for safe_gossip's push-pull round.
+
+Python host mirror of the reference crate's public surface
+(``src/lib.rs:62-65``: ``Gossiper``, ``Statistics``, ``Error``) over the C ABI
+in ``include/safe_gossip.h``.  One :class:`Network` is one simulated full-mesh
+network resident on one MI355X; :meth:`Network.gossiper` returns the per-node
+``Gossiper`` view (``send_new``, ``messages``, ``statistics``) and
+:meth:`Network.next_round` runs ``Gossiper::next_round`` for every node plus the
+delivery of every Push/Pull RPC (the reference harness round,
+``src/gossiper.rs:198-235``, in the 2P schedule).
+
+There is no CPU fallback: every call goes through ``libsafe_gossip_amd.so``
+(hand-written gfx950 kernels) and raises :class:`DeviceError` when the library
+or the GPU is unavailable.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+
+from .build import LIB_PATH
+
+__all__ = [
+    "Network", "Gossiper", "Statistics", "RoundReport", "GossipError", "NoPeers",
+    "AlreadyStarted", "DeviceError", "derive_params", "peer_of", "origin_of", "coin_of",
+    "send_messages", "load_library", "SYMBOLS",
+]
+
+# ----------------------------------------------------------------- errors
+class GossipError(Exception):
+    """Mirror of ``enum Error`` (src/error.rs:23-51)."""
+
+    code = None
+
+
+class NoPeers(GossipError):
+    """``Error::NoPeers``: there are no connected peers with which to gossip."""
+
+    code = 1
+
+
+class AlreadyStarted(GossipError):
+    """``Error::AlreadyStarted``."""
+
+    code = 2
+
+
+class DeviceError(GossipError):
+    """Engine-side failure (no library, no GPU, HIP error, device limit)."""
+
+
+_ERRORS = {1: NoPeers, 2: AlreadyStarted}
+
+# ------------------------------------------------------------------ ctypes
+class _Config(ctypes.Structure):
+    _fields_ = [
+        ("n_nodes", ctypes.c_uint32), ("n_rumors", ctypes.c_uint32),
+        ("seed", ctypes.c_uint64), ("epoch", ctypes.c_uint32),
+        ("counter_max", ctypes.c_uint8), ("max_c_rounds", ctypes.c_uint8),
+        ("max_rounds", ctypes.c_uint8), ("reserved0", ctypes.c_uint8),
+        ("device", ctypes.c_int32), ("reserved1", ctypes.c_uint32 * 7),
+    ]
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_uint64) for f in (
+        "rounds", "empty_pull_sent", "empty_push_sent", "full_message_sent",
+        "full_message_received")]
+
+
+class _Report(ctypes.Structure):
+    _fields_ = [("round", ctypes.c_uint32), ("any_live", ctypes.c_uint32)]
+
+
+_P = ctypes.c_void_p
+_U8P = ctypes.POINTER(ctypes.c_uint8)
+_U16P = ctypes.POINTER(ctypes.c_uint16)
+_U32P = ctypes.POINTER(ctypes.c_uint32)
+_U64P = ctypes.POINTER(ctypes.c_uint64)
+
+# name -> (restype, argtypes): every symbol include/safe_gossip.h declares.
+SYMBOLS = {
+    "gs_create": (ctypes.c_int, [ctypes.POINTER(_Config), ctypes.POINTER(_P)]),
+    "gs_destroy": (None, [_P]),
+    "gs_get_params": (ctypes.c_int, [_P, _U8P]),
+    "gs_send_new": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_uint32]),
+    "gs_next_round": (ctypes.c_int, [_P, ctypes.POINTER(_Report)]),
+    "gs_statistics": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.POINTER(_Stats)]),
+    "gs_statistics_all": (ctypes.c_int, [_P, _U64P]),
+    "gs_statistics_reduce": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_Stats)]),
+    "gs_messages": (ctypes.c_int, [_P, ctypes.c_uint32, _U64P]),
+    "gs_known_all": (ctypes.c_int, [_P, _U64P]),
+    "gs_known_counts": (ctypes.c_int, [_P, _U64P, _U64P]),
+    "gs_dump_state": (ctypes.c_int, [_P, _U16P]),
+    "gs_dump_records": (ctypes.c_int, [_P, _U16P, _U32P]),
+    "gs_clear": (ctypes.c_int, [_P, ctypes.c_uint32]),
+    "gs_sync": (ctypes.c_int, [_P]),
+    "gs_round": (ctypes.c_uint32, [_P]),
+    "gs_last_round_kernel_ms": (ctypes.c_float, [_P]),
+    "gs_set_timing": (None, [_P, ctypes.c_int]),
+    "gs_round_kernel_bytes": (ctypes.c_double, [_P]),
+    "gs_peer": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                  ctypes.c_uint32, ctypes.c_uint32]),
+    "gs_origin": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                    ctypes.c_uint32]),
+    "gs_coin": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                  ctypes.c_uint32]),
+    "gs_derive_params": (None, [ctypes.c_uint32, _U8P]),
+    "gs_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+}
+
+_LIB = None
+
+
+def load_library(path: Optional[str] = None):
+    """Load ``libsafe_gossip_amd.so`` (built by ``__graft_entry__.build()``)."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = path or os.environ.get("SAFE_GOSSIP_AMD_LIB", LIB_PATH)
+    if not os.path.exists(p):
+        raise DeviceError(f"engine library not built: {p} (run __graft_entry__.build())")
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in SYMBOLS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+def _check(status: int) -> None:
+    if status == 0:
+        return
+    lib = load_library()
+    msg = lib.gs_status_string(status).decode()
+    raise _ERRORS.get(status, DeviceError)(f"{msg} (status {status})")
+
+
+# ------------------------------------------------------------------ values
+@dataclass
+class Statistics:
+    """``struct Statistics`` (src/gossip.rs:209-264)."""
+
+    rounds: int = 0
+    empty_pull_sent: int = 0
+    empty_push_sent: int = 0
+    full_message_sent: int = 0
+    full_message_received: int = 0
+
+    FIELDS = ("rounds", "empty_pull_sent", "empty_push_sent", "full_message_sent",
+              "full_message_received")
+
+    @classmethod
+    def new_max(cls) -> "Statistics":
+        m = (1 << 64) - 1
+        return cls(m, m, m, m, m)
+
+    def add(self, other: "Statistics") -> None:
+        for f in self.FIELDS:
+            setattr(self, f, getattr(self, f) + getattr(other, f))
+
+    def min(self, other: "Statistics") -> None:
+        for f in self.FIELDS:
+            setattr(self, f, min(getattr(self, f), getattr(other, f)))
+
+    def max(self, other: "Statistics") -> None:
+        for f in self.FIELDS:
+            setattr(self, f, max(getattr(self, f), getattr(other, f)))
+
+    def as_tuple(self):
+        return tuple(getattr(self, f) for f in self.FIELDS)
+
+    @classmethod
+    def _from_c(cls, s: _Stats) -> "Statistics":
+        return cls(s.rounds, s.empty_pull_sent, s.empty_push_sent, s.full_message_sent,
+                   s.full_message_received)
+
+
+@dataclass
+class RoundReport:
+    round: int
+    any_live: bool
+
+
+def derive_params(n: int):
+    """``Gossip::add_peer`` parameters for network_size n (src/gossip.rs:59-64)."""
+    out = (ctypes.c_uint8 * 3)()
+    load_library().gs_derive_params(n, out)
+    return tuple(out)
+
+
+def peer_of(seed: int, epoch: int, rnd: int, node: int, n: int) -> int:
+    return load_library().gs_peer(seed, epoch, rnd, node, n)
+
+
+def origin_of(seed: int, epoch: int, rumor: int, n: int) -> int:
+    return load_library().gs_origin(seed, epoch, rumor, n)
+
+
+def coin_of(seed: int, epoch: int, rnd: int, node: int) -> int:
+    return load_library().gs_coin(seed, epoch, rnd, node)
+
+
+# ---------------------------------------------------------------- network
+class Network:
+    """A simulated full-mesh network of ``n_nodes`` Gossipers on one MI355X.
+
+    Equivalent to ``create_network(n)`` (src/gossiper.rs:157-171): every node
+    knows every other node, so the protocol parameters are those of
+    ``network_size == n``.  ``params`` overrides (counter_max, max_c_rounds,
+    max_rounds).
+    """
+
+    def __init__(self, n_nodes: int, n_rumors: int, seed: int = 0x5AFE6055, epoch: int = 0,
+                 params=None, device: int = 0):
+        self._lib = load_library()
+        cfg = _Config()
+        cfg.n_nodes = n_nodes
+        cfg.n_rumors = n_rumors
+        cfg.seed = seed
+        cfg.epoch = epoch
+        if params is not None:
+            cfg.counter_max, cfg.max_c_rounds, cfg.max_rounds = params
+        cfg.device = device
+        h = _P()
+        _check(self._lib.gs_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+        self.n = n_nodes
+        self.R = n_rumors
+        self.seed = seed
+        self.epoch = epoch
+        self.kw = (n_rumors + 63) // 64
+
+    # lifecycle
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.gs_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # reference API
+    def gossiper(self, node: int) -> "Gossiper":
+        if not 0 <= node < self.n:
+            raise IndexError(node)
+        return Gossiper(self, node)
+
+    @property
+    def params(self):
+        out = (ctypes.c_uint8 * 3)()
+        _check(self._lib.gs_get_params(self._h, out))
+        return tuple(out)
+
+    @property
+    def round(self) -> int:
+        return self._lib.gs_round(self._h)
+
+    def send_new(self, node: int, rumor: int) -> None:
+        _check(self._lib.gs_send_new(self._h, node, rumor))
+
+    def next_round(self, report: bool = True) -> Optional[RoundReport]:
+        if not report:
+            _check(self._lib.gs_next_round(self._h, None))
+            return None
+        r = _Report()
+        _check(self._lib.gs_next_round(self._h, ctypes.byref(r)))
+        return RoundReport(r.round, bool(r.any_live))
+
+    def statistics(self, node: int) -> Statistics:
+        s = _Stats()
+        _check(self._lib.gs_statistics(self._h, node, ctypes.byref(s)))
+        return Statistics._from_c(s)
+
+    def statistics_all(self) -> np.ndarray:
+        out = np.zeros((self.n, 5), dtype=np.uint64)
+        _check(self._lib.gs_statistics_all(self._h, out.ctypes.data_as(_U64P)))
+        return out
+
+    def statistics_reduce(self, op: str = "sum") -> Statistics:
+        s = _Stats()
+        _check(self._lib.gs_statistics_reduce(self._h, {"sum": 0, "min": 1, "max": 2}[op],
+                                              ctypes.byref(s)))
+        return Statistics._from_c(s)
+
+    def messages(self, node: int) -> List[int]:
+        w = np.zeros(self.kw, dtype=np.uint64)
+        _check(self._lib.gs_messages(self._h, node, w.ctypes.data_as(_U64P)))
+        bits = np.unpackbits(w.view(np.uint8), bitorder="little")[: self.R]
+        return [int(i) for i in np.nonzero(bits)[0]]
+
+    def known_all(self) -> np.ndarray:
+        out = np.zeros((self.n, self.kw), dtype=np.uint64)
+        _check(self._lib.gs_known_all(self._h, out.ctypes.data_as(_U64P)))
+        return out
+
+    def known_counts(self):
+        t = ctypes.c_uint64()
+        c = ctypes.c_uint64()
+        _check(self._lib.gs_known_counts(self._h, ctypes.byref(t), ctypes.byref(c)))
+        return int(t.value), int(c.value)
+
+    def dump_state(self) -> np.ndarray:
+        out = np.zeros((self.n, self.R), dtype=np.uint16)
+        _check(self._lib.gs_dump_state(self._h, out.ctypes.data_as(_U16P)))
+        return out
+
+    def dump_records(self):
+        rec = np.zeros((self.n, self.R), dtype=np.uint16)
+        ps = np.zeros(self.n, dtype=np.uint32)
+        _check(self._lib.gs_dump_records(self._h, rec.ctypes.data_as(_U16P),
+                                         ps.ctypes.data_as(_U32P)))
+        return rec, ps
+
+    def clear(self, epoch: Optional[int] = None) -> None:
+        """``Gossiper::clear`` for every node (src/gossiper.rs:111-115)."""
+        self.epoch = self.epoch + 1 if epoch is None else epoch
+        _check(self._lib.gs_clear(self._h, self.epoch))
+
+    def sync(self) -> None:
+        _check(self._lib.gs_sync(self._h))
+
+    # measurement hooks
+    def set_timing(self, on: bool) -> None:
+        self._lib.gs_set_timing(self._h, 1 if on else 0)
+
+    def last_round_kernel_ms(self) -> float:
+        return float(self._lib.gs_last_round_kernel_ms(self._h))
+
+    def round_kernel_bytes(self) -> float:
+        return float(self._lib.gs_round_kernel_bytes(self._h))
+
+
+class Gossiper:
+    """Per-node view with the reference ``Gossiper`` methods (src/gossiper.rs:36-109)."""
+
+    def __init__(self, net: Network, node: int):
+        self._net = net
+        self._node = node
+
+    def id(self) -> int:
+        """Node Id; Id order == index order."""
+        return self._node
+
+    def send_new(self, rumor: int) -> None:
+        self._net.send_new(self._node, rumor)
+
+    def messages(self) -> List[int]:
+        return self._net.messages(self._node)
+
+    def statistics(self) -> Statistics:
+        return self._net.statistics(self._node)
+
+
+def send_messages(net: Network, num_of_msgs: int):
+    """``send_messages`` (src/gossiper.rs:173-259) over the GPU engine.
+
+    Philox-chosen first origin, then 50% per node per round while rumors
+    remain, termination after a round in which no node pushed a live rumor.
+    Returns ``(nodes_missed, msgs_missed, Statistics, rounds_run, round_full)``
+    and clears the network (next epoch), like the reference.
+    """
+    assert num_of_msgs >= 1
+    n = net.n
+    next_rumor = 0
+    net.send_new(origin_of(net.seed, net.epoch, 0, n), next_rumor)
+    next_rumor += 1
+    processed = True
+    rounds_run = 0
+    round_full = 0
+    while processed:
+        rnd = net.round + 1
+        if next_rumor < num_of_msgs:
+            for x in range(n):
+                if next_rumor >= num_of_msgs:
+                    break
+                if coin_of(net.seed, net.epoch, rnd, x):
+                    net.send_new(x, next_rumor)
+                    next_rumor += 1
+        rep = net.next_round()
+        processed = rep.any_live
+        rounds_run += 1
+        if not round_full:
+            _, complete = net.known_counts()
+            if complete == n and next_rumor == num_of_msgs and num_of_msgs <= net.R:
+                round_full = net.round
+    st_all = net.statistics_all().astype(np.int64)
+    known = net.known_all()
+    counts = np.array([sum(bin(int(w)).count("1") for w in row) for row in known]) \
+        if net.kw > 1 else np.array([bin(int(w)).count("1") for w in known[:, 0]])
+    stats = Statistics(int(st_all[-1, 0]), int(st_all[:, 1].sum()) - n,
+                       int(st_all[:, 2].sum()) - n, int(st_all[:, 3].sum()),
+                       int(st_all[:, 4].sum()))
+    missed = counts < num_of_msgs
+    nodes_missed = int(missed.sum())
+    msgs_missed = int((num_of_msgs - counts[missed]).sum())
+    net.clear()
+    return nodes_missed, msgs_missed, stats, rounds_run, round_full

@@ -1,0 +1,70 @@
+"""Build helpers: compile the gfx950 engine library and the C++ examples.
+
+The engine is built in-tree (``safe_gossip_amd/libsafe_gossip_amd.so``) with an
+explicit ``hipcc --offload-arch=gfx950`` line so the artefact travels with the
+repository snapshot to the GPU box.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(PKG_DIR, "csrc")
+LIB_PATH = os.path.join(PKG_DIR, "libsafe_gossip_amd.so")
+SOURCES = [os.path.join(CSRC, "gs_kernels.hip"), os.path.join(CSRC, "gs_engine.cpp")]
+HEADERS = [os.path.join(CSRC, f) for f in ("gs_common.h", "gs_kernels.h")] + [
+    os.path.join(REPO_DIR, "include", "safe_gossip.h")
+]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+
+def _stale(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_engine(force: bool = False, verbose: bool = False) -> str:
+    """Compile libsafe_gossip_amd.so for gfx950 (no-op when up to date)."""
+    if not force and not _stale(LIB_PATH, SOURCES + HEADERS):
+        return LIB_PATH
+    cmd = [HIPCC, "-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17",
+           "-Wall", "-Wextra", "-Werror", "-o", LIB_PATH + ".tmp"] + SOURCES
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH
+
+
+def build_examples(force: bool = False) -> list[str]:
+    """Compile the C++ host examples (examples/*.cpp) against the C ABI."""
+    out = []
+    ex_dir = os.path.join(REPO_DIR, "examples")
+    if not os.path.isdir(ex_dir):
+        return out
+    for name in sorted(os.listdir(ex_dir)):
+        if not name.endswith(".cpp"):
+            continue
+        src = os.path.join(ex_dir, name)
+        exe = os.path.join(ex_dir, name[:-4])
+        deps = [src, LIB_PATH, os.path.join(REPO_DIR, "include", "safe_gossip.h"),
+                os.path.join(REPO_DIR, "include", "safe_gossip.hpp")]
+        if force or _stale(exe, [d for d in deps if os.path.exists(d)]):
+            subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-Werror",
+                            "-I", os.path.join(REPO_DIR, "include"), "-o", exe, src,
+                            "-L", PKG_DIR, "-lsafe_gossip_amd", f"-Wl,-rpath,{PKG_DIR}"],
+                           check=True)
+        out.append(exe)
+    return out
+
+
+if __name__ == "__main__":
+    print(build_engine(force="--force" in sys.argv, verbose=True))
+    for e in build_examples(force="--force" in sys.argv):
+        print(e)

@@ -1,0 +1,88 @@
+// gs_common.h -- host/device helpers shared by the engine and its kernels:
+// the injected Philox4x32-10 peer schedule and the packed state layout.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gs {
+
+typedef unsigned long long u64;
+
+// Philox4x32-10 (Salmon et al., Random123), the generator rocrand's
+// philox4x32_10 engine implements; KATs in tests/test_philox.py.
+constexpr uint32_t kPhM0 = 0xD2511F53u, kPhM1 = 0xCD9E8D57u;
+constexpr uint32_t kPhW0 = 0x9E3779B9u, kPhW1 = 0xBB67AE85u;
+
+// Counter word 2 selects the stream.
+constexpr uint32_t kStreamPeer = 0, kStreamOrigin = 1, kStreamCoin = 2;
+
+__host__ __device__ __forceinline__ uint32_t mulhi32(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umulhi(a, b);
+#else
+    return (uint32_t)(((uint64_t)a * b) >> 32);
+#endif
+}
+
+__host__ __device__ __forceinline__ u64 philox_u64(uint32_t c0, uint32_t c1, uint32_t c2,
+                                                   uint32_t c3, uint64_t seed) {
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint32_t hi0 = mulhi32(kPhM0, c0), lo0 = kPhM0 * c0;
+        uint32_t hi1 = mulhi32(kPhM1, c2), lo1 = kPhM1 * c2;
+        uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += kPhW0; k1 += kPhW1;
+    }
+    return ((u64)c1 << 32) | c0;
+}
+
+// floor(v * m / 2^64): uniform index in [0, m).
+__host__ __device__ __forceinline__ uint32_t mulhi64(u64 v, uint32_t m) {
+    u64 lo = (u64)(uint32_t)v * m;
+    u64 hi = (u64)(uint32_t)(v >> 32) * m;
+    return (uint32_t)((hi + (lo >> 32)) >> 32);
+}
+
+// Gossiper::next_round's rand::thread_rng().choose(&self.peers)
+// (src/gossiper.rs:71) over create_network's peer order
+// (src/gossiper.rs:157-171: node k's peers are [0..k-1, k+1..n-1]).
+__host__ __device__ __forceinline__ uint32_t peer_of(uint64_t seed, uint32_t epoch,
+                                                    uint32_t round, uint32_t node, uint32_t n) {
+    uint32_t u = mulhi64(philox_u64(round, node, kStreamPeer, epoch, seed), n - 1u);
+    return u + (u >= node ? 1u : 0u);
+}
+
+__host__ __device__ __forceinline__ uint32_t origin_of(uint64_t seed, uint32_t epoch,
+                                                      uint32_t rumor, uint32_t n) {
+    return mulhi64(philox_u64(rumor, 0u, kStreamOrigin, epoch, seed), n);
+}
+
+__host__ __device__ __forceinline__ uint32_t coin_of(uint64_t seed, uint32_t epoch,
+                                                    uint32_t round, uint32_t node) {
+    return (uint32_t)(philox_u64(round, node, kStreamCoin, epoch, seed) & 1u);
+}
+
+// ---------------------------------------------------------------------------
+// Packed per-(node, rumor) state: 8 bit-planes ("State layout").
+//   plane 0  isC        plane 1,2  a = f2 (2 bits)    planes 3..7  b = f1 (5 bits)
+//   A: isC=0 a=0        B: isC=0 a=our_counter (1|2)  b=round
+//   C: isC=1 a=round (0..2) b=rounds_in_state_b       D: isC=1 a=3 b=0
+// Valid while counter_max <= 3, max_c_rounds <= 3, max_rounds <= 32.
+constexpr int kPlanes = 8;
+constexpr int kClsPlanes = 3;   // isC, a0, a1: everything a neighbour reads
+
+struct Geometry {
+    uint32_t n;         // nodes
+    uint32_t R;         // rumors
+    uint32_t rpad;      // next pow2 >= R
+    uint32_t W;         // 64-bit words per node (rpad >= 64), else 1
+    uint32_t small;     // rpad < 64: several nodes per word
+    uint32_t lognpu;    // log2(nodes per unit word) when small
+    uint32_t logr;      // log2(rpad)
+    uint64_t units;     // records of kPlanes*W words
+    uint64_t nseg;      // lanes: n*W (big) or n (small)
+};
+
+}  // namespace gs

@@ -1,0 +1,536 @@
+// gs_engine.cpp -- host side of the C ABI (include/safe_gossip.h): device
+// memory, round sequencing, injections and observers.  All compute is in
+// gs_kernels.hip; there is no CPU fallback -- every entry point fails with
+// GS_ERR_HIP when the device path cannot run.
+#include "../../include/safe_gossip.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <utility>
+#include <vector>
+
+#include "gs_common.h"
+#include "gs_kernels.h"
+
+using gs::u64;
+
+struct gs_engine {
+    gs::Geometry g{};
+    uint64_t seed = 0;
+    uint32_t epoch = 0;
+    uint8_t cmax = 0, maxc = 0, maxr = 0;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    u64 *S[2] = {nullptr, nullptr};
+    int cur = 0;
+    uint32_t *off = nullptr, *src = nullptr, *tg = nullptr, *cnt = nullptr;
+    uint32_t *bsum = nullptr, *flags = nullptr;
+    u64 *stats = nullptr;
+    u64 *inj_key = nullptr, *inj_mask = nullptr;
+    u64 *inj_host = nullptr;  // pinned staging [2*cap]
+    uint32_t inj_cap = 0;
+    std::vector<std::pair<uint32_t, uint32_t>> pending;
+    uint32_t round = 0;
+    bool deliver_pending = false;
+    // observation buffers (lazy)
+    u64 *obs_known = nullptr, *obs_stats = nullptr, *partials = nullptr;
+    uint16_t *obs_state = nullptr, *obs_rec = nullptr;
+    uint32_t *obs_psize = nullptr;
+    bool obs_valid = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timing = false, timed = false;
+};
+
+namespace {
+
+constexpr uint32_t kReduceBlocks = 1024;
+
+#define GS_HIP(expr)                                   \
+    do {                                               \
+        hipError_t _e = (expr);                        \
+        if (_e != hipSuccess) return GS_ERR_HIP;       \
+    } while (0)
+
+uint32_t next_pow2(uint32_t v) {
+    uint32_t p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+uint32_t ilog2(uint32_t v) {
+    uint32_t l = 0;
+    while ((1u << l) < v) ++l;
+    return l;
+}
+
+gs_status set_device(gs_engine *e) {
+    return hipSetDevice(e->device) == hipSuccess ? GS_OK : GS_ERR_HIP;
+}
+
+template <typename T>
+hipError_t dalloc(T **p, size_t count) {
+    return hipMalloc((void **)p, std::max<size_t>(count, 1) * sizeof(T));
+}
+
+void release(gs_engine *e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    void *bufs[] = {e->S[0], e->S[1], e->off, e->src, e->tg, e->cnt, e->bsum, e->flags,
+                    e->stats, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
+                    e->partials, e->obs_state, e->obs_rec, e->obs_psize};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    if (e->inj_host) (void)hipHostFree(e->inj_host);
+    if (e->ev0) (void)hipEventDestroy(e->ev0);
+    if (e->ev1) (void)hipEventDestroy(e->ev1);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+gs_status reset_state(gs_engine *e) {
+    const gs::Geometry &g = e->g;
+    const size_t sw = (size_t)g.units * gs::kPlanes * g.W;
+    GS_HIP(hipMemsetAsync(e->S[0], 0, sw * sizeof(u64), e->stream));
+    GS_HIP(hipMemsetAsync(e->S[1], 0, sw * sizeof(u64), e->stream));
+    GS_HIP(hipMemsetAsync(e->stats, 0, (size_t)5 * g.n * sizeof(u64), e->stream));
+    GS_HIP(hipMemsetAsync(e->cnt, 0, (size_t)g.n * sizeof(uint32_t), e->stream));
+    GS_HIP(hipMemsetAsync(e->flags, 0, 4 * sizeof(uint32_t), e->stream));
+    e->cur = 0;
+    e->round = 0;
+    e->deliver_pending = false;
+    e->pending.clear();
+    e->obs_valid = false;
+    return GS_OK;
+}
+
+gs::RoundArgs base_args(gs_engine *e) {
+    gs::RoundArgs a{};
+    a.Scur = e->S[e->cur];
+    a.Snext = e->S[e->cur ^ 1];
+    a.off = e->off;
+    a.src = e->src;
+    a.tg = e->tg;
+    a.cnt = e->cnt;
+    a.stats = e->stats;
+    a.flags = e->flags;
+    a.g = e->g;
+    a.seed = e->seed;
+    a.epoch = e->epoch;
+    a.round_new = e->round + 1;
+    a.cmax = e->cmax;
+    a.maxc = e->maxc;
+    a.maxr = e->maxr;
+    return a;
+}
+
+gs_status upload_injections(gs_engine *e, uint32_t *n_inj) {
+    *n_inj = 0;
+    if (e->pending.empty()) return GS_OK;
+    const gs::Geometry &g = e->g;
+    std::vector<std::pair<u64, u64>> km;
+    km.reserve(e->pending.size());
+    for (auto &p : e->pending) {
+        const uint32_t x = p.first, r = p.second;
+        if (g.small) km.emplace_back((u64)x, 1ull << r);
+        else km.emplace_back((u64)x * g.W + (r >> 6), 1ull << (r & 63));
+    }
+    std::sort(km.begin(), km.end());
+    std::vector<std::pair<u64, u64>> merged;
+    for (auto &v : km) {
+        if (!merged.empty() && merged.back().first == v.first) merged.back().second |= v.second;
+        else merged.push_back(v);
+    }
+    const uint32_t m = (uint32_t)merged.size();
+    if (m > e->inj_cap) {
+        GS_HIP(hipStreamSynchronize(e->stream));
+        if (e->inj_key) (void)hipFree(e->inj_key);
+        if (e->inj_mask) (void)hipFree(e->inj_mask);
+        if (e->inj_host) (void)hipHostFree(e->inj_host);
+        e->inj_key = e->inj_mask = e->inj_host = nullptr;
+        uint32_t cap = std::max<uint32_t>(m, 1024);
+        GS_HIP(dalloc(&e->inj_key, cap));
+        GS_HIP(dalloc(&e->inj_mask, cap));
+        GS_HIP(hipHostMalloc((void **)&e->inj_host, 2 * (size_t)cap * sizeof(u64), 0));
+        e->inj_cap = cap;
+    }
+    // The staging buffer may still feed a copy of an earlier round.
+    GS_HIP(hipStreamSynchronize(e->stream));
+    for (uint32_t i = 0; i < m; ++i) {
+        e->inj_host[i] = merged[i].first;
+        e->inj_host[e->inj_cap + i] = merged[i].second;
+    }
+    GS_HIP(hipMemcpyAsync(e->inj_key, e->inj_host, m * sizeof(u64), hipMemcpyHostToDevice, e->stream));
+    GS_HIP(hipMemcpyAsync(e->inj_mask, e->inj_host + e->inj_cap, m * sizeof(u64),
+                          hipMemcpyHostToDevice, e->stream));
+    e->pending.clear();
+    *n_inj = m;
+    return GS_OK;
+}
+
+gs_status ensure_obs(gs_engine *e, bool dumps) {
+    const gs::Geometry &g = e->g;
+    const uint32_t KW = (g.R + 63) / 64;
+    if (!e->obs_known) {
+        GS_HIP(dalloc(&e->obs_known, (size_t)g.n * KW));
+        GS_HIP(dalloc(&e->obs_stats, (size_t)g.n * 5));
+        GS_HIP(dalloc(&e->partials, (size_t)kReduceBlocks * 5));
+        GS_HIP(dalloc(&e->obs_psize, (size_t)g.n));
+    }
+    if (dumps && !e->obs_state) {
+        GS_HIP(dalloc(&e->obs_state, (size_t)g.n * g.R));
+        GS_HIP(dalloc(&e->obs_rec, (size_t)g.n * g.R));
+    }
+    return GS_OK;
+}
+
+// Fill the observation buffers with the state after the last delivery.
+gs_status observe(gs_engine *e, bool dumps) {
+    if (e->obs_valid && !dumps) return GS_OK;
+    gs_status st = ensure_obs(e, dumps);
+    if (st != GS_OK) return st;
+    gs::RoundArgs a = base_args(e);
+    a.obs_known = e->obs_known;
+    a.obs_stats = e->obs_stats;
+    a.obs_psize = e->obs_psize;
+    if (dumps) {
+        a.obs_state = e->obs_state;
+        a.obs_rec = e->obs_rec;
+    }
+    GS_HIP(gs::launch_round(a, e->deliver_pending ? 2 : 3, e->stream));
+    uint32_t fl = 0;
+    GS_HIP(hipMemcpyAsync(&fl, e->flags + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    GS_HIP(hipStreamSynchronize(e->stream));
+    if (fl) return GS_ERR_DEVICE_LIMIT;
+    e->obs_valid = true;
+    return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *gs_status_string(gs_status s) {
+    switch (s) {
+    case GS_OK: return "ok";
+    case GS_ERR_NO_PEERS: return "There are no connected peers with which to gossip.";
+    case GS_ERR_ALREADY_STARTED: return "Connections to all other nodes must be made before sending any messages.";
+    case GS_ERR_SIG_FAILURE: return "The message or signature might be corrupted, or the signer is wrong.";
+    case GS_ERR_IO: return "I/O error";
+    case GS_ERR_SERIALISATION: return "Serialisation error";
+    case GS_ERR_INVALID_ARGUMENT: return "invalid argument";
+    case GS_ERR_UNSUPPORTED: return "parameters outside the packed state layout (counter_max<=3, max_c_rounds<=3, max_rounds<=32, R<=4096)";
+    case GS_ERR_HIP: return "HIP runtime error (no usable MI355X device?)";
+    case GS_ERR_OUT_OF_MEMORY: return "out of device memory";
+    case GS_ERR_DEVICE_LIMIT: return "in-degree beyond the packed counter range";
+    }
+    return "unknown";
+}
+
+void gs_derive_params(uint32_t n, uint8_t out[3]) {
+    // Gossip::add_peer (src/gossip.rs:59-64): network_size == n after the
+    // full mesh is built; f64 ln, ceil, `as u8` (saturating), max(1, .).
+    if (n <= 1) {
+        out[0] = out[1] = out[2] = 0;  // Gossip::new
+        return;
+    }
+    auto as_u8 = [](double v) -> uint8_t {
+        if (!(v > 0.0)) return 0;
+        if (v >= 255.0) return 255;
+        return (uint8_t)v;
+    };
+    const double ns = (double)n;
+    const uint8_t lnln = as_u8(std::ceil(std::log(std::log(ns))));
+    const uint8_t ln = as_u8(std::ceil(std::log(ns)));
+    out[0] = std::max<uint8_t>(1, lnln);
+    out[1] = std::max<uint8_t>(1, lnln);
+    out[2] = std::max<uint8_t>(1, ln);
+}
+
+uint32_t gs_peer(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node, uint32_t n) {
+    return gs::peer_of(seed, epoch, round, node, n);
+}
+uint32_t gs_origin(uint64_t seed, uint32_t epoch, uint32_t rumor, uint32_t n) {
+    return gs::origin_of(seed, epoch, rumor, n);
+}
+uint32_t gs_coin(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node) {
+    return gs::coin_of(seed, epoch, round, node);
+}
+
+gs_status gs_create(const gs_config *cfg, gs_engine **out) {
+    if (!cfg || !out) return GS_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    const uint32_t n = cfg->n_nodes, R = cfg->n_rumors;
+    if (n == 0 || n == 0xffffffffu || R == 0 || R > 4096) return GS_ERR_INVALID_ARGUMENT;
+    uint8_t p[3];
+    gs_derive_params(n, p);
+    if (cfg->counter_max) p[0] = cfg->counter_max;
+    if (cfg->max_c_rounds) p[1] = cfg->max_c_rounds;
+    if (cfg->max_rounds) p[2] = cfg->max_rounds;
+    if (n >= 2 && (p[0] > 3 || p[1] > 3 || p[2] > 32 || !p[0] || !p[1] || !p[2]))
+        return GS_ERR_UNSUPPORTED;
+
+    gs_engine *e = new gs_engine();
+    e->seed = cfg->seed;
+    e->epoch = cfg->epoch;
+    e->cmax = p[0];
+    e->maxc = p[1];
+    e->maxr = p[2];
+    int dev = cfg->device;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) {
+        delete e;
+        return GS_ERR_HIP;
+    }
+    e->device = dev;
+    if (hipSetDevice(dev) != hipSuccess) {
+        delete e;
+        return GS_ERR_HIP;
+    }
+    gs::Geometry &g = e->g;
+    g.n = n;
+    g.R = R;
+    g.rpad = next_pow2(R);
+    g.logr = ilog2(g.rpad);
+    if (g.rpad >= 64) {
+        g.small = 0;
+        g.W = g.rpad / 64;
+        g.lognpu = 0;
+        g.units = n;
+        g.nseg = (uint64_t)n * g.W;
+    } else {
+        g.small = 1;
+        g.W = 1;
+        g.lognpu = 6 - g.logr;
+        const uint64_t npu = 1ull << g.lognpu;
+        g.units = (n + npu - 1) / npu;
+        g.nseg = n;
+    }
+    const size_t sw = (size_t)g.units * gs::kPlanes * g.W;
+    bool ok = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreate(&e->ev0) == hipSuccess && hipEventCreate(&e->ev1) == hipSuccess;
+    ok = ok && dalloc(&e->S[0], sw) == hipSuccess && dalloc(&e->S[1], sw) == hipSuccess &&
+         dalloc(&e->off, (size_t)n + 1) == hipSuccess && dalloc(&e->src, n) == hipSuccess &&
+         dalloc(&e->tg, n) == hipSuccess && dalloc(&e->cnt, n) == hipSuccess &&
+         dalloc(&e->bsum, gs::csr_bsum_words(n)) == hipSuccess && dalloc(&e->flags, 4) == hipSuccess &&
+         dalloc(&e->stats, (size_t)5 * n) == hipSuccess;
+    if (!ok) {
+        hipError_t le = hipGetLastError();
+        release(e);
+        return le == hipErrorOutOfMemory ? GS_ERR_OUT_OF_MEMORY : GS_ERR_HIP;
+    }
+    if (reset_state(e) != GS_OK || hipStreamSynchronize(e->stream) != hipSuccess) {
+        release(e);
+        return GS_ERR_HIP;
+    }
+    *out = e;
+    return GS_OK;
+}
+
+void gs_destroy(gs_engine *e) { release(e); }
+
+gs_status gs_get_params(const gs_engine *e, uint8_t out[3]) {
+    if (!e || !out) return GS_ERR_INVALID_ARGUMENT;
+    out[0] = e->cmax;
+    out[1] = e->maxc;
+    out[2] = e->maxr;
+    return GS_OK;
+}
+
+uint32_t gs_round(const gs_engine *e) { return e ? e->round : 0; }
+
+gs_status gs_send_new(gs_engine *e, uint32_t node, uint32_t rumor) {
+    if (!e) return GS_ERR_INVALID_ARGUMENT;
+    if (e->g.n < 2) return GS_ERR_NO_PEERS;  // Gossiper::send_new, src/gossiper.rs:56-58
+    if (node >= e->g.n || rumor >= e->g.R) return GS_ERR_INVALID_ARGUMENT;
+    e->pending.emplace_back(node, rumor);
+    e->obs_valid = false;
+    return GS_OK;
+}
+
+gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
+    if (!e) return GS_ERR_INVALID_ARGUMENT;
+    if (e->g.n < 2) return GS_ERR_NO_PEERS;  // Gossiper::next_round, src/gossiper.rs:71-74
+    gs_status st = set_device(e);
+    if (st != GS_OK) return st;
+    uint32_t n_inj = 0;
+    st = upload_injections(e, &n_inj);
+    if (st != GS_OK) return st;
+    gs::RoundArgs a = base_args(e);
+    a.inj_key = e->inj_key;
+    a.inj_mask = e->inj_mask;
+    a.n_inj = n_inj;
+    if (e->timing) GS_HIP(hipEventRecord(e->ev0, e->stream));
+    GS_HIP(gs::launch_round(a, e->deliver_pending ? 1 : 0, e->stream));
+    if (e->timing) GS_HIP(hipEventRecord(e->ev1, e->stream));
+    e->timed = e->timing;
+    e->round += 1;
+    e->cur ^= 1;
+    e->deliver_pending = true;
+    e->obs_valid = false;
+    GS_HIP(gs::launch_build_csr(e->tg, e->cnt, e->off, e->src, e->bsum, e->g.n, e->flags,
+                                (e->round + 1) & 1u, e->stream));
+    if (report) {
+        uint32_t fl[4];
+        GS_HIP(hipMemcpyAsync(fl, e->flags, sizeof(fl), hipMemcpyDeviceToHost, e->stream));
+        GS_HIP(hipStreamSynchronize(e->stream));
+        report->round = e->round;
+        report->any_live = fl[e->round & 1u];
+        if (fl[2]) return GS_ERR_DEVICE_LIMIT;
+    }
+    return GS_OK;
+}
+
+gs_status gs_statistics_all(gs_engine *e, uint64_t *out) {
+    if (!e || !out) return GS_ERR_INVALID_ARGUMENT;
+    gs_status st = set_device(e);
+    if (st == GS_OK) st = observe(e, false);
+    if (st != GS_OK) return st;
+    GS_HIP(hipMemcpy(out, e->obs_stats, (size_t)e->g.n * 5 * sizeof(u64), hipMemcpyDeviceToHost));
+    return GS_OK;
+}
+
+gs_status gs_statistics(gs_engine *e, uint32_t node, gs_statistics_t *out) {
+    if (!e || !out || node >= e->g.n) return GS_ERR_INVALID_ARGUMENT;
+    gs_status st = set_device(e);
+    if (st == GS_OK) st = observe(e, false);
+    if (st != GS_OK) return st;
+    u64 v[5];
+    GS_HIP(hipMemcpy(v, e->obs_stats + (size_t)node * 5, sizeof(v), hipMemcpyDeviceToHost));
+    out->rounds = v[0];
+    out->empty_pull_sent = v[1];
+    out->empty_push_sent = v[2];
+    out->full_message_sent = v[3];
+    out->full_message_received = v[4];
+    return GS_OK;
+}
+
+gs_status gs_statistics_reduce(gs_engine *e, gs_reduce_op op, gs_statistics_t *out) {
+    if (!e || !out || (int)op < 0 || (int)op > 2) return GS_ERR_INVALID_ARGUMENT;
+    gs_status st = set_device(e);
+    if (st == GS_OK) st = observe(e, false);
+    if (st != GS_OK) return st;
+    GS_HIP(gs::launch_stats_reduce(e->obs_stats, e->g.n, (int)op, e->partials, kReduceBlocks, e->stream));
+    std::vector<u64> part((size_t)kReduceBlocks * 5);
+    GS_HIP(hipMemcpyAsync(part.data(), e->partials, part.size() * sizeof(u64), hipMemcpyDeviceToHost,
+                          e->stream));
+    GS_HIP(hipStreamSynchronize(e->stream));
+    u64 acc[5];
+    for (int f = 0; f < 5; ++f) acc[f] = op == GS_REDUCE_MIN ? ~0ull : 0ull;
+    for (uint32_t b = 0; b < kReduceBlocks; ++b)
+        for (int f = 0; f < 5; ++f) {
+            const u64 v = part[(size_t)b * 5 + f];
+            acc[f] = op == GS_REDUCE_SUM ? acc[f] + v : (op == GS_REDUCE_MIN ? std::min(acc[f], v) : std::max(acc[f], v));
+        }
+    out->rounds = acc[0];
+    out->empty_pull_sent = acc[1];
+    out->empty_push_sent = acc[2];
+    out->full_message_sent = acc[3];
+    out->full_message_received = acc[4];
+    return GS_OK;
+}
+
+gs_status gs_messages(gs_engine *e, uint32_t node, uint64_t *words) {
+    if (!e || !words || node >= e->g.n) return GS_ERR_INVALID_ARGUMENT;
+    gs_status st = set_device(e);
+    if (st == GS_OK) st = observe(e, false);
+    if (st != GS_OK) return st;
+    const uint32_t KW = (e->g.R + 63) / 64;
+    GS_HIP(hipMemcpy(words, e->obs_known + (size_t)node * KW, KW * sizeof(u64), hipMemcpyDeviceToHost));
+    return GS_OK;
+}
+
+gs_status gs_known_all(gs_engine *e, uint64_t *words) {
+    if (!e || !words) return GS_ERR_INVALID_ARGUMENT;
+    gs_status st = set_device(e);
+    if (st == GS_OK) st = observe(e, false);
+    if (st != GS_OK) return st;
+    const uint32_t KW = (e->g.R + 63) / 64;
+    GS_HIP(hipMemcpy(words, e->obs_known, (size_t)e->g.n * KW * sizeof(u64), hipMemcpyDeviceToHost));
+    return GS_OK;
+}
+
+gs_status gs_known_counts(gs_engine *e, uint64_t *known_total, uint64_t *nodes_complete) {
+    if (!e) return GS_ERR_INVALID_ARGUMENT;
+    gs_status st = set_device(e);
+    if (st == GS_OK) st = observe(e, false);
+    if (st != GS_OK) return st;
+    const uint32_t KW = (e->g.R + 63) / 64;
+    GS_HIP(gs::launch_known_reduce(e->obs_known, e->g.n, KW, e->g.R, e->partials, kReduceBlocks / 2,
+                                   e->stream));
+    std::vector<u64> part(kReduceBlocks);
+    GS_HIP(hipMemcpyAsync(part.data(), e->partials, part.size() * sizeof(u64), hipMemcpyDeviceToHost,
+                          e->stream));
+    GS_HIP(hipStreamSynchronize(e->stream));
+    u64 t = 0, c = 0;
+    for (uint32_t b = 0; b < kReduceBlocks / 2; ++b) {
+        t += part[2 * b];
+        c += part[2 * b + 1];
+    }
+    if (known_total) *known_total = t;
+    if (nodes_complete) *nodes_complete = c;
+    return GS_OK;
+}
+
+gs_status gs_dump_state(gs_engine *e, uint16_t *out) {
+    if (!e || !out) return GS_ERR_INVALID_ARGUMENT;
+    gs_status st = set_device(e);
+    if (st == GS_OK) st = observe(e, true);
+    if (st != GS_OK) return st;
+    GS_HIP(hipMemcpy(out, e->obs_state, (size_t)e->g.n * e->g.R * sizeof(uint16_t), hipMemcpyDeviceToHost));
+    return GS_OK;
+}
+
+gs_status gs_dump_records(gs_engine *e, uint16_t *rec, uint32_t *psize) {
+    if (!e || !rec) return GS_ERR_INVALID_ARGUMENT;
+    gs_status st = set_device(e);
+    if (st == GS_OK) st = observe(e, true);
+    if (st != GS_OK) return st;
+    GS_HIP(hipMemcpy(rec, e->obs_rec, (size_t)e->g.n * e->g.R * sizeof(uint16_t), hipMemcpyDeviceToHost));
+    if (psize)
+        GS_HIP(hipMemcpy(psize, e->obs_psize, (size_t)e->g.n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return GS_OK;
+}
+
+gs_status gs_clear(gs_engine *e, uint32_t epoch) {
+    if (!e) return GS_ERR_INVALID_ARGUMENT;
+    gs_status st = set_device(e);
+    if (st != GS_OK) return st;
+    e->epoch = epoch;
+    st = reset_state(e);
+    if (st != GS_OK) return st;
+    GS_HIP(hipStreamSynchronize(e->stream));
+    return GS_OK;
+}
+
+gs_status gs_sync(gs_engine *e) {
+    if (!e) return GS_ERR_INVALID_ARGUMENT;
+    GS_HIP(hipStreamSynchronize(e->stream));
+    return GS_OK;
+}
+
+void gs_set_timing(gs_engine *e, int enable) {
+    if (e) e->timing = enable != 0;
+}
+
+float gs_last_round_kernel_ms(gs_engine *e) {
+    if (!e || !e->timed) return -1.0f;
+    if (hipEventSynchronize(e->ev1) != hipSuccess) return -1.0f;
+    float ms = -1.0f;
+    if (hipEventElapsedTime(&ms, e->ev0, e->ev1) != hipSuccess) return -1.0f;
+    return ms;
+}
+
+double gs_round_kernel_bytes(const gs_engine *e) {
+    // DESIGN.md "Roofline": per (node, rumor slot) 1 B state read + 1 B state
+    // write (8 bit-planes) + 3/8 B class planes of each pusher (mean in-degree
+    // 1) + 3/8 B class planes of t(x); per node 104 B of CSR, target and
+    // Statistics traffic.
+    if (!e) return 0.0;
+    const double n = e->g.n, rp = e->g.rpad;
+    return n * (2.75 * rp + 104.0);
+}
+
+}  // extern "C"

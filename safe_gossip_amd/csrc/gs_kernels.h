@@ -1,0 +1,54 @@
+// gs_kernels.h -- launch interface of the round kernels (gs_kernels.hip).
+#pragma once
+#include "gs_common.h"
+
+namespace gs {
+
+struct RoundArgs {
+    const u64 *Scur;          // state planes, round t (post phase 0)
+    u64 *Snext;               // state planes, round t+1 (post phase 0)
+    const uint32_t *off;      // in-edge CSR of round t: offsets[n+1]
+    const uint32_t *src;      //   sources, ascending within a bucket
+    uint32_t *tg;             // tg[x]: round-t target in, round-(t+1) target out
+    uint32_t *cnt;            // in-degree histogram of round t+1 (accumulated)
+    u64 *stats;               // [5][n] Statistics SoA
+    const u64 *inj_key;       // sorted segment keys with injections (round t+1)
+    const u64 *inj_mask;      //   rumor masks in segment coordinates
+    uint32_t n_inj;
+    uint32_t *flags;          // [0..1] any_live per round parity, [2] device limit
+    // observation outputs (mode OBSERVE); any may be null
+    u64 *obs_known;           // [n][KW]
+    u64 *obs_stats;           // [n][5]
+    uint16_t *obs_state;      // [n][R]
+    uint16_t *obs_rec;        // [n][R]
+    uint32_t *obs_psize;      // [n]
+    Geometry g;
+    uint64_t seed;
+    uint32_t epoch;
+    uint32_t round_new;       // t+1
+    uint32_t cmax, maxc, maxr;
+};
+
+// mode: 0 = transition only (first round), 1 = deliver round t + transition
+// to t+1, 2 = deliver round t and write observation outputs only,
+// 3 = observe without pending deliveries.
+hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s);
+
+// In-edge CSR of the round whose targets are in tg (cnt holds its histogram;
+// it is consumed back to zero).  Also clears the any_live slot of the round
+// after it.
+hipError_t launch_build_csr(const uint32_t *tg, uint32_t *cnt, uint32_t *off,
+                            uint32_t *src, uint32_t *bsum, uint32_t n,
+                            uint32_t *flags, uint32_t next_round_slot, hipStream_t s);
+size_t csr_bsum_words(uint32_t n);
+
+// First-round targets + histogram (mode 0 does this itself; used after clear).
+// Reductions for observers.
+hipError_t launch_known_reduce(const u64 *known, uint32_t n, uint32_t KW, uint32_t R,
+                               u64 *partials /* [2*blocks] */, uint32_t blocks,
+                               hipStream_t s);
+hipError_t launch_stats_reduce(const u64 *stats, uint32_t n, int op,
+                               u64 *partials /* [5*blocks] */, uint32_t blocks,
+                               hipStream_t s);
+
+}  // namespace gs

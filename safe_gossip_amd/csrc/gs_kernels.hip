@@ -1,0 +1,608 @@
+// gs_kernels.hip -- hand-written gfx950 kernels of one safe_gossip push-pull
+// round over the whole population (2P schedule).
+//
+// One lane owns one SEGMENT: (node x, 64-rumor word j) when R >= 64, or the
+// whole R-bit rumor row of node x when R < 64 (several nodes share a word).
+// All per-rumor logic is bit-sliced over the segment (64 rumors per u64
+// operation); nothing is per-rumor scalar.
+//
+// The round kernel fuses, for every node x:
+//   phase 1 of round t at x  : Gossip::receive of every push batch x got,
+//                              ascending pusher order (src/gossip.rs:118-163)
+//   phase 2 of round t at x  : Gossip::receive of the pull batch from t(x)
+//   phase 0 of round t+1 at x: Gossip::new_message injections
+//                              (src/gossip.rs:71-75), then Gossip::next_round
+//                              = MessageState::next_round for every rumor
+//                              (src/message_state.rs:86-171) + push list +
+//                              Statistics (src/gossip.rs:79-113).
+// B.peer_counters are never materialised: the copies x received are
+// re-derived from the round-t class planes of its pushers and of t(x), which
+// is all MessageState::next_round consumes (anyC + a count of counters >= own).
+#include "gs_kernels.h"
+
+namespace gs {
+
+#define GS_DEV __device__ __forceinline__
+
+GS_DEV uint32_t popc(u64 v) { return (uint32_t)__popcll(v); }
+
+// c += in (bit-sliced 5-bit counters, one per rumor).
+GS_DEV void add5(u64 (&c)[5], u64 in) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        u64 t = c[i] & in;
+        c[i] ^= in;
+        in = t;
+    }
+}
+
+// Bit-sliced "x >= K" for an nb-bit number per rumor, K a per-lane constant.
+template <int NB>
+GS_DEV u64 ge_k(const u64 (&x)[NB], uint32_t K) {
+    if (K >= (1u << NB)) return 0ull;
+    u64 gt = 0ull, eq = ~0ull;
+#pragma unroll
+    for (int i = NB - 1; i >= 0; --i) {
+        u64 ki = ((K >> i) & 1u) ? ~0ull : 0ull;
+        gt |= eq & x[i] & ~ki;
+        eq &= ~(x[i] ^ ki);
+    }
+    return gt | eq;
+}
+
+struct Cls {
+    u64 c, a0, a1;
+};
+
+template <bool SMALL>
+struct Lane {
+    // segment geometry
+    uint32_t x, j;
+    u64 base;       // index of plane 0 of this lane's word
+    uint32_t sh;    // bit offset of the segment in its word (small)
+    u64 m;          // segment mask (after shifting down)
+    uint32_t W, lognpu, logr;
+
+    GS_DEV void init(const Geometry &g, u64 seg) {
+        W = g.W;
+        lognpu = g.lognpu;
+        logr = g.logr;
+        if (SMALL) {
+            x = (uint32_t)seg;
+            j = 0;
+            base = (u64)(x >> lognpu) * kPlanes;
+            sh = (x & ((1u << lognpu) - 1u)) << logr;
+            m = (1ull << g.rpad) - 1ull;  // rpad < 64 here
+        } else {
+            x = (uint32_t)(seg / W);
+            j = (uint32_t)(seg % W);
+            base = (u64)x * kPlanes * W + j;
+            sh = 0;
+            m = ~0ull;
+        }
+    }
+    GS_DEV u64 plane_index(uint32_t p) const { return SMALL ? base + p : base + (u64)p * W; }
+    // Class planes (isC, a0, a1) of node s for this lane's word.
+    GS_DEV Cls load_cls(const u64 *__restrict__ S, uint32_t s) const {
+        Cls r;
+        if (SMALL) {
+            u64 b = (u64)(s >> lognpu) * kPlanes;
+            uint32_t ss = (s & ((1u << lognpu) - 1u)) << logr;
+            r.c = (S[b] >> ss) & m;
+            r.a0 = (S[b + 1] >> ss) & m;
+            r.a1 = (S[b + 2] >> ss) & m;
+        } else {
+            u64 b = (u64)s * kPlanes * W + j;
+            r.c = S[b];
+            r.a0 = S[b + W];
+            r.a1 = S[b + 2 * (u64)W];
+        }
+        return r;
+    }
+};
+
+// Sum / min over the W lanes of one node (W a power of two <= 64, lanes of a
+// node are consecutive and W-aligned inside the wave).
+GS_DEV uint32_t group_sum(uint32_t v, uint32_t W) {
+    for (uint32_t o = 1; o < W; o <<= 1) v += __shfl_xor(v, (int)o, 64);
+    return v;
+}
+GS_DEV uint32_t group_min(uint32_t v, uint32_t W) {
+    for (uint32_t o = 1; o < W; o <<= 1) v = min(v, (uint32_t)__shfl_xor(v, (int)o, 64));
+    return v;
+}
+
+constexpr uint32_t kNone = 0xffffffffu;
+
+// MODE: 0 transition only, 1 deliver + transition, 2 deliver + observe,
+// 3 observe only.
+template <bool SMALL, int MODE>
+__global__ __launch_bounds__(256) void round_kernel(RoundArgs a) {
+    constexpr bool DELIVER = (MODE == 1 || MODE == 2);
+    constexpr bool TRANSITION = (MODE == 0 || MODE == 1);
+    const Geometry &g = a.g;
+    const u64 seg = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = seg < g.nseg;
+    Lane<SMALL> L;
+    L.init(g, valid ? seg : 0);
+    const uint32_t x = L.x;
+    const u64 *__restrict__ S = a.Scur;
+
+    // ---- own round-t state (post phase 0): 8 planes
+    u64 P[kPlanes];
+#pragma unroll
+    for (int p = 0; p < kPlanes; ++p) {
+        u64 v = valid ? S[L.plane_index(p)] : 0ull;
+        P[p] = SMALL ? ((v >> L.sh) & L.m) : v;
+    }
+    const u64 isC = P[0], a0 = P[1], a1 = P[2];
+    const u64 A = ~isC & ~a0 & ~a1 & L.m;
+    const u64 B = ~isC & (a0 | a1);
+    const u64 C = isC & ~(a0 & a1);
+    const u64 D = isC & a0 & a1;
+    const u64 liveX = B | C;
+
+    // ---- phases 1 and 2 of round t at x (Gossip::receive)
+    u64 crB = 0, crC = 0, anyC = 0;
+    u64 c1[5] = {0, 0, 0, 0, 0};  // recorded counters in [1, cmax)
+    u64 c2[5] = {0, 0, 0, 0, 0};  // recorded counters == 2 (< cmax)
+    uint32_t k = 0, psize = 0, part_cw = 0, first_create = kNone, recv = 0;
+    if (DELIVER && valid) {
+        const uint32_t z = a.tg[x];  // t_t(x): the pull batch comes from z
+        const uint32_t k0 = a.off[x];
+        k = a.off[x + 1] - k0;
+        if (k > 30u) atomicOr(&a.flags[2], 1u);
+        u64 notyet = A;  // still absent: the next live copy creates the entry
+        bool zin = false;
+        for (uint32_t i = 0; i < k; ++i) {
+            const uint32_t s = a.src[k0 + i];
+            const Cls q = L.load_cls(S, s);
+            const u64 vC = q.c & ~(q.a0 & q.a1);   // C: counter 255
+            const u64 vB = ~q.c & (q.a0 | q.a1);   // B: counter = our_counter
+            const u64 v2 = vB & q.a1 & ~q.a0;      // B with our_counter 2
+            const u64 sl = vB | vC;                // the push batch of s
+            const u64 newc = notyet & sl;          // new_from_peer (not recorded)
+            if (s != z) {
+                // MessageState::receive on B entries.  t(x)'s own push copy is
+                // superseded by its pull copy (same value), counted below.
+                const u64 rec = (B | crB) & sl;
+                anyC |= rec & vC;
+                add5(c1, rec & vB);
+                add5(c2, rec & v2);
+            } else {
+                zin = true;
+            }
+            crB |= newc & ~vC;
+            crC |= newc & vC;
+            notyet &= ~sl;
+            const uint32_t pc = popc(newc);
+            part_cw += (k - 1u - i) * pc;  // later pushers' pull rows include it
+            if (pc && first_create == kNone) first_create = i;
+            recv += popc(sl);
+        }
+        // Pull batch from z: z's live set plus entries z created from pushers
+        // ahead of x (Gossip::receive builds the pull list before absorbing
+        // x's push, src/gossip.rs:124-151).
+        const Cls zq = L.load_cls(S, z);
+        const u64 zA = ~zq.c & ~zq.a0 & ~zq.a1 & L.m;
+        const u64 zB = ~zq.c & (zq.a0 | zq.a1);
+        const u64 zC = zq.c & ~(zq.a0 & zq.a1);
+        u64 pB = 0, pC = 0, pnot = zA;
+        if (pnot) {
+            const uint32_t m0 = a.off[z], m1 = a.off[z + 1];
+            for (uint32_t q = m0; q < m1 && pnot; ++q) {
+                const uint32_t s = a.src[q];
+                if (s >= x) break;
+                const Cls sq = L.load_cls(S, s);
+                const u64 vC = sq.c & ~(sq.a0 & sq.a1);
+                const u64 sl = (~sq.c & (sq.a0 | sq.a1)) | vC;
+                const u64 nc = pnot & sl;
+                pB |= nc & ~vC;
+                pC |= nc & vC;
+                pnot &= ~sl;
+            }
+        }
+        const u64 pv2 = zB & zq.a1 & ~zq.a0;
+        const u64 pvB = (zB | pB);                 // counters 1 (created: 1) or 2
+        const u64 pCl = zC | pC;
+        const u64 pl = pvB | pCl;
+        {
+            const u64 newc = notyet & pl;
+            const u64 rec = (B | crB) & pl;
+            anyC |= rec & pCl;
+            add5(c1, rec & pvB);
+            add5(c2, rec & pv2);
+            crB |= newc & ~pCl;
+            crC |= newc & pCl;
+        }
+        recv += popc(pl);
+        psize = k + (zin ? 0u : 1u);  // |peers_in_this_round|
+    }
+
+    // ---- node-level statistics of the deliveries
+    uint32_t lc = popc(liveX);
+    if (DELIVER && !SMALL) {
+        lc = group_sum(lc, g.W);
+        part_cw = group_sum(part_cw, g.W);
+        recv = group_sum(recv, g.W);
+        first_create = group_min(first_create, g.W);
+    }
+    uint64_t d_full_sent = 0, d_empty_pull = 0, d_recv = 0;
+    if (DELIVER) {
+        d_full_sent = (uint64_t)k * lc + part_cw;  // pull rows sent by x
+        if (k > 0 && lc == 0) d_empty_pull = (first_create == kNone) ? k : first_create + 1u;
+        d_recv = recv;
+    }
+    const bool leader = valid && (SMALL || L.j == 0);
+
+    if (!TRANSITION) {
+        // ---------------- observation (post phase 2 of round t) -------------
+        if (!valid) return;
+        const uint32_t KW = (g.R + 63u) >> 6;
+        const u64 known = (~A | crB | crC) & L.m;
+        if (a.obs_known && (SMALL || L.j < KW)) a.obs_known[(u64)x * KW + L.j] = known;
+        if (leader) {
+            if (a.obs_stats) {
+                const u64 n = g.n;
+                a.obs_stats[(u64)x * 5 + 0] = a.stats[0 * n + x];
+                a.obs_stats[(u64)x * 5 + 1] = a.stats[1 * n + x] + d_empty_pull;
+                a.obs_stats[(u64)x * 5 + 2] = a.stats[2 * n + x];
+                a.obs_stats[(u64)x * 5 + 3] = a.stats[3 * n + x] + d_full_sent;
+                a.obs_stats[(u64)x * 5 + 4] = a.stats[4 * n + x] + d_recv;
+            }
+            if (a.obs_psize) a.obs_psize[x] = psize;
+        }
+        if (a.obs_state || a.obs_rec) {
+            const uint32_t nb = SMALL ? g.rpad : 64u;
+            for (uint32_t b = 0; b < nb; ++b) {
+                const uint32_t r = SMALL ? b : L.j * 64u + b;
+                if (r >= g.R) break;
+                const u64 bit = 1ull << b;
+                uint32_t bf = 0;
+#pragma unroll
+                for (int i = 0; i < 5; ++i) bf |= ((P[3 + i] >> b) & 1u) << i;
+                const uint32_t af = (uint32_t)((a0 >> b) & 1u) | ((uint32_t)((a1 >> b) & 1u) << 1);
+                uint16_t code = 0;
+                if (crB & bit) code = (uint16_t)((1u << 14) | (1u << 7));
+                else if (crC & bit) code = (uint16_t)(2u << 14);
+                else if (B & bit) code = (uint16_t)((1u << 14) | (af << 7) | bf);
+                else if (C & bit) code = (uint16_t)((2u << 14) | (af << 7) | bf);
+                else if (D & bit) code = (uint16_t)(3u << 14);
+                if (a.obs_state) a.obs_state[(u64)x * g.R + r] = code;
+                if (a.obs_rec) {
+                    uint16_t rv = 0;
+                    if ((B | crB) & bit) {
+                        uint32_t v1 = 0, v2 = 0;
+#pragma unroll
+                        for (int i = 0; i < 5; ++i) {
+                            v1 |= ((c1[i] >> b) & 1u) << i;
+                            v2 |= ((c2[i] >> b) & 1u) << i;
+                        }
+                        rv = (uint16_t)((((anyC >> b) & 1u) << 15) | (v2 << 7) | v1);
+                    }
+                    a.obs_rec[(u64)x * g.R + r] = rv;
+                }
+            }
+        }
+        return;
+    }
+
+    // ---------------- phase 0 of round t+1 at x ----------------------------
+    // Gossip::new_message (insert = replace with MessageState::new, records
+    // dropped) for the rumors injected at x this round.
+    u64 inj = 0;
+    if (a.n_inj && valid) {
+        const u64 key = SMALL ? (u64)x : seg;
+        uint32_t lo = 0, hi = a.n_inj;
+        while (lo < hi) {
+            uint32_t mid = (lo + hi) >> 1;
+            if (a.inj_key[mid] < key) lo = mid + 1; else hi = mid;
+        }
+        if (lo < a.n_inj && a.inj_key[lo] == key) inj = a.inj_mask[lo] & L.m;
+    }
+    const u64 ninj = ~inj;
+    const u64 Bold = B & ninj, Cold = C & ninj, Dold = D & ninj;
+    const u64 cB = crB & ninj, cC = crC & ninj;
+    const u64 Bf = Bold | cB | inj;  // entries in state B entering next_round
+    const u64 Cf = Cold | cC;        // entries in state C entering next_round
+
+    // B (src/message_state.rs:94-147).  0-filled peers vote "less", so with
+    // no C copy the median rule is: bump iff 2*ge > |P| iff ge >= |P|/2+1.
+    const u64 oc1 = (Bold & a0 & ~a1) | cB | inj;
+    const u64 oc2 = Bold & a1 & ~a0;
+    const uint32_t thr = psize / 2u + 1u;
+    const u64 bump = ((oc1 & ge_k<5>(c1, thr)) | (oc2 & ge_k<5>(c2, thr))) & ninj;
+    const u64 anyCe = anyC & ninj;
+    u64 nr[6];  // round + 1
+    {
+        u64 carry = ~0ull;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const u64 rb = P[3 + i] & Bold;
+            nr[i] = rb ^ carry;
+            carry &= rb;
+        }
+        nr[5] = carry;
+    }
+    const u64 toD = ge_k<6>(nr, a.maxr);
+    const u64 oc1n = oc1 & ~bump;
+    const u64 oc2n = (oc1 & bump) | (oc2 & ~bump);
+    const u64 oc3n = oc2 & bump;
+    const u64 ocge = a.cmax <= 1u ? ~0ull : (a.cmax == 2u ? (oc2n | oc3n) : oc3n);
+    const u64 toC = anyCe | ocge;
+    const u64 BD = Bf & toD, BC = Bf & ~toD & toC, BB = Bf & ~toD & ~toC;
+
+    // C (src/message_state.rs:148-168): round+1; D if round+rib >= max_rounds
+    // or round >= max_c_rounds.
+    const u64 cr0 = a0 & Cold, cr1 = a1 & Cold;
+    const u64 d[3] = {~cr0, cr1 ^ cr0, cr1 & cr0};
+    u64 rib[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) rib[i] = P[3 + i] & Cold;
+    u64 sum[6];
+    {
+        u64 c = 0;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const u64 di = i < 3 ? d[i] : 0ull;
+            sum[i] = rib[i] ^ di ^ c;
+            c = (rib[i] & di) | (c & (rib[i] ^ di));
+        }
+        sum[5] = c;
+    }
+    const u64 CtoD = ge_k<6>(sum, a.maxr) | ge_k<3>(d, a.maxc);
+    const u64 CD = Cf & CtoD, CC = Cf & ~CtoD;
+
+    const u64 Dn = BD | CD | Dold;
+    const u64 Cn = BC | CC;
+    const u64 Bn = BB;
+    u64 N[kPlanes];
+    N[0] = Cn | Dn;
+    N[1] = (Bn & oc1n) | (CC & d[0]) | Dn;
+    N[2] = (Bn & oc2n) | (CC & d[1]) | Dn;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) N[3 + i] = ((Bn | BC) & nr[i]) | (CC & rib[i]);
+
+    // ---- write round-(t+1) planes
+    if (SMALL) {
+        const uint32_t npu = 1u << g.lognpu;
+#pragma unroll
+        for (int p = 0; p < kPlanes; ++p) {
+            u64 v = valid ? ((N[p] & L.m) << L.sh) : 0ull;
+            for (uint32_t o = 1; o < npu; o <<= 1) v |= __shfl_xor(v, (int)o, 64);
+            if (valid && (x & (npu - 1u)) == 0) a.Snext[L.plane_index(p)] = v;
+        }
+    } else {
+        if (valid) {
+#pragma unroll
+            for (int p = 0; p < kPlanes; ++p) a.Snext[L.plane_index(p)] = N[p];
+        }
+    }
+
+    // ---- push list + Statistics (src/gossip.rs:80,103-111)
+    uint32_t live_new = valid ? popc(Bn | Cn) : 0u;
+    if (!SMALL) live_new = group_sum(live_new, g.W);
+    const int blk_live = __syncthreads_or(live_new != 0u);
+    if (threadIdx.x == 0 && blk_live) {
+        uint32_t *f = &a.flags[a.round_new & 1u];
+        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+            atomicOr(f, 1u);
+    }
+    if (leader) {
+        const u64 n = g.n;
+        u64 *st = a.stats;
+        st[0 * n + x] += 1u;                                     // rounds
+        if (DELIVER) {
+            st[1 * n + x] += d_empty_pull;                       // empty_pull_sent
+            st[4 * n + x] += d_recv;                             // full_message_received
+        }
+        st[2 * n + x] += (live_new == 0u) ? 1u : 0u;             // empty_push_sent
+        st[3 * n + x] += (uint64_t)live_new + d_full_sent;       // full_message_sent
+        // Peer choice of round t+1 and its in-degree histogram.
+        const uint32_t tn = peer_of(a.seed, a.epoch, a.round_new, x, g.n);
+        a.tg[x] = tn;
+        atomicAdd(&a.cnt[tn], 1u);
+    }
+}
+
+template <bool SMALL>
+static hipError_t launch_mode(const RoundArgs &a, int mode, hipStream_t s) {
+    const uint32_t block = 256;
+    const u64 grid = (a.g.nseg + block - 1) / block;
+    switch (mode) {
+    case 0: hipLaunchKernelGGL((round_kernel<SMALL, 0>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((round_kernel<SMALL, 1>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((round_kernel<SMALL, 2>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
+    default: hipLaunchKernelGGL((round_kernel<SMALL, 3>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s) {
+    return a.g.small ? launch_mode<true>(a, mode, s) : launch_mode<false>(a, mode, s);
+}
+
+// ------------------------------------------------------------ in-edge CSR
+constexpr uint32_t kScanBlock = 256;
+constexpr uint32_t kScanPer = 16;
+constexpr uint32_t kScanTile = kScanBlock * kScanPer;
+
+size_t csr_bsum_words(uint32_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
+
+// Block-wide exclusive scan of one value per thread; returns the block total.
+GS_DEV uint32_t block_exclusive_scan(uint32_t v, uint32_t *lds, uint32_t &total) {
+    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(inc, (unsigned)o, 64);
+        if (lane >= (uint32_t)o) inc += t;
+    }
+    if (lane == 63) lds[wid] = inc;
+    __syncthreads();
+    uint32_t wbase = 0, tot = 0;
+    for (uint32_t w = 0; w < kScanBlock / 64; ++w) {
+        if (w < wid) wbase += lds[w];
+        tot += lds[w];
+    }
+    __syncthreads();
+    total = tot;
+    return wbase + inc - v;
+}
+
+__global__ __launch_bounds__(kScanBlock) void scan_tile_sums(const uint32_t *__restrict__ cnt,
+                                                             uint32_t n, uint32_t *bsum) {
+    __shared__ uint32_t lds[kScanBlock / 64];
+    const u64 b0 = (u64)blockIdx.x * kScanTile + (u64)threadIdx.x * kScanPer;
+    uint32_t s = 0;
+    for (uint32_t i = 0; i < kScanPer; ++i)
+        if (b0 + i < n) s += cnt[b0 + i];
+    uint32_t tot;
+    block_exclusive_scan(s, lds, tot);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kScanBlock) void scan_bsums(uint32_t *bsum, uint32_t nb) {
+    __shared__ uint32_t lds[kScanBlock / 64];
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nb; base += kScanBlock) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < nb ? bsum[i] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_exclusive_scan(v, lds, tot);
+        if (i < nb) bsum[i] = carry + ex;
+        carry += tot;
+    }
+}
+
+__global__ __launch_bounds__(kScanBlock) void scan_tiles(const uint32_t *__restrict__ cnt, uint32_t n,
+                                                         const uint32_t *__restrict__ bsum,
+                                                         uint32_t *__restrict__ off) {
+    __shared__ uint32_t lds[kScanBlock / 64];
+    const u64 b0 = (u64)blockIdx.x * kScanTile + (u64)threadIdx.x * kScanPer;
+    uint32_t v[kScanPer];
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kScanPer; ++i) {
+        v[i] = (b0 + i < n) ? cnt[b0 + i] : 0u;
+        s += v[i];
+    }
+    uint32_t tot;
+    uint32_t run = bsum[blockIdx.x] + block_exclusive_scan(s, lds, tot);
+#pragma unroll
+    for (uint32_t i = 0; i < kScanPer; ++i) {
+        if (b0 + i < n) off[b0 + i] = run;
+        run += v[i];
+    }
+    if (b0 + kScanPer >= n && b0 < n) off[n] = run;  // the thread owning the last element
+}
+
+__global__ __launch_bounds__(256) void scatter_edges(const uint32_t *__restrict__ tg,
+                                                     const uint32_t *__restrict__ off,
+                                                     uint32_t *cnt, uint32_t *src, uint32_t n) {
+    const u64 x = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= n) return;
+    const uint32_t t = tg[x];
+    const uint32_t old = atomicSub(&cnt[t], 1u);  // leaves cnt all-zero
+    src[off[t] + old - 1u] = (uint32_t)x;
+}
+
+// Ascending sources per bucket: the order Gossip::receive sees its pushers in
+// (pairs delivered in (src, dst) order, src/gossiper.rs:217).
+__global__ __launch_bounds__(256) void sort_buckets(const uint32_t *__restrict__ off, uint32_t *src,
+                                                    uint32_t n, uint32_t *flags, uint32_t slot) {
+    const u64 y = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (y == 0) flags[slot] = 0u;
+    if (y >= n) return;
+    const uint32_t a = off[y], b = off[y + 1];
+    for (uint32_t i = a + 1; i < b; ++i) {
+        const uint32_t v = src[i];
+        uint32_t q = i;
+        while (q > a && src[q - 1] > v) {
+            src[q] = src[q - 1];
+            --q;
+        }
+        src[q] = v;
+    }
+}
+
+hipError_t launch_build_csr(const uint32_t *tg, uint32_t *cnt, uint32_t *off, uint32_t *src,
+                            uint32_t *bsum, uint32_t n, uint32_t *flags,
+                            uint32_t next_round_slot, hipStream_t s) {
+    const uint32_t nb = (n + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(scan_tile_sums, dim3(nb), dim3(kScanBlock), 0, s, cnt, n, bsum);
+    hipLaunchKernelGGL(scan_bsums, dim3(1), dim3(kScanBlock), 0, s, bsum, nb);
+    hipLaunchKernelGGL(scan_tiles, dim3(nb), dim3(kScanBlock), 0, s, cnt, n, bsum, off);
+    const uint32_t g = (n + 255) / 256;
+    hipLaunchKernelGGL(scatter_edges, dim3(g), dim3(256), 0, s, tg, off, cnt, src, n);
+    hipLaunchKernelGGL(sort_buckets, dim3(g), dim3(256), 0, s, off, src, n, flags, next_round_slot);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------ reductions
+__global__ __launch_bounds__(256) void known_reduce(const u64 *__restrict__ known, uint32_t n,
+                                                    uint32_t KW, uint32_t R, u64 *partials) {
+    __shared__ u64 s_tot[256], s_cmp[256];
+    u64 tot = 0, cmp = 0;
+    for (u64 x = (u64)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (u64)gridDim.x * blockDim.x) {
+        uint32_t c = 0;
+        for (uint32_t w = 0; w < KW; ++w) c += popc(known[x * KW + w]);
+        tot += c;
+        cmp += (c == R) ? 1u : 0u;
+    }
+    s_tot[threadIdx.x] = tot;
+    s_cmp[threadIdx.x] = cmp;
+    __syncthreads();
+    for (uint32_t o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) {
+            s_tot[threadIdx.x] += s_tot[threadIdx.x + o];
+            s_cmp[threadIdx.x] += s_cmp[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        partials[2 * blockIdx.x] = s_tot[0];
+        partials[2 * blockIdx.x + 1] = s_cmp[0];
+    }
+}
+
+hipError_t launch_known_reduce(const u64 *known, uint32_t n, uint32_t KW, uint32_t R,
+                               u64 *partials, uint32_t blocks, hipStream_t s) {
+    hipLaunchKernelGGL(known_reduce, dim3(blocks), dim3(256), 0, s, known, n, KW, R, partials);
+    return hipGetLastError();
+}
+
+// Statistics::add / min / max over [n][5] observed statistics.
+__global__ __launch_bounds__(256) void stats_reduce(const u64 *__restrict__ st, uint32_t n, int op,
+                                                    u64 *partials) {
+    __shared__ u64 sm[5][256];
+    u64 acc[5];
+    for (int f = 0; f < 5; ++f) acc[f] = (op == 1) ? ~0ull : 0ull;
+    for (u64 x = (u64)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (u64)gridDim.x * blockDim.x) {
+        for (int f = 0; f < 5; ++f) {
+            const u64 v = st[x * 5 + f];
+            acc[f] = op == 0 ? acc[f] + v : (op == 1 ? min(acc[f], v) : max(acc[f], v));
+        }
+    }
+    for (int f = 0; f < 5; ++f) sm[f][threadIdx.x] = acc[f];
+    __syncthreads();
+    for (uint32_t o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) {
+            for (int f = 0; f < 5; ++f) {
+                const u64 u = sm[f][threadIdx.x], v = sm[f][threadIdx.x + o];
+                sm[f][threadIdx.x] = op == 0 ? u + v : (op == 1 ? min(u, v) : max(u, v));
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        for (int f = 0; f < 5; ++f) partials[5 * blockIdx.x + f] = sm[f][0];
+}
+
+hipError_t launch_stats_reduce(const u64 *stats, uint32_t n, int op, u64 *partials,
+                               uint32_t blocks, hipStream_t s) {
+    hipLaunchKernelGGL(stats_reduce, dim3(blocks), dim3(256), 0, s, stats, n, op, partials);
+    return hipGetLastError();
+}
+
+}  // namespace gs

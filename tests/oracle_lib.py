@@ -1,0 +1,192 @@
+"""ctypes wrapper of the CPU oracle (oracle/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, always as the checker, never as the product.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+
+SCHED_2P = 0
+SCHED_SEQ = 1
+
+
+class OrStats(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_uint64) for f in (
+        "rounds", "empty_pull_sent", "empty_push_sent", "full_message_sent",
+        "full_message_received")]
+
+
+class OrMetrics(ctypes.Structure):
+    _fields_ = [("nodes_missed", ctypes.c_uint64), ("msgs_missed", ctypes.c_uint64),
+                ("stats", OrStats), ("rounds_run", ctypes.c_uint32),
+                ("round_full", ctypes.c_uint32)]
+
+
+_P = ctypes.c_void_p
+_U8P = ctypes.POINTER(ctypes.c_uint8)
+_U16P = ctypes.POINTER(ctypes.c_uint16)
+_U32P = ctypes.POINTER(ctypes.c_uint32)
+_U64P = ctypes.POINTER(ctypes.c_uint64)
+
+_SIGS = {
+    "or_create": (_P, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32]),
+    "or_destroy": (None, [_P]),
+    "or_set_params": (None, [_P, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8]),
+    "or_get_params": (None, [_P, _U8P]),
+    "or_send_new": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_uint32]),
+    "or_next_round": (ctypes.c_int, [_P, ctypes.c_int, _U32P]),
+    "or_clear": (None, [_P, ctypes.c_uint32]),
+    "or_round": (ctypes.c_uint32, [_P]),
+    "or_dump_state": (None, [_P, _U16P]),
+    "or_dump_records": (None, [_P, _U16P, _U32P]),
+    "or_statistics": (None, [_P, _U64P]),
+    "or_messages": (None, [_P, ctypes.c_uint32, _U64P]),
+    "or_known_total": (ctypes.c_uint64, [_P]),
+    "or_send_messages": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_int,
+                                         ctypes.POINTER(OrMetrics)]),
+    "or_philox": (None, [_U32P, _U32P, _U32P]),
+    "or_peer": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                  ctypes.c_uint32, ctypes.c_uint32]),
+    "or_origin": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                    ctypes.c_uint32]),
+    "or_coin": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                  ctypes.c_uint32]),
+    "or_derive_params": (None, [ctypes.c_uint32, _U8P]),
+    "or_ms_step": (None, [_U8P, _U32P, _U8P, ctypes.c_uint32, _U32P, ctypes.c_uint32,
+                          ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_int]),
+    "or_ms_new": (None, [_U8P]),
+    "or_ms_our_counter": (ctypes.c_int, [_U8P]),
+}
+
+_LIB = None
+
+
+def build_oracle() -> str:
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR, "liboracle.so"], check=True)
+    return ORACLE_LIB
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(ORACLE_LIB):
+            build_oracle()
+        _LIB = ctypes.CDLL(ORACLE_LIB)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(_LIB, name)
+            f.restype = res
+            f.argtypes = args
+    return _LIB
+
+
+def philox(ctr, key):
+    c = (ctypes.c_uint32 * 4)(*ctr)
+    k = (ctypes.c_uint32 * 2)(*key)
+    o = (ctypes.c_uint32 * 4)()
+    lib().or_philox(c, k, o)
+    return tuple(o)
+
+
+def derive_params(n):
+    o = (ctypes.c_uint8 * 3)()
+    lib().or_derive_params(n, o)
+    return tuple(o)
+
+
+TAGS = {"A": 0, "B": 1, "C": 2, "D": 3}
+
+
+def ms_step(state, records, pir, params, next_round=True):
+    """state = (tag, round, our_counter, rib); records = [(peer, counter)]."""
+    io = (ctypes.c_uint8 * 4)(*state)
+    peers = (ctypes.c_uint32 * max(1, len(records)))(*[p for p, _ in records])
+    vals = (ctypes.c_uint8 * max(1, len(records)))(*[v for _, v in records])
+    pr = (ctypes.c_uint32 * max(1, len(pir)))(*sorted(pir))
+    lib().or_ms_step(io, peers, vals, len(records), pr, len(pir), params[0], params[1],
+                     params[2], 1 if next_round else 0)
+    return tuple(io)
+
+
+class OracleNet:
+    """One oracle network (per-node ordered maps, reference-faithful)."""
+
+    def __init__(self, n, R, seed=0x5AFE6055, epoch=0, params=None):
+        self._l = lib()
+        self.h = self._l.or_create(n, R, seed, epoch)
+        self.n, self.R, self.seed, self.epoch = n, R, seed, epoch
+        if params is not None:
+            self._l.or_set_params(self.h, *params)
+
+    def close(self):
+        if self.h:
+            self._l.or_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def params(self):
+        o = (ctypes.c_uint8 * 3)()
+        self._l.or_get_params(self.h, o)
+        return tuple(o)
+
+    @property
+    def round(self):
+        return self._l.or_round(self.h)
+
+    def send_new(self, node, rumor):
+        return self._l.or_send_new(self.h, node, rumor)
+
+    def next_round(self, schedule=SCHED_2P):
+        live = ctypes.c_uint32()
+        rc = self._l.or_next_round(self.h, schedule, ctypes.byref(live))
+        return rc, bool(live.value)
+
+    def clear(self, epoch):
+        self._l.or_clear(self.h, epoch)
+        self.epoch = epoch
+
+    def dump_state(self):
+        out = np.zeros((self.n, self.R), dtype=np.uint16)
+        self._l.or_dump_state(self.h, out.ctypes.data_as(_U16P))
+        return out
+
+    def dump_records(self):
+        rec = np.zeros((self.n, self.R), dtype=np.uint16)
+        ps = np.zeros(self.n, dtype=np.uint32)
+        self._l.or_dump_records(self.h, rec.ctypes.data_as(_U16P), ps.ctypes.data_as(_U32P))
+        return rec, ps
+
+    def statistics(self):
+        out = np.zeros((self.n, 5), dtype=np.uint64)
+        self._l.or_statistics(self.h, out.ctypes.data_as(_U64P))
+        return out
+
+    def known_all(self):
+        kw = (self.R + 63) // 64
+        out = np.zeros((self.n, kw), dtype=np.uint64)
+        for x in range(self.n):
+            self._l.or_messages(self.h, x, out[x].ctypes.data_as(_U64P))
+        return out
+
+    def known_total(self):
+        return int(self._l.or_known_total(self.h))
+
+    def send_messages(self, num_msgs, schedule=SCHED_SEQ):
+        m = OrMetrics()
+        rc = self._l.or_send_messages(self.h, num_msgs, schedule, ctypes.byref(m))
+        assert rc == 0
+        return m

@@ -1,0 +1,171 @@
+"""GPU engine vs CPU oracle, round by round, bit-exact (2P schedule).
+
+Each round compares, for every (node, rumor): the MessageState after delivery
+(tag, round, our_counter, rounds_in_state_b), the summary of B.peer_counters
+that the next MessageState::next_round consumes (anyC, #counters in [1,cmax),
+#counters == 2), |peers_in_this_round|, the five Statistics counters of every
+node, the known-rumor sets (Gossiper::messages) and the harness's
+`processed` flag.  Integer work: the bar is exact equality.
+"""
+import numpy as np
+import pytest
+
+from oracle_lib import SCHED_2P, OracleNet
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5AFE6055
+
+
+def _injections(kind, n, R, seed, epoch, rnd, eng):
+    """Injections (node, rumor) applied before round `rnd` (1-based)."""
+    out = []
+    if kind == "origins":          # every rumor injected in round 1 (cfg3/cfg4)
+        if rnd == 1:
+            out = [(eng.origin_of(seed, epoch, r, n), r) for r in range(R)]
+    elif kind == "example":        # examples/network.rs:467-469: random, random, node 0
+        if rnd == 1:
+            out = [(eng.origin_of(seed, epoch, 0, n), 0), (eng.origin_of(seed, epoch, 1, n), 1),
+                   (0, 2)][:R]
+    elif kind == "trickle":        # first at a random node, then 50%/node/round
+        st = _injections.state
+        if rnd == 1:
+            st["next"] = 0
+            out.append((eng.origin_of(seed, epoch, 0, n), 0))
+            st["next"] = 1
+        for x in range(n):
+            if st["next"] >= R:
+                break
+            if eng.coin_of(seed, epoch, rnd, x):
+                out.append((x, st["next"]))
+                st["next"] += 1
+    elif kind == "reinject":       # re-sending known rumors exercises insert-replace
+        if rnd in (1, 2, 4, 5):
+            rng = np.random.default_rng(rnd * 7919 + n)
+            out = [(int(rng.integers(n)), int(rng.integers(R))) for _ in range(max(1, R // 2))]
+    return out
+
+
+_injections.state = {}
+
+
+def _first_diff(a, b):
+    idx = np.argwhere(a != b)
+    return tuple(idx[0]) if len(idx) else None
+
+
+def run_parity(engine, n, R, kind, params=None, max_rounds=60, seed=SEED, epoch=0,
+               check_every=1):
+    net = engine.Network(n, R, seed=seed, epoch=epoch, params=params)
+    orc = OracleNet(n, R, seed=seed, epoch=epoch, params=params)
+    assert net.params == orc.params
+    rounds = 0
+    try:
+        for rnd in range(1, max_rounds + 1):
+            for (x, r) in _injections(kind, n, R, seed, epoch, rnd, engine):
+                net.send_new(x, r)
+                orc.send_new(x, r)
+            rep = net.next_round()
+            rc, olive = orc.next_round(SCHED_2P)
+            assert rc == 0
+            assert rep.round == rnd == orc.round
+            assert rep.any_live == olive, f"round {rnd}: any_live"
+            rounds = rnd
+            if rnd % check_every == 0 or not olive:
+                gs = net.dump_state()
+                os_ = orc.dump_state()
+                d = _first_diff(gs, os_)
+                assert d is None, (f"round {rnd}: state differs at (node,rumor)={d}: "
+                                   f"gpu {gs[d]:#06x} oracle {os_[d]:#06x}")
+                grec, gps = net.dump_records()
+                orec, ops = orc.dump_records()
+                d = _first_diff(gps, ops)
+                assert d is None, f"round {rnd}: |P| differs at node {d}"
+                d = _first_diff(grec, orec)
+                assert d is None, (f"round {rnd}: records differ at {d}: gpu {grec[d]:#06x} "
+                                   f"oracle {orec[d]:#06x}")
+                gst = net.statistics_all()
+                ost = orc.statistics()
+                d = _first_diff(gst, ost)
+                assert d is None, f"round {rnd}: statistics differ at {d}: {gst[d[0]]} vs {ost[d[0]]}"
+                np.testing.assert_array_equal(net.known_all(), orc.known_all())
+            if not olive:
+                break
+    finally:
+        net.close()
+        orc.close()
+    return rounds
+
+
+@pytest.mark.parametrize("n,R,kind,params", [
+    (8, 3, "example", None),        # config 1: examples/network.rs default network
+    (2, 1, "origins", None),        # smallest mesh: max_rounds 1
+    (3, 2, "origins", None),
+    (5, 3, "trickle", None),
+    (20, 1, "trickle", None),       # README row 1 size
+    (200, 1, "trickle", None),      # README row 2 size
+    (2000, 1, "trickle", None),     # README row 3 size (cmax 3)
+    (16, 5, "origins", None),       # cmax 2 boundary (n=16)
+    (1619, 4, "origins", None),     # cmax 3 boundary (n > e^e^2)
+    (97, 16, "origins", None),
+    (101, 32, "reinject", None),
+    (64, 64, "origins", None),
+    (300, 64, "trickle", None),
+    (77, 100, "origins", None),     # R not a power of two (padded to 128)
+    (50, 256, "origins", None),
+    (130, 256, "reinject", None),
+    (33, 512, "origins", None),
+    (40, 7, "origins", (1, 1, 3)),
+    (40, 7, "origins", (2, 3, 5)),
+    (300, 16, "origins", (3, 3, 14)),
+    (500, 8, "reinject", (3, 2, 9)),
+    (1000, 3, "trickle", (3, 3, 32)),
+])
+def test_round_parity(engine, n, R, kind, params):
+    rounds = run_parity(engine, n, R, kind, params)
+    assert rounds >= 1
+
+
+@pytest.mark.parametrize("seed,epoch", [(1, 0), (0xDEADBEEF, 3), (2**63 + 5, 77)])
+def test_round_parity_seeds(engine, seed, epoch):
+    run_parity(engine, 600, 48, "origins", seed=seed, epoch=epoch)
+
+
+def test_parity_larger(engine):
+    # 20k nodes x 64 rumors: one u64 word per node (the ballot-path config at
+    # a size the oracle finishes in seconds); full dumps every 4th round.
+    run_parity(engine, 20000, 64, "origins", check_every=4)
+
+
+def test_no_peers(engine):
+    net = engine.Network(1, 4)
+    with pytest.raises(engine.NoPeers):
+        net.send_new(0, 0)
+    with pytest.raises(engine.NoPeers):
+        net.next_round()
+    net.close()
+
+
+def test_clear_and_observe_idempotent(engine):
+    net = engine.Network(500, 32)
+    orc = OracleNet(500, 32)
+    for r in range(32):
+        x = engine.origin_of(SEED, 0, r, 500)
+        net.send_new(x, r)
+        orc.send_new(x, r)
+    for _ in range(3):
+        net.next_round()
+        orc.next_round(SCHED_2P)
+    a = net.dump_state()
+    b = net.dump_state()          # observing twice changes nothing
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(a, orc.dump_state())
+    net.next_round()
+    orc.next_round(SCHED_2P)
+    np.testing.assert_array_equal(net.dump_state(), orc.dump_state())
+    net.clear(epoch=9)
+    orc.clear(9)
+    assert net.known_counts() == (0, 0)
+    assert int(net.statistics_all().sum()) == 0
+    net.close()
+    orc.close()
