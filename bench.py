@@ -1,0 +1,212 @@
+"""Benchmark: node-rumor updates/sec of the safe_gossip push-pull round on MI355X.
+
+A "step" is one round (phase 0 + push/pull delivery, 2P schedule) over the
+whole simulated network.  Default workload (config 4 of BASELINE.json, which
+fits one MI355X): n = 2^24 nodes x R = 256 rumors, all rumors injected in round
+1 at Philox-chosen origins, seed 0x5AFE6055.  Inputs are synthetic and resident
+in HBM (the state is created on the device; nothing crosses PCIe in the timed
+region).
+
+value  = n * R * K / wall seconds of K timed rounds (summed over ranks).
+roofline: algorithmic HBM bytes of the round kernel (DESIGN.md "Roofline") per
+          launch / its average duration measured with HIP events on the
+          engine's stream over the timed rounds; peak 8.0 TB/s.
+cpu_baseline: the CPU oracle (reference-faithful port: per-node ordered maps,
+          one thread, same 2P schedule) on a bounded sample of the same
+          workload (fewer nodes, same R and injection), rank 0 at N=1 only.
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process
+per GPU, each rank simulates its own network of the same size (independent
+replicas with distinct Philox epochs; DESIGN.md "Multi-GPU").  Barrier +
+synchronize around the timed region, time = max over ranks.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0
+METRIC = "node-rumor updates/sec (whole node) + % HBM roofline; rounds-to-full-spread"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--nodes", type=int, default=1 << 24)
+    p.add_argument("--rumors", type=int, default=256)
+    p.add_argument("--seed", type=lambda s: int(s, 0), default=0x5AFE6055)
+    p.add_argument("--cpu-seconds", type=float, default=15.0,
+                   help="budget of the CPU-oracle sample")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-spread", action="store_true", help="skip the rounds-to-full-spread run")
+    return p.parse_args()
+
+
+def inject_all(net, epoch):
+    import safe_gossip_amd as sg
+    for r in range(net.R):
+        net.send_new(sg.origin_of(net.seed, epoch, r, net.n), r)
+
+
+def spread_run(net, epoch, max_rounds=200):
+    """Untimed: rounds until termination and first round with full spread."""
+    net.clear(epoch)
+    inject_all(net, epoch)
+    r_full = 0
+    rounds = 0
+    for _ in range(max_rounds):
+        rep = net.next_round()
+        rounds = rep.round
+        if not r_full:
+            _, complete = net.known_counts()
+            if complete == net.n:
+                r_full = rep.round
+        if not rep.any_live:
+            break
+    known, complete = net.known_counts()
+    return dict(rounds=rounds, round_full=r_full, nodes_complete=complete,
+                known_fraction=known / float(net.n * net.R))
+
+
+def cpu_baseline(R, seed, budget_s):
+    """Time the CPU oracle (port) on a bounded sample: n_cpu nodes, same R."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib
+    oracle_lib.build_oracle()
+    n_cpu = 1 << 15
+    net = oracle_lib.OracleNet(n_cpu, R, seed=seed)
+    L = oracle_lib.lib()
+    for r in range(R):
+        net.send_new(L.or_origin(seed, 0, r, n_cpu), r)
+    t0 = time.perf_counter()
+    rounds = 0
+    while True:
+        _, live = net.next_round(oracle_lib.SCHED_2P)
+        rounds += 1
+        el = time.perf_counter() - t0
+        if not live or el > budget_s:
+            break
+    net.close()
+    return dict(value=n_cpu * R * rounds / el, unit="node-rumor updates/s", cores=1,
+                kind="port",
+                sample=f"CPU oracle (per-node ordered maps, 1 thread, 2P), n={n_cpu}, R={R}, "
+                       f"all rumors injected round 1, {rounds} rounds in {el:.1f}s")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+
+    import numpy as np
+    import safe_gossip_amd as sg
+
+    n, R = args.nodes, args.rumors
+    net = sg.Network(n, R, seed=args.seed, epoch=rank * 1000, device=local)
+
+    def barrier_sync():
+        net.sync()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    # warmup: W rounds of a dissemination (epoch rank*1000)
+    inject_all(net, rank * 1000)
+    for _ in range(args.warmup):
+        net.next_round(report=False)
+    # timed: K rounds of a fresh dissemination from round 1
+    epoch = rank * 1000 + 1
+    net.clear(epoch)
+    inject_all(net, epoch)
+    net.set_timing(True)
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        net.next_round(report=False)
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    ktimes = net.round_kernel_times()
+    net.set_timing(False)
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # rounds 2.. run the fused deliver+transition kernel (round 1 has nothing
+    # to deliver); that is the dominant kernel the roofline describes.
+    kt = ktimes[1:] if len(ktimes) > 1 else ktimes
+    kernel_ms = float(np.mean(kt)) if len(kt) else float("nan")
+    bytes_per = net.round_kernel_bytes()
+    achieved = bytes_per / (kernel_ms * 1e-3) / 1e9
+
+    spread = None if args.no_spread else spread_run(net, epoch)
+
+    traffic = None
+    pmc_path = os.path.join(REPO, "profiles", "pmc_latest.json")
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            if pmc.get("nodes") == n and pmc.get("rumors") == R:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(R, args.seed, args.cpu_seconds)
+
+    if rank == 0:
+        total_updates = float(n) * R * args.steps * world
+        line = {
+            "metric": METRIC,
+            "value": total_updates / elapsed,
+            "unit": "node-rumor updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic",
+            "config": {
+                "workload": f"cfg4: {n} nodes x {R} rumors, full mesh, all rumors injected in "
+                            f"round 1 at Philox origins, 2P schedule, {args.steps} rounds",
+                "n_nodes": n, "n_rumors": R, "seed": hex(args.seed),
+                "params": list(net.params),
+                "parallelism": "replicas" if world > 1 else "single-gpu",
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "kernel": "round_kernel<false,1> (deliver round t + transition to t+1)",
+                "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": bytes_per,
+            },
+            "cpu_baseline": cpu,
+            "spread": spread,
+        }
+        print(json.dumps(line), flush=True)
+    net.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

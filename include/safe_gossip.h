@@ -116,8 +116,12 @@ uint32_t    gs_round(const gs_engine *e);
 /* Device-time of the last `gs_next_round`'s round kernel (HIP events on the
  * engine stream), ms; for bench.py's roofline.  Returns <0 if unavailable. */
 float       gs_last_round_kernel_ms(gs_engine *e);
-/* Enable/disable HIP-event timing of the round kernel (default off). */
+/* Enable/disable HIP-event timing of the round kernel (default off); enabling
+ * (re)starts a ring of up to 4096 per-round timings. */
 void        gs_set_timing(gs_engine *e, int enable);
+/* Copy the recorded per-round kernel times (ms, oldest first) into out_ms,
+ * return how many were copied (or <0) and restart the ring.  Synchronises. */
+int32_t     gs_round_kernel_times(gs_engine *e, float *out_ms, uint32_t max);
 /* Algorithmic HBM bytes of one round kernel (DESIGN.md, section Roofline). */
 double      gs_round_kernel_bytes(const gs_engine *e);
 

@@ -102,6 +102,7 @@ SYMBOLS = {
     "gs_round": (ctypes.c_uint32, [_P]),
     "gs_last_round_kernel_ms": (ctypes.c_float, [_P]),
     "gs_set_timing": (None, [_P, ctypes.c_int]),
+    "gs_round_kernel_times": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_float), ctypes.c_uint32]),
     "gs_round_kernel_bytes": (ctypes.c_double, [_P]),
     "gs_peer": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.c_uint32, ctypes.c_uint32]),
@@ -341,6 +342,15 @@ class Network:
 
     def last_round_kernel_ms(self) -> float:
         return float(self._lib.gs_last_round_kernel_ms(self._h))
+
+    def round_kernel_times(self, max_n: int = 4096) -> np.ndarray:
+        """Per-round device times (ms) of the round kernel since set_timing(True)."""
+        out = np.zeros(max_n, dtype=np.float32)
+        m = self._lib.gs_round_kernel_times(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                            max_n)
+        if m < 0:
+            raise DeviceError("kernel timing unavailable")
+        return out[:m]
 
     def round_kernel_bytes(self) -> float:
         return float(self._lib.gs_round_kernel_bytes(self._h))

@@ -43,11 +43,15 @@ struct gs_engine {
     bool obs_valid = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timing = false, timed = false;
+    // per-round kernel timing ring (gs_round_kernel_times)
+    std::vector<hipEvent_t> tev;  // pairs
+    uint32_t tcount = 0;
 };
 
 namespace {
 
 constexpr uint32_t kReduceBlocks = 1024;
+constexpr uint32_t kTimingSlots = 4096;
 
 #define GS_HIP(expr)                                   \
     do {                                               \
@@ -85,6 +89,7 @@ void release(gs_engine *e) {
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (e->inj_host) (void)hipHostFree(e->inj_host);
+    for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -362,9 +367,17 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
     a.inj_key = e->inj_key;
     a.inj_mask = e->inj_mask;
     a.n_inj = n_inj;
-    if (e->timing) GS_HIP(hipEventRecord(e->ev0, e->stream));
+    hipEvent_t t0 = e->ev0, t1 = e->ev1;
+    if (e->timing && e->tcount < kTimingSlots) {
+        t0 = e->tev[2 * e->tcount];
+        t1 = e->tev[2 * e->tcount + 1];
+        e->tcount++;
+    }
+    if (e->timing) GS_HIP(hipEventRecord(t0, e->stream));
     GS_HIP(gs::launch_round(a, e->deliver_pending ? 1 : 0, e->stream));
-    if (e->timing) GS_HIP(hipEventRecord(e->ev1, e->stream));
+    if (e->timing) GS_HIP(hipEventRecord(t1, e->stream));
+    e->ev0 = t0;
+    e->ev1 = t1;
     e->timed = e->timing;
     e->round += 1;
     e->cur ^= 1;
@@ -512,7 +525,31 @@ gs_status gs_sync(gs_engine *e) {
 }
 
 void gs_set_timing(gs_engine *e, int enable) {
-    if (e) e->timing = enable != 0;
+    if (!e) return;
+    e->timing = enable != 0;
+    if (e->timing && e->tev.empty()) {
+        (void)hipSetDevice(e->device);
+        e->tev.resize(2 * (size_t)kTimingSlots, nullptr);
+        for (auto &ev : e->tev)
+            if (hipEventCreate(&ev) != hipSuccess) {
+                e->timing = false;
+                return;
+            }
+    }
+    e->tcount = 0;
+}
+
+int32_t gs_round_kernel_times(gs_engine *e, float *out_ms, uint32_t max) {
+    if (!e || !out_ms) return -1;
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return -1;
+    const uint32_t m = std::min(max, e->tcount);
+    for (uint32_t i = 0; i < m; ++i) {
+        float ms = -1.0f;
+        if (hipEventElapsedTime(&ms, e->tev[2 * i], e->tev[2 * i + 1]) != hipSuccess) return -1;
+        out_ms[i] = ms;
+    }
+    e->tcount = 0;
+    return (int32_t)m;
 }
 
 float gs_last_round_kernel_ms(gs_engine *e) {

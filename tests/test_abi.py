@@ -1,0 +1,78 @@
+"""The C-ABI library: loads, exports every symbol include/safe_gossip.h
+declares, host-side helpers agree with the oracle, and the product fails
+loudly (no CPU fallback) when no GPU is present."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "safe_gossip.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(gs_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_header_symbols_exported(engine):
+    lib = engine.load_library()
+    syms = declared_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+    # the Python binding declares a signature for every header symbol
+    assert set(syms) == set(engine.SYMBOLS)
+
+
+def test_exported_symbols_nm(engine):
+    from safe_gossip_amd.build import LIB_PATH
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (gs_[a-z_0-9]+)\b", out))
+    assert set(declared_symbols()) <= exported
+
+
+def test_derive_params_equal_oracle(engine, oracle):
+    for n in list(range(1, 100)) + [1618, 1619, 2000, 5000, 10**4, 10**6, 2**24, 10**8,
+                                    528491311, 2**32 - 2]:
+        assert engine.derive_params(n) == oracle_lib.derive_params(n), n
+
+
+def test_status_strings(engine):
+    lib = engine.load_library()
+    assert b"no connected peers" in lib.gs_status_string(1)
+    assert b"before sending" in lib.gs_status_string(2)
+
+
+def _has_gpu():
+    return os.path.exists("/dev/kfd")
+
+
+@pytest.mark.skipif(_has_gpu(), reason="checks the no-GPU failure mode")
+def test_fails_loudly_without_gpu(engine):
+    with pytest.raises(engine.DeviceError):
+        engine.Network(8, 3)
+
+
+def test_invalid_config_rejected(engine):
+    lib = engine.load_library()
+    from safe_gossip_amd import _Config
+    cfg = _Config()
+    cfg.n_nodes = 10
+    cfg.n_rumors = 0
+    h = ctypes.c_void_p()
+    assert lib.gs_create(ctypes.byref(cfg), ctypes.byref(h)) == -1
+    cfg.n_rumors = 5000
+    assert lib.gs_create(ctypes.byref(cfg), ctypes.byref(h)) == -1
+    cfg.n_rumors = 8
+    cfg.counter_max, cfg.max_c_rounds, cfg.max_rounds = 4, 3, 10
+    assert lib.gs_create(ctypes.byref(cfg), ctypes.byref(h)) == -2   # unsupported layout
+    cfg.counter_max, cfg.max_c_rounds, cfg.max_rounds = 3, 3, 33
+    assert lib.gs_create(ctypes.byref(cfg), ctypes.byref(h)) == -2
