@@ -1,0 +1,113 @@
+// one_message_test -- the reference's convergence experiment
+// (src/gossiper.rs:173-323: send_messages / one_message_test / print_metric)
+// driven through the C++ host API on the MI355X engine (2P schedule).
+//
+//   ./examples/one_message_test [nodes=2000] [iterations=1000] [messages=1]
+//
+// Prints the AVERAGE / MIN / MAX lines in the reference's format.
+#include <cinttypes>
+#include <cstdio>
+#include <cstdlib>
+#include <algorithm>
+#include <tuple>
+#include <vector>
+
+#include "safe_gossip.hpp"
+
+using safe_gossip::Network;
+using safe_gossip::Statistics;
+
+struct Metric {
+    uint64_t nodes_missed, msgs_missed;
+    Statistics stats;
+};
+
+// send_messages (src/gossiper.rs:173-259): first rumor at a Philox-chosen
+// node, then 50%/node/round while rumors remain; stop after a round with no
+// live push; empties of the final confirmation round subtracted.
+static Metric send_messages(Network &net, uint32_t num_msgs) {
+    const uint32_t n = net.size();
+    uint32_t next = 0;
+    net.send_new(gs_origin(net.seed(), net.epoch(), 0, n), next++);
+    bool processed = true;
+    while (processed) {
+        const uint32_t rnd = net.round() + 1;
+        for (uint32_t x = 0; x < n && next < num_msgs; ++x)
+            if (gs_coin(net.seed(), net.epoch(), rnd, x)) net.send_new(x, next++);
+        processed = net.next_round();
+    }
+    const std::vector<uint64_t> st = net.statistics_all();
+    const std::vector<uint64_t> known = net.known_all();
+    const uint32_t kw = (net.rumors() + 63) / 64;
+    Metric m{0, 0, Statistics()};
+    for (uint32_t x = 0; x < n; ++x) {
+        Statistics s;
+        s.rounds = st[5 * (size_t)x];
+        s.empty_pull_sent = st[5 * (size_t)x + 1];
+        s.empty_push_sent = st[5 * (size_t)x + 2];
+        s.full_message_sent = st[5 * (size_t)x + 3];
+        s.full_message_received = st[5 * (size_t)x + 4];
+        m.stats.add(s);
+        m.stats.rounds = s.rounds;
+        uint32_t c = 0;
+        for (uint32_t w = 0; w < kw; ++w) c += (uint32_t)__builtin_popcountll(known[(size_t)x * kw + w]);
+        if (c != num_msgs) {
+            m.nodes_missed += 1;
+            m.msgs_missed += num_msgs - c;
+        }
+    }
+    m.stats.empty_pull_sent -= n;
+    m.stats.empty_push_sent -= n;
+    net.clear(net.epoch() + 1);
+    return m;
+}
+
+static void print_metric(double nodes_missed, double msgs_missed, const Statistics &s,
+                         uint32_t n, uint32_t msgs) {
+    printf("rounds: %" PRIu64 ", empty_pulls: %" PRIu64 ", empty_pushes: %" PRIu64
+           ", full_msgs_sent: %" PRIu64 ", msgs_missed: %g (%.2f%%), nodes_missed: %g (%.2f%%)\n",
+           s.rounds, s.empty_pull_sent, s.empty_push_sent, s.full_message_sent, msgs_missed,
+           100.0 * msgs_missed / n / msgs, nodes_missed, 100.0 * nodes_missed / n / msgs);
+}
+
+int main(int argc, char **argv) {
+    const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 2000;
+    const uint32_t iterations = argc > 2 ? (uint32_t)atoi(argv[2]) : 1000;
+    const uint32_t msgs = argc > 3 ? (uint32_t)atoi(argv[3]) : 1;
+    try {
+        Network net(n, msgs);
+        printf("Network of %u nodes:\n", n);
+        Statistics avg, mx, mn = Statistics::new_max();
+        double nm_avg = 0, mm_avg = 0;
+        uint64_t nm_max = 0, nm_min = UINT64_MAX, mm_max = 0, mm_min = UINT64_MAX;
+        for (uint32_t i = 0; i < iterations; ++i) {
+            Metric m = send_messages(net, msgs);
+            nm_avg += (double)m.nodes_missed;
+            mm_avg += (double)m.msgs_missed;
+            nm_max = std::max(nm_max, m.nodes_missed);
+            nm_min = std::min(nm_min, m.nodes_missed);
+            mm_max = std::max(mm_max, m.msgs_missed);
+            mm_min = std::min(mm_min, m.msgs_missed);
+            avg.add(m.stats);
+            mx.max(m.stats);
+            mn.min(m.stats);
+        }
+        nm_avg /= iterations;
+        mm_avg /= iterations;
+        avg.rounds /= iterations;
+        avg.empty_pull_sent /= iterations;
+        avg.empty_push_sent /= iterations;
+        avg.full_message_sent /= iterations;
+        avg.full_message_received /= iterations;
+        printf("    AVERAGE ---- ");
+        print_metric(nm_avg, mm_avg, avg, n, msgs);
+        printf("    MIN -------- ");
+        print_metric((double)nm_min, (double)mm_min, mn, n, msgs);
+        printf("    MAX -------- ");
+        print_metric((double)nm_max, (double)mm_max, mx, n, msgs);
+    } catch (const safe_gossip::GossipError &e) {
+        fprintf(stderr, "error: %s\n", e.what());
+        return 1;
+    }
+    return 0;
+}

@@ -1,0 +1,62 @@
+"""The kernel's bit-sliced 2P algebra (tests/model_bitsliced.py, a line-by-line
+Python model of gs_kernels.hip) equals the reference-faithful oracle, round by
+round, on CPU.  Separates derivation errors from HIP-level errors."""
+import numpy as np
+import pytest
+
+import oracle_lib
+from model_bitsliced import Model
+from oracle_lib import SCHED_2P, OracleNet
+
+
+def run(n, R, params=None, seed=0x5AFE6055, epoch=0, kind="origins", max_rounds=40):
+    orc = OracleNet(n, R, seed=seed, epoch=epoch, params=params)
+    L = oracle_lib.lib()
+    mdl = Model(n, R, seed, epoch, orc.params, L.or_peer)
+    rng = np.random.default_rng(n * 31 + R)
+    for rnd in range(1, max_rounds + 1):
+        inj = []
+        if kind == "origins" and rnd == 1:
+            inj = [(L.or_origin(seed, epoch, r, n), r) for r in range(R)]
+        if kind == "reinject" and rnd in (1, 2, 4, 5):
+            inj = [(int(rng.integers(n)), int(rng.integers(R))) for _ in range(max(1, R // 2))]
+        for x, r in inj:
+            orc.send_new(x, r)
+            mdl.send_new(x, r)
+        _, olive = orc.next_round(SCHED_2P)
+        mlive = mdl.next_round()
+        assert mlive == olive, rnd
+        codes, recs, psz, stats, known = mdl.observe()
+        np.testing.assert_array_equal(np.array(codes, np.uint16), orc.dump_state(),
+                                      err_msg=f"state round {rnd}")
+        orec, ops = orc.dump_records()
+        np.testing.assert_array_equal(np.array(psz, np.uint32), ops, err_msg=f"|P| round {rnd}")
+        np.testing.assert_array_equal(np.array(recs, np.uint16), orec,
+                                      err_msg=f"records round {rnd}")
+        np.testing.assert_array_equal(np.array(stats, np.uint64), orc.statistics(),
+                                      err_msg=f"stats round {rnd}")
+        ok = orc.known_all()
+        for x in range(n):
+            got = known[x]
+            exp = sum(int(w) << (64 * i) for i, w in enumerate(ok[x]))
+            assert got == exp, (rnd, x)
+        if not olive:
+            break
+    orc.close()
+
+
+@pytest.mark.parametrize("n,R,params,kind", [
+    (8, 3, None, "origins"),
+    (2, 1, None, "origins"),
+    (3, 2, None, "origins"),
+    (20, 4, None, "reinject"),
+    (60, 8, None, "origins"),
+    (200, 5, None, "reinject"),
+    (40, 7, (2, 3, 5), "origins"),
+    (40, 7, (1, 1, 3), "reinject"),
+    (300, 6, (3, 3, 14), "origins"),
+    (400, 6, (3, 2, 9), "reinject"),
+    (1700, 3, None, "origins"),
+])
+def test_model_equals_oracle(oracle, n, R, params, kind):
+    run(n, R, params, kind=kind)
