@@ -29,17 +29,23 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_engine(force: bool = False, verbose: bool = False) -> str:
-    """Compile libsafe_gossip_amd.so for gfx950 (no-op when up to date)."""
-    if not force and not _stale(LIB_PATH, SOURCES + HEADERS):
-        return LIB_PATH
+def build_engine(force: bool = False, verbose: bool = False, defines=(), out: str = None) -> str:
+    """Compile libsafe_gossip_amd.so for gfx950 (no-op when up to date).
+
+    ``defines``/``out`` build an experiment variant (timing-only flags such as
+    GS_EXP_*) into another file; the product library never carries them.
+    """
+    target = out or LIB_PATH
+    if not force and not defines and not _stale(target, SOURCES + HEADERS):
+        return target
     cmd = [HIPCC, "-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17",
-           "-Wall", "-Wextra", "-Werror", "-o", LIB_PATH + ".tmp"] + SOURCES
+           "-Wall", "-Wextra", "-Werror"] + [f"-D{d}" for d in defines] + [
+           "-o", target + ".tmp"] + SOURCES
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    return LIB_PATH
+    os.replace(target + ".tmp", target)
+    return target
 
 
 def build_examples(force: bool = False) -> list[str]:

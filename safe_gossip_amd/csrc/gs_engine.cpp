@@ -27,8 +27,10 @@ struct gs_engine {
     hipStream_t stream = nullptr;
     u64 *S[2] = {nullptr, nullptr};
     int cur = 0;
-    uint32_t *off = nullptr, *src = nullptr, *tg = nullptr, *cnt = nullptr;
-    uint32_t *bsum = nullptr, *flags = nullptr;
+    uint32_t *off = nullptr, *src = nullptr, *tg = nullptr;
+    uint32_t *csr_scratch = nullptr, *flags = nullptr;
+    u64 *pairs = nullptr;
+    gs::CsrPlan plan{};
     u64 *stats = nullptr;
     u64 *inj_key = nullptr, *inj_mask = nullptr;
     u64 *inj_host = nullptr;  // pinned staging [2*cap]
@@ -83,7 +85,7 @@ void release(gs_engine *e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
-    void *bufs[] = {e->S[0], e->S[1], e->off, e->src, e->tg, e->cnt, e->bsum, e->flags,
+    void *bufs[] = {e->S[0], e->S[1], e->off, e->src, e->tg, e->csr_scratch, e->pairs, e->flags,
                     e->stats, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
                     e->partials, e->obs_state, e->obs_rec, e->obs_psize};
     for (void *b : bufs)
@@ -102,7 +104,6 @@ gs_status reset_state(gs_engine *e) {
     GS_HIP(hipMemsetAsync(e->S[0], 0, sw * sizeof(u64), e->stream));
     GS_HIP(hipMemsetAsync(e->S[1], 0, sw * sizeof(u64), e->stream));
     GS_HIP(hipMemsetAsync(e->stats, 0, (size_t)5 * g.n * sizeof(u64), e->stream));
-    GS_HIP(hipMemsetAsync(e->cnt, 0, (size_t)g.n * sizeof(uint32_t), e->stream));
     GS_HIP(hipMemsetAsync(e->flags, 0, 4 * sizeof(uint32_t), e->stream));
     e->cur = 0;
     e->round = 0;
@@ -119,7 +120,6 @@ gs::RoundArgs base_args(gs_engine *e) {
     a.off = e->off;
     a.src = e->src;
     a.tg = e->tg;
-    a.cnt = e->cnt;
     a.stats = e->stats;
     a.flags = e->flags;
     a.g = e->g;
@@ -314,12 +314,14 @@ gs_status gs_create(const gs_config *cfg, gs_engine **out) {
         g.nseg = n;
     }
     const size_t sw = (size_t)g.units * gs::kPlanes * g.W;
+    e->plan = gs::csr_plan(n);
     bool ok = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreate(&e->ev0) == hipSuccess && hipEventCreate(&e->ev1) == hipSuccess;
     ok = ok && dalloc(&e->S[0], sw) == hipSuccess && dalloc(&e->S[1], sw) == hipSuccess &&
          dalloc(&e->off, (size_t)n + 1) == hipSuccess && dalloc(&e->src, n) == hipSuccess &&
-         dalloc(&e->tg, n) == hipSuccess && dalloc(&e->cnt, n) == hipSuccess &&
-         dalloc(&e->bsum, gs::csr_bsum_words(n)) == hipSuccess && dalloc(&e->flags, 4) == hipSuccess &&
+         dalloc(&e->tg, n) == hipSuccess && dalloc(&e->pairs, n) == hipSuccess &&
+         dalloc(&e->csr_scratch, gs::csr_scratch_words(e->plan)) == hipSuccess &&
+         dalloc(&e->flags, 4) == hipSuccess &&
          dalloc(&e->stats, (size_t)5 * n) == hipSuccess;
     if (!ok) {
         hipError_t le = hipGetLastError();
@@ -383,7 +385,7 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
     e->cur ^= 1;
     e->deliver_pending = true;
     e->obs_valid = false;
-    GS_HIP(gs::launch_build_csr(e->tg, e->cnt, e->off, e->src, e->bsum, e->g.n, e->flags,
+    GS_HIP(gs::launch_build_csr(e->tg, e->plan, e->csr_scratch, e->pairs, e->off, e->src, e->flags,
                                 (e->round + 1) & 1u, e->stream));
     if (report) {
         uint32_t fl[4];

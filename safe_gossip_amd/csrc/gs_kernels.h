@@ -10,7 +10,6 @@ struct RoundArgs {
     const uint32_t *off;      // in-edge CSR of round t: offsets[n+1]
     const uint32_t *src;      //   sources, ascending within a bucket
     uint32_t *tg;             // tg[x]: round-t target in, round-(t+1) target out
-    uint32_t *cnt;            // in-degree histogram of round t+1 (accumulated)
     u64 *stats;               // [5][n] Statistics SoA
     const u64 *inj_key;       // sorted segment keys with injections (round t+1)
     const u64 *inj_mask;      //   rumor masks in segment coordinates
@@ -34,15 +33,24 @@ struct RoundArgs {
 // 3 = observe without pending deliveries.
 hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s);
 
-// In-edge CSR of the round whose targets are in tg (cnt holds its histogram;
-// it is consumed back to zero).  Also clears the any_live slot of the round
-// after it.
-hipError_t launch_build_csr(const uint32_t *tg, uint32_t *cnt, uint32_t *off,
-                            uint32_t *src, uint32_t *bsum, uint32_t n,
-                            uint32_t *flags, uint32_t next_round_slot, hipStream_t s);
-size_t csr_bsum_words(uint32_t n);
+// Plan of the two-stage counting sort that builds the in-edge CSR.
+struct CsrPlan {
+    uint32_t n;       // nodes (= edges)
+    uint32_t bin;     // target nodes per bin (power of two >= 4096)
+    uint32_t logbin;
+    uint32_t nb;      // bins (<= 16384)
+    uint32_t ba;      // source chunks (<= 256)
+    uint32_t chunk;   // sources per chunk
+};
+CsrPlan csr_plan(uint32_t n);
+size_t csr_scratch_words(const CsrPlan &p);  // u32 words of scratch
 
-// First-round targets + histogram (mode 0 does this itself; used after clear).
+// In-edge CSR of the round whose targets are in tg.  Also clears the any_live
+// slot of the round after it.
+hipError_t launch_build_csr(const uint32_t *tg, const CsrPlan &p, uint32_t *scratch, u64 *pairs,
+                            uint32_t *off, uint32_t *src, uint32_t *flags,
+                            uint32_t next_round_slot, hipStream_t s);
+
 // Reductions for observers.
 hipError_t launch_known_reduce(const u64 *known, uint32_t n, uint32_t KW, uint32_t R,
                                u64 *partials /* [2*blocks] */, uint32_t blocks,

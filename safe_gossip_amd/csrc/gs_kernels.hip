@@ -116,8 +116,12 @@ constexpr uint32_t kNone = 0xffffffffu;
 
 // MODE: 0 transition only, 1 deliver + transition, 2 deliver + observe,
 // 3 observe only.
+#ifndef GS_RK_MINW
+#define GS_RK_MINW 1
+#endif
+
 template <bool SMALL, int MODE>
-__global__ __launch_bounds__(256) void round_kernel(RoundArgs a) {
+__global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     constexpr bool DELIVER = (MODE == 1 || MODE == 2);
     constexpr bool TRANSITION = (MODE == 0 || MODE == 1);
     const Geometry &g = a.g;
@@ -398,10 +402,8 @@ __global__ __launch_bounds__(256) void round_kernel(RoundArgs a) {
         }
         st[2 * n + x] += (live_new == 0u) ? 1u : 0u;             // empty_push_sent
         st[3 * n + x] += (uint64_t)live_new + d_full_sent;       // full_message_sent
-        // Peer choice of round t+1 and its in-degree histogram.
-        const uint32_t tn = peer_of(a.seed, a.epoch, a.round_new, x, g.n);
-        a.tg[x] = tn;
-        atomicAdd(&a.cnt[tn], 1u);
+        // Peer choice of round t+1; its in-edge CSR is built by build_csr.
+        a.tg[x] = peer_of(a.seed, a.epoch, a.round_new, x, g.n);
     }
 }
 
@@ -423,11 +425,19 @@ hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s) {
 }
 
 // ------------------------------------------------------------ in-edge CSR
+// Two-stage counting sort of the n edges (x -> tg[x]) by target, with no
+// global atomics (the round kernel's targets are uniform, so fixed-width
+// target bins are balanced):
+//   bin_count   : per source chunk, an LDS histogram over target bins
+//                 -> M[chunk][bin]
+//   col_scan    : per bin, exclusive prefix over chunks; bin totals
+//   scan (1 blk): exclusive prefix of the bin totals -> bin bases
+//   bin_scatter : (local target, source) pairs into their bin's range
+//                 (runs of ~C/NB pairs per chunk and bin)
+//   bin_sort    : per bin, LDS counting sort by local target -> off[], src[],
+//                 then each node's few sources sorted ascending (the order
+//                 Gossip::receive sees its pushers in, src/gossiper.rs:217).
 constexpr uint32_t kScanBlock = 256;
-constexpr uint32_t kScanPer = 16;
-constexpr uint32_t kScanTile = kScanBlock * kScanPer;
-
-size_t csr_bsum_words(uint32_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
 
 // Block-wide exclusive scan of one value per thread; returns the block total.
 GS_DEV uint32_t block_exclusive_scan(uint32_t v, uint32_t *lds, uint32_t &total) {
@@ -450,92 +460,151 @@ GS_DEV uint32_t block_exclusive_scan(uint32_t v, uint32_t *lds, uint32_t &total)
     return wbase + inc - v;
 }
 
-__global__ __launch_bounds__(kScanBlock) void scan_tile_sums(const uint32_t *__restrict__ cnt,
-                                                             uint32_t n, uint32_t *bsum) {
-    __shared__ uint32_t lds[kScanBlock / 64];
-    const u64 b0 = (u64)blockIdx.x * kScanTile + (u64)threadIdx.x * kScanPer;
-    uint32_t s = 0;
-    for (uint32_t i = 0; i < kScanPer; ++i)
-        if (b0 + i < n) s += cnt[b0 + i];
-    uint32_t tot;
-    block_exclusive_scan(s, lds, tot);
-    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+CsrPlan csr_plan(uint32_t n) {
+    CsrPlan p{};
+    p.n = n;
+    uint32_t bin = 4096;
+    while ((u64)bin * 16384u < n) bin <<= 1;  // <= 16384 bins: bin_count LDS <= 64 KiB
+    p.bin = bin;
+    p.logbin = 0;
+    while ((1u << p.logbin) < bin) ++p.logbin;
+    p.nb = (uint32_t)(((u64)n + bin - 1) / bin);
+    uint32_t ba = (uint32_t)(((u64)n + 4095) / 4096);
+    p.ba = ba < 256u ? (ba ? ba : 1u) : 256u;
+    p.chunk = (uint32_t)(((u64)n + p.ba - 1) / p.ba);
+    return p;
 }
 
-__global__ __launch_bounds__(kScanBlock) void scan_bsums(uint32_t *bsum, uint32_t nb) {
+size_t csr_scratch_words(const CsrPlan &p) {
+    // M[ba][nb] + tot[nb] + base[nb] (u32 words) ; pairs are separate (u64 [n])
+    return (size_t)p.ba * p.nb + 2 * (size_t)p.nb;
+}
+
+__global__ __launch_bounds__(256) void csr_bin_count(const uint32_t *__restrict__ tg, CsrPlan p,
+                                                     uint32_t *M) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+    for (uint32_t i = threadIdx.x; i < p.nb; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    const u64 lo = (u64)blockIdx.x * p.chunk;
+    const u64 hi = min((u64)p.n, lo + p.chunk);
+    for (u64 x = lo + threadIdx.x; x < hi; x += blockDim.x) atomicAdd(&hist[tg[x] >> p.logbin], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < p.nb; i += blockDim.x) M[(u64)blockIdx.x * p.nb + i] = hist[i];
+}
+
+__global__ __launch_bounds__(256) void csr_col_scan(uint32_t *M, CsrPlan p, uint32_t *tot) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= p.nb) return;
+    uint32_t run = 0;
+    for (uint32_t c = 0; c < p.ba; ++c) {
+        const uint32_t v = M[(u64)c * p.nb + b];
+        M[(u64)c * p.nb + b] = run;
+        run += v;
+    }
+    tot[b] = run;
+}
+
+// Exclusive scan of a small array (one block).
+__global__ __launch_bounds__(kScanBlock) void scan_small(const uint32_t *in, uint32_t *out, uint32_t m) {
     __shared__ uint32_t lds[kScanBlock / 64];
     uint32_t carry = 0;
-    for (uint32_t base = 0; base < nb; base += kScanBlock) {
+    for (uint32_t base = 0; base < m; base += kScanBlock) {
         const uint32_t i = base + threadIdx.x;
-        const uint32_t v = i < nb ? bsum[i] : 0u;
+        const uint32_t v = i < m ? in[i] : 0u;
         uint32_t tot;
         const uint32_t ex = block_exclusive_scan(v, lds, tot);
-        if (i < nb) bsum[i] = carry + ex;
+        if (i < m) out[i] = carry + ex;
         carry += tot;
     }
 }
 
-__global__ __launch_bounds__(kScanBlock) void scan_tiles(const uint32_t *__restrict__ cnt, uint32_t n,
-                                                         const uint32_t *__restrict__ bsum,
-                                                         uint32_t *__restrict__ off) {
-    __shared__ uint32_t lds[kScanBlock / 64];
-    const u64 b0 = (u64)blockIdx.x * kScanTile + (u64)threadIdx.x * kScanPer;
-    uint32_t v[kScanPer];
-    uint32_t s = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < kScanPer; ++i) {
-        v[i] = (b0 + i < n) ? cnt[b0 + i] : 0u;
-        s += v[i];
+__global__ __launch_bounds__(256) void csr_bin_scatter(const uint32_t *__restrict__ tg, CsrPlan p,
+                                                       const uint32_t *__restrict__ M,
+                                                       const uint32_t *__restrict__ base, u64 *pairs) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
+    for (uint32_t i = threadIdx.x; i < p.nb; i += blockDim.x)
+        cur[i] = base[i] + M[(u64)blockIdx.x * p.nb + i];
+    __syncthreads();
+    const u64 lo = (u64)blockIdx.x * p.chunk;
+    const u64 hi = min((u64)p.n, lo + p.chunk);
+    const uint32_t lm = p.bin - 1u;
+    for (u64 x = lo + threadIdx.x; x < hi; x += blockDim.x) {
+        const uint32_t t = tg[x];
+        const uint32_t pos = atomicAdd(&cur[t >> p.logbin], 1u);
+        pairs[pos] = ((u64)(t & lm) << 32) | (uint32_t)x;
     }
-    uint32_t tot;
-    uint32_t run = bsum[blockIdx.x] + block_exclusive_scan(s, lds, tot);
-#pragma unroll
-    for (uint32_t i = 0; i < kScanPer; ++i) {
-        if (b0 + i < n) off[b0 + i] = run;
-        run += v[i];
-    }
-    if (b0 + kScanPer >= n && b0 < n) off[n] = run;  // the thread owning the last element
 }
 
-__global__ __launch_bounds__(256) void scatter_edges(const uint32_t *__restrict__ tg,
-                                                     const uint32_t *__restrict__ off,
-                                                     uint32_t *cnt, uint32_t *src, uint32_t n) {
-    const u64 x = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= n) return;
-    const uint32_t t = tg[x];
-    const uint32_t old = atomicSub(&cnt[t], 1u);  // leaves cnt all-zero
-    src[off[t] + old - 1u] = (uint32_t)x;
-}
-
-// Ascending sources per bucket: the order Gossip::receive sees its pushers in
-// (pairs delivered in (src, dst) order, src/gossiper.rs:217).
-__global__ __launch_bounds__(256) void sort_buckets(const uint32_t *__restrict__ off, uint32_t *src,
-                                                    uint32_t n, uint32_t *flags, uint32_t slot) {
-    const u64 y = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (y == 0) flags[slot] = 0u;
-    if (y >= n) return;
-    const uint32_t a = off[y], b = off[y + 1];
-    for (uint32_t i = a + 1; i < b; ++i) {
-        const uint32_t v = src[i];
-        uint32_t q = i;
-        while (q > a && src[q - 1] > v) {
-            src[q] = src[q - 1];
-            --q;
+__global__ __launch_bounds__(256) void csr_bin_sort(const u64 *__restrict__ pairs, CsrPlan p,
+                                                    const uint32_t *__restrict__ base,
+                                                    const uint32_t *__restrict__ tot, uint32_t *off,
+                                                    uint32_t *src, uint32_t *flags, uint32_t slot) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t h[];  // [bin] + 4 scan words
+    uint32_t *lds_scan = h + p.bin;
+    const uint32_t b = blockIdx.x;
+    if (b == 0 && threadIdx.x == 0) flags[slot] = 0u;  // any_live slot of the round after
+    const uint32_t start = base[b], cnt = tot[b];
+    const uint32_t nb0 = b << p.logbin;
+    const uint32_t nodes = min(p.bin, p.n - nb0);
+    for (uint32_t i = threadIdx.x; i < p.bin; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) atomicAdd(&h[pairs[start + i] >> 32], 1u);
+    __syncthreads();
+    // exclusive scan of h[0..bin): each thread owns bin/256 consecutive counters
+    const uint32_t per = p.bin / blockDim.x;
+    const uint32_t i0 = threadIdx.x * per;
+    uint32_t sum = 0;
+    for (uint32_t q = 0; q < per; ++q) sum += h[i0 + q];
+    uint32_t total;
+    uint32_t run = block_exclusive_scan(sum, lds_scan, total);
+    for (uint32_t q = 0; q < per; ++q) {
+        const uint32_t v = h[i0 + q];
+        h[i0 + q] = run;
+        if (i0 + q < nodes) off[nb0 + i0 + q] = start + run;
+        run += v;
+    }
+    if (b == p.nb - 1 && threadIdx.x == 0) off[p.n] = p.n;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+        const u64 pr = pairs[start + i];
+        const uint32_t pos = atomicAdd(&h[(uint32_t)(pr >> 32)], 1u);
+        src[start + pos] = (uint32_t)pr;
+    }
+    __syncthreads();
+    // h[i] is now the end of node i's bucket; sort each (Poisson(1)-sized) bucket.
+    for (uint32_t i = threadIdx.x; i < nodes; i += blockDim.x) {
+        const uint32_t a = start + (i ? h[i - 1] : 0u), e = start + h[i];
+        for (uint32_t q = a + 1; q < e; ++q) {
+            const uint32_t v = src[q];
+            uint32_t r = q;
+            while (r > a && src[r - 1] > v) {
+                src[r] = src[r - 1];
+                --r;
+            }
+            src[r] = v;
         }
-        src[q] = v;
     }
 }
 
-hipError_t launch_build_csr(const uint32_t *tg, uint32_t *cnt, uint32_t *off, uint32_t *src,
-                            uint32_t *bsum, uint32_t n, uint32_t *flags,
+hipError_t launch_build_csr(const uint32_t *tg, const CsrPlan &p, uint32_t *scratch, u64 *pairs,
+                            uint32_t *off, uint32_t *src, uint32_t *flags,
                             uint32_t next_round_slot, hipStream_t s) {
-    const uint32_t nb = (n + kScanTile - 1) / kScanTile;
-    hipLaunchKernelGGL(scan_tile_sums, dim3(nb), dim3(kScanBlock), 0, s, cnt, n, bsum);
-    hipLaunchKernelGGL(scan_bsums, dim3(1), dim3(kScanBlock), 0, s, bsum, nb);
-    hipLaunchKernelGGL(scan_tiles, dim3(nb), dim3(kScanBlock), 0, s, cnt, n, bsum, off);
-    const uint32_t g = (n + 255) / 256;
-    hipLaunchKernelGGL(scatter_edges, dim3(g), dim3(256), 0, s, tg, off, cnt, src, n);
-    hipLaunchKernelGGL(sort_buckets, dim3(g), dim3(256), 0, s, off, src, n, flags, next_round_slot);
+    uint32_t *M = scratch;
+    uint32_t *tot = M + (size_t)p.ba * p.nb;
+    uint32_t *base = tot + p.nb;
+    const size_t lds_nb = (size_t)p.nb * sizeof(uint32_t);
+    hipLaunchKernelGGL(csr_bin_count, dim3(p.ba), dim3(256), lds_nb, s, tg, p, M);
+    hipLaunchKernelGGL(csr_col_scan, dim3((p.nb + 255) / 256), dim3(256), 0, s, M, p, tot);
+    hipLaunchKernelGGL(scan_small, dim3(1), dim3(kScanBlock), 0, s, tot, base, p.nb);
+    hipLaunchKernelGGL(csr_bin_scatter, dim3(p.ba), dim3(256), lds_nb, s, tg, p, M, base, pairs);
+    const size_t lds_sort = ((size_t)p.bin + 16) * sizeof(uint32_t);
+    if (lds_sort > 65536) {  // n > 2^28: bins of 32768 nodes need 128 KiB of the 160 KiB LDS
+        hipError_t e = hipFuncSetAttribute((const void *)csr_bin_sort,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sort);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(csr_bin_sort, dim3(p.nb), dim3(256), lds_sort, s, pairs, p, base, tot, off, src,
+                       flags, next_round_slot);
     return hipGetLastError();
 }
 
