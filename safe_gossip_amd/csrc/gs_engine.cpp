@@ -27,11 +27,14 @@ struct gs_engine {
     hipStream_t stream = nullptr;
     u64 *S[2] = {nullptr, nullptr};
     int cur = 0;
-    uint32_t *off = nullptr, *src = nullptr, *tg = nullptr;
+    uint32_t *src = nullptr, *tg = nullptr;
+    uint4 *IN = nullptr, *SIB = nullptr;
     uint32_t *csr_scratch = nullptr, *flags = nullptr;
     u64 *pairs = nullptr;
     gs::CsrPlan plan{};
-    u64 *stats = nullptr;
+    uint32_t *st32 = nullptr;  // [n][4] u32 deltas
+    u64 *st64 = nullptr;       // [n][4] folded totals
+    uint32_t fold_every = 1, since_fold = 0;
     u64 *inj_key = nullptr, *inj_mask = nullptr;
     u64 *inj_host = nullptr;  // pinned staging [2*cap]
     uint32_t inj_cap = 0;
@@ -85,8 +88,8 @@ void release(gs_engine *e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
-    void *bufs[] = {e->S[0], e->S[1], e->off, e->src, e->tg, e->csr_scratch, e->pairs, e->flags,
-                    e->stats, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
+    void *bufs[] = {e->S[0], e->S[1], e->IN, e->SIB, e->src, e->tg, e->csr_scratch, e->pairs,
+                    e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
                     e->partials, e->obs_state, e->obs_rec, e->obs_psize};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -103,7 +106,9 @@ gs_status reset_state(gs_engine *e) {
     const size_t sw = (size_t)g.units * gs::kPlanes * g.W;
     GS_HIP(hipMemsetAsync(e->S[0], 0, sw * sizeof(u64), e->stream));
     GS_HIP(hipMemsetAsync(e->S[1], 0, sw * sizeof(u64), e->stream));
-    GS_HIP(hipMemsetAsync(e->stats, 0, (size_t)5 * g.n * sizeof(u64), e->stream));
+    GS_HIP(hipMemsetAsync(e->st32, 0, (size_t)4 * g.n * sizeof(uint32_t), e->stream));
+    GS_HIP(hipMemsetAsync(e->st64, 0, (size_t)4 * g.n * sizeof(u64), e->stream));
+    e->since_fold = 0;
     GS_HIP(hipMemsetAsync(e->flags, 0, 4 * sizeof(uint32_t), e->stream));
     e->cur = 0;
     e->round = 0;
@@ -117,10 +122,12 @@ gs::RoundArgs base_args(gs_engine *e) {
     gs::RoundArgs a{};
     a.Scur = e->S[e->cur];
     a.Snext = e->S[e->cur ^ 1];
-    a.off = e->off;
+    a.IN = e->IN;
+    a.SIB = e->SIB;
     a.src = e->src;
-    a.tg = e->tg;
-    a.stats = e->stats;
+    a.st32 = e->st32;
+    a.st64 = e->st64;
+    a.obs_rounds = e->round;
     a.flags = e->flags;
     a.g = e->g;
     a.seed = e->seed;
@@ -315,14 +322,18 @@ gs_status gs_create(const gs_config *cfg, gs_engine **out) {
     }
     const size_t sw = (size_t)g.units * gs::kPlanes * g.W;
     e->plan = gs::csr_plan(n);
+    // Per round a node's u32 Statistics deltas grow by at most 32*R_pad + 32
+    // (in-degree <= 30 is enforced); fold them into u64 well before a wrap.
+    e->fold_every = (uint32_t)std::max<uint64_t>(1, 0xFFFFFFFFull / (32ull * g.rpad + 32) / 2);
     bool ok = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreate(&e->ev0) == hipSuccess && hipEventCreate(&e->ev1) == hipSuccess;
     ok = ok && dalloc(&e->S[0], sw) == hipSuccess && dalloc(&e->S[1], sw) == hipSuccess &&
-         dalloc(&e->off, (size_t)n + 1) == hipSuccess && dalloc(&e->src, n) == hipSuccess &&
+         dalloc(&e->IN, n) == hipSuccess && dalloc(&e->SIB, n) == hipSuccess &&
+         dalloc(&e->src, n) == hipSuccess &&
          dalloc(&e->tg, n) == hipSuccess && dalloc(&e->pairs, n) == hipSuccess &&
          dalloc(&e->csr_scratch, gs::csr_scratch_words(e->plan)) == hipSuccess &&
-         dalloc(&e->flags, 4) == hipSuccess &&
-         dalloc(&e->stats, (size_t)5 * n) == hipSuccess;
+         dalloc(&e->flags, 4) == hipSuccess && dalloc(&e->st32, (size_t)4 * n) == hipSuccess &&
+         dalloc(&e->st64, (size_t)4 * n) == hipSuccess;
     if (!ok) {
         hipError_t le = hipGetLastError();
         release(e);
@@ -385,8 +396,12 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
     e->cur ^= 1;
     e->deliver_pending = true;
     e->obs_valid = false;
-    GS_HIP(gs::launch_build_csr(e->tg, e->plan, e->csr_scratch, e->pairs, e->off, e->src, e->flags,
-                                (e->round + 1) & 1u, e->stream));
+    if (++e->since_fold >= e->fold_every) {
+        GS_HIP(gs::launch_stats_fold(e->st32, e->st64, e->g.n, e->stream));
+        e->since_fold = 0;
+    }
+    GS_HIP(gs::launch_build_csr(e->tg, e->plan, e->csr_scratch, e->pairs, e->src, e->IN, e->SIB,
+                                e->flags, e->seed, e->epoch, e->round, e->stream));
     if (report) {
         uint32_t fl[4];
         GS_HIP(hipMemcpyAsync(fl, e->flags, sizeof(fl), hipMemcpyDeviceToHost, e->stream));
@@ -565,11 +580,11 @@ float gs_last_round_kernel_ms(gs_engine *e) {
 double gs_round_kernel_bytes(const gs_engine *e) {
     // DESIGN.md "Roofline": per (node, rumor slot) 1 B state read + 1 B state
     // write (8 bit-planes) + 3/8 B class planes of each pusher (mean in-degree
-    // 1) + 3/8 B class planes of t(x); per node 104 B of CSR, target and
-    // Statistics traffic.
+    // 1) + 3/8 B class planes of t(x); per node 64 B: IN and SIB records
+    // (16 + 16), Statistics deltas (16 r + 16 w).
     if (!e) return 0.0;
     const double n = e->g.n, rp = e->g.rpad;
-    return n * (2.75 * rp + 104.0);
+    return n * (2.75 * rp + 64.0);
 }
 
 }  // extern "C"

@@ -7,10 +7,13 @@ namespace gs {
 struct RoundArgs {
     const u64 *Scur;          // state planes, round t (post phase 0)
     u64 *Snext;               // state planes, round t+1 (post phase 0)
-    const uint32_t *off;      // in-edge CSR of round t: offsets[n+1]
-    const uint32_t *src;      //   sources, ascending within a bucket
-    uint32_t *tg;             // tg[x]: round-t target in, round-(t+1) target out
-    u64 *stats;               // [5][n] Statistics SoA
+    const uint4 *IN;          // round t, per node y: {first edge, in-degree, s0, s1}
+    const uint4 *SIB;         // round t, per source x: {t(x), rank in in(t(x)), e0, e1}
+    const uint32_t *src;      // round t in-edge sources, ascending per target
+    uint32_t *st32;           // [n][4] u32 Statistics deltas (empty_pull, empty_push,
+                              //   full_sent, full_received)
+    const u64 *st64;          // [n][4] folded u64 totals (observation only)
+    u64 obs_rounds;           // Statistics.rounds of every node (observation)
     const u64 *inj_key;       // sorted segment keys with injections (round t+1)
     const u64 *inj_mask;      //   rumor masks in segment coordinates
     uint32_t n_inj;
@@ -45,11 +48,12 @@ struct CsrPlan {
 CsrPlan csr_plan(uint32_t n);
 size_t csr_scratch_words(const CsrPlan &p);  // u32 words of scratch
 
-// In-edge CSR of the round whose targets are in tg.  Also clears the any_live
-// slot of the round after it.
-hipError_t launch_build_csr(const uint32_t *tg, const CsrPlan &p, uint32_t *scratch, u64 *pairs,
-                            uint32_t *off, uint32_t *src, uint32_t *flags,
-                            uint32_t next_round_slot, hipStream_t s);
+// Peer choices of `round` (into tg) and their in-edge lists (src, IN, SIB).
+// Also clears the any_live slot of the round after it.
+hipError_t launch_build_csr(uint32_t *tg, const CsrPlan &p, uint32_t *scratch, u64 *pairs,
+                            uint32_t *src, uint4 *IN, uint4 *SIB, uint32_t *flags,
+                            uint64_t seed, uint32_t epoch, uint32_t round, hipStream_t s);
+hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, hipStream_t s);
 
 // Reductions for observers.
 hipError_t launch_known_reduce(const u64 *known, uint32_t n, uint32_t KW, uint32_t R,

@@ -18,6 +18,11 @@
 // B.peer_counters are never materialised: the copies x received are
 // re-derived from the round-t class planes of its pushers and of t(x), which
 // is all MessageState::next_round consumes (anyC + a count of counters >= own).
+//
+// Latency structure: every per-node metadata read (IN[x], SIB[x], own planes,
+// statistics) is coalesced; the only random accesses are the class-plane
+// gathers of the pushers, of t(x) and of t(x)'s earlier pushers, and they are
+// all issued together, one dependent level after the coalesced reads.
 #include "gs_kernels.h"
 
 namespace gs {
@@ -46,6 +51,23 @@ GS_DEV u64 ge_k(const u64 (&x)[NB], uint32_t K) {
         u64 ki = ((K >> i) & 1u) ? ~0ull : 0ull;
         gt |= eq & x[i] & ~ki;
         eq &= ~(x[i] ^ ki);
+    }
+    return gt | eq;
+}
+
+// Same with K wave-uniform (max_rounds, max_c_rounds): scalar branches on the
+// bits of K, 2 ops per bit.
+template <int NB>
+GS_DEV u64 ge_u(const u64 (&x)[NB], uint32_t K) {
+    if (K >= (1u << NB)) return 0ull;
+    u64 gt = 0ull, eq = ~0ull;
+#pragma unroll
+    for (int i = NB - 1; i >= 0; --i) {
+        if ((K >> i) & 1u) {
+            eq &= x[i];
+        } else {
+            gt |= eq & x[i];
+        }
     }
     return gt | eq;
 }
@@ -114,12 +136,89 @@ GS_DEV uint32_t group_min(uint32_t v, uint32_t W) {
 
 constexpr uint32_t kNone = 0xffffffffu;
 
-// MODE: 0 transition only, 1 deliver + transition, 2 deliver + observe,
-// 3 observe only.
+// Receiver-side state of phases 1-2 at x for one segment.  The transition
+// path keeps one bit-sliced counter of the recorded counters that vote ">= own"
+// (MessageState::next_round's greater_or_equal, src/message_state.rs:118-129);
+// the observation path (OBS) keeps the two counters the parity dumps report.
+template <bool OBS>
+struct Recv {
+    u64 notyet;          // still absent: the next live copy creates the entry
+    u64 recB;            // entries in state B (existing or created): record copies
+    u64 oc1;             // B entries whose our_counter is 1 (created ones included)
+    u64 crB, crC;        // created this round as B{0,1} / C{0,0}
+    u64 anyC;            // a recorded counter >= counter_max
+    u64 cv[5];           // #recorded counters >= our_counter (and < counter_max)
+    u64 c1[5];           // OBS only: #recorded counters in [1, counter_max)
+    u64 c2[5];           // OBS only: #recorded counters == 2 (< counter_max)
+    uint32_t part_cw;    // sum over pushers i of (k-1-i) * |created by i|
+    uint32_t first_create;
+    uint32_t recv;       // copies received (push rows + pull row)
+
+    GS_DEV void init(u64 A, u64 B, u64 Boc1) {
+        notyet = A;
+        recB = B;
+        oc1 = Boc1;
+        crB = crC = anyC = 0;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) cv[i] = 0;
+        if constexpr (OBS) {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) c1[i] = c2[i] = 0;
+        }
+        part_cw = 0;
+        first_create = kNone;
+        recv = 0;
+    }
+    // Record copies `rec` of class (vB: a B counter, v2: counter 2, vC: 255).
+    GS_DEV void record(u64 rec, u64 vB, u64 v2, u64 vC) {
+        anyC |= rec & vC;
+        add5(cv, rec & vB & (v2 | oc1));
+        if constexpr (OBS) {
+            add5(c1, rec & vB);
+            add5(c2, rec & v2);
+        }
+    }
+    GS_DEV void create(u64 newc, u64 vC) {
+        crB |= newc & ~vC;
+        crC |= newc & vC;
+        recB |= newc & ~vC;
+        oc1 |= newc & ~vC;
+        notyet &= ~newc;
+    }
+    // One push batch from pusher i of k (Gossip::receive, src/gossip.rs:153-163);
+    // `rec_on` is false for t(x)'s own push, superseded by its pull copy.
+    GS_DEV void push(const Cls &q, uint32_t i, uint32_t k, bool rec_on) {
+        const u64 vC = q.c & ~(q.a0 & q.a1);   // C: counter 255
+        const u64 vB = ~q.c & (q.a0 | q.a1);   // B: counter = our_counter
+        const u64 v2 = vB & q.a1 & ~q.a0;      // B with our_counter 2
+        const u64 sl = vB | vC;                // the push batch
+        const u64 newc = notyet & sl;          // new_from_peer: not recorded
+        if (rec_on) record(recB & sl, vB, v2, vC);  // MessageState::receive on B
+        create(newc, vC);
+        const uint32_t pc = popc(newc);
+        part_cw += (k - 1u - i) * pc;  // later pushers' pull rows include it
+        if (pc && first_create == kNone) first_create = i;
+        recv += popc(sl);
+    }
+};
+
+// First-carrier class of the entries z created from its pushers ahead of x
+// (the pull row is built before x's push is absorbed, src/gossip.rs:124-151).
+GS_DEV void sibling(const Cls &q, u64 &pnot, u64 &pB, u64 &pC) {
+    const u64 vC = q.c & ~(q.a0 & q.a1);
+    const u64 sl = (~q.c & (q.a0 | q.a1)) | vC;
+    const u64 nc = pnot & sl;
+    pB |= nc & ~vC;
+    pC |= nc & vC;
+    pnot &= ~sl;
+}
+
 #ifndef GS_RK_MINW
 #define GS_RK_MINW 1
 #endif
 
+// MODE: 0 transition only (first round), 1 deliver round t + transition to
+// t+1, 2 deliver round t + observe, 3 observe only.
 template <bool SMALL, int MODE>
 __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     constexpr bool DELIVER = (MODE == 1 || MODE == 2);
@@ -132,13 +231,39 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     const uint32_t x = L.x;
     const u64 *__restrict__ S = a.Scur;
 
-    // ---- own round-t state (post phase 0): 8 planes
+    // ---- coalesced per-node metadata and own round-t planes
+    uint4 in = {0, 0, 0, 0}, sb = {0, 0, 0, 0};
+    if (DELIVER && valid) {
+        in = a.IN[x];   // {first edge, k, s0, s1}
+        sb = a.SIB[x];  // {z = t_t(x), rank of x in in(z), e0, e1}
+    }
     u64 P[kPlanes];
 #pragma unroll
     for (int p = 0; p < kPlanes; ++p) {
         u64 v = valid ? S[L.plane_index(p)] : 0ull;
         P[p] = SMALL ? ((v >> L.sh) & L.m) : v;
     }
+
+    // ---- the random gathers, all issued together
+    uint32_t k = 0, r = 0, z = 0;
+    Cls q0 = {0, 0, 0}, q1 = {0, 0, 0}, qz = {0, 0, 0}, e0 = {0, 0, 0}, e1 = {0, 0, 0};
+    if (DELIVER && valid) {
+        k = in.y;
+        z = sb.x;
+        r = sb.y;
+#ifdef GS_EXP_NO_PUSHERS
+        k = 0;
+#endif
+#ifdef GS_EXP_NO_ZPUSHERS
+        r = 0;
+#endif
+        if (k > 0) q0 = L.load_cls(S, in.z);
+        if (k > 1) q1 = L.load_cls(S, in.w);
+        qz = L.load_cls(S, z);
+        if (r > 0) e0 = L.load_cls(S, sb.z);
+        if (r > 1) e1 = L.load_cls(S, sb.w);
+    }
+
     const u64 isC = P[0], a0 = P[1], a1 = P[2];
     const u64 A = ~isC & ~a0 & ~a1 & L.m;
     const u64 B = ~isC & (a0 | a1);
@@ -147,93 +272,62 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     const u64 liveX = B | C;
 
     // ---- phases 1 and 2 of round t at x (Gossip::receive)
-    u64 crB = 0, crC = 0, anyC = 0;
-    u64 c1[5] = {0, 0, 0, 0, 0};  // recorded counters in [1, cmax)
-    u64 c2[5] = {0, 0, 0, 0, 0};  // recorded counters == 2 (< cmax)
-    uint32_t k = 0, psize = 0, part_cw = 0, first_create = kNone, recv = 0;
+    Recv<!TRANSITION> rv;
+    rv.init(A, B, B & a0 & ~a1);
+    uint32_t psize = 0;
     if (DELIVER && valid) {
-        const uint32_t z = a.tg[x];  // t_t(x): the pull batch comes from z
-        const uint32_t k0 = a.off[x];
-        k = a.off[x + 1] - k0;
         if (k > 30u) atomicOr(&a.flags[2], 1u);
-        u64 notyet = A;  // still absent: the next live copy creates the entry
         bool zin = false;
-        for (uint32_t i = 0; i < k; ++i) {
-            const uint32_t s = a.src[k0 + i];
-            const Cls q = L.load_cls(S, s);
-            const u64 vC = q.c & ~(q.a0 & q.a1);   // C: counter 255
-            const u64 vB = ~q.c & (q.a0 | q.a1);   // B: counter = our_counter
-            const u64 v2 = vB & q.a1 & ~q.a0;      // B with our_counter 2
-            const u64 sl = vB | vC;                // the push batch of s
-            const u64 newc = notyet & sl;          // new_from_peer (not recorded)
-            if (s != z) {
-                // MessageState::receive on B entries.  t(x)'s own push copy is
-                // superseded by its pull copy (same value), counted below.
-                const u64 rec = (B | crB) & sl;
-                anyC |= rec & vC;
-                add5(c1, rec & vB);
-                add5(c2, rec & v2);
-            } else {
-                zin = true;
-            }
-            crB |= newc & ~vC;
-            crC |= newc & vC;
-            notyet &= ~sl;
-            const uint32_t pc = popc(newc);
-            part_cw += (k - 1u - i) * pc;  // later pushers' pull rows include it
-            if (pc && first_create == kNone) first_create = i;
-            recv += popc(sl);
+        if (k > 0) {
+            zin |= in.z == z;
+            rv.push(q0, 0, k, in.z != z);
         }
-        // Pull batch from z: z's live set plus entries z created from pushers
-        // ahead of x (Gossip::receive builds the pull list before absorbing
-        // x's push, src/gossip.rs:124-151).
-        const Cls zq = L.load_cls(S, z);
-        const u64 zA = ~zq.c & ~zq.a0 & ~zq.a1 & L.m;
-        const u64 zB = ~zq.c & (zq.a0 | zq.a1);
-        const u64 zC = zq.c & ~(zq.a0 & zq.a1);
-        u64 pB = 0, pC = 0, pnot = zA;
-        if (pnot) {
-            const uint32_t m0 = a.off[z], m1 = a.off[z + 1];
-            for (uint32_t q = m0; q < m1 && pnot; ++q) {
-                const uint32_t s = a.src[q];
-                if (s >= x) break;
-                const Cls sq = L.load_cls(S, s);
-                const u64 vC = sq.c & ~(sq.a0 & sq.a1);
-                const u64 sl = (~sq.c & (sq.a0 | sq.a1)) | vC;
-                const u64 nc = pnot & sl;
-                pB |= nc & ~vC;
-                pC |= nc & vC;
-                pnot &= ~sl;
-            }
+        if (k > 1) {
+            zin |= in.w == z;
+            rv.push(q1, 1, k, in.w != z);
         }
-        const u64 pv2 = zB & zq.a1 & ~zq.a0;
-        const u64 pvB = (zB | pB);                 // counters 1 (created: 1) or 2
+        for (uint32_t i = 2; i < k; ++i) {  // in-degree >= 3 (8% of nodes)
+            const uint32_t s = a.src[in.x + i];
+            zin |= s == z;
+            rv.push(L.load_cls(S, s), i, k, s != z);
+        }
+        // Pull batch from z: z's live set plus what z created from pushers
+        // ahead of x.
+        const u64 zB = ~qz.c & (qz.a0 | qz.a1);
+        const u64 zC = qz.c & ~(qz.a0 & qz.a1);
+        u64 pnot = ~qz.c & ~qz.a0 & ~qz.a1 & L.m, pB = 0, pC = 0;
+        if (r > 0) sibling(e0, pnot, pB, pC);
+        if (r > 1) sibling(e1, pnot, pB, pC);
+        if (r > 2 && pnot) {
+            const uint32_t zb = a.IN[z].x;  // rare: rank >= 3
+            for (uint32_t i = 2; i < r && pnot; ++i) sibling(L.load_cls(S, a.src[zb + i]), pnot, pB, pC);
+        }
+        const u64 pv2 = zB & qz.a1 & ~qz.a0;
+        const u64 pvB = zB | pB;  // counter 1 (created entries: 1) or 2
         const u64 pCl = zC | pC;
         const u64 pl = pvB | pCl;
         {
-            const u64 newc = notyet & pl;
-            const u64 rec = (B | crB) & pl;
-            anyC |= rec & pCl;
-            add5(c1, rec & pvB);
-            add5(c2, rec & pv2);
-            crB |= newc & ~pCl;
-            crC |= newc & pCl;
+            const u64 newc = rv.notyet & pl;
+            rv.record(rv.recB & pl, pvB, pv2, pCl);
+            rv.create(newc, pCl);
         }
-        recv += popc(pl);
+        rv.recv += popc(pl);
         psize = k + (zin ? 0u : 1u);  // |peers_in_this_round|
     }
+    const u64 crB = rv.crB, crC = rv.crC, anyC = rv.anyC;
 
     // ---- node-level statistics of the deliveries
     uint32_t lc = popc(liveX);
+    uint32_t part_cw = rv.part_cw, recv = rv.recv, first_create = rv.first_create;
     if (DELIVER && !SMALL) {
         lc = group_sum(lc, g.W);
         part_cw = group_sum(part_cw, g.W);
         recv = group_sum(recv, g.W);
         first_create = group_min(first_create, g.W);
     }
-    uint64_t d_full_sent = 0, d_empty_pull = 0, d_recv = 0;
+    uint32_t d_full_sent = 0, d_empty_pull = 0, d_recv = 0;
     if (DELIVER) {
-        d_full_sent = (uint64_t)k * lc + part_cw;  // pull rows sent by x
+        d_full_sent = k * lc + part_cw;  // pull rows sent by x
         if (k > 0 && lc == 0) d_empty_pull = (first_create == kNone) ? k : first_create + 1u;
         d_recv = recv;
     }
@@ -247,24 +341,26 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         if (a.obs_known && (SMALL || L.j < KW)) a.obs_known[(u64)x * KW + L.j] = known;
         if (leader) {
             if (a.obs_stats) {
-                const u64 n = g.n;
-                a.obs_stats[(u64)x * 5 + 0] = a.stats[0 * n + x];
-                a.obs_stats[(u64)x * 5 + 1] = a.stats[1 * n + x] + d_empty_pull;
-                a.obs_stats[(u64)x * 5 + 2] = a.stats[2 * n + x];
-                a.obs_stats[(u64)x * 5 + 3] = a.stats[3 * n + x] + d_full_sent;
-                a.obs_stats[(u64)x * 5 + 4] = a.stats[4 * n + x] + d_recv;
+                const uint4 d32 = reinterpret_cast<const uint4 *>(a.st32)[x];
+                const u64 *b64 = a.st64 + (u64)x * 4;
+                u64 *o = a.obs_stats + (u64)x * 5;
+                o[0] = a.obs_rounds;
+                o[1] = b64[0] + d32.x + d_empty_pull;
+                o[2] = b64[1] + d32.y;
+                o[3] = b64[2] + d32.z + d_full_sent;
+                o[4] = b64[3] + d32.w + d_recv;
             }
             if (a.obs_psize) a.obs_psize[x] = psize;
         }
         if (a.obs_state || a.obs_rec) {
             const uint32_t nb = SMALL ? g.rpad : 64u;
             for (uint32_t b = 0; b < nb; ++b) {
-                const uint32_t r = SMALL ? b : L.j * 64u + b;
-                if (r >= g.R) break;
+                const uint32_t rr = SMALL ? b : L.j * 64u + b;
+                if (rr >= g.R) break;
                 const u64 bit = 1ull << b;
                 uint32_t bf = 0;
 #pragma unroll
-                for (int i = 0; i < 5; ++i) bf |= ((P[3 + i] >> b) & 1u) << i;
+                for (int i = 0; i < 5; ++i) bf |= (uint32_t)((P[3 + i] >> b) & 1u) << i;
                 const uint32_t af = (uint32_t)((a0 >> b) & 1u) | ((uint32_t)((a1 >> b) & 1u) << 1);
                 uint16_t code = 0;
                 if (crB & bit) code = (uint16_t)((1u << 14) | (1u << 7));
@@ -272,19 +368,19 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                 else if (B & bit) code = (uint16_t)((1u << 14) | (af << 7) | bf);
                 else if (C & bit) code = (uint16_t)((2u << 14) | (af << 7) | bf);
                 else if (D & bit) code = (uint16_t)(3u << 14);
-                if (a.obs_state) a.obs_state[(u64)x * g.R + r] = code;
+                if (a.obs_state) a.obs_state[(u64)x * g.R + rr] = code;
                 if (a.obs_rec) {
-                    uint16_t rv = 0;
+                    uint16_t rvv = 0;
                     if ((B | crB) & bit) {
                         uint32_t v1 = 0, v2 = 0;
 #pragma unroll
                         for (int i = 0; i < 5; ++i) {
-                            v1 |= ((c1[i] >> b) & 1u) << i;
-                            v2 |= ((c2[i] >> b) & 1u) << i;
+                            v1 |= (uint32_t)((rv.c1[i] >> b) & 1u) << i;
+                            v2 |= (uint32_t)((rv.c2[i] >> b) & 1u) << i;
                         }
-                        rv = (uint16_t)((((anyC >> b) & 1u) << 15) | (v2 << 7) | v1);
+                        rvv = (uint16_t)((((anyC >> b) & 1u) << 15) | (v2 << 7) | v1);
                     }
-                    a.obs_rec[(u64)x * g.R + r] = rv;
+                    a.obs_rec[(u64)x * g.R + rr] = rvv;
                 }
             }
         }
@@ -315,7 +411,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     const u64 oc1 = (Bold & a0 & ~a1) | cB | inj;
     const u64 oc2 = Bold & a1 & ~a0;
     const uint32_t thr = psize / 2u + 1u;
-    const u64 bump = ((oc1 & ge_k<5>(c1, thr)) | (oc2 & ge_k<5>(c2, thr))) & ninj;
+    const u64 bump = ge_k<5>(rv.cv, thr) & (Bold | cB);  // cv counts only B entries' votes
     const u64 anyCe = anyC & ninj;
     u64 nr[6];  // round + 1
     {
@@ -328,7 +424,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         }
         nr[5] = carry;
     }
-    const u64 toD = ge_k<6>(nr, a.maxr);
+    const u64 toD = ge_u<6>(nr, a.maxr);
     const u64 oc1n = oc1 & ~bump;
     const u64 oc2n = (oc1 & bump) | (oc2 & ~bump);
     const u64 oc3n = oc2 & bump;
@@ -354,7 +450,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         }
         sum[5] = c;
     }
-    const u64 CtoD = ge_k<6>(sum, a.maxr) | ge_k<3>(d, a.maxc);
+    const u64 CtoD = ge_u<6>(sum, a.maxr) | ge_u<3>(d, a.maxc);
     const u64 CD = Cf & CtoD, CC = Cf & ~CtoD;
 
     const u64 Dn = BD | CD | Dold;
@@ -393,17 +489,17 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             atomicOr(f, 1u);
     }
     if (leader) {
-        const u64 n = g.n;
-        u64 *st = a.stats;
-        st[0 * n + x] += 1u;                                     // rounds
-        if (DELIVER) {
-            st[1 * n + x] += d_empty_pull;                       // empty_pull_sent
-            st[4 * n + x] += d_recv;                             // full_message_received
-        }
-        st[2 * n + x] += (live_new == 0u) ? 1u : 0u;             // empty_push_sent
-        st[3 * n + x] += (uint64_t)live_new + d_full_sent;       // full_message_sent
-        // Peer choice of round t+1; its in-edge CSR is built by build_csr.
-        a.tg[x] = peer_of(a.seed, a.epoch, a.round_new, x, g.n);
+#ifndef GS_EXP_NO_STATS
+        // rounds is the engine's round count (every node runs every round);
+        // the other four are u32 deltas folded into u64 before they can wrap.
+        uint4 *st = reinterpret_cast<uint4 *>(a.st32) + x;
+        uint4 v = *st;
+        v.x += d_empty_pull;                       // empty_pull_sent
+        v.y += (live_new == 0u) ? 1u : 0u;         // empty_push_sent
+        v.z += live_new + d_full_sent;             // full_message_sent
+        v.w += d_recv;                             // full_message_received
+        *st = v;
+#endif
     }
 }
 
@@ -424,19 +520,35 @@ hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s) {
     return a.g.small ? launch_mode<true>(a, mode, s) : launch_mode<false>(a, mode, s);
 }
 
-// ------------------------------------------------------------ in-edge CSR
+// Fold the u32 statistics deltas into the u64 totals (before they can wrap).
+__global__ __launch_bounds__(256) void stats_fold(uint32_t *st32, u64 *st64, u64 words) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= words) return;
+    st64[i] += st32[i];
+    st32[i] = 0u;
+}
+
+hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, hipStream_t s) {
+    const u64 words = (u64)n * 4;
+    hipLaunchKernelGGL(stats_fold, dim3((uint32_t)((words + 255) / 256)), dim3(256), 0, s, st32, st64,
+                       words);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------ in-edge lists
 // Two-stage counting sort of the n edges (x -> tg[x]) by target, with no
-// global atomics (the round kernel's targets are uniform, so fixed-width
-// target bins are balanced):
+// global atomics (targets are uniform, so fixed-width target bins balance):
 //   bin_count   : per source chunk, an LDS histogram over target bins
 //                 -> M[chunk][bin]
 //   col_scan    : per bin, exclusive prefix over chunks; bin totals
 //   scan (1 blk): exclusive prefix of the bin totals -> bin bases
 //   bin_scatter : (local target, source) pairs into their bin's range
-//                 (runs of ~C/NB pairs per chunk and bin)
-//   bin_sort    : per bin, LDS counting sort by local target -> off[], src[],
-//                 then each node's few sources sorted ascending (the order
-//                 Gossip::receive sees its pushers in, src/gossiper.rs:217).
+//                 (runs of ~chunk/nb pairs per chunk and bin)
+//   bin_sort    : per bin, LDS counting sort by local target -> src[] with each
+//                 node's sources ascending (the order Gossip::receive sees its
+//                 pushers in, src/gossiper.rs:217), then the per-node records
+//                 IN[y] = {first edge, in-degree, s0, s1}          (node order)
+//                 SIB[x] = {t(x), rank of x in in(t(x)), e0, e1}   (per source)
 constexpr uint32_t kScanBlock = 256;
 
 // Block-wide exclusive scan of one value per thread; returns the block total.
@@ -476,18 +588,25 @@ CsrPlan csr_plan(uint32_t n) {
 }
 
 size_t csr_scratch_words(const CsrPlan &p) {
-    // M[ba][nb] + tot[nb] + base[nb] (u32 words) ; pairs are separate (u64 [n])
+    // M[ba][nb] + tot[nb] + base[nb] (u32 words); pairs are separate (u64 [n])
     return (size_t)p.ba * p.nb + 2 * (size_t)p.nb;
 }
 
-__global__ __launch_bounds__(256) void csr_bin_count(const uint32_t *__restrict__ tg, CsrPlan p,
-                                                     uint32_t *M) {
+// Also draws the round's peer choices (Gossiper::next_round's
+// thread_rng().choose, src/gossiper.rs:71, as the injected Philox stream).
+__global__ __launch_bounds__(256) void csr_bin_count(uint32_t *__restrict__ tg, CsrPlan p,
+                                                     uint32_t *M, uint64_t seed, uint32_t epoch,
+                                                     uint32_t round) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
     for (uint32_t i = threadIdx.x; i < p.nb; i += blockDim.x) hist[i] = 0;
     __syncthreads();
     const u64 lo = (u64)blockIdx.x * p.chunk;
     const u64 hi = min((u64)p.n, lo + p.chunk);
-    for (u64 x = lo + threadIdx.x; x < hi; x += blockDim.x) atomicAdd(&hist[tg[x] >> p.logbin], 1u);
+    for (u64 x = lo + threadIdx.x; x < hi; x += blockDim.x) {
+        const uint32_t t = peer_of(seed, epoch, round, (uint32_t)x, p.n);
+        tg[x] = t;
+        atomicAdd(&hist[t >> p.logbin], 1u);
+    }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < p.nb; i += blockDim.x) M[(u64)blockIdx.x * p.nb + i] = hist[i];
 }
@@ -537,9 +656,10 @@ __global__ __launch_bounds__(256) void csr_bin_scatter(const uint32_t *__restric
 
 __global__ __launch_bounds__(256) void csr_bin_sort(const u64 *__restrict__ pairs, CsrPlan p,
                                                     const uint32_t *__restrict__ base,
-                                                    const uint32_t *__restrict__ tot, uint32_t *off,
-                                                    uint32_t *src, uint32_t *flags, uint32_t slot) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t h[];  // [bin] + 4 scan words
+                                                    const uint32_t *__restrict__ tot, uint32_t *src,
+                                                    uint4 *IN, uint4 *SIB, uint32_t *flags,
+                                                    uint32_t slot) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t h[];  // [bin] + 16 scan words
     uint32_t *lds_scan = h + p.bin;
     const uint32_t b = blockIdx.x;
     if (b == 0 && threadIdx.x == 0) flags[slot] = 0u;  // any_live slot of the round after
@@ -560,10 +680,8 @@ __global__ __launch_bounds__(256) void csr_bin_sort(const u64 *__restrict__ pair
     for (uint32_t q = 0; q < per; ++q) {
         const uint32_t v = h[i0 + q];
         h[i0 + q] = run;
-        if (i0 + q < nodes) off[nb0 + i0 + q] = start + run;
         run += v;
     }
-    if (b == p.nb - 1 && threadIdx.x == 0) off[p.n] = p.n;
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
         const u64 pr = pairs[start + i];
@@ -571,7 +689,8 @@ __global__ __launch_bounds__(256) void csr_bin_sort(const u64 *__restrict__ pair
         src[start + pos] = (uint32_t)pr;
     }
     __syncthreads();
-    // h[i] is now the end of node i's bucket; sort each (Poisson(1)-sized) bucket.
+    // h[i] is now the end of node i's bucket: sort each (Poisson(1)-sized)
+    // bucket, then emit IN[] and SIB[].
     for (uint32_t i = threadIdx.x; i < nodes; i += blockDim.x) {
         const uint32_t a = start + (i ? h[i - 1] : 0u), e = start + h[i];
         for (uint32_t q = a + 1; q < e; ++q) {
@@ -583,17 +702,26 @@ __global__ __launch_bounds__(256) void csr_bin_sort(const u64 *__restrict__ pair
             }
             src[r] = v;
         }
+        const uint32_t k = e - a;
+        const uint32_t s0 = k > 0 ? src[a] : 0u, s1 = k > 1 ? src[a + 1] : 0u;
+        const uint32_t y = nb0 + i;
+        IN[y] = make_uint4(a, k, s0, s1);
+        for (uint32_t q = a; q < e; ++q) {
+            const uint32_t rank = q - a;
+            SIB[src[q]] = make_uint4(y, rank, rank > 0 ? s0 : 0u, rank > 1 ? s1 : 0u);
+        }
     }
 }
 
-hipError_t launch_build_csr(const uint32_t *tg, const CsrPlan &p, uint32_t *scratch, u64 *pairs,
-                            uint32_t *off, uint32_t *src, uint32_t *flags,
-                            uint32_t next_round_slot, hipStream_t s) {
+hipError_t launch_build_csr(uint32_t *tg, const CsrPlan &p, uint32_t *scratch, u64 *pairs,
+                            uint32_t *src, uint4 *IN, uint4 *SIB, uint32_t *flags,
+                            uint64_t seed, uint32_t epoch, uint32_t round, hipStream_t s) {
+    const uint32_t next_round_slot = (round + 1u) & 1u;
     uint32_t *M = scratch;
     uint32_t *tot = M + (size_t)p.ba * p.nb;
     uint32_t *base = tot + p.nb;
     const size_t lds_nb = (size_t)p.nb * sizeof(uint32_t);
-    hipLaunchKernelGGL(csr_bin_count, dim3(p.ba), dim3(256), lds_nb, s, tg, p, M);
+    hipLaunchKernelGGL(csr_bin_count, dim3(p.ba), dim3(256), lds_nb, s, tg, p, M, seed, epoch, round);
     hipLaunchKernelGGL(csr_col_scan, dim3((p.nb + 255) / 256), dim3(256), 0, s, M, p, tot);
     hipLaunchKernelGGL(scan_small, dim3(1), dim3(kScanBlock), 0, s, tot, base, p.nb);
     hipLaunchKernelGGL(csr_bin_scatter, dim3(p.ba), dim3(256), lds_nb, s, tg, p, M, base, pairs);
@@ -603,8 +731,8 @@ hipError_t launch_build_csr(const uint32_t *tg, const CsrPlan &p, uint32_t *scra
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sort);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(csr_bin_sort, dim3(p.nb), dim3(256), lds_sort, s, pairs, p, base, tot, off, src,
-                       flags, next_round_slot);
+    hipLaunchKernelGGL(csr_bin_sort, dim3(p.nb), dim3(256), lds_sort, s, pairs, p, base, tot, src, IN,
+                       SIB, flags, next_round_slot);
     return hipGetLastError();
 }
 
