@@ -27,10 +27,20 @@ struct gs_engine {
     hipStream_t stream = nullptr;
     u64 *S[2] = {nullptr, nullptr};
     int cur = 0;
-    uint32_t *src = nullptr, *tg = nullptr;
-    uint4 *IN = nullptr, *SIB = nullptr;
-    uint32_t *csr_scratch = nullptr, *flags = nullptr;
-    u64 *pairs = nullptr;
+    // In-edge lists, double-buffered: set (r & 1) holds round r's lists.  The
+    // set of round r+1 is built on cstream while the round kernel of round
+    // r+1 (which reads round r's set) runs on `stream`.
+    struct CsrSet {
+        uint32_t *src = nullptr, *tg = nullptr, *scratch = nullptr;
+        uint4 *IN = nullptr, *SIB = nullptr;
+        u64 *pairs = nullptr;
+        uint32_t serial = 0;
+    } csr[2];
+    hipStream_t cstream = nullptr;
+    hipEvent_t ev_built[2] = {nullptr, nullptr};  // set i complete
+    hipEvent_t ev_read[2] = {nullptr, nullptr};   // last reader of set i done
+    uint32_t build_serial = 0;
+    uint32_t *flags = nullptr;
     gs::CsrPlan plan{};
     uint32_t *st32 = nullptr;  // [n][4] u32 deltas
     u64 *st64 = nullptr;       // [n][4] folded totals
@@ -88,8 +98,18 @@ void release(gs_engine *e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
-    void *bufs[] = {e->S[0], e->S[1], e->IN, e->SIB, e->src, e->tg, e->csr_scratch, e->pairs,
-                    e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
+    if (e->cstream) (void)hipStreamSynchronize(e->cstream);
+    for (auto &c : e->csr) {
+        void *cb[] = {c.src, c.tg, c.scratch, c.IN, c.SIB, c.pairs};
+        for (void *b : cb)
+            if (b) (void)hipFree(b);
+    }
+    for (int i = 0; i < 2; ++i) {
+        if (e->ev_built[i]) (void)hipEventDestroy(e->ev_built[i]);
+        if (e->ev_read[i]) (void)hipEventDestroy(e->ev_read[i]);
+    }
+    if (e->cstream) (void)hipStreamDestroy(e->cstream);
+    void *bufs[] = {e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
                     e->partials, e->obs_state, e->obs_rec, e->obs_psize};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -103,6 +123,7 @@ void release(gs_engine *e) {
 
 gs_status reset_state(gs_engine *e) {
     const gs::Geometry &g = e->g;
+    GS_HIP(hipStreamSynchronize(e->cstream));
     const size_t sw = (size_t)g.units * gs::kPlanes * g.W;
     GS_HIP(hipMemsetAsync(e->S[0], 0, sw * sizeof(u64), e->stream));
     GS_HIP(hipMemsetAsync(e->S[1], 0, sw * sizeof(u64), e->stream));
@@ -122,9 +143,12 @@ gs::RoundArgs base_args(gs_engine *e) {
     gs::RoundArgs a{};
     a.Scur = e->S[e->cur];
     a.Snext = e->S[e->cur ^ 1];
-    a.IN = e->IN;
-    a.SIB = e->SIB;
-    a.src = e->src;
+    const auto &cs = e->csr[e->round & 1u];  // round-t lists (t = e->round)
+    a.IN = cs.IN;
+    a.SIB = cs.SIB;
+    a.src = cs.src;
+    a.tg = cs.tg;
+    a.serial = cs.serial;
     a.st32 = e->st32;
     a.st64 = e->st64;
     a.obs_rounds = e->round;
@@ -212,6 +236,7 @@ gs_status observe(gs_engine *e, bool dumps) {
         a.obs_state = e->obs_state;
         a.obs_rec = e->obs_rec;
     }
+    if (e->deliver_pending) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
     GS_HIP(gs::launch_round(a, e->deliver_pending ? 2 : 3, e->stream));
     uint32_t fl = 0;
     GS_HIP(hipMemcpyAsync(&fl, e->flags + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
@@ -326,12 +351,19 @@ gs_status gs_create(const gs_config *cfg, gs_engine **out) {
     // (in-degree <= 30 is enforced); fold them into u64 well before a wrap.
     e->fold_every = (uint32_t)std::max<uint64_t>(1, 0xFFFFFFFFull / (32ull * g.rpad + 32) / 2);
     bool ok = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&e->cstream, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreate(&e->ev0) == hipSuccess && hipEventCreate(&e->ev1) == hipSuccess;
+    for (int i = 0; i < 2 && ok; ++i) {
+        auto &c = e->csr[i];
+        ok = hipEventCreateWithFlags(&e->ev_built[i], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&e->ev_read[i], hipEventDisableTiming) == hipSuccess &&
+             dalloc(&c.IN, n) == hipSuccess && dalloc(&c.SIB, n) == hipSuccess &&
+             dalloc(&c.src, n) == hipSuccess && dalloc(&c.tg, n) == hipSuccess &&
+             dalloc(&c.pairs, n) == hipSuccess &&
+             dalloc(&c.scratch, gs::csr_scratch_words(e->plan)) == hipSuccess &&
+             hipMemset(c.SIB, 0, (size_t)n * sizeof(uint4)) == hipSuccess;
+    }
     ok = ok && dalloc(&e->S[0], sw) == hipSuccess && dalloc(&e->S[1], sw) == hipSuccess &&
-         dalloc(&e->IN, n) == hipSuccess && dalloc(&e->SIB, n) == hipSuccess &&
-         dalloc(&e->src, n) == hipSuccess &&
-         dalloc(&e->tg, n) == hipSuccess && dalloc(&e->pairs, n) == hipSuccess &&
-         dalloc(&e->csr_scratch, gs::csr_scratch_words(e->plan)) == hipSuccess &&
          dalloc(&e->flags, 4) == hipSuccess && dalloc(&e->st32, (size_t)4 * n) == hipSuccess &&
          dalloc(&e->st64, (size_t)4 * n) == hipSuccess;
     if (!ok) {
@@ -386,9 +418,12 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
         t1 = e->tev[2 * e->tcount + 1];
         e->tcount++;
     }
+    const uint32_t rs = e->round & 1u;  // set holding round t = e->round
+    if (e->deliver_pending) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[rs], 0));
     if (e->timing) GS_HIP(hipEventRecord(t0, e->stream));
     GS_HIP(gs::launch_round(a, e->deliver_pending ? 1 : 0, e->stream));
     if (e->timing) GS_HIP(hipEventRecord(t1, e->stream));
+    GS_HIP(hipEventRecord(e->ev_read[rs], e->stream));
     e->ev0 = t0;
     e->ev1 = t1;
     e->timed = e->timing;
@@ -400,8 +435,17 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
         GS_HIP(gs::launch_stats_fold(e->st32, e->st64, e->g.n, e->stream));
         e->since_fold = 0;
     }
-    GS_HIP(gs::launch_build_csr(e->tg, e->plan, e->csr_scratch, e->pairs, e->src, e->IN, e->SIB,
-                                e->flags, e->seed, e->epoch, e->round, e->stream));
+    {
+        // Lists of the new round t+1 into the other set, whose last reader
+        // was the round kernel before this one; runs beside this round's kernel.
+        const uint32_t ns = e->round & 1u;
+        auto &c = e->csr[ns];
+        GS_HIP(hipStreamWaitEvent(e->cstream, e->ev_read[ns], 0));
+        c.serial = ++e->build_serial;
+        GS_HIP(gs::launch_build_csr(c.tg, e->plan, c.scratch, c.pairs, c.src, c.IN, c.SIB, c.serial,
+                                    e->seed, e->epoch, e->round, e->cstream));
+        GS_HIP(hipEventRecord(e->ev_built[ns], e->cstream));
+    }
     if (report) {
         uint32_t fl[4];
         GS_HIP(hipMemcpyAsync(fl, e->flags, sizeof(fl), hipMemcpyDeviceToHost, e->stream));
@@ -538,6 +582,7 @@ gs_status gs_clear(gs_engine *e, uint32_t epoch) {
 gs_status gs_sync(gs_engine *e) {
     if (!e) return GS_ERR_INVALID_ARGUMENT;
     GS_HIP(hipStreamSynchronize(e->stream));
+    GS_HIP(hipStreamSynchronize(e->cstream));
     return GS_OK;
 }
 

@@ -8,8 +8,10 @@ struct RoundArgs {
     const u64 *Scur;          // state planes, round t (post phase 0)
     u64 *Snext;               // state planes, round t+1 (post phase 0)
     const uint4 *IN;          // round t, per node y: {first edge, in-degree, s0, s1}
-    const uint4 *SIB;         // round t, per source x: {t(x), rank in in(t(x)), e0, e1}
+    const uint4 *SIB;         // round t, per source x: {serial, rank in in(t(x)), e0, e1}
     const uint32_t *src;      // round t in-edge sources, ascending per target
+    const uint32_t *tg;       // round t targets
+    uint32_t serial;          // build serial of the round-t lists (SIB validity)
     uint32_t *st32;           // [n][4] u32 Statistics deltas (empty_pull, empty_push,
                               //   full_sent, full_received)
     const u64 *st64;          // [n][4] folded u64 totals (observation only)
@@ -17,7 +19,8 @@ struct RoundArgs {
     const u64 *inj_key;       // sorted segment keys with injections (round t+1)
     const u64 *inj_mask;      //   rumor masks in segment coordinates
     uint32_t n_inj;
-    uint32_t *flags;          // [0..1] any_live per round parity, [2] device limit
+    uint32_t *flags;          // [0..1] any_live per round parity (the kernel of round
+                              // t+1 clears round t's slot), [2] device limit
     // observation outputs (mode OBSERVE); any may be null
     u64 *obs_known;           // [n][KW]
     u64 *obs_stats;           // [n][5]
@@ -48,10 +51,11 @@ struct CsrPlan {
 CsrPlan csr_plan(uint32_t n);
 size_t csr_scratch_words(const CsrPlan &p);  // u32 words of scratch
 
-// Peer choices of `round` (into tg) and their in-edge lists (src, IN, SIB).
-// Also clears the any_live slot of the round after it.
+// Peer choices of `round` (into tg) and their in-edge lists (src, IN, SIB
+// tagged with `serial`).  Depends on nothing but the Philox stream, so it runs
+// on its own stream concurrently with the round kernel of the round before.
 hipError_t launch_build_csr(uint32_t *tg, const CsrPlan &p, uint32_t *scratch, u64 *pairs,
-                            uint32_t *src, uint4 *IN, uint4 *SIB, uint32_t *flags,
+                            uint32_t *src, uint4 *IN, uint4 *SIB, uint32_t serial,
                             uint64_t seed, uint32_t epoch, uint32_t round, hipStream_t s);
 hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, hipStream_t s);
 

@@ -233,9 +233,11 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
 
     // ---- coalesced per-node metadata and own round-t planes
     uint4 in = {0, 0, 0, 0}, sb = {0, 0, 0, 0};
+    uint32_t z = 0;
     if (DELIVER && valid) {
         in = a.IN[x];   // {first edge, k, s0, s1}
-        sb = a.SIB[x];  // {z = t_t(x), rank of x in in(z), e0, e1}
+        sb = a.SIB[x];  // {serial, rank of x in in(z), e0, e1}; stale unless rank >= 1
+        z = a.tg[x];    // t_t(x)
     }
     u64 P[kPlanes];
 #pragma unroll
@@ -245,12 +247,11 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     }
 
     // ---- the random gathers, all issued together
-    uint32_t k = 0, r = 0, z = 0;
+    uint32_t k = 0, r = 0;
     Cls q0 = {0, 0, 0}, q1 = {0, 0, 0}, qz = {0, 0, 0}, e0 = {0, 0, 0}, e1 = {0, 0, 0};
     if (DELIVER && valid) {
         k = in.y;
-        z = sb.x;
-        r = sb.y;
+        r = sb.x == a.serial ? sb.y : 0u;
 #ifdef GS_EXP_NO_PUSHERS
         k = 0;
 #endif
@@ -483,6 +484,9 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     uint32_t live_new = valid ? popc(Bn | Cn) : 0u;
     if (!SMALL) live_new = group_sum(live_new, g.W);
     const int blk_live = __syncthreads_or(live_new != 0u);
+    if (blockIdx.x == 0 && threadIdx.x == 0)  // slot of round t, read by the host already
+        __hip_atomic_store(&a.flags[(a.round_new + 1u) & 1u], 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 0 && blk_live) {
         uint32_t *f = &a.flags[a.round_new & 1u];
         if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
@@ -548,7 +552,8 @@ hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, hipStream_t 
 //                 node's sources ascending (the order Gossip::receive sees its
 //                 pushers in, src/gossiper.rs:217), then the per-node records
 //                 IN[y] = {first edge, in-degree, s0, s1}          (node order)
-//                 SIB[x] = {t(x), rank of x in in(t(x)), e0, e1}   (per source)
+//                 SIB[x] = {serial, rank of x in in(t(x)), e0, e1}  (per source,
+//                          written only when rank >= 1; stale serial = rank 0)
 constexpr uint32_t kScanBlock = 256;
 
 // Block-wide exclusive scan of one value per thread; returns the block total.
@@ -657,12 +662,10 @@ __global__ __launch_bounds__(256) void csr_bin_scatter(const uint32_t *__restric
 __global__ __launch_bounds__(256) void csr_bin_sort(const u64 *__restrict__ pairs, CsrPlan p,
                                                     const uint32_t *__restrict__ base,
                                                     const uint32_t *__restrict__ tot, uint32_t *src,
-                                                    uint4 *IN, uint4 *SIB, uint32_t *flags,
-                                                    uint32_t slot) {
+                                                    uint4 *IN, uint4 *SIB, uint32_t serial) {
     extern __shared__ __attribute__((aligned(16))) uint32_t h[];  // [bin] + 16 scan words
     uint32_t *lds_scan = h + p.bin;
     const uint32_t b = blockIdx.x;
-    if (b == 0 && threadIdx.x == 0) flags[slot] = 0u;  // any_live slot of the round after
     const uint32_t start = base[b], cnt = tot[b];
     const uint32_t nb0 = b << p.logbin;
     const uint32_t nodes = min(p.bin, p.n - nb0);
@@ -706,17 +709,17 @@ __global__ __launch_bounds__(256) void csr_bin_sort(const u64 *__restrict__ pair
         const uint32_t s0 = k > 0 ? src[a] : 0u, s1 = k > 1 ? src[a + 1] : 0u;
         const uint32_t y = nb0 + i;
         IN[y] = make_uint4(a, k, s0, s1);
-        for (uint32_t q = a; q < e; ++q) {
+        (void)y;
+        for (uint32_t q = a + 1; q < e; ++q) {
             const uint32_t rank = q - a;
-            SIB[src[q]] = make_uint4(y, rank, rank > 0 ? s0 : 0u, rank > 1 ? s1 : 0u);
+            SIB[src[q]] = make_uint4(serial, rank, s0, rank > 1 ? s1 : 0u);
         }
     }
 }
 
 hipError_t launch_build_csr(uint32_t *tg, const CsrPlan &p, uint32_t *scratch, u64 *pairs,
-                            uint32_t *src, uint4 *IN, uint4 *SIB, uint32_t *flags,
+                            uint32_t *src, uint4 *IN, uint4 *SIB, uint32_t serial,
                             uint64_t seed, uint32_t epoch, uint32_t round, hipStream_t s) {
-    const uint32_t next_round_slot = (round + 1u) & 1u;
     uint32_t *M = scratch;
     uint32_t *tot = M + (size_t)p.ba * p.nb;
     uint32_t *base = tot + p.nb;
@@ -732,7 +735,7 @@ hipError_t launch_build_csr(uint32_t *tg, const CsrPlan &p, uint32_t *scratch, u
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(csr_bin_sort, dim3(p.nb), dim3(256), lds_sort, s, pairs, p, base, tot, src, IN,
-                       SIB, flags, next_round_slot);
+                       SIB, serial);
     return hipGetLastError();
 }
 
