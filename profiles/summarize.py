@@ -1,0 +1,66 @@
+"""Summarise a rocprofv3 run of bench.py (profiles/rocprof_r1.sh) into profiles/<tag>/.
+
+Writes kernel_stats.csv (copied), summary.json and pmc_latest.json (traffic of
+the dominant kernel per launch).  HBM bytes = 2*FETCH_SIZE + WRITE_SIZE (KiB
+units): on gfx950 FETCH_SIZE reports half of a wide coalesced streaming read
+(MI355X_MICROARCH.md section HBM); WRITE_SIZE is exact for our stores (it
+equals the algorithmic write bytes of the round kernel to 0.1%).
+
+    python profiles/summarize.py gpurun_out/prof_r1c r1 --nodes 16777216 --rumors 256
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+import shutil
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+DOMINANT = "round_kernel<false, 1>"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("prof_dir")
+    ap.add_argument("tag")
+    ap.add_argument("--nodes", type=int, default=1 << 24)
+    ap.add_argument("--rumors", type=int, default=256)
+    a = ap.parse_args()
+    out = os.path.join(HERE, a.tag)
+    os.makedirs(out, exist_ok=True)
+    stats_csv = os.path.join(a.prof_dir, "trace", "run_kernel_stats.csv")
+    shutil.copy(stats_csv, os.path.join(out, "kernel_stats.csv"))
+    kernels = []
+    for x in csv.DictReader(open(stats_csv)):
+        kernels.append(dict(name=x["Name"], calls=int(x["Calls"]),
+                            avg_ms=float(x["AverageNs"]) / 1e6, pct=float(x["Percentage"])))
+    pmc = collections.defaultdict(dict)
+    for sub, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        path = os.path.join(a.prof_dir, sub, "run_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        vals = collections.defaultdict(list)
+        for x in csv.DictReader(open(path)):
+            vals[x["Kernel_Name"]].append(float(x["Counter_Value"]))
+        for k, v in vals.items():
+            pmc[k][counter + "_KiB_mean"] = sum(v) / len(v)
+    dom = next((k for k in pmc if DOMINANT in k), None)
+    summary = dict(kernels=kernels, pmc=pmc)
+    if dom and "FETCH_SIZE_KiB_mean" in pmc[dom] and "WRITE_SIZE_KiB_mean" in pmc[dom]:
+        f = pmc[dom]["FETCH_SIZE_KiB_mean"] * 1024
+        w = pmc[dom]["WRITE_SIZE_KiB_mean"] * 1024
+        dom_ms = next(k["avg_ms"] for k in kernels if DOMINANT in k["name"])
+        latest = dict(tag=a.tag, kernel=dom, nodes=a.nodes, rumors=a.rumors,
+                      fetch_bytes_raw=f, write_bytes=w, hbm_bytes_per_launch=2 * f + w,
+                      kernel_avg_ms_rocprof=dom_ms,
+                      hbm_gbs=(2 * f + w) / (dom_ms * 1e-3) / 1e9,
+                      note="hbm_bytes = 2*FETCH_SIZE + WRITE_SIZE per launch (gfx950 FETCH_SIZE "
+                           "under-reports wide streaming reads by 2x)")
+        summary["dominant"] = latest
+        json.dump(latest, open(os.path.join(HERE, "pmc_latest.json"), "w"), indent=1)
+    json.dump(summary, open(os.path.join(out, "summary.json"), "w"), indent=1)
+    print(json.dumps(summary.get("dominant", {}), indent=1))
+
+
+if __name__ == "__main__":
+    main()
