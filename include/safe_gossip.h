@@ -125,6 +125,31 @@ int32_t     gs_round_kernel_times(gs_engine *e, float *out_ms, uint32_t max);
 /* Algorithmic HBM bytes of one round kernel (DESIGN.md, section Roofline). */
 double      gs_round_kernel_bytes(const gs_engine *e);
 
+/* ---- Sharded network (multi-GPU): one engine per rank owns the node range
+ * [lo, lo+m).  Per round t the caller moves two sets of rows between ranks
+ * (DESIGN.md section 7): A = push rows (class planes of every node, sent to
+ * the owner of its target) and B = pull rows (returned in the reverse layout).
+ * Sequence per round, after gs_next_round has produced round t:
+ *   gs_shard_counts -> exchange A (sendA -> recvA) -> gs_shard_pull ->
+ *   exchange B (sendB -> recvB, counts swapped) -> gs_next_round (round t+1).
+ * Rows are u64 words: push row = info[3] words, pull row = info[4] words;
+ * row counts per peer rank come from gs_shard_counts.  gs_send_new takes global
+ * node ids owned by this rank; observers report the owned nodes only. */
+gs_status   gs_shard_create(const gs_config *cfg, uint32_t rank, uint32_t world, gs_engine **out);
+/* info = {lo, m, recv capacity (rows), push row words, pull row words, world,
+ *         rank, nodes per rank} */
+gs_status   gs_shard_info(const gs_engine *e, uint32_t info[8]);
+/* Device buffers (u64 words): sendA m*info[3], recvA cap*info[3],
+ * sendB cap*info[4], recvB m*info[4]. */
+gs_status   gs_shard_bind(gs_engine *e, void *sendA, void *recvA, void *sendB, void *recvB);
+/* Rows this rank sends to / receives from each rank in the exchanges of the
+ * current round (A; B is the reverse). */
+gs_status   gs_shard_counts(gs_engine *e, uint32_t *send_rows, uint32_t *recv_rows);
+/* Pull rows of the current round (after exchange A). */
+gs_status   gs_shard_pull(gs_engine *e);
+/* The engine's HIP stream (hipStream_t), to order collectives on it. */
+uint64_t    gs_stream(const gs_engine *e);
+
 /* Injected peer schedule: the peer node `node` chooses in `round`. */
 uint32_t    gs_peer(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node, uint32_t n);
 /* Origin for rumor `rumor` in the benchmark / harness schedules. */

@@ -1,0 +1,162 @@
+// gs_device.h -- device helpers shared by the round, CSR and shard kernels.
+#pragma once
+#include "gs_common.h"
+
+namespace gs {
+
+#define GS_DEV __device__ __forceinline__
+
+GS_DEV uint32_t popc(u64 v) { return (uint32_t)__popcll(v); }
+
+// c += in (bit-sliced 5-bit counters, one per rumor).
+GS_DEV void add5(u64 (&c)[5], u64 in) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        u64 t = c[i] & in;
+        c[i] ^= in;
+        in = t;
+    }
+}
+
+// Bit-sliced "x >= K" for an nb-bit number per rumor, K a per-lane constant.
+template <int NB>
+GS_DEV u64 ge_k(const u64 (&x)[NB], uint32_t K) {
+    if (K >= (1u << NB)) return 0ull;
+    u64 gt = 0ull, eq = ~0ull;
+#pragma unroll
+    for (int i = NB - 1; i >= 0; --i) {
+        u64 ki = ((K >> i) & 1u) ? ~0ull : 0ull;
+        gt |= eq & x[i] & ~ki;
+        eq &= ~(x[i] ^ ki);
+    }
+    return gt | eq;
+}
+
+// Same with K wave-uniform (max_rounds, max_c_rounds): scalar branches on the
+// bits of K, 2 ops per bit.
+template <int NB>
+GS_DEV u64 ge_u(const u64 (&x)[NB], uint32_t K) {
+    if (K >= (1u << NB)) return 0ull;
+    u64 gt = 0ull, eq = ~0ull;
+#pragma unroll
+    for (int i = NB - 1; i >= 0; --i) {
+        if ((K >> i) & 1u) {
+            eq &= x[i];
+        } else {
+            gt |= eq & x[i];
+        }
+    }
+    return gt | eq;
+}
+
+struct Cls {
+    u64 c, a0, a1;
+};
+
+template <bool SMALL>
+struct Lane {
+    // segment geometry
+    uint32_t x, j;
+    u64 base;       // index of plane 0 of this lane's word
+    uint32_t sh;    // bit offset of the segment in its word (small)
+    u64 m;          // segment mask (after shifting down)
+    uint32_t W, lognpu, logr;
+
+    GS_DEV void init(const Geometry &g, u64 seg) {
+        W = g.W;
+        lognpu = g.lognpu;
+        logr = g.logr;
+        if (SMALL) {
+            x = (uint32_t)seg;
+            j = 0;
+            base = (u64)(x >> lognpu) * kPlanes;
+            sh = (x & ((1u << lognpu) - 1u)) << logr;
+            m = (1ull << g.rpad) - 1ull;  // rpad < 64 here
+        } else {
+            x = (uint32_t)(seg / W);
+            j = (uint32_t)(seg % W);
+            base = (u64)x * kPlanes * W + j;
+            sh = 0;
+            m = ~0ull;
+        }
+    }
+    GS_DEV u64 plane_index(uint32_t p) const { return SMALL ? base + p : base + (u64)p * W; }
+    // Exchange rows (SHARD): row e holds `np` planes of W words, [e][np][W]; a
+    // node with R < 64 keeps its segment in the low bits of one word per plane.
+    GS_DEV u64 row_index(uint32_t e, uint32_t np, uint32_t p) const {
+        return ((u64)e * np + p) * W + j;
+    }
+    GS_DEV Cls load_row3(const u64 *__restrict__ rows, uint32_t e) const {
+        Cls r;
+        r.c = rows[row_index(e, 3, 0)];
+        r.a0 = rows[row_index(e, 3, 1)];
+        r.a1 = rows[row_index(e, 3, 2)];
+        return r;
+    }
+    // Class planes (isC, a0, a1) of node s for this lane's word.
+    GS_DEV Cls load_cls(const u64 *__restrict__ S, uint32_t s) const {
+        Cls r;
+        if (SMALL) {
+            u64 b = (u64)(s >> lognpu) * kPlanes;
+            uint32_t ss = (s & ((1u << lognpu) - 1u)) << logr;
+            r.c = (S[b] >> ss) & m;
+            r.a0 = (S[b + 1] >> ss) & m;
+            r.a1 = (S[b + 2] >> ss) & m;
+        } else {
+            u64 b = (u64)s * kPlanes * W + j;
+            r.c = S[b];
+            r.a0 = S[b + W];
+            r.a1 = S[b + 2 * (u64)W];
+        }
+        return r;
+    }
+};
+
+// Sum / min over the W lanes of one node (W a power of two <= 64, lanes of a
+// node are consecutive and W-aligned inside the wave).
+GS_DEV uint32_t group_sum(uint32_t v, uint32_t W) {
+    for (uint32_t o = 1; o < W; o <<= 1) v += __shfl_xor(v, (int)o, 64);
+    return v;
+}
+GS_DEV uint32_t group_min(uint32_t v, uint32_t W) {
+    for (uint32_t o = 1; o < W; o <<= 1) v = min(v, (uint32_t)__shfl_xor(v, (int)o, 64));
+    return v;
+}
+
+constexpr uint32_t kNone = 0xffffffffu;
+
+// First-carrier class of the entries z created from its pushers ahead of x
+// (the pull row is built before x's push is absorbed, src/gossip.rs:124-151).
+GS_DEV void sibling(const Cls &q, u64 &pnot, u64 &pB, u64 &pC) {
+    const u64 vC = q.c & ~(q.a0 & q.a1);
+    const u64 sl = (~q.c & (q.a0 | q.a1)) | vC;
+    const u64 nc = pnot & sl;
+    pB |= nc & ~vC;
+    pC |= nc & vC;
+    pnot &= ~sl;
+}
+
+constexpr uint32_t kScanBlock = 256;
+
+// Block-wide exclusive scan of one value per thread; returns the block total.
+GS_DEV uint32_t block_exclusive_scan(uint32_t v, uint32_t *lds, uint32_t &total) {
+    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(inc, (unsigned)o, 64);
+        if (lane >= (uint32_t)o) inc += t;
+    }
+    if (lane == 63) lds[wid] = inc;
+    __syncthreads();
+    uint32_t wbase = 0, tot = 0;
+    for (uint32_t w = 0; w < kScanBlock / 64; ++w) {
+        if (w < wid) wbase += lds[w];
+        tot += lds[w];
+    }
+    __syncthreads();
+    total = tot;
+    return wbase + inc - v;
+}
+
+}  // namespace gs

@@ -42,6 +42,16 @@ struct gs_engine {
     uint32_t build_serial = 0;
     uint32_t *flags = nullptr;
     gs::CsrPlan plan{};
+    // Shard engine (gs_shard_create): this rank's node range of a network
+    // sharded over `world` ranks; plans of rounds r live in set r % 3.
+    bool shard = false;
+    uint32_t n_global = 0;
+    gs::ShardPlan sp{};
+    gs::ShardPlanLayout spl{};
+    uint32_t *planw[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev_plan[3] = {nullptr, nullptr, nullptr};  // plan of set i built
+    hipEvent_t ev_kr[3] = {nullptr, nullptr, nullptr};    // round kernel r (set r%3) done
+    u64 *sendA = nullptr, *recvA = nullptr, *sendB = nullptr, *recvB = nullptr;
     uint32_t *st32 = nullptr;  // [n][4] u32 deltas
     u64 *st64 = nullptr;       // [n][4] folded totals
     uint32_t fold_every = 1, since_fold = 0;
@@ -108,6 +118,11 @@ void release(gs_engine *e) {
         if (e->ev_built[i]) (void)hipEventDestroy(e->ev_built[i]);
         if (e->ev_read[i]) (void)hipEventDestroy(e->ev_read[i]);
     }
+    for (int i = 0; i < 3; ++i) {
+        if (e->planw[i]) (void)hipFree(e->planw[i]);
+        if (e->ev_plan[i]) (void)hipEventDestroy(e->ev_plan[i]);
+        if (e->ev_kr[i]) (void)hipEventDestroy(e->ev_kr[i]);
+    }
     if (e->cstream) (void)hipStreamDestroy(e->cstream);
     void *bufs[] = {e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
                     e->partials, e->obs_state, e->obs_rec, e->obs_psize};
@@ -143,12 +158,23 @@ gs::RoundArgs base_args(gs_engine *e) {
     gs::RoundArgs a{};
     a.Scur = e->S[e->cur];
     a.Snext = e->S[e->cur ^ 1];
-    const auto &cs = e->csr[e->round & 1u];  // round-t lists (t = e->round)
-    a.IN = cs.IN;
-    a.SIB = cs.SIB;
-    a.src = cs.src;
-    a.tg = cs.tg;
-    a.serial = cs.serial;
+    if (e->shard) {
+        uint32_t *cur = e->planw[e->round % 3], *nxt = e->planw[(e->round + 1) % 3];
+        a.IN = reinterpret_cast<const uint4 *>(cur + e->spl.IN);
+        a.src = cur + e->spl.EP;
+        a.spos_cur = cur + e->spl.SPOS;
+        a.spos_next = nxt + e->spl.SPOS;
+        a.recvA = e->recvA;
+        a.recvB = e->recvB;
+        a.sendA = e->sendA;
+    } else {
+        const auto &cs = e->csr[e->round & 1u];  // round-t lists (t = e->round)
+        a.IN = cs.IN;
+        a.SIB = cs.SIB;
+        a.src = cs.src;
+        a.tg = cs.tg;
+        a.serial = cs.serial;
+    }
     a.st32 = e->st32;
     a.st64 = e->st64;
     a.obs_rounds = e->round;
@@ -236,7 +262,10 @@ gs_status observe(gs_engine *e, bool dumps) {
         a.obs_state = e->obs_state;
         a.obs_rec = e->obs_rec;
     }
-    if (e->deliver_pending) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
+    if (e->deliver_pending) {
+        if (e->shard) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[e->round % 3], 0));
+        else GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
+    }
     GS_HIP(gs::launch_round(a, e->deliver_pending ? 2 : 3, e->stream));
     uint32_t fl = 0;
     GS_HIP(hipMemcpyAsync(&fl, e->flags + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
@@ -297,20 +326,33 @@ uint32_t gs_coin(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node) {
     return gs::coin_of(seed, epoch, round, node);
 }
 
-gs_status gs_create(const gs_config *cfg, gs_engine **out) {
+}  // extern "C"
+
+namespace {
+
+// Common constructor: a whole network (world == 0) or the node range of rank
+// `rank` of a network sharded over `world` ranks.
+gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_engine **out) {
     if (!cfg || !out) return GS_ERR_INVALID_ARGUMENT;
     *out = nullptr;
-    const uint32_t n = cfg->n_nodes, R = cfg->n_rumors;
-    if (n == 0 || n == 0xffffffffu || R == 0 || R > 4096) return GS_ERR_INVALID_ARGUMENT;
+    const uint32_t nglob = cfg->n_nodes, R = cfg->n_rumors;
+    if (nglob == 0 || nglob == 0xffffffffu || R == 0 || R > 4096) return GS_ERR_INVALID_ARGUMENT;
+    if (world && (rank >= world || world > 64)) return GS_ERR_INVALID_ARGUMENT;
+    gs::ShardPlan sp{};
+    if (world) sp = gs::shard_plan(nglob, world, rank);
+    const uint32_t n = world ? sp.m : nglob;  // nodes owned by this engine
     uint8_t p[3];
-    gs_derive_params(n, p);
+    gs_derive_params(nglob, p);
     if (cfg->counter_max) p[0] = cfg->counter_max;
     if (cfg->max_c_rounds) p[1] = cfg->max_c_rounds;
     if (cfg->max_rounds) p[2] = cfg->max_rounds;
-    if (n >= 2 && (p[0] > 3 || p[1] > 3 || p[2] > 32 || !p[0] || !p[1] || !p[2]))
+    if (nglob >= 2 && (p[0] > 3 || p[1] > 3 || p[2] > 32 || !p[0] || !p[1] || !p[2]))
         return GS_ERR_UNSUPPORTED;
 
     gs_engine *e = new gs_engine();
+    e->shard = world != 0;
+    e->n_global = nglob;
+    e->sp = sp;
     e->seed = cfg->seed;
     e->epoch = cfg->epoch;
     e->cmax = p[0];
@@ -353,7 +395,13 @@ gs_status gs_create(const gs_config *cfg, gs_engine **out) {
     bool ok = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&e->cstream, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreate(&e->ev0) == hipSuccess && hipEventCreate(&e->ev1) == hipSuccess;
-    for (int i = 0; i < 2 && ok; ++i) {
+    for (int i = 0; i < 3 && ok && e->shard; ++i) {
+        const size_t words = gs::shard_plan_words(e->sp, &e->spl);
+        ok = hipEventCreateWithFlags(&e->ev_plan[i], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&e->ev_kr[i], hipEventDisableTiming) == hipSuccess &&
+             dalloc(&e->planw[i], words) == hipSuccess;
+    }
+    for (int i = 0; i < 2 && ok && !e->shard; ++i) {
         auto &c = e->csr[i];
         ok = hipEventCreateWithFlags(&e->ev_built[i], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&e->ev_read[i], hipEventDisableTiming) == hipSuccess &&
@@ -379,6 +427,81 @@ gs_status gs_create(const gs_config *cfg, gs_engine **out) {
     return GS_OK;
 }
 
+gs_status launch_plan(gs_engine *e, uint32_t r) {
+    GS_HIP(gs::launch_shard_plan(e->sp, e->spl, e->planw[r % 3], e->seed, e->epoch, r, e->cstream));
+    GS_HIP(hipEventRecord(e->ev_plan[r % 3], e->cstream));
+    return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+gs_status gs_create(const gs_config *cfg, gs_engine **out) { return create_engine(cfg, 0, 0, out); }
+
+gs_status gs_shard_create(const gs_config *cfg, uint32_t rank, uint32_t world, gs_engine **out) {
+    if (world == 0) return GS_ERR_INVALID_ARGUMENT;
+    return create_engine(cfg, rank, world, out);
+}
+
+gs_status gs_shard_info(const gs_engine *e, uint32_t info[8]) {
+    if (!e || !info || !e->shard) return GS_ERR_INVALID_ARGUMENT;
+    info[0] = e->sp.lo;
+    info[1] = e->sp.m;
+    info[2] = e->sp.cap_in;
+    info[3] = 3 * e->g.W;  // u64 words per push row
+    info[4] = 2 * e->g.W;  // u64 words per pull row
+    info[5] = e->sp.G;
+    info[6] = e->sp.g;
+    info[7] = e->sp.chunk;
+    return GS_OK;
+}
+
+gs_status gs_shard_bind(gs_engine *e, void *sendA, void *recvA, void *sendB, void *recvB) {
+    if (!e || !e->shard || !sendA || !recvA || !sendB || !recvB) return GS_ERR_INVALID_ARGUMENT;
+    e->sendA = (u64 *)sendA;
+    e->recvA = (u64 *)recvA;
+    e->sendB = (u64 *)sendB;
+    e->recvB = (u64 *)recvB;
+    return GS_OK;
+}
+
+gs_status gs_shard_counts(gs_engine *e, uint32_t *send_rows, uint32_t *recv_rows) {
+    if (!e || !e->shard || e->round == 0 || !send_rows || !recv_rows) return GS_ERR_INVALID_ARGUMENT;
+    gs_status st = set_device(e);
+    if (st != GS_OK) return st;
+    GS_HIP(hipEventSynchronize(e->ev_plan[e->round % 3]));
+    const uint32_t G = e->sp.G;
+    std::vector<uint32_t> c(2 + 2 * (size_t)G);
+    GS_HIP(hipMemcpy(c.data(), e->planw[e->round % 3] + e->spl.cnt, c.size() * sizeof(uint32_t),
+                     hipMemcpyDeviceToHost));
+    if (c[1]) return GS_ERR_DEVICE_LIMIT;  // more sources than receive rows
+    for (uint32_t i = 0; i < G; ++i) {
+        send_rows[i] = c[2 + i];
+        recv_rows[i] = c[2 + G + i];
+    }
+    return GS_OK;
+}
+
+gs_status gs_shard_pull(gs_engine *e) {
+    if (!e || !e->shard || e->round == 0 || !e->recvA) return GS_ERR_INVALID_ARGUMENT;
+    gs_status st = set_device(e);
+    if (st != GS_OK) return st;
+    uint32_t *pw = e->planw[e->round % 3];
+    GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[e->round % 3], 0));
+    gs::PullArgs a{};
+    a.S = e->S[e->cur];
+    a.IN = reinterpret_cast<const uint4 *>(pw + e->spl.IN);
+    a.EP = pw + e->spl.EP;
+    a.recvA = e->recvA;
+    a.sendB = e->sendB;
+    a.g = e->g;
+    GS_HIP(gs::launch_pull(a, e->stream));
+    return GS_OK;
+}
+
+uint64_t gs_stream(const gs_engine *e) { return e ? (uint64_t)(uintptr_t)e->stream : 0; }
+
 void gs_destroy(gs_engine *e) { release(e); }
 
 gs_status gs_get_params(const gs_engine *e, uint8_t out[3]) {
@@ -393,7 +516,11 @@ uint32_t gs_round(const gs_engine *e) { return e ? e->round : 0; }
 
 gs_status gs_send_new(gs_engine *e, uint32_t node, uint32_t rumor) {
     if (!e) return GS_ERR_INVALID_ARGUMENT;
-    if (e->g.n < 2) return GS_ERR_NO_PEERS;  // Gossiper::send_new, src/gossiper.rs:56-58
+    if ((e->shard ? e->n_global : e->g.n) < 2) return GS_ERR_NO_PEERS;  // src/gossiper.rs:56-58
+    if (e->shard) {  // global node id; must be owned by this rank
+        if (node < e->sp.lo || node - e->sp.lo >= e->sp.m) return GS_ERR_INVALID_ARGUMENT;
+        node -= e->sp.lo;
+    }
     if (node >= e->g.n || rumor >= e->g.R) return GS_ERR_INVALID_ARGUMENT;
     e->pending.emplace_back(node, rumor);
     e->obs_valid = false;
@@ -402,9 +529,14 @@ gs_status gs_send_new(gs_engine *e, uint32_t node, uint32_t rumor) {
 
 gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
     if (!e) return GS_ERR_INVALID_ARGUMENT;
-    if (e->g.n < 2) return GS_ERR_NO_PEERS;  // Gossiper::next_round, src/gossiper.rs:71-74
+    if ((e->shard ? e->n_global : e->g.n) < 2) return GS_ERR_NO_PEERS;  // src/gossiper.rs:71-74
+    if (e->shard && !e->sendA) return GS_ERR_INVALID_ARGUMENT;  // gs_shard_bind first
     gs_status st = set_device(e);
     if (st != GS_OK) return st;
+    if (e->shard && e->round == 0) {
+        st = launch_plan(e, 1);  // send rows of round 1's push rows
+        if (st != GS_OK) return st;
+    }
     uint32_t n_inj = 0;
     st = upload_injections(e, &n_inj);
     if (st != GS_OK) return st;
@@ -418,12 +550,19 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
         t1 = e->tev[2 * e->tcount + 1];
         e->tcount++;
     }
-    const uint32_t rs = e->round & 1u;  // set holding round t = e->round
-    if (e->deliver_pending) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[rs], 0));
+    const uint32_t R0 = e->round;
+    const uint32_t rs = R0 & 1u;  // set holding round t = e->round
+    if (e->shard) {
+        GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[(R0 + 1) % 3], 0));
+        if (e->deliver_pending) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[R0 % 3], 0));
+    } else if (e->deliver_pending) {
+        GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[rs], 0));
+    }
     if (e->timing) GS_HIP(hipEventRecord(t0, e->stream));
     GS_HIP(gs::launch_round(a, e->deliver_pending ? 1 : 0, e->stream));
     if (e->timing) GS_HIP(hipEventRecord(t1, e->stream));
-    GS_HIP(hipEventRecord(e->ev_read[rs], e->stream));
+    if (e->shard) GS_HIP(hipEventRecord(e->ev_kr[(R0 + 1) % 3], e->stream));
+    else GS_HIP(hipEventRecord(e->ev_read[rs], e->stream));
     e->ev0 = t0;
     e->ev1 = t1;
     e->timed = e->timing;
@@ -435,7 +574,13 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
         GS_HIP(gs::launch_stats_fold(e->st32, e->st64, e->g.n, e->stream));
         e->since_fold = 0;
     }
-    {
+    if (e->shard) {
+        // Plan of round t+2 into set (t+2)%3, last read by the round kernel
+        // of round t (and the pull kernel before it).
+        GS_HIP(hipStreamWaitEvent(e->cstream, e->ev_kr[R0 % 3], 0));
+        st = launch_plan(e, R0 + 2);
+        if (st != GS_OK) return st;
+    } else {
         // Lists of the new round t+1 into the other set, whose last reader
         // was the round kernel before this one; runs beside this round's kernel.
         const uint32_t ns = e->round & 1u;

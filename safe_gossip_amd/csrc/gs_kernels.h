@@ -27,6 +27,12 @@ struct RoundArgs {
     uint16_t *obs_state;      // [n][R]
     uint16_t *obs_rec;        // [n][R]
     uint32_t *obs_psize;      // [n]
+    // shard engine only (null otherwise): exchange rows, see gs_shard.hip
+    const u64 *recvA;         // round-t push rows of this shard's pushers [e][3][W]
+    const u64 *recvB;         // round-t pull rows for this shard's nodes [pos][2][W]
+    u64 *sendA;               // round-(t+1) push rows of this shard's nodes [pos][3][W]
+    const uint32_t *spos_cur; // row of x in recvB (= its round-t push row position)
+    const uint32_t *spos_next;// row of x in sendA for round t+1
     Geometry g;
     uint64_t seed;
     uint32_t epoch;
@@ -58,6 +64,39 @@ hipError_t launch_build_csr(uint32_t *tg, const CsrPlan &p, uint32_t *scratch, u
                             uint32_t *src, uint4 *IN, uint4 *SIB, uint32_t serial,
                             uint64_t seed, uint32_t epoch, uint32_t round, hipStream_t s);
 hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, hipStream_t s);
+
+// ---------------------------------------------------------------- shards
+// One rank's slice of a network sharded over G ranks (gs_shard.hip).
+struct ShardPlan {
+    uint32_t n;         // global nodes
+    uint32_t G, g;      // ranks, this rank
+    uint32_t chunk;     // nodes per rank (multiple of 256)
+    uint32_t lo, m;     // owned range [lo, lo+m)
+    uint32_t nblk;      // 256-source plan blocks over all n
+    uint32_t blk_lo;    // first owned plan block
+    uint32_t nblk_own;  // owned plan blocks
+    uint32_t cap_in;    // capacity of the receive rows (sources targeting g)
+    CsrPlan edges;      // counting sort of the received edges over the m targets
+};
+// u32-word offsets of one plan's buffers inside a single allocation.
+struct ShardPlanLayout {
+    size_t tg_all, bc_me, bc_d, cnt, E_id, E_key, SPOS, M, tot, base, EP, IN, pairs;
+};
+ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g);
+size_t shard_plan_words(const ShardPlan &P, ShardPlanLayout *L);
+// Plan of `round`: cnt = {m_in, overflow, scnt[G], rcnt[G]}, SPOS, IN, EP.
+hipError_t launch_shard_plan(const ShardPlan &P, const ShardPlanLayout &L, uint32_t *words,
+                             uint64_t seed, uint32_t epoch, uint32_t round, hipStream_t s);
+
+struct PullArgs {
+    const u64 *S;          // round-t planes of the owned nodes
+    const uint4 *IN;       // round-t in-lists of receive rows
+    const uint32_t *EP;
+    const u64 *recvA;      // round-t push rows received [e][3][W]
+    u64 *sendB;            // pull rows out [e][2][W]
+    Geometry g;            // local geometry (n = m)
+};
+hipError_t launch_pull(const PullArgs &a, hipStream_t s);
 
 // Reductions for observers.
 hipError_t launch_known_reduce(const u64 *known, uint32_t n, uint32_t KW, uint32_t R,

@@ -24,117 +24,10 @@
 // gathers of the pushers, of t(x) and of t(x)'s earlier pushers, and they are
 // all issued together, one dependent level after the coalesced reads.
 #include "gs_kernels.h"
+#include "gs_device.h"
 
 namespace gs {
 
-#define GS_DEV __device__ __forceinline__
-
-GS_DEV uint32_t popc(u64 v) { return (uint32_t)__popcll(v); }
-
-// c += in (bit-sliced 5-bit counters, one per rumor).
-GS_DEV void add5(u64 (&c)[5], u64 in) {
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        u64 t = c[i] & in;
-        c[i] ^= in;
-        in = t;
-    }
-}
-
-// Bit-sliced "x >= K" for an nb-bit number per rumor, K a per-lane constant.
-template <int NB>
-GS_DEV u64 ge_k(const u64 (&x)[NB], uint32_t K) {
-    if (K >= (1u << NB)) return 0ull;
-    u64 gt = 0ull, eq = ~0ull;
-#pragma unroll
-    for (int i = NB - 1; i >= 0; --i) {
-        u64 ki = ((K >> i) & 1u) ? ~0ull : 0ull;
-        gt |= eq & x[i] & ~ki;
-        eq &= ~(x[i] ^ ki);
-    }
-    return gt | eq;
-}
-
-// Same with K wave-uniform (max_rounds, max_c_rounds): scalar branches on the
-// bits of K, 2 ops per bit.
-template <int NB>
-GS_DEV u64 ge_u(const u64 (&x)[NB], uint32_t K) {
-    if (K >= (1u << NB)) return 0ull;
-    u64 gt = 0ull, eq = ~0ull;
-#pragma unroll
-    for (int i = NB - 1; i >= 0; --i) {
-        if ((K >> i) & 1u) {
-            eq &= x[i];
-        } else {
-            gt |= eq & x[i];
-        }
-    }
-    return gt | eq;
-}
-
-struct Cls {
-    u64 c, a0, a1;
-};
-
-template <bool SMALL>
-struct Lane {
-    // segment geometry
-    uint32_t x, j;
-    u64 base;       // index of plane 0 of this lane's word
-    uint32_t sh;    // bit offset of the segment in its word (small)
-    u64 m;          // segment mask (after shifting down)
-    uint32_t W, lognpu, logr;
-
-    GS_DEV void init(const Geometry &g, u64 seg) {
-        W = g.W;
-        lognpu = g.lognpu;
-        logr = g.logr;
-        if (SMALL) {
-            x = (uint32_t)seg;
-            j = 0;
-            base = (u64)(x >> lognpu) * kPlanes;
-            sh = (x & ((1u << lognpu) - 1u)) << logr;
-            m = (1ull << g.rpad) - 1ull;  // rpad < 64 here
-        } else {
-            x = (uint32_t)(seg / W);
-            j = (uint32_t)(seg % W);
-            base = (u64)x * kPlanes * W + j;
-            sh = 0;
-            m = ~0ull;
-        }
-    }
-    GS_DEV u64 plane_index(uint32_t p) const { return SMALL ? base + p : base + (u64)p * W; }
-    // Class planes (isC, a0, a1) of node s for this lane's word.
-    GS_DEV Cls load_cls(const u64 *__restrict__ S, uint32_t s) const {
-        Cls r;
-        if (SMALL) {
-            u64 b = (u64)(s >> lognpu) * kPlanes;
-            uint32_t ss = (s & ((1u << lognpu) - 1u)) << logr;
-            r.c = (S[b] >> ss) & m;
-            r.a0 = (S[b + 1] >> ss) & m;
-            r.a1 = (S[b + 2] >> ss) & m;
-        } else {
-            u64 b = (u64)s * kPlanes * W + j;
-            r.c = S[b];
-            r.a0 = S[b + W];
-            r.a1 = S[b + 2 * (u64)W];
-        }
-        return r;
-    }
-};
-
-// Sum / min over the W lanes of one node (W a power of two <= 64, lanes of a
-// node are consecutive and W-aligned inside the wave).
-GS_DEV uint32_t group_sum(uint32_t v, uint32_t W) {
-    for (uint32_t o = 1; o < W; o <<= 1) v += __shfl_xor(v, (int)o, 64);
-    return v;
-}
-GS_DEV uint32_t group_min(uint32_t v, uint32_t W) {
-    for (uint32_t o = 1; o < W; o <<= 1) v = min(v, (uint32_t)__shfl_xor(v, (int)o, 64));
-    return v;
-}
-
-constexpr uint32_t kNone = 0xffffffffu;
 
 // Receiver-side state of phases 1-2 at x for one segment.  The transition
 // path keeps one bit-sliced counter of the recorded counters that vote ">= own"
@@ -202,24 +95,16 @@ struct Recv {
     }
 };
 
-// First-carrier class of the entries z created from its pushers ahead of x
-// (the pull row is built before x's push is absorbed, src/gossip.rs:124-151).
-GS_DEV void sibling(const Cls &q, u64 &pnot, u64 &pB, u64 &pC) {
-    const u64 vC = q.c & ~(q.a0 & q.a1);
-    const u64 sl = (~q.c & (q.a0 | q.a1)) | vC;
-    const u64 nc = pnot & sl;
-    pB |= nc & ~vC;
-    pC |= nc & vC;
-    pnot &= ~sl;
-}
-
 #ifndef GS_RK_MINW
 #define GS_RK_MINW 1
 #endif
 
 // MODE: 0 transition only (first round), 1 deliver round t + transition to
 // t+1, 2 deliver round t + observe, 3 observe only.
-template <bool SMALL, int MODE>
+// SHARD: this engine owns a node range of a sharded network; pusher class rows
+// and the pull row come from the exchange buffers (recvA, recvB) instead of
+// gathers, and the new class planes are also written as push rows (sendA).
+template <bool SMALL, int MODE, bool SHARD>
 __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     constexpr bool DELIVER = (MODE == 1 || MODE == 2);
     constexpr bool TRANSITION = (MODE == 0 || MODE == 1);
@@ -233,11 +118,16 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
 
     // ---- coalesced per-node metadata and own round-t planes
     uint4 in = {0, 0, 0, 0}, sb = {0, 0, 0, 0};
-    uint32_t z = 0;
+    uint32_t z = 0, zi = 0xFFFFu;
     if (DELIVER && valid) {
-        in = a.IN[x];   // {first edge, k, s0, s1}
-        sb = a.SIB[x];  // {serial, rank of x in in(z), e0, e1}; stale unless rank >= 1
-        z = a.tg[x];    // t_t(x)
+        in = a.IN[x];   // {first edge, k, s0, s1}  (SHARD: {first, k|zi<<16, e0, e1})
+        if (SHARD) {
+            zi = in.y >> 16;
+            in.y &= 0xFFFFu;
+        } else {
+            sb = a.SIB[x];  // {serial, rank of x in in(z), e0, e1}; stale unless rank >= 1
+            z = a.tg[x];    // t_t(x)
+        }
     }
     u64 P[kPlanes];
 #pragma unroll
@@ -258,11 +148,20 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
 #ifdef GS_EXP_NO_ZPUSHERS
         r = 0;
 #endif
-        if (k > 0) q0 = L.load_cls(S, in.z);
-        if (k > 1) q1 = L.load_cls(S, in.w);
-        qz = L.load_cls(S, z);
-        if (r > 0) e0 = L.load_cls(S, sb.z);
-        if (r > 1) e1 = L.load_cls(S, sb.w);
+        if (SHARD) {
+            if (k > 0) q0 = L.load_row3(a.recvA, in.z);
+            if (k > 1) q1 = L.load_row3(a.recvA, in.w);
+            const uint32_t sp = a.spos_cur[x];  // the pull row z returned to x
+            qz.c = a.recvB[L.row_index(sp, 2, 0)];
+            qz.a0 = a.recvB[L.row_index(sp, 2, 1)];
+            qz.a1 = 0;
+        } else {
+            if (k > 0) q0 = L.load_cls(S, in.z);
+            if (k > 1) q1 = L.load_cls(S, in.w);
+            qz = L.load_cls(S, z);
+            if (r > 0) e0 = L.load_cls(S, sb.z);
+            if (r > 1) e1 = L.load_cls(S, sb.w);
+        }
     }
 
     const u64 isC = P[0], a0 = P[1], a1 = P[2];
@@ -279,33 +178,46 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     if (DELIVER && valid) {
         if (k > 30u) atomicOr(&a.flags[2], 1u);
         bool zin = false;
-        if (k > 0) {
-            zin |= in.z == z;
-            rv.push(q0, 0, k, in.z != z);
+        u64 pv2, pvB, pCl;
+        if (SHARD) {
+            // zi = index of t(x) among x's pushers (0xFFFF: t(x) did not push to x)
+            zin = zi != 0xFFFFu;
+            if (k > 0) rv.push(q0, 0, k, zi != 0);
+            if (k > 1) rv.push(q1, 1, k, zi != 1);
+            for (uint32_t i = 2; i < k; ++i) rv.push(L.load_row3(a.recvA, a.src[in.x + i]), i, k, zi != i);
+            // pull row code (b0, b1): 01 counter 1, 10 counter 2, 11 counter 255
+            pv2 = qz.a0 & ~qz.c;
+            pvB = qz.c ^ qz.a0;
+            pCl = qz.c & qz.a0;
+        } else {
+            if (k > 0) {
+                zin |= in.z == z;
+                rv.push(q0, 0, k, in.z != z);
+            }
+            if (k > 1) {
+                zin |= in.w == z;
+                rv.push(q1, 1, k, in.w != z);
+            }
+            for (uint32_t i = 2; i < k; ++i) {  // in-degree >= 3 (8% of nodes)
+                const uint32_t s = a.src[in.x + i];
+                zin |= s == z;
+                rv.push(L.load_cls(S, s), i, k, s != z);
+            }
+            // Pull batch from z: z's live set plus what z created from pushers
+            // ahead of x.
+            const u64 zB = ~qz.c & (qz.a0 | qz.a1);
+            const u64 zC = qz.c & ~(qz.a0 & qz.a1);
+            u64 pnot = ~qz.c & ~qz.a0 & ~qz.a1 & L.m, pB = 0, pC = 0;
+            if (r > 0) sibling(e0, pnot, pB, pC);
+            if (r > 1) sibling(e1, pnot, pB, pC);
+            if (r > 2 && pnot) {
+                const uint32_t zb = a.IN[z].x;  // rare: rank >= 3
+                for (uint32_t i = 2; i < r && pnot; ++i) sibling(L.load_cls(S, a.src[zb + i]), pnot, pB, pC);
+            }
+            pv2 = zB & qz.a1 & ~qz.a0;
+            pvB = zB | pB;  // counter 1 (created entries: 1) or 2
+            pCl = zC | pC;
         }
-        if (k > 1) {
-            zin |= in.w == z;
-            rv.push(q1, 1, k, in.w != z);
-        }
-        for (uint32_t i = 2; i < k; ++i) {  // in-degree >= 3 (8% of nodes)
-            const uint32_t s = a.src[in.x + i];
-            zin |= s == z;
-            rv.push(L.load_cls(S, s), i, k, s != z);
-        }
-        // Pull batch from z: z's live set plus what z created from pushers
-        // ahead of x.
-        const u64 zB = ~qz.c & (qz.a0 | qz.a1);
-        const u64 zC = qz.c & ~(qz.a0 & qz.a1);
-        u64 pnot = ~qz.c & ~qz.a0 & ~qz.a1 & L.m, pB = 0, pC = 0;
-        if (r > 0) sibling(e0, pnot, pB, pC);
-        if (r > 1) sibling(e1, pnot, pB, pC);
-        if (r > 2 && pnot) {
-            const uint32_t zb = a.IN[z].x;  // rare: rank >= 3
-            for (uint32_t i = 2; i < r && pnot; ++i) sibling(L.load_cls(S, a.src[zb + i]), pnot, pB, pC);
-        }
-        const u64 pv2 = zB & qz.a1 & ~qz.a0;
-        const u64 pvB = zB | pB;  // counter 1 (created entries: 1) or 2
-        const u64 pCl = zC | pC;
         const u64 pl = pvB | pCl;
         {
             const u64 newc = rv.notyet & pl;
@@ -479,6 +391,11 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             for (int p = 0; p < kPlanes; ++p) a.Snext[L.plane_index(p)] = N[p];
         }
     }
+    if (SHARD && valid) {  // push row of round t+1: the class planes, to owner(t_{t+1}(x))
+        const uint32_t sp = a.spos_next[x];
+#pragma unroll
+        for (int p = 0; p < kClsPlanes; ++p) a.sendA[L.row_index(sp, 3, p)] = N[p] & L.m;
+    }
 
     // ---- push list + Statistics (src/gossip.rs:80,103-111)
     uint32_t live_new = valid ? popc(Bn | Cn) : 0u;
@@ -507,21 +424,24 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     }
 }
 
-template <bool SMALL>
+template <bool SMALL, bool SHARD>
 static hipError_t launch_mode(const RoundArgs &a, int mode, hipStream_t s) {
     const uint32_t block = 256;
     const u64 grid = (a.g.nseg + block - 1) / block;
+    if (grid == 0) return hipSuccess;
     switch (mode) {
-    case 0: hipLaunchKernelGGL((round_kernel<SMALL, 0>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
-    case 1: hipLaunchKernelGGL((round_kernel<SMALL, 1>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((round_kernel<SMALL, 2>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
-    default: hipLaunchKernelGGL((round_kernel<SMALL, 3>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
+    case 0: hipLaunchKernelGGL((round_kernel<SMALL, 0, SHARD>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((round_kernel<SMALL, 1, SHARD>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((round_kernel<SMALL, 2, SHARD>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
+    default: hipLaunchKernelGGL((round_kernel<SMALL, 3, SHARD>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
     }
     return hipGetLastError();
 }
 
 hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s) {
-    return a.g.small ? launch_mode<true>(a, mode, s) : launch_mode<false>(a, mode, s);
+    if (a.recvA)  // shard engine
+        return a.g.small ? launch_mode<true, true>(a, mode, s) : launch_mode<false, true>(a, mode, s);
+    return a.g.small ? launch_mode<true, false>(a, mode, s) : launch_mode<false, false>(a, mode, s);
 }
 
 // Fold the u32 statistics deltas into the u64 totals (before they can wrap).
@@ -534,6 +454,7 @@ __global__ __launch_bounds__(256) void stats_fold(uint32_t *st32, u64 *st64, u64
 
 hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, hipStream_t s) {
     const u64 words = (u64)n * 4;
+    if (words == 0) return hipSuccess;
     hipLaunchKernelGGL(stats_fold, dim3((uint32_t)((words + 255) / 256)), dim3(256), 0, s, st32, st64,
                        words);
     return hipGetLastError();
@@ -554,29 +475,6 @@ hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, hipStream_t 
 //                 IN[y] = {first edge, in-degree, s0, s1}          (node order)
 //                 SIB[x] = {serial, rank of x in in(t(x)), e0, e1}  (per source,
 //                          written only when rank >= 1; stale serial = rank 0)
-constexpr uint32_t kScanBlock = 256;
-
-// Block-wide exclusive scan of one value per thread; returns the block total.
-GS_DEV uint32_t block_exclusive_scan(uint32_t v, uint32_t *lds, uint32_t &total) {
-    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-    uint32_t inc = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t t = __shfl_up(inc, (unsigned)o, 64);
-        if (lane >= (uint32_t)o) inc += t;
-    }
-    if (lane == 63) lds[wid] = inc;
-    __syncthreads();
-    uint32_t wbase = 0, tot = 0;
-    for (uint32_t w = 0; w < kScanBlock / 64; ++w) {
-        if (w < wid) wbase += lds[w];
-        tot += lds[w];
-    }
-    __syncthreads();
-    total = tot;
-    return wbase + inc - v;
-}
-
 CsrPlan csr_plan(uint32_t n) {
     CsrPlan p{};
     p.n = n;

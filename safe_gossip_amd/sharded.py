@@ -1,0 +1,319 @@
+"""Sharded network: the node-id space split across ranks.
+
+Each rank's engine (``gs_shard_create``) owns a contiguous node range.  Every
+round moves two sets of rows between ranks:
+
+* A -- push rows: the class planes of each node go to the owner of its target;
+* B -- pull rows: the owner of each target returns, per pusher, the pull batch
+  ``Gossip::receive`` built (``src/gossip.rs:124-151``), in the reverse layout.
+
+Transports:
+
+* ``"dist"``  -- one shard per process, ``torch.distributed.all_to_all_single``
+  on the engine's own HIP stream (backend ``nccl`` = RCCL over xGMI).  With the
+  ``gloo`` backend the rows are staged through host memory.
+* ``"local"`` -- all ``world`` shards in this process on one device, exchanged
+  by device copies (used to test the sharded algorithm on a single GPU).
+
+PyTorch is plumbing here (device buffers, streams, collectives); all protocol
+work runs in the engine's gfx950 kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional
+
+import numpy as np
+
+from . import (DeviceError, GossipError, NoPeers, RoundReport, Statistics, _check, _Config,
+               _Report, _Stats, load_library, origin_of)
+
+_P = ctypes.c_void_p
+_U32P = ctypes.POINTER(ctypes.c_uint32)
+_U64P = ctypes.POINTER(ctypes.c_uint64)
+_U16P = ctypes.POINTER(ctypes.c_uint16)
+
+
+def _lib():
+    return load_library()
+
+
+class _Shard:
+    """One rank's engine plus its exchange buffers (torch device tensors)."""
+
+    def __init__(self, lib, cfg, rank, world, torch, device):
+        self.lib = lib
+        h = _P()
+        _check(lib.gs_shard_create(ctypes.byref(cfg), rank, world, ctypes.byref(h)))
+        self.h = h
+        info = (ctypes.c_uint32 * 8)()
+        _check(lib.gs_shard_info(h, info))
+        self.lo, self.m, self.cap, self.wa, self.wb, self.world, self.rank, self.chunk = list(info)
+        dev = torch.device("cuda", device)
+        i64 = torch.int64
+        self.sendA = torch.zeros(max(1, self.m) * self.wa, dtype=i64, device=dev)
+        self.recvA = torch.zeros(max(1, self.cap) * self.wa, dtype=i64, device=dev)
+        self.sendB = torch.zeros(max(1, self.cap) * self.wb, dtype=i64, device=dev)
+        self.recvB = torch.zeros(max(1, self.m) * self.wb, dtype=i64, device=dev)
+        _check(lib.gs_shard_bind(h, self.sendA.data_ptr(), self.recvA.data_ptr(),
+                                 self.sendB.data_ptr(), self.recvB.data_ptr()))
+        self.stream = torch.cuda.ExternalStream(lib.gs_stream(h), device=dev)
+
+    def counts(self):
+        s = (ctypes.c_uint32 * self.world)()
+        r = (ctypes.c_uint32 * self.world)()
+        _check(self.lib.gs_shard_counts(self.h, s, r))
+        return list(s), list(r)
+
+    def close(self):
+        if self.h:
+            self.lib.gs_destroy(self.h)
+            self.h = None
+
+
+def _displ(c):
+    return [0] + list(np.cumsum(c)[:-1]) if len(c) else []
+
+
+class ShardedNetwork:
+    """A network of ``n_nodes`` gossipers sharded over ``world`` ranks.
+
+    Mirrors :class:`safe_gossip_amd.Network`: ``send_new``, ``next_round``,
+    ``statistics_all``, ``known_all``, ``dump_state``, ``dump_records``,
+    ``known_counts`` and ``clear``.  With ``transport="dist"`` every rank makes
+    the same calls; observers return the whole network on every rank
+    (all-gathered) only when ``gather=True``, otherwise this rank's slice.
+    """
+
+    def __init__(self, n_nodes: int, n_rumors: int, world: int, seed: int = 0x5AFE6055,
+                 epoch: int = 0, params=None, device: int = 0, transport: str = "local",
+                 group=None):
+        import torch
+        self.torch = torch
+        self.lib = _lib()
+        self.n, self.R, self.seed, self.epoch = n_nodes, n_rumors, seed, epoch
+        self.world = world
+        self.transport = transport
+        self.group = group
+        self.device = device
+        self.kw = (n_rumors + 63) // 64
+        cfg = _Config()
+        cfg.n_nodes = n_nodes
+        cfg.n_rumors = n_rumors
+        cfg.seed = seed
+        cfg.epoch = epoch
+        if params is not None:
+            cfg.counter_max, cfg.max_c_rounds, cfg.max_rounds = params
+        cfg.device = device
+        self._cfg = cfg
+        if transport == "local":
+            self.shards = [_Shard(self.lib, cfg, r, world, torch, device) for r in range(world)]
+        elif transport == "dist":
+            import torch.distributed as dist
+            self.dist = dist
+            self.rank = dist.get_rank(group)
+            assert dist.get_world_size(group) == world
+            self.shards = [_Shard(self.lib, cfg, self.rank, world, torch, device)]
+            self.host_staged = dist.get_backend(group) == "gloo"
+        else:
+            raise ValueError(transport)
+        self.round = 0
+        self._delivered = True
+
+    # ------------------------------------------------------------ lifecycle
+    def close(self):
+        for s in getattr(self, "shards", []):
+            s.close()
+        self.shards = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def params(self):
+        out = (ctypes.c_uint8 * 3)()
+        _check(self.lib.gs_get_params(self.shards[0].h, out))
+        return tuple(out)
+
+    def owner(self, node: int) -> int:
+        return node // self.shards[0].chunk
+
+    # ------------------------------------------------------------ protocol
+    def send_new(self, node: int, rumor: int) -> None:
+        if self.n < 2:
+            raise NoPeers("There are no connected peers with which to gossip.")
+        if not 0 <= node < self.n:
+            raise GossipError(f"node {node} out of range")
+        for s in self.shards:
+            if s.lo <= node < s.lo + s.m:
+                _check(self.lib.gs_send_new(s.h, node, rumor))
+
+    def _sync_all(self):
+        for s in self.shards:
+            _check(self.lib.gs_sync(s.h))
+
+    def _deliver(self):
+        """Exchange A, pull rows, exchange B for the current round."""
+        if self._delivered or self.round == 0:
+            return
+        counts = [s.counts() for s in self.shards]
+        if self.transport == "local":
+            self._sync_all()
+            self._local_exchange(counts, "A")
+            self._sync_all()
+            for s in self.shards:
+                _check(self.lib.gs_shard_pull(s.h))
+            self._sync_all()
+            self._local_exchange(counts, "B")
+            self._sync_all()
+        else:
+            s = self.shards[0]
+            scnt, rcnt = counts[0]
+            self._dist_exchange(s, s.sendA, s.recvA, scnt, rcnt, s.wa)
+            _check(self.lib.gs_shard_pull(s.h))
+            self._dist_exchange(s, s.sendB, s.recvB, rcnt, scnt, s.wb)
+        self._delivered = True
+
+    def _local_exchange(self, counts, which):
+        torch = self.torch
+        G = self.world
+        for d in range(G):
+            dst = self.shards[d]
+            rcnt_d = counts[d][1]
+            rdis_d = _displ(rcnt_d)
+            for src_rank in range(G):
+                s = self.shards[src_rank]
+                scnt_s = counts[src_rank][0]
+                sdis_s = _displ(scnt_s)
+                rows = scnt_s[d]
+                assert rows == rcnt_d[src_rank], "send/recv counts disagree"
+                if rows == 0:
+                    continue
+                if which == "A":      # s.sendA[sdis_s[d]] -> dst.recvA[rdis_d[src]]
+                    w = s.wa
+                    dst.recvA[rdis_d[src_rank] * w:(rdis_d[src_rank] + rows) * w].copy_(
+                        s.sendA[sdis_s[d] * w:(sdis_s[d] + rows) * w])
+                else:                 # dst.sendB[rdis_d[src]] -> s.recvB[sdis_s[d]]
+                    w = s.wb
+                    s.recvB[sdis_s[d] * w:(sdis_s[d] + rows) * w].copy_(
+                        dst.sendB[rdis_d[src_rank] * w:(rdis_d[src_rank] + rows) * w])
+        torch.cuda.synchronize(self.device)
+
+    def _dist_exchange(self, s, send, recv, scnt, rcnt, w):
+        torch, dist = self.torch, self.dist
+        ss = [int(c) * w for c in scnt]
+        rs = [int(c) * w for c in rcnt]
+        out = recv[:sum(rs)]
+        inp = send[:sum(ss)]
+        if self.host_staged:
+            _check(self.lib.gs_sync(s.h))
+            hout = torch.empty(sum(rs), dtype=torch.int64)
+            dist.all_to_all_single(hout, inp.cpu(), output_split_sizes=rs, input_split_sizes=ss,
+                                   group=self.group)
+            out.copy_(hout.to(out.device))
+            torch.cuda.synchronize(self.device)
+        else:
+            with torch.cuda.stream(s.stream):
+                dist.all_to_all_single(out, inp, output_split_sizes=rs, input_split_sizes=ss,
+                                       group=self.group)
+
+    def next_round(self, report: bool = True) -> Optional[RoundReport]:
+        self._deliver()
+        live = False
+        for s in self.shards:
+            if report:
+                r = _Report()
+                _check(self.lib.gs_next_round(s.h, ctypes.byref(r)))
+                live |= bool(r.any_live)
+            else:
+                _check(self.lib.gs_next_round(s.h, None))
+        self.round += 1
+        self._delivered = False
+        if not report:
+            return None
+        if self.transport == "dist":
+            t = self.torch.tensor([1 if live else 0], dtype=self.torch.int32,
+                                  device=("cpu" if self.host_staged else f"cuda:{self.device}"))
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+            live = bool(int(t.item()))
+        return RoundReport(self.round, live)
+
+    def clear(self, epoch: Optional[int] = None) -> None:
+        self.epoch = self.epoch + 1 if epoch is None else epoch
+        for s in self.shards:
+            _check(self.lib.gs_clear(s.h, self.epoch))
+        self.round = 0
+        self._delivered = True
+
+    def sync(self) -> None:
+        self._sync_all()
+
+    # ------------------------------------------------------------ observers
+    def _per_shard(self, fn):
+        self._deliver()
+        return [fn(s) for s in self.shards]
+
+    def _gather_rows(self, parts):
+        """Concatenate per-shard row blocks (dist: all-gather, rows in rank order)."""
+        if self.transport == "local":
+            return np.concatenate(parts, axis=0)
+        torch, dist = self.torch, self.dist
+        part = parts[0]
+        objs = [None] * self.world
+        dist.all_gather_object(objs, part, group=self.group)
+        return np.concatenate(objs, axis=0)
+
+    def statistics_all(self) -> np.ndarray:
+        def f(s):
+            out = np.zeros((s.m, 5), dtype=np.uint64)
+            if s.m:
+                _check(self.lib.gs_statistics_all(s.h, out.ctypes.data_as(_U64P)))
+            return out
+        return self._gather_rows(self._per_shard(f))
+
+    def known_all(self) -> np.ndarray:
+        def f(s):
+            out = np.zeros((s.m, self.kw), dtype=np.uint64)
+            if s.m:
+                _check(self.lib.gs_known_all(s.h, out.ctypes.data_as(_U64P)))
+            return out
+        return self._gather_rows(self._per_shard(f))
+
+    def dump_state(self) -> np.ndarray:
+        def f(s):
+            out = np.zeros((s.m, self.R), dtype=np.uint16)
+            if s.m:
+                _check(self.lib.gs_dump_state(s.h, out.ctypes.data_as(_U16P)))
+            return out
+        return self._gather_rows(self._per_shard(f))
+
+    def dump_records(self):
+        def f(s):
+            rec = np.zeros((s.m, self.R), dtype=np.uint16)
+            ps = np.zeros(s.m, dtype=np.uint32)
+            if s.m:
+                _check(self.lib.gs_dump_records(s.h, rec.ctypes.data_as(_U16P),
+                                                ps.ctypes.data_as(_U32P)))
+            return np.concatenate([rec.astype(np.uint32), ps[:, None]], axis=1)
+        both = self._gather_rows(self._per_shard(f))
+        return both[:, :-1].astype(np.uint16), both[:, -1].astype(np.uint32)
+
+    def known_counts(self):
+        def f(s):
+            if not s.m:
+                return (0, 0)
+            t, c = ctypes.c_uint64(), ctypes.c_uint64()
+            _check(self.lib.gs_known_counts(s.h, ctypes.byref(t), ctypes.byref(c)))
+            return (int(t.value), int(c.value))
+        parts = self._per_shard(f)
+        tot = sum(p[0] for p in parts)
+        comp = sum(p[1] for p in parts)
+        if self.transport == "dist":
+            t = self.torch.tensor([tot, comp], dtype=self.torch.int64,
+                                  device=("cpu" if self.host_staged else f"cuda:{self.device}"))
+            self.dist.all_reduce(t, group=self.group)
+            tot, comp = int(t[0].item()), int(t[1].item())
+        return tot, comp

@@ -51,8 +51,39 @@ class Model:
         p = self.P[s]
         return p[0], p[1], p[2]
 
+    def pull_row(self, z, x, pushers):
+        """Pull batch z returns to pusher x (src/gossip.rs:124-151) as the
+        shard exchange's 2-plane class code (b0, b1): 01 counter 1, 10 counter
+        2, 11 counter 255 (C).  `pushers` = (source, class) of z's in-edges."""
+        M = self.M
+        zc, z0, z1 = self.cls(z)
+        zA = ~zc & ~z0 & ~z1 & M
+        zB = ~zc & (z0 | z1) & M
+        zC = zc & ~(z0 & z1) & M
+        pB = pC = 0
+        pnot = zA
+        for s, (qc, q0, q1) in pushers:
+            if not pnot or s >= x:
+                break
+            vC = qc & ~(q0 & q1) & M
+            sl = (~qc & (q0 | q1) & M) | vC
+            nc = pnot & sl
+            pB |= nc & ~vC & M
+            pC |= nc & vC
+            pnot &= ~sl & M
+        pcl = zC | pC
+        return (zB & z0 & ~z1 & M) | pB | pcl, (zB & z1 & ~z0 & M) | pcl
+
     def deliver(self, x):
         """Phases 1+2 of round t at x: returns the kernel's per-lane values."""
+        z = self.tg[x]
+        ins = [(s, self.cls(s)) for s in self.src[x]]
+        pull = self.pull_row(z, x, [(s, self.cls(s)) for s in self.src[z]])
+        return self.deliver_rows(x, z, ins, pull)
+
+    def deliver_rows(self, x, z, ins, pull):
+        """`ins` = (source, class planes) of x's pushers ascending; `pull` = the
+        (b0, b1) code of the pull batch t(x) returned to x."""
         M = self.M
         isC, a0, a1 = self.cls(x)
         A = ~isC & ~a0 & ~a1 & M
@@ -62,16 +93,13 @@ class Model:
         crB = crC = anyC = 0
         c1 = [0] * 5
         c2 = [0] * 5
-        z = self.tg[x]
-        ins = self.src[x]
         k = len(ins)
         notyet = A
         zin = False
         part_cw = 0
         first = None
         recv = 0
-        for i, s in enumerate(ins):
-            qc, q0, q1 = self.cls(s)
+        for i, (s, (qc, q0, q1)) in enumerate(ins):
             vC = qc & ~(q0 & q1) & M
             vB = ~qc & (q0 | q1) & M
             v2 = vB & q1 & ~q0 & M
@@ -92,25 +120,10 @@ class Model:
             if pc and first is None:
                 first = i
             recv += popc(sl)
-        zc, z0, z1 = self.cls(z)
-        zA = ~zc & ~z0 & ~z1 & M
-        zB = ~zc & (z0 | z1) & M
-        zC = zc & ~(z0 & z1) & M
-        pB = pC = 0
-        pnot = zA
-        for s in self.src[z]:
-            if not pnot or s >= x:
-                break
-            qc, q0, q1 = self.cls(s)
-            vC = qc & ~(q0 & q1) & M
-            sl = (~qc & (q0 | q1) & M) | vC
-            nc = pnot & sl
-            pB |= nc & ~vC & M
-            pC |= nc & vC
-            pnot &= ~sl & M
-        pv2 = zB & z1 & ~z0 & M
-        pvB = zB | pB
-        pCl = zC | pC
+        b0, b1 = pull
+        pv2 = b1 & ~b0 & M
+        pvB = (b0 ^ b1) & M
+        pCl = b0 & b1
         pl = pvB | pCl
         newc = notyet & pl
         rec = (B | crB) & pl

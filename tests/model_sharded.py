@@ -1,0 +1,136 @@
+"""Pure-Python model of the SHARDED round, test only.
+
+Each rank owns the node range [lo, lo+m) (shard_plan in gs_shard.hip: chunk =
+ceil(n/G) rounded up to 256 nodes) and runs, per round, the same two row
+exchanges as the engine over a caller-supplied all-to-all
+``a2a(rows_per_dest, width, recv_counts) -> rows_per_source``:
+
+  A  every owned node x sends (x, isC, a0, a1) to owner(t(x)), rows per
+     destination in ascending x, so each rank receives its pushers' rows in
+     ascending source order (rank order = node order);
+  B  the owner of z answers each received row, in the same order, with the pull
+     batch z returned to that pusher (Model.pull_row: z's live set plus the
+     entries z created from earlier pushers, as a 2-plane class code).
+
+Delivery and transition then use Model's bit-sliced algebra on the received
+rows only, so a rank never reads another rank's state directly.  Rumor sets are
+Python ints (R <= 62 so a plane fits one int64 of the gloo transport).
+"""
+from model_bitsliced import Model
+
+
+def shard_range(n, G, g):
+    chunk = -(-n // G)
+    chunk = -(-chunk // 256) * 256
+    lo = min(g * chunk, n)
+    return lo, min(lo + chunk, n) - lo, chunk
+
+
+class ShardModel(Model):
+    def __init__(self, n, R, seed, epoch, params, peer_fn, rank, world, a2a):
+        super().__init__(n, R, seed, epoch, params, peer_fn)
+        assert R <= 62
+        self.rank, self.world, self.a2a = rank, world, a2a
+        self.lo, self.m, self.chunk = shard_range(n, world, rank)
+        self.P = {x: [0] * 8 for x in self.owned()}
+        self.stats = {x: [0] * 5 for x in self.owned()}
+        self.exchanged = False
+
+    def owned(self):
+        return range(self.lo, self.lo + self.m)
+
+    def owner(self, x):
+        return x // self.chunk
+
+    def exchange(self):
+        """Exchanges A and B of the current round (needs self.tg of round t)."""
+        if self.exchanged or not self.deliver_pending:
+            return
+        G = self.world
+        sendA = [[] for _ in range(G)]
+        for x in self.owned():
+            sendA[self.owner(self.tg[x])].append([x] + list(self.cls(x)))
+        # receive counts from the local plan (every rank knows all targets)
+        rcA = [0] * G
+        for x in range(self.n):
+            if self.owner(self.tg[x]) == self.rank:
+                rcA[self.owner(x)] += 1
+        recvA = self.a2a(sendA, 4, rcA)
+        rows = [r for part in recvA for r in part]
+        srcs = [r[0] for r in rows]
+        assert srcs == sorted(srcs), "receive rows must be in ascending source order"
+        ins = {z: [] for z in self.owned()}
+        for s, qc, q0, q1 in rows:
+            ins[self.tg[s]].append((s, (qc, q0, q1)))
+        sendB = []
+        for part in recvA:
+            sendB.append([[r[0]] + list(self.pull_row(self.tg[r[0]], r[0], ins[self.tg[r[0]]]))
+                          for r in part])
+        recvB = self.a2a(sendB, 3, [len(p) for p in sendA])
+        pull = {}
+        for d in range(G):
+            assert [r[0] for r in recvB[d]] == [r[0] for r in sendA[d]], "B order = A order"
+            for x, b0, b1 in recvB[d]:
+                pull[x] = (b0, b1)
+        self.ins, self.pull = ins, pull
+        self.exchanged = True
+
+    def deliver(self, x):
+        return self.deliver_rows(x, self.tg[x], self.ins[x], self.pull[x])
+
+    def next_round(self):
+        """Local part of the round; returns this shard's any-live flag."""
+        self.exchange()
+        inj = {x: 0 for x in self.owned()}
+        for x, r in self.pending:
+            inj[x] |= 1 << r
+        self.pending = []
+        zero = dict(crB=0, crC=0, anyC=0, c1=[0] * 5, c2=[0] * 5, psize=0, d_full=0,
+                    d_empty_pull=0, d_recv=0)
+        newP = {}
+        live_any = False
+        for x in self.owned():
+            d = self.deliver(x) if self.deliver_pending else zero
+            N, live = self.transition(x, d, inj[x])
+            newP[x] = N
+            st = self.stats[x]
+            st[0] += 1
+            st[1] += d["d_empty_pull"]
+            st[4] += d["d_recv"]
+            st[2] += 1 if live == 0 else 0
+            st[3] += live + d["d_full"]
+            live_any |= live > 0
+        self.P = newP
+        self.round += 1
+        # every rank derives the whole round-(t+1) peer schedule (Philox): the
+        # plan's counts and send positions need the targets of all n sources
+        self.tg = [self.peer_fn(self.seed, self.epoch, self.round, x, self.n) for x in range(self.n)]
+        self.deliver_pending = True
+        self.exchanged = False
+        return live_any
+
+    def observe_local(self):
+        """(codes, records, psize, stats, known) rows of the owned nodes."""
+        self.exchange()
+        out = ([], [], [], [], [])
+        for x in self.owned():
+            for acc, v in zip(out, _Single(self, x).observe()):
+                acc.append(v[0])
+        return out
+
+
+class _Single:
+    """View of one owned node through Model.observe."""
+
+    def __init__(self, sm, x):
+        self.sm, self.x = sm, x
+        self.n, self.R, self.M = 1, sm.R, sm.M
+        self.P = [sm.P[x]]
+        self.stats = [sm.stats[x]]
+        self.deliver_pending = sm.deliver_pending
+
+    def deliver(self, _):
+        return self.sm.deliver(self.x)
+
+    def observe(self):
+        return Model.observe(self)

@@ -55,8 +55,11 @@ def _first_diff(a, b):
 
 
 def run_parity(engine, n, R, kind, params=None, max_rounds=60, seed=SEED, epoch=0,
-               check_every=1):
-    net = engine.Network(n, R, seed=seed, epoch=epoch, params=params)
+               check_every=1, make_net=None):
+    if make_net is None:
+        net = engine.Network(n, R, seed=seed, epoch=epoch, params=params)
+    else:
+        net = make_net(n, R, seed=seed, epoch=epoch, params=params)
     orc = OracleNet(n, R, seed=seed, epoch=epoch, params=params)
     assert net.params == orc.params
     rounds = 0

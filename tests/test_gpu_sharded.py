@@ -1,0 +1,79 @@
+"""Sharded engine (node range per rank) vs CPU oracle, bit-exact.
+
+The sharded path moves push rows to the owner of each target and pull rows
+back; here `world` shard engines share one GPU and the
+two exchanges are device copies (transport "local").  The observable result
+must equal the unsharded network's, which the oracle restates
+(src/gossip.rs:95-151, src/message_state.rs).
+"""
+import numpy as np
+import pytest
+
+from oracle_lib import SCHED_2P, OracleNet
+from test_gpu_parity import SEED, run_parity
+
+pytestmark = pytest.mark.gpu
+
+
+def _maker(world):
+    from safe_gossip_amd.sharded import ShardedNetwork
+
+    def make(n, R, seed, epoch, params):
+        return ShardedNetwork(n, R, world, seed=seed, epoch=epoch, params=params,
+                              transport="local")
+    return make
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("n,R,kind,params", [
+    (8, 3, "example", None),
+    (5, 3, "trickle", None),
+    (200, 1, "trickle", None),
+    (97, 16, "origins", None),
+    (101, 32, "reinject", None),
+    (300, 64, "trickle", None),
+    (77, 100, "origins", None),
+    (130, 256, "reinject", None),
+    (300, 16, "origins", (3, 3, 14)),
+    (1619, 4, "origins", None),
+    # every rank owns nodes (chunks are whole 256-node blocks)
+    (700, 3, "trickle", None),
+    (520, 100, "reinject", None),
+    (1000, 256, "origins", None),
+    (900, 7, "origins", (2, 3, 5)),
+    (1100, 1, "trickle", (1, 1, 3)),
+])
+def test_sharded_parity(engine, world, n, R, kind, params):
+    run_parity(engine, n, R, kind, params, make_net=_maker(world))
+
+
+def test_sharded_larger(engine):
+    # 3 shards whose chunk boundaries fall inside 256-node blocks' neighbours.
+    run_parity(engine, 20000, 64, "origins", check_every=4, make_net=_maker(3))
+
+
+def test_sharded_more_ranks_than_chunks(engine):
+    # world 8 over 600 nodes: chunk rounding leaves trailing ranks empty.
+    run_parity(engine, 600, 48, "origins", make_net=_maker(8))
+
+
+def test_sharded_clear(engine):
+    from safe_gossip_amd.sharded import ShardedNetwork
+    n, R = 500, 32
+    net = ShardedNetwork(n, R, 2, transport="local")
+    orc = OracleNet(n, R)
+    for epoch in (0, 5):
+        for r in range(R):
+            x = engine.origin_of(SEED, epoch, r, n)
+            net.send_new(x, r)
+            orc.send_new(x, r)
+        for _ in range(4):
+            net.next_round()
+            orc.next_round(SCHED_2P)
+        np.testing.assert_array_equal(net.dump_state(), orc.dump_state())
+        np.testing.assert_array_equal(net.statistics_all(), orc.statistics())
+        net.clear(epoch=5)
+        orc.clear(5)
+        assert net.known_counts() == (0, 0)
+    net.close()
+    orc.close()
