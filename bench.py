@@ -15,10 +15,12 @@ cpu_baseline: the CPU oracle (reference-faithful port: per-node ordered maps,
           one thread, same 2P schedule) on a bounded sample of the same
           workload (fewer nodes, same R and injection), rank 0 at N=1 only.
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process
-per GPU, each rank simulates its own network of the same size (independent
-replicas with distinct Philox epochs; DESIGN.md "Multi-GPU").  Barrier +
-synchronize around the timed region, time = max over ranks.
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): ONE network
+of the same n x R sharded by node range over the N ranks (safe_gossip_amd.sharded,
+DESIGN.md section 7): every round exchanges push rows and pull rows with RCCL
+all_to_all_single over xGMI on the engine's stream.  Total work is fixed, so
+"scaling" is "strong".  Barrier + synchronize around the timed region, time =
+max over ranks.  The roofline line describes rank 0's round kernel.
 """
 import argparse
 import json
@@ -45,13 +47,22 @@ def parse():
                    help="budget of the CPU-oracle sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-spread", action="store_true", help="skip the rounds-to-full-spread run")
+    p.add_argument("--dist-backend", default="nccl",
+                   help="nccl (RCCL, one GPU per rank) or gloo (host-staged rows; rehearsal of "
+                        "the N>1 path with several ranks on one GPU)")
     return p.parse_args()
 
 
 def inject_all(net, epoch):
+    """Every rumor at its Philox origin (sharded: only the owner takes it)."""
     import safe_gossip_amd as sg
     for r in range(net.R):
-        net.send_new(sg.origin_of(net.seed, epoch, r, net.n), r)
+        x = sg.origin_of(net.seed, epoch, r, net.n)
+        if getattr(net, "transport", None) == "dist":
+            s = net.shards[0]
+            if not s.lo <= x < s.lo + s.m:
+                continue
+        net.send_new(x, r)
 
 
 def spread_run(net, epoch, max_rounds=200):
@@ -108,8 +119,10 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        if args.dist_backend == "gloo":
+            local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(0)
 
@@ -117,7 +130,12 @@ def main():
     import safe_gossip_amd as sg
 
     n, R = args.nodes, args.rumors
-    net = sg.Network(n, R, seed=args.seed, epoch=rank * 1000, device=local)
+    if world > 1:
+        from safe_gossip_amd.sharded import ShardedNetwork
+        net = ShardedNetwork(n, R, world, seed=args.seed, epoch=0, device=local,
+                             transport="dist")
+    else:
+        net = sg.Network(n, R, seed=args.seed, epoch=0, device=local)
 
     def barrier_sync():
         net.sync()
@@ -126,12 +144,12 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
-    # warmup: W rounds of a dissemination (epoch rank*1000)
-    inject_all(net, rank * 1000)
+    # warmup: W rounds of a dissemination (epoch 0)
+    inject_all(net, 0)
     for _ in range(args.warmup):
         net.next_round(report=False)
     # timed: K rounds of a fresh dissemination from round 1
-    epoch = rank * 1000 + 1
+    epoch = 1
     net.clear(epoch)
     inject_all(net, epoch)
     net.set_timing(True)
@@ -144,7 +162,8 @@ def main():
     ktimes = net.round_kernel_times()
     net.set_timing(False)
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -172,7 +191,7 @@ def main():
         cpu = cpu_baseline(R, args.seed, args.cpu_seconds)
 
     if rank == 0:
-        total_updates = float(n) * R * args.steps * world
+        total_updates = float(n) * R * args.steps
         line = {
             "metric": METRIC,
             "value": total_updates / elapsed,
@@ -182,7 +201,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic",
@@ -191,7 +210,9 @@ def main():
                             f"round 1 at Philox origins, 2P schedule, {args.steps} rounds",
                 "n_nodes": n, "n_rumors": R, "seed": hex(args.seed),
                 "params": list(net.params),
-                "parallelism": "replicas" if world > 1 else "single-gpu",
+                "parallelism": (f"node-range shards x{world}, "
+                                + ("RCCL" if args.dist_backend == "nccl" else args.dist_backend)
+                                + " all-to-all push/pull rows") if world > 1 else "single-gpu",
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -125,6 +125,27 @@ SYMBOLS = {
 _LIB = None
 
 
+def _share_torch_hip_runtime() -> None:
+    """One HIP runtime per process.
+
+    PyTorch-ROCm wheels carry their own ``libamdhip64.so`` (soname
+    ``libamdhip64.so.7``, the engine's DT_NEEDED).  Loading it first makes the
+    engine bind to the same runtime torch and its RCCL use, so the engine's
+    streams and device pointers are valid for torch.distributed (the sharded
+    transport) and the two never bring up the device twice.  Processes without
+    torch use the system ROCm runtime.
+    """
+    if os.environ.get("SAFE_GOSSIP_AMD_HIP_RUNTIME") == "system":
+        return
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    rt = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(rt):
+        ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)
+
+
 def load_library(path: Optional[str] = None):
     """Load ``libsafe_gossip_amd.so`` (built by ``__graft_entry__.build()``)."""
     global _LIB
@@ -133,6 +154,7 @@ def load_library(path: Optional[str] = None):
     p = path or os.environ.get("SAFE_GOSSIP_AMD_LIB", LIB_PATH)
     if not os.path.exists(p):
         raise DeviceError(f"engine library not built: {p} (run __graft_entry__.build())")
+    _share_torch_hip_runtime()
     lib = ctypes.CDLL(p)
     for name, (res, args) in SYMBOLS.items():
         fn = getattr(lib, name)

@@ -21,12 +21,11 @@ work runs in the engine's gfx950 kernels.
 from __future__ import annotations
 
 import ctypes
-from typing import List, Optional
+from typing import Optional
 
 import numpy as np
 
-from . import (DeviceError, GossipError, NoPeers, RoundReport, Statistics, _check, _Config,
-               _Report, _Stats, load_library, origin_of)
+from . import DeviceError, GossipError, NoPeers, RoundReport, _check, _Config, _Report, load_library
 
 _P = ctypes.c_void_p
 _U32P = ctypes.POINTER(ctypes.c_uint32)
@@ -81,8 +80,9 @@ class ShardedNetwork:
     Mirrors :class:`safe_gossip_amd.Network`: ``send_new``, ``next_round``,
     ``statistics_all``, ``known_all``, ``dump_state``, ``dump_records``,
     ``known_counts`` and ``clear``.  With ``transport="dist"`` every rank makes
-    the same calls; observers return the whole network on every rank
-    (all-gathered) only when ``gather=True``, otherwise this rank's slice.
+    the same calls (``send_new`` is ignored by ranks that do not own the node)
+    and observers return the whole network on every rank (all-gathered in rank
+    order).
     """
 
     def __init__(self, n_nodes: int, n_rumors: int, world: int, seed: int = 0x5AFE6055,
@@ -250,6 +250,22 @@ class ShardedNetwork:
 
     def sync(self) -> None:
         self._sync_all()
+
+    # measurement hooks (this process's first shard)
+    def set_timing(self, on: bool) -> None:
+        for s in self.shards:
+            self.lib.gs_set_timing(s.h, 1 if on else 0)
+
+    def round_kernel_times(self, max_n: int = 4096) -> np.ndarray:
+        out = np.zeros(max_n, dtype=np.float32)
+        m = self.lib.gs_round_kernel_times(self.shards[0].h,
+                                           out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), max_n)
+        if m < 0:
+            raise DeviceError("kernel timing unavailable")
+        return out[:m]
+
+    def round_kernel_bytes(self) -> float:
+        return float(self.lib.gs_round_kernel_bytes(self.shards[0].h))
 
     # ------------------------------------------------------------ observers
     def _per_shard(self, fn):

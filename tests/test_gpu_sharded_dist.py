@@ -1,0 +1,65 @@
+"""Sharded engine, "dist" transport: 2 processes (gloo, host-staged rows) on
+the box's one GPU, each one rank of a network sharded over 2 ranks; every rank
+checks the all-gathered state against the oracle each round (bit-exact).  The
+RCCL transport differs only in where the all_to_all_single runs (on the
+engine's stream); it needs one GPU per rank and runs in bench.py --gpus N.
+"""
+import os
+import socket
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, cases, q):
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.dirname(HERE))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import safe_gossip_amd as sg
+        from safe_gossip_amd.sharded import ShardedNetwork
+        from test_gpu_parity import run_parity
+
+        def make(n, R, seed, epoch, params):
+            return ShardedNetwork(n, R, world, seed=seed, epoch=epoch, params=params, device=0,
+                                  transport="dist")
+        for n, R, kind in cases:
+            run_parity(sg, n, R, kind, make_net=make)
+        q.put(("ok", rank))
+    except BaseException as e:
+        q.put(("fail", f"rank {rank}: {type(e).__name__}: {e}"))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_dist_gloo_two_ranks(engine):
+    import torch.multiprocessing as mp
+    world = 2
+    cases = [(600, 48, "origins"), (1000, 3, "trickle"), (700, 256, "reinject")]
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=200)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    msgs = []
+    while not q.empty():
+        msgs.append(q.get())
+    assert len(msgs) == world and all(m[0] == "ok" for m in msgs), msgs
