@@ -85,4 +85,24 @@ struct Geometry {
     uint64_t nseg;      // lanes: n*W (big) or n (small)
 };
 
+// In-edge records of one round (gs_inlist.hip):
+//   InRec[y]  = {first, k, s0..s5} (32 B): y's k pushers in ascending index
+//               order (the order Gossip::receive sees them); pushers
+//               i >= kInline are at src[first + i - kInline].
+//   SibRec[x] = {serial << 8 | rank, e0, e1, e2} (16 B): x's rank among the
+//               pushers of t(x) and the first kSibInline pushers ahead of it
+//               (the rest are InRec[t(x)].s / its tail); valid iff the serial
+//               is the round build's (stale records are never cleared).
+// Both are read coalesced by the round kernel, so every gather of a node with
+// in-degree <= kInline is issued from one level of metadata reads.
+constexpr uint32_t kInline = 6;
+constexpr uint32_t kSibInline = 3;
+constexpr uint32_t kSerialMask = 0xFFFFFFu;
+struct alignas(16) InRec {
+    uint32_t first, k, s[kInline];
+};
+struct alignas(16) SibRec {
+    uint32_t tag, e[kSibInline];
+};
+
 }  // namespace gs

@@ -105,8 +105,16 @@ struct Lane {
         } else {
             u64 b = (u64)s * kPlanes * W + j;
             r.c = S[b];
+#if defined(GS_EXP_G1)
+            r.a0 = r.c >> 1;
+            r.a1 = r.c << 1;
+#elif defined(GS_EXP_G2)
+            r.a0 = S[b + W];
+            r.a1 = r.c ^ r.a0;
+#else
             r.a0 = S[b + W];
             r.a1 = S[b + 2 * (u64)W];
+#endif
         }
         return r;
     }
@@ -136,6 +144,21 @@ GS_DEV void sibling(const Cls &q, u64 &pnot, u64 &pB, u64 &pC) {
     pnot &= ~sl;
 }
 
+// v[i] for a runtime i < kInline without dynamic register indexing.
+GS_DEV uint32_t pick_inline(const uint32_t (&v)[kInline], uint32_t i) {
+    uint32_t r = v[0];
+#pragma unroll
+    for (uint32_t q = 1; q < kInline; ++q) r = (i == q) ? v[q] : r;
+    return r;
+}
+
+GS_DEV uint32_t pick_sib(const uint32_t (&v)[kSibInline], uint32_t i) {
+    uint32_t r = v[0];
+#pragma unroll
+    for (uint32_t q = 1; q < kSibInline; ++q) r = (i == q) ? v[q] : r;
+    return r;
+}
+
 constexpr uint32_t kScanBlock = 256;
 
 // Block-wide exclusive scan of one value per thread; returns the block total.
@@ -153,6 +176,31 @@ GS_DEV uint32_t block_exclusive_scan(uint32_t v, uint32_t *lds, uint32_t &total)
     for (uint32_t w = 0; w < kScanBlock / 64; ++w) {
         if (w < wid) wbase += lds[w];
         tot += lds[w];
+    }
+    __syncthreads();
+    total = tot;
+    return wbase + inc - v;
+}
+
+// Exclusive scan over a block of NT threads (NT a multiple of 64, <= 1024);
+// `lds` holds NT/64 words.
+template <uint32_t NT>
+GS_DEV uint32_t block_exclusive_scan_t(uint32_t v, uint32_t *lds, uint32_t &total) {
+    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(inc, (unsigned)o, 64);
+        if (lane >= (uint32_t)o) inc += t;
+    }
+    if (lane == 63) lds[wid] = inc;
+    __syncthreads();
+    uint32_t wbase = 0, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NT / 64; ++w) {
+        const uint32_t c = lds[w];
+        wbase += (w < wid) ? c : 0u;
+        tot += c;
     }
     __syncthreads();
     total = tot;

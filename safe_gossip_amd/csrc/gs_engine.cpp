@@ -31,15 +31,16 @@ struct gs_engine {
     // set of round r+1 is built on cstream while the round kernel of round
     // r+1 (which reads round r's set) runs on `stream`.
     struct CsrSet {
-        uint32_t *src = nullptr, *tg = nullptr, *scratch = nullptr;
-        uint4 *IN = nullptr, *SIB = nullptr;
-        u64 *pairs = nullptr;
+        uint32_t *src = nullptr, *tg = nullptr, *scratch = nullptr, *region = nullptr;
+        gs::InRec *IN8 = nullptr;
+        gs::SibRec *SIB8 = nullptr;
         uint32_t serial = 0;
     } csr[2];
     hipStream_t cstream = nullptr;
     hipEvent_t ev_built[2] = {nullptr, nullptr};  // set i complete
     hipEvent_t ev_read[2] = {nullptr, nullptr};   // last reader of set i done
     uint32_t build_serial = 0;
+    bool concurrent_inlists = false;  // SAFE_GOSSIP_AMD_CONCURRENT_INLISTS=1: build on cstream
     uint32_t *flags = nullptr;
     gs::CsrPlan plan{};
     // Shard engine (gs_shard_create): this rank's node range of a network
@@ -110,7 +111,7 @@ void release(gs_engine *e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->cstream) (void)hipStreamSynchronize(e->cstream);
     for (auto &c : e->csr) {
-        void *cb[] = {c.src, c.tg, c.scratch, c.IN, c.SIB, c.pairs};
+        void *cb[] = {c.src, c.tg, c.scratch, c.region, c.IN8, c.SIB8};
         for (void *b : cb)
             if (b) (void)hipFree(b);
     }
@@ -169,8 +170,8 @@ gs::RoundArgs base_args(gs_engine *e) {
         a.sendA = e->sendA;
     } else {
         const auto &cs = e->csr[e->round & 1u];  // round-t lists (t = e->round)
-        a.IN = cs.IN;
-        a.SIB = cs.SIB;
+        a.IN8 = cs.IN8;
+        a.SIB8 = cs.SIB8;
         a.src = cs.src;
         a.tg = cs.tg;
         a.serial = cs.serial;
@@ -389,6 +390,10 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
     }
     const size_t sw = (size_t)g.units * gs::kPlanes * g.W;
     e->plan = gs::csr_plan(n);
+    {
+        const char *v = std::getenv("SAFE_GOSSIP_AMD_CONCURRENT_INLISTS");
+        e->concurrent_inlists = v && *v && *v != '0';
+    }
     // Per round a node's u32 Statistics deltas grow by at most 32*R_pad + 32
     // (in-degree <= 30 is enforced); fold them into u64 well before a wrap.
     e->fold_every = (uint32_t)std::max<uint64_t>(1, 0xFFFFFFFFull / (32ull * g.rpad + 32) / 2);
@@ -401,15 +406,17 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
              hipEventCreateWithFlags(&e->ev_kr[i], hipEventDisableTiming) == hipSuccess &&
              dalloc(&e->planw[i], words) == hipSuccess;
     }
+    const gs::InListSizes isz = gs::inlist_sizes(e->plan);
     for (int i = 0; i < 2 && ok && !e->shard; ++i) {
         auto &c = e->csr[i];
         ok = hipEventCreateWithFlags(&e->ev_built[i], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&e->ev_read[i], hipEventDisableTiming) == hipSuccess &&
-             dalloc(&c.IN, n) == hipSuccess && dalloc(&c.SIB, n) == hipSuccess &&
-             dalloc(&c.src, n) == hipSuccess && dalloc(&c.tg, n) == hipSuccess &&
-             dalloc(&c.pairs, n) == hipSuccess &&
-             dalloc(&c.scratch, gs::csr_scratch_words(e->plan)) == hipSuccess &&
-             hipMemset(c.SIB, 0, (size_t)n * sizeof(uint4)) == hipSuccess;
+             dalloc(&c.IN8, n) == hipSuccess && dalloc(&c.SIB8, n) == hipSuccess &&
+             dalloc(&c.src, isz.src_words) == hipSuccess && dalloc(&c.tg, n) == hipSuccess &&
+             dalloc(&c.region, isz.region_words) == hipSuccess &&
+             dalloc(&c.scratch, isz.scratch_words) == hipSuccess &&
+             hipMemset(c.scratch, 0, std::max<size_t>(isz.scratch_words, 1) * sizeof(uint32_t)) == hipSuccess &&
+             hipMemset(c.SIB8, 0, std::max<size_t>(n, 1) * sizeof(gs::SibRec)) == hipSuccess;
     }
     ok = ok && dalloc(&e->S[0], sw) == hipSuccess && dalloc(&e->S[1], sw) == hipSuccess &&
          dalloc(&e->flags, 4) == hipSuccess && dalloc(&e->st32, (size_t)4 * n) == hipSuccess &&
@@ -585,11 +592,33 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
         // was the round kernel before this one; runs beside this round's kernel.
         const uint32_t ns = e->round & 1u;
         auto &c = e->csr[ns];
-        GS_HIP(hipStreamWaitEvent(e->cstream, e->ev_read[ns], 0));
-        c.serial = ++e->build_serial;
-        GS_HIP(gs::launch_build_csr(c.tg, e->plan, c.scratch, c.pairs, c.src, c.IN, c.SIB, c.serial,
-                                    e->seed, e->epoch, e->round, e->cstream));
-        GS_HIP(hipEventRecord(e->ev_built[ns], e->cstream));
+        // Built on the round stream right after the round kernel by default:
+        // both are HBM-bound, and the in-list kernels hold whole CUs (1024
+        // threads, >100 KiB LDS), so running them beside the round kernel
+        // measured slower than in sequence.
+        hipStream_t bs = e->concurrent_inlists ? e->cstream : e->stream;
+        GS_HIP(hipStreamWaitEvent(bs, e->ev_read[ns], 0));
+        c.serial = ++e->build_serial & gs::kSerialMask;
+        if (c.serial == 0) {  // 24-bit serial wrapped: no stale SibRec may match a new serial
+            GS_HIP(hipStreamSynchronize(e->stream));
+            for (auto &cc : e->csr) GS_HIP(hipMemsetAsync(cc.SIB8, 0, (size_t)e->g.n * sizeof(gs::SibRec), bs));
+            c.serial = ++e->build_serial & gs::kSerialMask;
+        }
+        gs::InListArgs la{};
+        la.p = e->plan;
+        la.tg = c.tg;
+        la.IN8 = c.IN8;
+        la.SIB8 = c.SIB8;
+        la.src = c.src;
+        la.region = c.region;
+        la.scratch = c.scratch;
+        la.flags = e->flags;
+        la.serial = c.serial;
+        la.seed = e->seed;
+        la.epoch = e->epoch;
+        la.round = e->round;
+        GS_HIP(gs::launch_build_inlists(la, bs));
+        GS_HIP(hipEventRecord(e->ev_built[ns], bs));
     }
     if (report) {
         uint32_t fl[4];
@@ -770,11 +799,11 @@ float gs_last_round_kernel_ms(gs_engine *e) {
 double gs_round_kernel_bytes(const gs_engine *e) {
     // DESIGN.md "Roofline": per (node, rumor slot) 1 B state read + 1 B state
     // write (8 bit-planes) + 3/8 B class planes of each pusher (mean in-degree
-    // 1) + 3/8 B class planes of t(x); per node 64 B: IN and SIB records
-    // (16 + 16), Statistics deltas (16 r + 16 w).
+    // 1) + 3/8 B class planes of t(x); per node 84 B: InRec 32 + SibRec 16 +
+    // target 4 + Statistics deltas (16 r + 16 w).
     if (!e) return 0.0;
     const double n = e->g.n, rp = e->g.rpad;
-    return n * (2.75 * rp + 64.0);
+    return n * (2.75 * rp + 84.0);
 }
 
 }  // extern "C"

@@ -1,0 +1,440 @@
+// gs_inlist.hip -- the in-edge lists of one round: every node's peer choice
+// (Gossiper::next_round's thread_rng().choose, src/gossiper.rs:71, replaced by
+// the injected Philox stream) inverted into, per receiver y, its pushers in
+// ascending index order -- the order in which the reference harness delivers
+// push batches (src/gossiper.rs:217-231 walks (src, dst) pairs by src Id) --
+// and, per source x, the pushers of t(x) ahead of x (what t(x) created from
+// them before it answered x, src/gossip.rs:124-151).  Output records: InRec /
+// SibRec (gs_common.h).
+//
+// Targets are uniform and independent of the source, so the inversion is a
+// bucket sort with a known distribution; no global prefix sum is needed:
+//
+//   binned path (n <= kBinnedMaxNodes), two launches, no atomics on HBM
+//   except one returning add per (chunk, bin) run:
+//     inl_bin  : per chunk of kChunk sources: Philox targets (-> tg), an LDS
+//                counting sort of the chunk by target bin, one reservation
+//                per non-empty bin in that bin's fixed-capacity region, and
+//                coalesced stores of the chunk's sources, bin-run by bin-run
+//     inl_sort : per bin of kBin targets: LDS counting sort by target (16-bit
+//                packed counters), per-target insertion sort by source, and
+//                the InRec / SibRec records (+ the rare in-degree > kInline
+//                tails)
+//   generic path (larger n): the two-stage LDS counting sort through an exact
+//   global CSR (csr_*), same records.
+//
+// Region capacity is kBin + kBin/4 sources per bin (the mean is kBin, the
+// standard deviation sqrt(kBin) = 128): an overflow, like an in-degree > 30,
+// is reported as GS_ERR_DEVICE_LIMIT (flags[2]) rather than handled.
+#include <cstdlib>
+
+#include "gs_kernels.h"
+#include "gs_device.h"
+
+namespace gs {
+
+namespace {
+
+constexpr uint32_t kBinLog = 14;
+constexpr uint32_t kBin = 1u << kBinLog;          // targets per bin
+constexpr uint32_t kBinCap = kBin + kBin / 4;     // region capacity per bin
+constexpr uint32_t kChunk = 16384;                // sources per inl_bin block
+constexpr uint32_t kInlThreads = 1024;
+constexpr uint32_t kBinnedMaxBins = 4096;         // n <= 2^26
+constexpr uint32_t kFlagLimit = 2u;               // flags[2] bit: a device limit was hit
+
+GS_DEV uint32_t target_of(const InListArgs &a, uint32_t x) {
+    return peer_of(a.seed, a.epoch, a.round, x, a.p.n);
+}
+
+// Per-target record emission, shared by both paths.  `lst` holds y's k
+// sources ascending (LDS or global); `first` is where lst[kInline..k) are
+// (already) stored in a.src.
+GS_DEV void emit_target(const InListArgs &a, uint32_t y, const uint32_t *lst, uint32_t k,
+                        uint32_t first) {
+    InRec r;
+    r.first = first;
+    r.k = k;
+#pragma unroll
+    for (uint32_t i = 0; i < kInline; ++i) r.s[i] = i < k ? lst[i] : 0u;
+    a.IN8[y] = r;
+    for (uint32_t j = 1; j < k; ++j) {
+        SibRec sr;
+        sr.tag = ((a.serial & kSerialMask) << 8) | j;
+#pragma unroll
+        for (uint32_t i = 0; i < kSibInline; ++i) sr.e[i] = i < j ? lst[i] : 0u;
+        a.SIB8[lst[j]] = sr;
+    }
+}
+
+// ------------------------------------------------------------ binned path
+// Region of bin b: sources at region[b*kBinCap ...], their targets relative to
+// the bin (u16) at region_lt[b*kBinCap ...].  Each target is drawn once, here:
+// a Philox4x32-10 draw is ~40 quarter-rate multiplies, so redrawing it in
+// inl_sort would cost more than carrying 2 bytes.
+__global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
+    const CsrPlan &p = a.p;
+    uint32_t *stage = sh;                                      // [kChunk] sources by bin
+    uint16_t *stage_lt = reinterpret_cast<uint16_t *>(sh + kChunk);  // [kChunk]
+    uint32_t *cnt = sh + kChunk + kChunk / 2;  // [nb] counts, then cursors
+    uint32_t *off = cnt + p.nb;                // [nb] chunk-local bin starts
+    uint32_t *res = off + p.nb;                // [nb] reserved start in the bin's region
+    __shared__ uint32_t lds_scan[kInlThreads / 64];
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.scratch[p.nb] = 0u;  // tail count; inl_sort runs after
+    for (uint32_t i = threadIdx.x; i < p.nb; i += kInlThreads) cnt[i] = 0u;
+    __syncthreads();
+    const uint32_t lo = blockIdx.x * kChunk;
+    const uint32_t hi = min(p.n, lo + kChunk);
+    for (uint32_t x = lo + threadIdx.x; x < hi; x += kInlThreads) {
+        const uint32_t t = target_of(a, x);
+        a.tg[x] = t;
+        atomicAdd(&cnt[t >> kBinLog], 1u);
+    }
+    __syncthreads();
+    // exclusive scan of the bin counts: thread i owns bins [i*per, i*per + per)
+    const uint32_t per = (p.nb + kInlThreads - 1) / kInlThreads;
+    const uint32_t b0 = threadIdx.x * per;
+    uint32_t sum = 0;
+    for (uint32_t q = 0; q < per; ++q)
+        if (b0 + q < p.nb) sum += cnt[b0 + q];
+    uint32_t total;
+    uint32_t run = block_exclusive_scan_t<kInlThreads>(sum, lds_scan, total);
+    for (uint32_t q = 0; q < per; ++q) {
+        const uint32_t b = b0 + q;
+        if (b >= p.nb) break;
+        const uint32_t c = cnt[b];
+        off[b] = run;
+        uint32_t r0 = 0;
+        if (c) {
+            r0 = atomicAdd(&a.scratch[b], c);
+            if (r0 + c > kBinCap) {
+                atomicOr(&a.flags[2], kFlagLimit);
+                r0 = kBinCap;  // drop this run; the round reports the limit
+            }
+        }
+        res[b] = r0;
+        cnt[b] = run;  // cursor
+        run += c;
+    }
+    __syncthreads();
+    for (uint32_t x = lo + threadIdx.x; x < hi; x += kInlThreads) {
+        const uint32_t t = a.tg[x];  // written above by this thread
+        const uint32_t pos = atomicAdd(&cnt[t >> kBinLog], 1u);
+        stage[pos] = x;
+        stage_lt[pos] = (uint16_t)(t & (kBin - 1u));
+    }
+    __syncthreads();
+    // Consecutive stage entries of one bin go to consecutive region slots; the
+    // bin of entry i is found by a binary search over the chunk-local starts.
+    for (uint32_t i = threadIdx.x; i < hi - lo; i += kInlThreads) {
+        uint32_t lo_b = 0, hi_b = p.nb;  // last bin with off[b] <= i and a non-empty run
+        while (hi_b - lo_b > 1) {
+            const uint32_t mid = (lo_b + hi_b) >> 1;
+            if (off[mid] <= i) lo_b = mid; else hi_b = mid;
+        }
+        // (empty bins share their start with the next bin, so the last bin
+        // whose start is <= i is the one whose run holds entry i)
+        const uint32_t b = lo_b;
+        const uint32_t slot = res[b] + (i - off[b]);
+        if (slot < kBinCap) {
+            a.region[(u64)b * kBinCap + slot] = stage[i];
+            a.region_lt[(u64)b * kBinCap + slot] = stage_lt[i];
+        }
+    }
+}
+
+// Packed 16-bit counter `i` of h (two per word).
+GS_DEV uint32_t half_of(const uint32_t *h, uint32_t i) { return (h[i >> 1] >> ((i & 1u) << 4)) & 0xFFFFu; }
+
+constexpr uint32_t kSortPer = (kBinCap + kInlThreads - 1) / kInlThreads;  // region entries per thread
+
+__global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
+    const CsrPlan &p = a.p;
+    uint32_t *h = sh;                  // [kBin/2] packed per-target counters
+    uint32_t *sorted = sh + kBin / 2;  // [kBinCap]
+    __shared__ uint32_t lds_scan[kInlThreads / 64];
+    const uint32_t b = blockIdx.x;
+    const uint32_t cnt = min(a.scratch[b], kBinCap);
+    const uint32_t t0 = b << kBinLog;
+    const uint32_t nodes = min(kBin, p.n - t0);
+    // the bin's entries, held in registers (coalesced loads, issued first)
+    uint32_t ex[kSortPer], el[kSortPer];
+#pragma unroll
+    for (uint32_t q = 0; q < kSortPer; ++q) {
+        const uint32_t i = threadIdx.x + q * kInlThreads;
+        const bool ok = i < cnt;
+        ex[q] = ok ? a.region[(u64)b * kBinCap + i] : 0u;
+        el[q] = ok ? (uint32_t)a.region_lt[(u64)b * kBinCap + i] : kNone;
+    }
+    for (uint32_t i = threadIdx.x; i < kBin / 2; i += kInlThreads) h[i] = 0u;
+    __syncthreads();
+    if (threadIdx.x == 0) a.scratch[b] = 0u;  // ready for the next build of this set
+#pragma unroll
+    for (uint32_t q = 0; q < kSortPer; ++q)
+        if (el[q] != kNone) atomicAdd(&h[el[q] >> 1], 1u << ((el[q] & 1u) << 4));
+    __syncthreads();
+    // exclusive scan over the kBin targets, kBin/kInlThreads per thread
+    constexpr uint32_t per = kBin / kInlThreads;
+    const uint32_t i0 = threadIdx.x * per;
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < per; ++q) sum += half_of(h, i0 + q);
+    uint32_t total;
+    uint32_t run = block_exclusive_scan_t<kInlThreads>(sum, lds_scan, total);
+#pragma unroll
+    for (uint32_t q = 0; q < per; q += 2) {
+        const uint32_t c0 = half_of(h, i0 + q), c1 = half_of(h, i0 + q + 1);
+        h[(i0 + q) >> 1] = run | ((run + c0) << 16);
+        run += c0 + c1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < kSortPer; ++q) {
+        if (el[q] != kNone) {
+            const uint32_t shf = (el[q] & 1u) << 4;
+            const uint32_t old = atomicAdd(&h[el[q] >> 1], 1u << shf);
+            sorted[(old >> shf) & 0xFFFFu] = ex[q];
+        }
+    }
+    __syncthreads();
+    // counters are now the ends of each target's run; lanes take consecutive
+    // targets so the InRec stores are coalesced
+    for (uint32_t lt = threadIdx.x; lt < nodes; lt += kInlThreads) {
+        const uint32_t e = half_of(h, lt);
+        const uint32_t s = lt ? half_of(h, lt - 1) : 0u;
+        uint32_t *lst = sorted + s;
+        const uint32_t k = e - s;
+        for (uint32_t q = 1; q < k; ++q) {  // Poisson(1)-sized: insertion sort
+            const uint32_t v = lst[q];
+            uint32_t r = q;
+            while (r > 0 && lst[r - 1] > v) {
+                lst[r] = lst[r - 1];
+                --r;
+            }
+            lst[r] = v;
+        }
+        uint32_t first = 0;
+        if (k > kInline) {
+            first = atomicAdd(&a.scratch[p.nb], k - kInline);
+            if (first + (k - kInline) > p.tailcap) {
+                atomicOr(&a.flags[2], kFlagLimit);
+                first = 0;
+            } else {
+                for (uint32_t j = kInline; j < k; ++j) a.src[first + j - kInline] = lst[j];
+            }
+        }
+        emit_target(a, t0 + lt, lst, k, first);
+    }
+}
+
+// ------------------------------------------------------------ generic path
+// Two-stage counting sort of the n edges (x -> tg[x]) by target through an
+// exact CSR (src[n]), for networks beyond the binned path's bin count:
+//   bin_count   : per source chunk, an LDS histogram over target bins -> M
+//   col_scan    : per bin, exclusive prefix over chunks; bin totals
+//   scan_small  : exclusive prefix of the bin totals -> bin bases
+//   bin_scatter : (local target, source) pairs into their bin's range
+//   bin_sort    : per bin, LDS counting sort by local target -> src[] with each
+//                 node's sources ascending, then the records
+__global__ __launch_bounds__(256) void csr_bin_count(InListArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+    const CsrPlan &p = a.p;
+    for (uint32_t i = threadIdx.x; i < p.nb; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    const u64 lo = (u64)blockIdx.x * p.chunk;
+    const u64 hi = min((u64)p.n, lo + p.chunk);
+    for (u64 x = lo + threadIdx.x; x < hi; x += blockDim.x) {
+        const uint32_t t = target_of(a, (uint32_t)x);
+        a.tg[x] = t;
+        atomicAdd(&hist[t >> p.logbin], 1u);
+    }
+    __syncthreads();
+    uint32_t *M = a.scratch;
+    for (uint32_t i = threadIdx.x; i < p.nb; i += blockDim.x) M[(u64)blockIdx.x * p.nb + i] = hist[i];
+}
+
+__global__ __launch_bounds__(256) void csr_col_scan(InListArgs a) {
+    const CsrPlan &p = a.p;
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= p.nb) return;
+    uint32_t *M = a.scratch;
+    uint32_t *tot = M + (size_t)p.ba * p.nb;
+    uint32_t run = 0;
+    for (uint32_t c = 0; c < p.ba; ++c) {
+        const uint32_t v = M[(u64)c * p.nb + b];
+        M[(u64)c * p.nb + b] = run;
+        run += v;
+    }
+    tot[b] = run;
+}
+
+// Exclusive scan of the bin totals (one block).
+__global__ __launch_bounds__(kScanBlock) void csr_scan_small(InListArgs a) {
+    __shared__ uint32_t lds[kScanBlock / 64];
+    const CsrPlan &p = a.p;
+    const uint32_t *in = a.scratch + (size_t)p.ba * p.nb;
+    uint32_t *out = a.scratch + (size_t)p.ba * p.nb + p.nb;
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < p.nb; base += kScanBlock) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < p.nb ? in[i] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_exclusive_scan(v, lds, tot);
+        if (i < p.nb) out[i] = carry + ex;
+        carry += tot;
+    }
+}
+
+__global__ __launch_bounds__(256) void csr_bin_scatter(InListArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
+    const CsrPlan &p = a.p;
+    const uint32_t *M = a.scratch;
+    const uint32_t *base = a.scratch + (size_t)p.ba * p.nb + p.nb;
+    u64 *pairs = reinterpret_cast<u64 *>(a.region);
+    for (uint32_t i = threadIdx.x; i < p.nb; i += blockDim.x) cur[i] = base[i] + M[(u64)blockIdx.x * p.nb + i];
+    __syncthreads();
+    const u64 lo = (u64)blockIdx.x * p.chunk;
+    const u64 hi = min((u64)p.n, lo + p.chunk);
+    const uint32_t lm = p.bin - 1u;
+    for (u64 x = lo + threadIdx.x; x < hi; x += blockDim.x) {
+        const uint32_t t = a.tg[x];
+        const uint32_t pos = atomicAdd(&cur[t >> p.logbin], 1u);
+        pairs[pos] = ((u64)(t & lm) << 32) | (uint32_t)x;
+    }
+}
+
+__global__ __launch_bounds__(256) void csr_bin_sort(InListArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t h[];  // [bin] + 16 scan words
+    const CsrPlan &p = a.p;
+    const u64 *pairs = reinterpret_cast<const u64 *>(a.region);
+    const uint32_t *tot = a.scratch + (size_t)p.ba * p.nb;
+    const uint32_t *base = tot + p.nb;
+    uint32_t *lds_scan = h + p.bin;
+    const uint32_t b = blockIdx.x;
+    const uint32_t start = base[b], cnt = tot[b];
+    const uint32_t nb0 = b << p.logbin;
+    const uint32_t nodes = min(p.bin, p.n - nb0);
+    for (uint32_t i = threadIdx.x; i < p.bin; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) atomicAdd(&h[pairs[start + i] >> 32], 1u);
+    __syncthreads();
+    const uint32_t per = p.bin / blockDim.x;
+    const uint32_t i0 = threadIdx.x * per;
+    uint32_t sum = 0;
+    for (uint32_t q = 0; q < per; ++q) sum += h[i0 + q];
+    uint32_t total;
+    uint32_t run = block_exclusive_scan(sum, lds_scan, total);
+    for (uint32_t q = 0; q < per; ++q) {
+        const uint32_t v = h[i0 + q];
+        h[i0 + q] = run;
+        run += v;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+        const u64 pr = pairs[start + i];
+        const uint32_t pos = atomicAdd(&h[(uint32_t)(pr >> 32)], 1u);
+        a.src[start + pos] = (uint32_t)pr;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nodes; i += blockDim.x) {
+        const uint32_t s = start + (i ? h[i - 1] : 0u), e = start + h[i];
+        uint32_t *lst = a.src + s;
+        const uint32_t k = e - s;
+        for (uint32_t q = 1; q < k; ++q) {
+            const uint32_t v = lst[q];
+            uint32_t r = q;
+            while (r > 0 && lst[r - 1] > v) {
+                lst[r] = lst[r - 1];
+                --r;
+            }
+            lst[r] = v;
+        }
+        emit_target(a, nb0 + i, lst, k, s + kInline);  // src[first + i - kInline] = lst[i]
+    }
+}
+
+// Test hook: SAFE_GOSSIP_AMD_GENERIC_INLISTS=1 forces the generic path.
+bool getenv_generic_inlists() {
+    const char *v = std::getenv("SAFE_GOSSIP_AMD_GENERIC_INLISTS");
+    return v && *v && *v != '0';
+}
+
+}  // namespace
+
+CsrPlan csr_plan(uint32_t n) {
+    CsrPlan p{};
+    p.n = n;
+    const uint32_t nb_binned = (uint32_t)(((u64)n + kBin - 1) / kBin);
+    if (nb_binned <= kBinnedMaxBins && !getenv_generic_inlists()) {
+        p.binned = 1;
+        p.bin = kBin;
+        p.logbin = kBinLog;
+        p.nb = nb_binned;
+        p.ba = (uint32_t)(((u64)n + kChunk - 1) / kChunk);
+        p.chunk = kChunk;
+        p.tailcap = n / 32u + 1024u;
+        return p;
+    }
+    uint32_t bin = 4096;
+    while ((u64)bin * 16384u < n) bin <<= 1;  // <= 16384 bins: bin_count LDS <= 64 KiB
+    p.bin = bin;
+    p.logbin = 0;
+    while ((1u << p.logbin) < bin) ++p.logbin;
+    p.nb = (uint32_t)(((u64)n + bin - 1) / bin);
+    uint32_t ba = (uint32_t)(((u64)n + 4095) / 4096);
+    p.ba = ba < 256u ? (ba ? ba : 1u) : 256u;
+    p.chunk = (uint32_t)(((u64)n + p.ba - 1) / p.ba);
+    p.tailcap = 0;
+    return p;
+}
+
+InListSizes inlist_sizes(const CsrPlan &p) {
+    InListSizes z{};
+    if (p.binned) {
+        z.src_words = p.tailcap;
+        z.region_words = (size_t)p.nb * kBinCap * 3 / 2;  // sources (u32) + local targets (u16)
+        z.scratch_words = (size_t)p.nb + 1;  // fill[nb], tailcnt
+    } else {
+        z.src_words = p.n;
+        z.region_words = 2 * (size_t)p.n;  // u64 pairs
+        z.scratch_words = (size_t)p.ba * p.nb + 2 * (size_t)p.nb;
+    }
+    return z;
+}
+
+hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
+    const CsrPlan &p = a.p;
+    if (p.n == 0) return hipSuccess;
+    if (p.binned) {
+        const size_t lds_bin = ((size_t)3 * p.nb + kChunk + kChunk / 2) * sizeof(uint32_t);
+        const size_t lds_sort = ((size_t)kBin / 2 + kBinCap) * sizeof(uint32_t);
+        hipError_t e = hipFuncSetAttribute((const void *)inl_bin, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds_bin);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void *)inl_sort, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds_sort);
+        if (e != hipSuccess) return e;
+        InListArgs ab = a;
+        ab.region_lt = reinterpret_cast<uint16_t *>(a.region + (size_t)p.nb * kBinCap);
+        hipLaunchKernelGGL(inl_bin, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
+        hipLaunchKernelGGL(inl_sort, dim3(p.nb), dim3(kInlThreads), lds_sort, s, ab);
+        return hipGetLastError();
+    }
+    const size_t lds_nb = (size_t)p.nb * sizeof(uint32_t);
+    hipLaunchKernelGGL(csr_bin_count, dim3(p.ba), dim3(256), lds_nb, s, a);
+    hipLaunchKernelGGL(csr_col_scan, dim3((p.nb + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(csr_scan_small, dim3(1), dim3(kScanBlock), 0, s, a);
+    hipLaunchKernelGGL(csr_bin_scatter, dim3(p.ba), dim3(256), lds_nb, s, a);
+    const size_t lds_sort = ((size_t)p.bin + 16) * sizeof(uint32_t);
+    if (lds_sort > 65536) {  // n > 2^28: bins of 32768 nodes need 128 KiB of the 160 KiB LDS
+        hipError_t e = hipFuncSetAttribute((const void *)csr_bin_sort,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sort);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(csr_bin_sort, dim3(p.nb), dim3(256), lds_sort, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace gs

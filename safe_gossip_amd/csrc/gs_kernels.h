@@ -7,9 +7,10 @@ namespace gs {
 struct RoundArgs {
     const u64 *Scur;          // state planes, round t (post phase 0)
     u64 *Snext;               // state planes, round t+1 (post phase 0)
-    const uint4 *IN;          // round t, per node y: {first edge, in-degree, s0, s1}
-    const uint4 *SIB;         // round t, per source x: {serial, rank in in(t(x)), e0, e1}
-    const uint32_t *src;      // round t in-edge sources, ascending per target
+    const InRec *IN8;         // round t, per node y: in-list record (gs_common.h)
+    const SibRec *SIB8;       // round t, per source x: pushers of t(x) ahead of x
+    const uint4 *IN;          // shard engine: per node {first edge, k | zi<<16, e0, e1}
+    const uint32_t *src;      // round t in-list tails (shard engine: receive rows)
     const uint32_t *tg;       // round t targets
     uint32_t serial;          // build serial of the round-t lists (SIB validity)
     uint32_t *st32;           // [n][4] u32 Statistics deltas (empty_pull, empty_push,
@@ -45,24 +46,41 @@ struct RoundArgs {
 // 3 = observe without pending deliveries.
 hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s);
 
-// Plan of the two-stage counting sort that builds the in-edge CSR.
+// Plan of the in-list build (gs_inlist.hip).
 struct CsrPlan {
     uint32_t n;       // nodes (= edges)
-    uint32_t bin;     // target nodes per bin (power of two >= 4096)
+    uint32_t binned;  // 1: binned two-launch path; 0: generic CSR path
+    uint32_t bin;     // target nodes per bin (power of two)
     uint32_t logbin;
-    uint32_t nb;      // bins (<= 16384)
-    uint32_t ba;      // source chunks (<= 256)
+    uint32_t nb;      // bins
+    uint32_t ba;      // source chunks
     uint32_t chunk;   // sources per chunk
+    uint32_t tailcap; // binned: capacity of the in-degree > kInline tail list
 };
 CsrPlan csr_plan(uint32_t n);
-size_t csr_scratch_words(const CsrPlan &p);  // u32 words of scratch
+struct InListSizes {
+    size_t src_words, region_words, scratch_words;  // u32 words
+};
+InListSizes inlist_sizes(const CsrPlan &p);
 
-// Peer choices of `round` (into tg) and their in-edge lists (src, IN, SIB
-// tagged with `serial`).  Depends on nothing but the Philox stream, so it runs
-// on its own stream concurrently with the round kernel of the round before.
-hipError_t launch_build_csr(uint32_t *tg, const CsrPlan &p, uint32_t *scratch, u64 *pairs,
-                            uint32_t *src, uint4 *IN, uint4 *SIB, uint32_t serial,
-                            uint64_t seed, uint32_t epoch, uint32_t round, hipStream_t s);
+struct InListArgs {
+    CsrPlan p;
+    uint32_t *tg;       // [n] targets of the round
+    InRec *IN8;         // [n]
+    SibRec *SIB8;       // [n]
+    uint32_t *src;      // tails (binned) or the full CSR (generic)
+    uint32_t *region;   // binned: [nb][cap] sources by bin; generic: u64 pairs[n]
+    uint16_t *region_lt;  // binned: [nb][cap] their targets within the bin (set internally)
+    uint32_t *scratch;  // binned: fill[nb], tailcnt (zero between builds); generic: M, tot, base
+    uint32_t *flags;    // flags[2]: device-limit bit
+    uint32_t serial;
+    uint64_t seed;
+    uint32_t epoch, round;
+};
+// Peer choices of `round` (into tg) and their in-lists (IN8, SIB8 tagged with
+// `serial`).  Depends on nothing but the Philox stream, so it runs on its own
+// stream concurrently with the round kernel of the round before.
+hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s);
 hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, hipStream_t s);
 
 // ---------------------------------------------------------------- shards

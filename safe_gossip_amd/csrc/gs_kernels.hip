@@ -28,6 +28,21 @@
 
 namespace gs {
 
+// Words of planes one 256-lane block owns (its records are contiguous).
+constexpr uint32_t kBlockWords = 256u * kPlanes;
+constexpr uint32_t kStageIters = kBlockWords / 2u / 256u;  // uint4 loads per thread
+
+// Gathers issued in the first batch: pushers (in-degree is Poisson(1): <= 3
+// for 98% of nodes) and pushers of t(x) ahead of x (rank <= 2 for 98.6%).
+#ifndef GS_BATCH_K
+#define GS_BATCH_K 3
+#endif
+#ifndef GS_BATCH_E
+#define GS_BATCH_E 2
+#endif
+static_assert(GS_BATCH_E <= kSibInline, "SIB records hold kSibInline pushers");
+constexpr uint32_t kBatchK = GS_BATCH_K;
+constexpr uint32_t kBatchE = GS_BATCH_E;
 
 // Receiver-side state of phases 1-2 at x for one segment.  The transition
 // path keeps one bit-sliced counter of the recorded counters that vote ">= own"
@@ -116,52 +131,94 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     const uint32_t x = L.x;
     const u64 *__restrict__ S = a.Scur;
 
-    // ---- coalesced per-node metadata and own round-t planes
-    uint4 in = {0, 0, 0, 0}, sb = {0, 0, 0, 0};
-    uint32_t z = 0, zi = 0xFFFFu;
-    if (DELIVER && valid) {
-        in = a.IN[x];   // {first edge, k, s0, s1}  (SHARD: {first, k|zi<<16, e0, e1})
-        if (SHARD) {
-            zi = in.y >> 16;
-            in.y &= 0xFFFFu;
-        } else {
-            sb = a.SIB[x];  // {serial, rank of x in in(z), e0, e1}; stale unless rank >= 1
-            z = a.tg[x];    // t_t(x)
-        }
-    }
-    u64 P[kPlanes];
-#pragma unroll
-    for (int p = 0; p < kPlanes; ++p) {
-        u64 v = valid ? S[L.plane_index(p)] : 0ull;
-        P[p] = SMALL ? ((v >> L.sh) & L.m) : v;
-    }
+    // ---- own round-t planes: the block's records are one contiguous range
+    // (W <= 256), loaded first with 16-byte coalesced loads (clamped, so every
+    // load is unconditional) and transposed through LDS below, instead of
+    // eight strided 8-byte loads per lane.
+    __shared__ __attribute__((aligned(16))) u64 stage[kBlockWords];
+    const uint32_t npu_blk = SMALL ? (1u << g.lognpu) : 1u;
+    const u64 blk_base = (u64)blockIdx.x * (kBlockWords / npu_blk);
+    const uint32_t blk_v4 = (uint32_t)min((u64)(kBlockWords / npu_blk),
+                                          g.units * kPlanes * (SMALL ? 1u : g.W) - blk_base) / 2u;
+    static_assert(kStageIters == 4, "stage loads are unrolled by hand");
+    const uint4 *src4 = reinterpret_cast<const uint4 *>(S + blk_base);
+    const uint4 st0 = src4[min(threadIdx.x, blk_v4 - 1u)];
+    const uint4 st1 = src4[min(threadIdx.x + 256u, blk_v4 - 1u)];
+    const uint4 st2 = src4[min(threadIdx.x + 512u, blk_v4 - 1u)];
+    const uint4 st3 = src4[min(threadIdx.x + 768u, blk_v4 - 1u)];
 
-    // ---- the random gathers, all issued together
-    uint32_t k = 0, r = 0;
-    Cls q0 = {0, 0, 0}, q1 = {0, 0, 0}, qz = {0, 0, 0}, e0 = {0, 0, 0}, e1 = {0, 0, 0};
-    if (DELIVER && valid) {
-        k = in.y;
-        r = sb.x == a.serial ? sb.y : 0u;
+    // ---- coalesced per-node metadata (level 1)
+    uint4 in = {0, 0, 0, 0};   // SHARD: {first, k|zi<<16, e0, e1}
+    InRec in8 = {};            // {first (tail), k, s0..s5}
+    SibRec sb8 = {};           // {serial<<8 | rank of x in in(z), e0..e2}; stale unless rank >= 1
+    uint32_t z = x, zi = 0xFFFFu, k = 0, r = 0;
+    if (DELIVER) {
+        if (SHARD) {
+            if (valid) {
+                in = a.IN[x];
+                zi = in.y >> 16;
+                k = in.y & 0xFFFFu;
+            }
+        } else {
+            in8 = a.IN8[x];  // x = 0 on invalid lanes: a harmless valid address
+            sb8 = a.SIB8[x];
+            z = a.tg[x];  // t_t(x)
+            k = valid ? in8.k : 0u;
+            r = (valid && (sb8.tag >> 8) == (a.serial & kSerialMask)) ? (sb8.tag & 0xFFu) : 0u;
+        }
 #ifdef GS_EXP_NO_PUSHERS
         k = 0;
 #endif
 #ifdef GS_EXP_NO_ZPUSHERS
         r = 0;
 #endif
+#ifdef GS_EXP_NO_GATHER
+        k = 0;
+        r = 0;
+        z = x;
+#endif
+    }
+
+    // ---- the random gathers (level 2), issued together before the LDS
+    // barrier: the first kBatchK pushers, t(x), and the first kBatchE pushers
+    // of t(x) ahead of x.  Slots past k / r load x's own row (an L2 hit) so no
+    // load is conditional.  Rarer deeper in-lists are walked afterwards.
+    Cls q[kBatchK], e[kBatchE], qz = {0, 0, 0};
+#pragma unroll
+    for (uint32_t i = 0; i < kBatchK; ++i) q[i] = {0, 0, 0};
+#pragma unroll
+    for (uint32_t i = 0; i < kBatchE; ++i) e[i] = {0, 0, 0};
+    if (DELIVER) {
         if (SHARD) {
-            if (k > 0) q0 = L.load_row3(a.recvA, in.z);
-            if (k > 1) q1 = L.load_row3(a.recvA, in.w);
-            const uint32_t sp = a.spos_cur[x];  // the pull row z returned to x
-            qz.c = a.recvB[L.row_index(sp, 2, 0)];
-            qz.a0 = a.recvB[L.row_index(sp, 2, 1)];
-            qz.a1 = 0;
+            if (valid) {
+                if (k > 0) q[0] = L.load_row3(a.recvA, in.z);
+                if (k > 1) q[1] = L.load_row3(a.recvA, in.w);
+                const uint32_t sp = a.spos_cur[x];  // the pull row z returned to x
+                qz.c = a.recvB[L.row_index(sp, 2, 0)];
+                qz.a0 = a.recvB[L.row_index(sp, 2, 1)];
+                qz.a1 = 0;
+            }
         } else {
-            if (k > 0) q0 = L.load_cls(S, in.z);
-            if (k > 1) q1 = L.load_cls(S, in.w);
+#pragma unroll
+            for (uint32_t i = 0; i < kBatchK; ++i) q[i] = L.load_cls(S, i < k ? in8.s[i] : x);
             qz = L.load_cls(S, z);
-            if (r > 0) e0 = L.load_cls(S, sb.z);
-            if (r > 1) e1 = L.load_cls(S, sb.w);
+#pragma unroll
+            for (uint32_t i = 0; i < kBatchE; ++i) e[i] = L.load_cls(S, i < r ? sb8.e[i] : x);
         }
+    }
+    {
+        uint4 *dst4 = reinterpret_cast<uint4 *>(stage);
+        dst4[threadIdx.x] = st0;
+        dst4[threadIdx.x + 256u] = st1;
+        dst4[threadIdx.x + 512u] = st2;
+        dst4[threadIdx.x + 768u] = st3;
+    }
+    __syncthreads();
+    u64 P[kPlanes];
+#pragma unroll
+    for (int p = 0; p < kPlanes; ++p) {
+        u64 v = valid ? stage[L.plane_index(p) - blk_base] : 0ull;
+        P[p] = SMALL ? ((v >> L.sh) & L.m) : v;
     }
 
     const u64 isC = P[0], a0 = P[1], a1 = P[2];
@@ -182,24 +239,23 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         if (SHARD) {
             // zi = index of t(x) among x's pushers (0xFFFF: t(x) did not push to x)
             zin = zi != 0xFFFFu;
-            if (k > 0) rv.push(q0, 0, k, zi != 0);
-            if (k > 1) rv.push(q1, 1, k, zi != 1);
+            if (k > 0) rv.push(q[0], 0, k, zi != 0);
+            if (k > 1) rv.push(q[1], 1, k, zi != 1);
             for (uint32_t i = 2; i < k; ++i) rv.push(L.load_row3(a.recvA, a.src[in.x + i]), i, k, zi != i);
             // pull row code (b0, b1): 01 counter 1, 10 counter 2, 11 counter 255
             pv2 = qz.a0 & ~qz.c;
             pvB = qz.c ^ qz.a0;
             pCl = qz.c & qz.a0;
         } else {
-            if (k > 0) {
-                zin |= in.z == z;
-                rv.push(q0, 0, k, in.z != z);
+#pragma unroll
+            for (uint32_t i = 0; i < kBatchK; ++i) {
+                if (i < k) {
+                    zin |= in8.s[i] == z;
+                    rv.push(q[i], i, k, in8.s[i] != z);
+                }
             }
-            if (k > 1) {
-                zin |= in.w == z;
-                rv.push(q1, 1, k, in.w != z);
-            }
-            for (uint32_t i = 2; i < k; ++i) {  // in-degree >= 3 (8% of nodes)
-                const uint32_t s = a.src[in.x + i];
+            for (uint32_t i = kBatchK; i < k; ++i) {  // in-degree > kBatchK (1.9% of nodes)
+                const uint32_t s = i < kInline ? pick_inline(in8.s, i) : a.src[in8.first + (i - kInline)];
                 zin |= s == z;
                 rv.push(L.load_cls(S, s), i, k, s != z);
             }
@@ -208,11 +264,20 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             const u64 zB = ~qz.c & (qz.a0 | qz.a1);
             const u64 zC = qz.c & ~(qz.a0 & qz.a1);
             u64 pnot = ~qz.c & ~qz.a0 & ~qz.a1 & L.m, pB = 0, pC = 0;
-            if (r > 0) sibling(e0, pnot, pB, pC);
-            if (r > 1) sibling(e1, pnot, pB, pC);
-            if (r > 2 && pnot) {
-                const uint32_t zb = a.IN[z].x;  // rare: rank >= 3
-                for (uint32_t i = 2; i < r && pnot; ++i) sibling(L.load_cls(S, a.src[zb + i]), pnot, pB, pC);
+#pragma unroll
+            for (uint32_t i = 0; i < kBatchE; ++i)
+                if (i < r) sibling(e[i], pnot, pB, pC);
+            if (r > kBatchE && pnot) {  // rank > kBatchE (rare)
+                for (uint32_t i = kBatchE; i < min(r, kSibInline); ++i)
+                    sibling(L.load_cls(S, pick_sib(sb8.e, i)), pnot, pB, pC);
+                if (r > kSibInline && pnot) {  // rank > 3: 0.2% of nodes
+                    const InRec zin8 = a.IN8[z];
+                    for (uint32_t i = kSibInline; i < r && pnot; ++i) {
+                        const uint32_t s = i < kInline ? pick_inline(zin8.s, i)
+                                                       : a.src[zin8.first + (i - kInline)];
+                        sibling(L.load_cls(S, s), pnot, pB, pC);
+                    }
+                }
             }
             pv2 = zB & qz.a1 & ~qz.a0;
             pvB = zB | pB;  // counter 1 (created entries: 1) or 2
@@ -376,20 +441,27 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
 #pragma unroll
     for (int i = 0; i < 5; ++i) N[3 + i] = ((Bn | BC) & nr[i]) | (CC & rib[i]);
 
-    // ---- write round-(t+1) planes
+    // ---- write round-(t+1) planes (through LDS, 16-byte coalesced stores)
+    uint32_t live_new = valid ? popc(Bn | Cn) : 0u;
+    if (!SMALL) live_new = group_sum(live_new, g.W);
+    const int blk_live = __syncthreads_or(live_new != 0u);  // also: every lane is done reading stage
     if (SMALL) {
         const uint32_t npu = 1u << g.lognpu;
 #pragma unroll
         for (int p = 0; p < kPlanes; ++p) {
             u64 v = valid ? ((N[p] & L.m) << L.sh) : 0ull;
             for (uint32_t o = 1; o < npu; o <<= 1) v |= __shfl_xor(v, (int)o, 64);
-            if (valid && (x & (npu - 1u)) == 0) a.Snext[L.plane_index(p)] = v;
+            if (valid && (x & (npu - 1u)) == 0) stage[L.plane_index(p) - blk_base] = v;
         }
-    } else {
-        if (valid) {
+    } else if (valid) {
 #pragma unroll
-            for (int p = 0; p < kPlanes; ++p) a.Snext[L.plane_index(p)] = N[p];
-        }
+        for (int p = 0; p < kPlanes; ++p) stage[L.plane_index(p) - blk_base] = N[p];
+    }
+    __syncthreads();
+    {
+        const uint4 *src4 = reinterpret_cast<const uint4 *>(stage);
+        uint4 *dst4 = reinterpret_cast<uint4 *>(a.Snext + blk_base);
+        for (uint32_t i = threadIdx.x; i < blk_v4; i += blockDim.x) dst4[i] = src4[i];
     }
     if (SHARD && valid) {  // push row of round t+1: the class planes, to owner(t_{t+1}(x))
         const uint32_t sp = a.spos_next[x];
@@ -398,9 +470,6 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     }
 
     // ---- push list + Statistics (src/gossip.rs:80,103-111)
-    uint32_t live_new = valid ? popc(Bn | Cn) : 0u;
-    if (!SMALL) live_new = group_sum(live_new, g.W);
-    const int blk_live = __syncthreads_or(live_new != 0u);
     if (blockIdx.x == 0 && threadIdx.x == 0)  // slot of round t, read by the host already
         __hip_atomic_store(&a.flags[(a.round_new + 1u) & 1u], 0u, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -457,183 +526,6 @@ hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, hipStream_t 
     if (words == 0) return hipSuccess;
     hipLaunchKernelGGL(stats_fold, dim3((uint32_t)((words + 255) / 256)), dim3(256), 0, s, st32, st64,
                        words);
-    return hipGetLastError();
-}
-
-// ------------------------------------------------------------ in-edge lists
-// Two-stage counting sort of the n edges (x -> tg[x]) by target, with no
-// global atomics (targets are uniform, so fixed-width target bins balance):
-//   bin_count   : per source chunk, an LDS histogram over target bins
-//                 -> M[chunk][bin]
-//   col_scan    : per bin, exclusive prefix over chunks; bin totals
-//   scan (1 blk): exclusive prefix of the bin totals -> bin bases
-//   bin_scatter : (local target, source) pairs into their bin's range
-//                 (runs of ~chunk/nb pairs per chunk and bin)
-//   bin_sort    : per bin, LDS counting sort by local target -> src[] with each
-//                 node's sources ascending (the order Gossip::receive sees its
-//                 pushers in, src/gossiper.rs:217), then the per-node records
-//                 IN[y] = {first edge, in-degree, s0, s1}          (node order)
-//                 SIB[x] = {serial, rank of x in in(t(x)), e0, e1}  (per source,
-//                          written only when rank >= 1; stale serial = rank 0)
-CsrPlan csr_plan(uint32_t n) {
-    CsrPlan p{};
-    p.n = n;
-    uint32_t bin = 4096;
-    while ((u64)bin * 16384u < n) bin <<= 1;  // <= 16384 bins: bin_count LDS <= 64 KiB
-    p.bin = bin;
-    p.logbin = 0;
-    while ((1u << p.logbin) < bin) ++p.logbin;
-    p.nb = (uint32_t)(((u64)n + bin - 1) / bin);
-    uint32_t ba = (uint32_t)(((u64)n + 4095) / 4096);
-    p.ba = ba < 256u ? (ba ? ba : 1u) : 256u;
-    p.chunk = (uint32_t)(((u64)n + p.ba - 1) / p.ba);
-    return p;
-}
-
-size_t csr_scratch_words(const CsrPlan &p) {
-    // M[ba][nb] + tot[nb] + base[nb] (u32 words); pairs are separate (u64 [n])
-    return (size_t)p.ba * p.nb + 2 * (size_t)p.nb;
-}
-
-// Also draws the round's peer choices (Gossiper::next_round's
-// thread_rng().choose, src/gossiper.rs:71, as the injected Philox stream).
-__global__ __launch_bounds__(256) void csr_bin_count(uint32_t *__restrict__ tg, CsrPlan p,
-                                                     uint32_t *M, uint64_t seed, uint32_t epoch,
-                                                     uint32_t round) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
-    for (uint32_t i = threadIdx.x; i < p.nb; i += blockDim.x) hist[i] = 0;
-    __syncthreads();
-    const u64 lo = (u64)blockIdx.x * p.chunk;
-    const u64 hi = min((u64)p.n, lo + p.chunk);
-    for (u64 x = lo + threadIdx.x; x < hi; x += blockDim.x) {
-        const uint32_t t = peer_of(seed, epoch, round, (uint32_t)x, p.n);
-        tg[x] = t;
-        atomicAdd(&hist[t >> p.logbin], 1u);
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < p.nb; i += blockDim.x) M[(u64)blockIdx.x * p.nb + i] = hist[i];
-}
-
-__global__ __launch_bounds__(256) void csr_col_scan(uint32_t *M, CsrPlan p, uint32_t *tot) {
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= p.nb) return;
-    uint32_t run = 0;
-    for (uint32_t c = 0; c < p.ba; ++c) {
-        const uint32_t v = M[(u64)c * p.nb + b];
-        M[(u64)c * p.nb + b] = run;
-        run += v;
-    }
-    tot[b] = run;
-}
-
-// Exclusive scan of a small array (one block).
-__global__ __launch_bounds__(kScanBlock) void scan_small(const uint32_t *in, uint32_t *out, uint32_t m) {
-    __shared__ uint32_t lds[kScanBlock / 64];
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < m; base += kScanBlock) {
-        const uint32_t i = base + threadIdx.x;
-        const uint32_t v = i < m ? in[i] : 0u;
-        uint32_t tot;
-        const uint32_t ex = block_exclusive_scan(v, lds, tot);
-        if (i < m) out[i] = carry + ex;
-        carry += tot;
-    }
-}
-
-__global__ __launch_bounds__(256) void csr_bin_scatter(const uint32_t *__restrict__ tg, CsrPlan p,
-                                                       const uint32_t *__restrict__ M,
-                                                       const uint32_t *__restrict__ base, u64 *pairs) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
-    for (uint32_t i = threadIdx.x; i < p.nb; i += blockDim.x)
-        cur[i] = base[i] + M[(u64)blockIdx.x * p.nb + i];
-    __syncthreads();
-    const u64 lo = (u64)blockIdx.x * p.chunk;
-    const u64 hi = min((u64)p.n, lo + p.chunk);
-    const uint32_t lm = p.bin - 1u;
-    for (u64 x = lo + threadIdx.x; x < hi; x += blockDim.x) {
-        const uint32_t t = tg[x];
-        const uint32_t pos = atomicAdd(&cur[t >> p.logbin], 1u);
-        pairs[pos] = ((u64)(t & lm) << 32) | (uint32_t)x;
-    }
-}
-
-__global__ __launch_bounds__(256) void csr_bin_sort(const u64 *__restrict__ pairs, CsrPlan p,
-                                                    const uint32_t *__restrict__ base,
-                                                    const uint32_t *__restrict__ tot, uint32_t *src,
-                                                    uint4 *IN, uint4 *SIB, uint32_t serial) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t h[];  // [bin] + 16 scan words
-    uint32_t *lds_scan = h + p.bin;
-    const uint32_t b = blockIdx.x;
-    const uint32_t start = base[b], cnt = tot[b];
-    const uint32_t nb0 = b << p.logbin;
-    const uint32_t nodes = min(p.bin, p.n - nb0);
-    for (uint32_t i = threadIdx.x; i < p.bin; i += blockDim.x) h[i] = 0;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) atomicAdd(&h[pairs[start + i] >> 32], 1u);
-    __syncthreads();
-    // exclusive scan of h[0..bin): each thread owns bin/256 consecutive counters
-    const uint32_t per = p.bin / blockDim.x;
-    const uint32_t i0 = threadIdx.x * per;
-    uint32_t sum = 0;
-    for (uint32_t q = 0; q < per; ++q) sum += h[i0 + q];
-    uint32_t total;
-    uint32_t run = block_exclusive_scan(sum, lds_scan, total);
-    for (uint32_t q = 0; q < per; ++q) {
-        const uint32_t v = h[i0 + q];
-        h[i0 + q] = run;
-        run += v;
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-        const u64 pr = pairs[start + i];
-        const uint32_t pos = atomicAdd(&h[(uint32_t)(pr >> 32)], 1u);
-        src[start + pos] = (uint32_t)pr;
-    }
-    __syncthreads();
-    // h[i] is now the end of node i's bucket: sort each (Poisson(1)-sized)
-    // bucket, then emit IN[] and SIB[].
-    for (uint32_t i = threadIdx.x; i < nodes; i += blockDim.x) {
-        const uint32_t a = start + (i ? h[i - 1] : 0u), e = start + h[i];
-        for (uint32_t q = a + 1; q < e; ++q) {
-            const uint32_t v = src[q];
-            uint32_t r = q;
-            while (r > a && src[r - 1] > v) {
-                src[r] = src[r - 1];
-                --r;
-            }
-            src[r] = v;
-        }
-        const uint32_t k = e - a;
-        const uint32_t s0 = k > 0 ? src[a] : 0u, s1 = k > 1 ? src[a + 1] : 0u;
-        const uint32_t y = nb0 + i;
-        IN[y] = make_uint4(a, k, s0, s1);
-        (void)y;
-        for (uint32_t q = a + 1; q < e; ++q) {
-            const uint32_t rank = q - a;
-            SIB[src[q]] = make_uint4(serial, rank, s0, rank > 1 ? s1 : 0u);
-        }
-    }
-}
-
-hipError_t launch_build_csr(uint32_t *tg, const CsrPlan &p, uint32_t *scratch, u64 *pairs,
-                            uint32_t *src, uint4 *IN, uint4 *SIB, uint32_t serial,
-                            uint64_t seed, uint32_t epoch, uint32_t round, hipStream_t s) {
-    uint32_t *M = scratch;
-    uint32_t *tot = M + (size_t)p.ba * p.nb;
-    uint32_t *base = tot + p.nb;
-    const size_t lds_nb = (size_t)p.nb * sizeof(uint32_t);
-    hipLaunchKernelGGL(csr_bin_count, dim3(p.ba), dim3(256), lds_nb, s, tg, p, M, seed, epoch, round);
-    hipLaunchKernelGGL(csr_col_scan, dim3((p.nb + 255) / 256), dim3(256), 0, s, M, p, tot);
-    hipLaunchKernelGGL(scan_small, dim3(1), dim3(kScanBlock), 0, s, tot, base, p.nb);
-    hipLaunchKernelGGL(csr_bin_scatter, dim3(p.ba), dim3(256), lds_nb, s, tg, p, M, base, pairs);
-    const size_t lds_sort = ((size_t)p.bin + 16) * sizeof(uint32_t);
-    if (lds_sort > 65536) {  // n > 2^28: bins of 32768 nodes need 128 KiB of the 160 KiB LDS
-        hipError_t e = hipFuncSetAttribute((const void *)csr_bin_sort,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sort);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(csr_bin_sort, dim3(p.nb), dim3(256), lds_sort, s, pairs, p, base, tot, src, IN,
-                       SIB, serial);
     return hipGetLastError();
 }
 
