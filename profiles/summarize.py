@@ -16,7 +16,7 @@ import os
 import shutil
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-DOMINANT = "round_kernel<false, 1>"
+DOMINANT = "round_kernel<false, 1"
 
 
 def main():
