@@ -15,6 +15,11 @@ cpu_baseline: the CPU oracle (reference-faithful port: per-node ordered maps,
           one thread, same 2P schedule) on a bounded sample of the same
           workload (fewer nodes, same R and injection), rank 0 at N=1 only.
 
+Other BASELINE configurations (--config): cfg2 (2^20 x 1), cfg3 (2^20 x 64) and
+cfg5 (10^8 x 16 with harness-injected faults: 1% churn, 1% push-batch drop, 1%
+pull-batch drop per node per round, Philox stream 3).  The default line is
+cfg4, the configuration the metric is quoted on that fits one GPU.
+
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): ONE network
 of the same n x R sharded by node range over the N ranks (safe_gossip_amd.sharded,
 DESIGN.md section 7): every round exchanges push rows and pull rows with RCCL
@@ -35,13 +40,26 @@ HBM_PEAK_GBS = 8000.0
 METRIC = "node-rumor updates/sec (whole node) + % HBM roofline; rounds-to-full-spread"
 
 
+# BASELINE.json configs: (nodes, rumors, (churn, drop_push, drop_pull))
+CONFIGS = {
+    "cfg2": (1 << 20, 1, (0.0, 0.0, 0.0)),
+    "cfg3": (1 << 20, 64, (0.0, 0.0, 0.0)),
+    "cfg4": (1 << 24, 256, (0.0, 0.0, 0.0)),
+    "cfg5": (100_000_000, 16, (0.01, 0.01, 0.01)),
+}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--nodes", type=int, default=1 << 24)
-    p.add_argument("--rumors", type=int, default=256)
+    p.add_argument("--config", default="cfg4", choices=sorted(CONFIGS))
+    p.add_argument("--nodes", type=int, default=None, help="override the config's node count")
+    p.add_argument("--rumors", type=int, default=None)
+    p.add_argument("--churn", type=float, default=None, help="P(node offline) per round")
+    p.add_argument("--drop-push", type=float, default=None, help="P(push batch dropped)")
+    p.add_argument("--drop-pull", type=float, default=None, help="P(pull batch dropped)")
     p.add_argument("--seed", type=lambda s: int(s, 0), default=0x5AFE6055)
     p.add_argument("--cpu-seconds", type=float, default=15.0,
                    help="budget of the CPU-oracle sample")
@@ -50,7 +68,13 @@ def parse():
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (RCCL, one GPU per rank) or gloo (host-staged rows; rehearsal of "
                         "the N>1 path with several ranks on one GPU)")
-    return p.parse_args()
+    a = p.parse_args()
+    n, R, f = CONFIGS[a.config]
+    a.nodes = n if a.nodes is None else a.nodes
+    a.rumors = R if a.rumors is None else a.rumors
+    a.faults = (f[0] if a.churn is None else a.churn, f[1] if a.drop_push is None else a.drop_push,
+                f[2] if a.drop_pull is None else a.drop_pull)
+    return a
 
 
 def inject_all(net, epoch):
@@ -85,13 +109,14 @@ def spread_run(net, epoch, max_rounds=200):
                 known_fraction=known / float(net.n * net.R))
 
 
-def cpu_baseline(R, seed, budget_s):
+def cpu_baseline(R, seed, budget_s, faults=(0.0, 0.0, 0.0)):
     """Time the CPU oracle (port) on a bounded sample: n_cpu nodes, same R."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib
     oracle_lib.build_oracle()
     n_cpu = 1 << 15
-    net = oracle_lib.OracleNet(n_cpu, R, seed=seed)
+    thr = [oracle_lib.fault_threshold(p) for p in faults] if any(faults) else None
+    net = oracle_lib.OracleNet(n_cpu, R, seed=seed, faults=thr)
     L = oracle_lib.lib()
     for r in range(R):
         net.send_new(L.or_origin(seed, 0, r, n_cpu), r)
@@ -107,7 +132,8 @@ def cpu_baseline(R, seed, budget_s):
     return dict(value=n_cpu * R * rounds / el, unit="node-rumor updates/s", cores=1,
                 kind="port",
                 sample=f"CPU oracle (per-node ordered maps, 1 thread, 2P), n={n_cpu}, R={R}, "
-                       f"all rumors injected round 1, {rounds} rounds in {el:.1f}s")
+                       f"all rumors injected round 1, {rounds} rounds in {el:.1f}s"
+                       + (f", faults {faults}" if thr else ""))
 
 
 def main():
@@ -130,12 +156,13 @@ def main():
     import safe_gossip_amd as sg
 
     n, R = args.nodes, args.rumors
+    fk = dict(churn=args.faults[0], drop_push=args.faults[1], drop_pull=args.faults[2])
     if world > 1:
         from safe_gossip_amd.sharded import ShardedNetwork
         net = ShardedNetwork(n, R, world, seed=args.seed, epoch=0, device=local,
-                             transport="dist")
+                             transport="dist", **fk)
     else:
-        net = sg.Network(n, R, seed=args.seed, epoch=0, device=local)
+        net = sg.Network(n, R, seed=args.seed, epoch=0, device=local, **fk)
 
     def barrier_sync():
         net.sync()
@@ -188,7 +215,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(R, args.seed, args.cpu_seconds)
+        cpu = cpu_baseline(R, args.seed, args.cpu_seconds, args.faults)
 
     if rank == 0:
         total_updates = float(n) * R * args.steps
@@ -206,9 +233,13 @@ def main():
             "dtype": "u64",
             "data": "synthetic",
             "config": {
-                "workload": f"cfg4: {n} nodes x {R} rumors, full mesh, all rumors injected in "
-                            f"round 1 at Philox origins, 2P schedule, {args.steps} rounds",
+                "workload": f"{args.config}: {n} nodes x {R} rumors, full mesh, all rumors injected in "
+                            f"round 1 at Philox origins, 2P schedule, {args.steps} rounds"
+                            + (", faults churn/drop_push/drop_pull = %g/%g/%g per node-round"
+                               % args.faults if any(args.faults) else ""),
                 "n_nodes": n, "n_rumors": R, "seed": hex(args.seed),
+                "faults": {"churn": args.faults[0], "drop_push": args.faults[1],
+                           "drop_pull": args.faults[2]},
                 "params": list(net.params),
                 "parallelism": (f"node-range shards x{world}, "
                                 + ("RCCL" if args.dist_backend == "nccl" else args.dist_backend)
@@ -217,7 +248,8 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "round_kernel<false,1> (deliver round t + transition to t+1)",
+                "kernel": "round_kernel<%s,1> (deliver round t + transition to t+1)"
+                          % ("true" if R < 64 else "false"),
                 "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": bytes_per,
             },
             "cpu_baseline": cpu,

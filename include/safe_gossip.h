@@ -61,7 +61,14 @@ typedef struct {
     uint8_t max_rounds;      /* 0 = derive from n (src/gossip.rs:63)         */
     uint8_t reserved0;
     int32_t device;          /* HIP device ordinal, -1 = current             */
-    uint32_t reserved1[7];
+    /* Harness-injected faults (BASELINE config 5), thresholds over 2^32
+     * (probability = value / 2^32), drawn per (round, node) from the Philox
+     * stream 3 (gs_fault): the calls the reference harness would skip.      */
+    uint32_t churn;          /* node offline for the round: no next_round,
+                                every RPC to or from it dropped, state kept  */
+    uint32_t drop_push;      /* push batch not delivered (so never answered) */
+    uint32_t drop_pull;      /* pull batch not delivered                     */
+    uint32_t reserved1[4];
 } gs_config;
 
 /* src/gossip.rs:209-221, same field order. */
@@ -156,6 +163,10 @@ uint32_t    gs_peer(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node
 uint32_t    gs_origin(uint64_t seed, uint32_t epoch, uint32_t rumor, uint32_t n);
 /* Harness coin (rng.gen::<bool>(), src/gossiper.rs:204). */
 uint32_t    gs_coin(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node);
+/* Fault bits of (round, node) for the given thresholds: 1 offline (churn),
+ * 2 push batch dropped, 4 pull batch dropped (gs_config.churn/drop_*). */
+uint32_t    gs_fault(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node,
+                     uint32_t churn, uint32_t drop_push, uint32_t drop_pull);
 /* Parameter derivation of Gossip::add_peer for network_size = n. */
 void        gs_derive_params(uint32_t n, uint8_t out[3]);
 const char *gs_status_string(gs_status s);

@@ -78,6 +78,20 @@ uint32_t or_coin(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node)
     return (uint32_t)(ph_u64(seed, round, node, 2u, epoch) & 1u);
 }
 
+/* Harness-injected faults of round `round` at `node` (SURVEY.md section 8d,
+ * config 5): Philox stream 3, word 0 churn, word 1 push-batch drop, word 2
+ * pull-batch drop, each against its threshold (probability = thr / 2^32). */
+uint32_t or_fault(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node,
+                  uint32_t churn, uint32_t drop_push, uint32_t drop_pull)
+{
+    uint32_t ctr[4] = {round, node, 3u, epoch};
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t o[4];
+    or_philox(ctr, key, o);
+    return (o[0] < churn ? OR_FAULT_OFFLINE : 0u) | (o[1] < drop_push ? OR_FAULT_PUSH : 0u) |
+           (o[2] < drop_pull ? OR_FAULT_PULL : 0u);
+}
+
 /* ------------------------------------------------------------ parameters */
 /* Gossip::add_peer, src/gossip.rs:59-64: after (n-1) add_peer calls
  * network_size == n.  f64 ln -> ln -> ceil -> `as u8` (saturating) -> max 1. */
@@ -135,8 +149,11 @@ struct or_net {
     uint32_t round;
     or_gossip *g;
     inj *pend; uint32_t npend, cap_pend;
+    /* harness-injected faults (thresholds over 2^32, 0 = none) */
+    uint32_t f_churn, f_push, f_pull;
     /* per-round scratch */
     uint32_t *target;
+    uint8_t *fault;       /* or_fault bits of the round, per node */
     rpc_vec *push, *pull;
 };
 
@@ -396,9 +413,10 @@ or_net *or_create(uint32_t n, uint32_t R, uint64_t seed, uint32_t epoch)
     net->n = n; net->R = R; net->seed = seed; net->epoch = epoch;
     net->g = (or_gossip *)calloc(n ? n : 1, sizeof(or_gossip));
     net->target = (uint32_t *)calloc(n ? n : 1, sizeof(uint32_t));
+    net->fault = (uint8_t *)calloc(n ? n : 1, 1);
     net->push = (rpc_vec *)calloc(n ? n : 1, sizeof(rpc_vec));
     net->pull = (rpc_vec *)calloc(n ? n : 1, sizeof(rpc_vec));
-    if (!net->g || !net->target || !net->push || !net->pull) abort();
+    if (!net->g || !net->target || !net->fault || !net->push || !net->pull) abort();
     /* create_network: every node add_peer's the n-1 others; the parameters
      * after the last add_peer are those of network_size == n. */
     uint8_t p[3];
@@ -421,7 +439,7 @@ void or_destroy(or_net *net)
         free(net->push[i].v);
         free(net->pull[i].v);
     }
-    free(net->g); free(net->target); free(net->push); free(net->pull);
+    free(net->g); free(net->target); free(net->fault); free(net->push); free(net->pull);
     free(net->pend);
     free(net);
 }
@@ -433,6 +451,13 @@ void or_set_params(or_net *net, uint8_t cmax, uint8_t maxc, uint8_t maxr)
         net->g[i].max_c_rounds = maxc;
         net->g[i].max_rounds = maxr;
     }
+}
+
+void or_set_faults(or_net *net, uint32_t churn, uint32_t drop_push, uint32_t drop_pull)
+{
+    net->f_churn = churn;
+    net->f_push = drop_push;
+    net->f_pull = drop_pull;
 }
 
 void or_get_params(const or_net *net, uint8_t out[3])
@@ -463,6 +488,15 @@ static int inj_cmp(const void *a, const void *b)
     return 0;  /* stable w.r.t. rumor order not needed: distinct rumors */
 }
 
+/* The push batch of x reaches d: x and d online and the batch not dropped.
+ * A dropped push is never answered (the harness only calls
+ * handle_received_message on what it delivers, src/gossiper.rs:217-231). */
+static int edge_alive(const or_net *net, uint32_t x, uint32_t d)
+{
+    return net->push[x].n > 0 && !(net->fault[d] & OR_FAULT_OFFLINE) &&
+           !(net->fault[x] & OR_FAULT_PUSH);
+}
+
 int or_next_round(or_net *net, int schedule, uint32_t *any_live)
 {
     const uint32_t n = net->n;
@@ -473,10 +507,21 @@ int or_next_round(or_net *net, int schedule, uint32_t *any_live)
      * Gossiper::next_round (peer choice + Gossip::next_round). */
     qsort(net->pend, net->npend, sizeof(inj), inj_cmp);
     uint32_t pi = 0;
+    const int faults = net->f_churn | net->f_push | net->f_pull;
+    for (uint32_t x = 0; x < n; ++x)
+        net->fault[x] = faults ? (uint8_t)or_fault(net->seed, net->epoch, net->round, x, net->f_churn,
+                                                   net->f_push, net->f_pull) : 0u;
     for (uint32_t x = 0; x < n; ++x) {
         while (pi < net->npend && net->pend[pi].node == x) {
             gossip_new_message(&net->g[x], net->pend[pi].rumor);
             pi++;
+        }
+        net->pull[x].n = 0;
+        if (net->fault[x] & OR_FAULT_OFFLINE) {
+            /* churn: the harness skips this node's next_round (no peer
+             * choice, no transition, no push); its state is kept */
+            net->push[x].n = 0;
+            continue;
         }
         net->target[x] = or_peer(net->seed, net->epoch, net->round, x, n);
         gossip_next_round(&net->g[x], &net->push[x]);
@@ -490,7 +535,7 @@ int or_next_round(or_net *net, int schedule, uint32_t *any_live)
             uint32_t d = net->target[x];
             rpc_vec *pv = &net->push[x];
             rpc_vec *pl = &net->pull[x];
-            pl->n = 0;
+            if (!edge_alive(net, x, d)) continue;
             for (uint32_t i = 0; i < pv->n; ++i) {
                 if (i == 0) {
                     gossip_receive(&net->g[d], x, &pv->v[i], pl);
@@ -501,6 +546,7 @@ int or_next_round(or_net *net, int schedule, uint32_t *any_live)
                     free(tmp.v);
                 }
             }
+            if (net->fault[x] & OR_FAULT_PULL) continue;   /* pull batch dropped */
             for (uint32_t i = 0; i < pl->n; ++i) {
                 rpc_vec tmp = {0, 0, 0};
                 gossip_receive(&net->g[x], d, &pl->v[i], &tmp);
@@ -515,7 +561,7 @@ int or_next_round(or_net *net, int schedule, uint32_t *any_live)
             uint32_t d = net->target[x];
             rpc_vec *pv = &net->push[x];
             rpc_vec *pl = &net->pull[x];
-            pl->n = 0;
+            if (!edge_alive(net, x, d)) continue;
             for (uint32_t i = 0; i < pv->n; ++i) {
                 if (i == 0) {
                     gossip_receive(&net->g[d], x, &pv->v[i], pl);
@@ -530,6 +576,7 @@ int or_next_round(or_net *net, int schedule, uint32_t *any_live)
         for (uint32_t x = 0; x < n; ++x) {
             uint32_t d = net->target[x];
             rpc_vec *pl = &net->pull[x];
+            if (net->fault[x] & OR_FAULT_PULL) continue;   /* pull batch dropped */
             for (uint32_t i = 0; i < pl->n; ++i) {
                 rpc_vec tmp = {0, 0, 0};
                 gossip_receive(&net->g[x], d, &pl->v[i], &tmp);

@@ -37,6 +37,9 @@ extern "C" {
 
 enum { OR_SCHED_2P = 0, OR_SCHED_SEQ = 1 };
 
+/* or_fault bits (harness-injected faults). */
+enum { OR_FAULT_OFFLINE = 1, OR_FAULT_PUSH = 2, OR_FAULT_PULL = 4 };
+
 /* Statistics, src/gossip.rs:209-221 (field order kept). */
 typedef struct {
     uint64_t rounds;
@@ -63,6 +66,12 @@ void     or_destroy(or_net *net);
 /* Override the derived parameters (counter_max, max_c_rounds, max_rounds). */
 void     or_set_params(or_net *net, uint8_t cmax, uint8_t maxc, uint8_t maxr);
 void     or_get_params(const or_net *net, uint8_t out[3]);
+/* Harness-injected faults, as thresholds over 2^32 (probability = thr/2^32):
+ * churn = a node is offline for a round (the harness skips its next_round
+ * and every RPC to or from it; its state is kept), drop_push = a
+ * push batch is not delivered (and so never answered), drop_pull = a pull
+ * batch is not delivered.  Drawn per (round, node) from or_fault. */
+void     or_set_faults(or_net *net, uint32_t churn, uint32_t drop_push, uint32_t drop_pull);
 /* Gossiper::send_new: queued, applied in the next round's phase 0 right before
  * that node's next_round (src/gossiper.rs:203-208).  1 = NoPeers. */
 int      or_send_new(or_net *net, uint32_t node, uint32_t rumor);
@@ -93,6 +102,8 @@ uint32_t or_peer(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node,
                  uint32_t n);
 uint32_t or_origin(uint64_t seed, uint32_t epoch, uint32_t rumor, uint32_t n);
 uint32_t or_coin(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node);
+uint32_t or_fault(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node,
+                  uint32_t churn, uint32_t drop_push, uint32_t drop_pull);
 /* Parameter derivation, src/gossip.rs:59-64 (f64 ln, ceil, as u8, max 1). */
 void     or_derive_params(uint32_t network_size, uint8_t out[3]);
 

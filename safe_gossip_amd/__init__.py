@@ -62,7 +62,9 @@ class _Config(ctypes.Structure):
         ("seed", ctypes.c_uint64), ("epoch", ctypes.c_uint32),
         ("counter_max", ctypes.c_uint8), ("max_c_rounds", ctypes.c_uint8),
         ("max_rounds", ctypes.c_uint8), ("reserved0", ctypes.c_uint8),
-        ("device", ctypes.c_int32), ("reserved1", ctypes.c_uint32 * 7),
+        ("device", ctypes.c_int32), ("churn", ctypes.c_uint32),
+        ("drop_push", ctypes.c_uint32), ("drop_pull", ctypes.c_uint32),
+        ("reserved1", ctypes.c_uint32 * 4),
     ]
 
 
@@ -110,6 +112,9 @@ SYMBOLS = {
                                     ctypes.c_uint32]),
     "gs_coin": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.c_uint32]),
+    "gs_fault": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                   ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                   ctypes.c_uint32]),
     "gs_derive_params": (None, [ctypes.c_uint32, _U8P]),
     "gs_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     # sharded engines (safe_gossip_amd.sharded)
@@ -234,6 +239,21 @@ def origin_of(seed: int, epoch: int, rumor: int, n: int) -> int:
     return load_library().gs_origin(seed, epoch, rumor, n)
 
 
+def fault_threshold(p: float) -> int:
+    """Probability -> the engine's fault threshold over 2^32."""
+    if not 0.0 <= p <= 1.0:
+        raise ValueError(f"fault probability {p} outside [0, 1]")
+    return min(int(round(p * 2.0 ** 32)), 0xFFFFFFFF)
+
+
+FAULT_OFFLINE, FAULT_PUSH, FAULT_PULL = 1, 2, 4
+
+
+def fault_of(seed: int, epoch: int, rnd: int, node: int, faults) -> int:
+    """Fault bits of (round, node); faults = (churn, drop_push, drop_pull) thresholds."""
+    return load_library().gs_fault(seed, epoch, rnd, node, *faults)
+
+
 def coin_of(seed: int, epoch: int, rnd: int, node: int) -> int:
     return load_library().gs_coin(seed, epoch, rnd, node)
 
@@ -249,9 +269,13 @@ class Network:
     """
 
     def __init__(self, n_nodes: int, n_rumors: int, seed: int = 0x5AFE6055, epoch: int = 0,
-                 params=None, device: int = 0):
+                 params=None, device: int = 0, churn: float = 0.0, drop_push: float = 0.0,
+                 drop_pull: float = 0.0):
         self._lib = load_library()
         cfg = _Config()
+        # harness-injected faults (config 5): probabilities per (round, node)
+        self.faults = (fault_threshold(churn), fault_threshold(drop_push), fault_threshold(drop_pull))
+        cfg.churn, cfg.drop_push, cfg.drop_pull = self.faults
         cfg.n_nodes = n_nodes
         cfg.n_rumors = n_rumors
         cfg.seed = seed

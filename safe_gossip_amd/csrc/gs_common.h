@@ -14,7 +14,7 @@ constexpr uint32_t kPhM0 = 0xD2511F53u, kPhM1 = 0xCD9E8D57u;
 constexpr uint32_t kPhW0 = 0x9E3779B9u, kPhW1 = 0xBB67AE85u;
 
 // Counter word 2 selects the stream.
-constexpr uint32_t kStreamPeer = 0, kStreamOrigin = 1, kStreamCoin = 2;
+constexpr uint32_t kStreamPeer = 0, kStreamOrigin = 1, kStreamCoin = 2, kStreamFault = 3;
 
 __host__ __device__ __forceinline__ uint32_t mulhi32(uint32_t a, uint32_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -24,8 +24,12 @@ __host__ __device__ __forceinline__ uint32_t mulhi32(uint32_t a, uint32_t b) {
 #endif
 }
 
-__host__ __device__ __forceinline__ u64 philox_u64(uint32_t c0, uint32_t c1, uint32_t c2,
-                                                   uint32_t c3, uint64_t seed) {
+struct Ph4 {
+    uint32_t w0, w1, w2, w3;
+};
+
+__host__ __device__ __forceinline__ Ph4 philox4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                                uint64_t seed) {
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
@@ -35,7 +39,13 @@ __host__ __device__ __forceinline__ u64 philox_u64(uint32_t c0, uint32_t c1, uin
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
         k0 += kPhW0; k1 += kPhW1;
     }
-    return ((u64)c1 << 32) | c0;
+    return {c0, c1, c2, c3};
+}
+
+__host__ __device__ __forceinline__ u64 philox_u64(uint32_t c0, uint32_t c1, uint32_t c2,
+                                                   uint32_t c3, uint64_t seed) {
+    const Ph4 w = philox4(c0, c1, c2, c3, seed);
+    return ((u64)w.w1 << 32) | w.w0;
 }
 
 // floor(v * m / 2^64): uniform index in [0, m).
@@ -62,6 +72,43 @@ __host__ __device__ __forceinline__ uint32_t origin_of(uint64_t seed, uint32_t e
 __host__ __device__ __forceinline__ uint32_t coin_of(uint64_t seed, uint32_t epoch,
                                                     uint32_t round, uint32_t node) {
     return (uint32_t)(philox_u64(round, node, kStreamCoin, epoch, seed) & 1u);
+}
+
+// Harness-injected faults, thresholds over
+// 2^32: churn = the node is offline for the round (no next_round, every RPC to
+// or from it dropped, state kept), push = its push batch is dropped (and so
+// never answered), pull = the pull batch answering it is dropped.  One Philox
+// draw per (round, node) on stream kStreamFault: word 0 churn, 1 push, 2 pull.
+struct Faults {
+    uint32_t churn, push, pull;
+};
+
+__host__ __device__ __forceinline__ bool faults_on(const Faults &f) {
+    return (f.churn | f.push | f.pull) != 0u;
+}
+
+__host__ __device__ __forceinline__ bool offline_of(uint64_t seed, uint32_t epoch, uint32_t round,
+                                                   uint32_t node, uint32_t churn) {
+    return churn != 0u && philox4(round, node, kStreamFault, epoch, seed).w0 < churn;
+}
+
+// Target word of (round, node): t(x) in the low 29 bits (n < 2^29 is implied
+// by the state layout's n < e^(e^3)) plus the delivery flags of x's edge.
+constexpr uint32_t kTgDead = 1u << 31;    // x's push batch is not delivered
+constexpr uint32_t kTgNoPull = 1u << 30;  // no pull batch reaches x
+constexpr uint32_t kTgOff = 1u << 29;     // x is offline this round
+constexpr uint32_t kTgMask = kTgOff - 1u;
+
+__host__ __device__ __forceinline__ uint32_t target_word(uint64_t seed, uint32_t epoch,
+                                                        uint32_t round, uint32_t node, uint32_t n,
+                                                        const Faults &f) {
+    const uint32_t t = peer_of(seed, epoch, round, node, n);
+    if (!faults_on(f)) return t;
+    const Ph4 w = philox4(round, node, kStreamFault, epoch, seed);
+    if (w.w0 < f.churn) return t | kTgDead | kTgNoPull | kTgOff;
+    if (w.w1 < f.push || offline_of(seed, epoch, round, t, f.churn)) return t | kTgDead | kTgNoPull;
+    if (w.w2 < f.pull) return t | kTgNoPull;
+    return t;
 }
 
 // ---------------------------------------------------------------------------

@@ -22,6 +22,9 @@ struct gs_engine {
     gs::Geometry g{};
     uint64_t seed = 0;
     uint32_t epoch = 0;
+    gs::Faults faults{};
+    u64 *pend = nullptr;       // churn: votes of frozen (offline) nodes [n][2][W]
+    uint32_t *offc = nullptr;  // churn: rounds offline per node
     uint8_t cmax = 0, maxc = 0, maxr = 0;
     int device = 0;
     hipStream_t stream = nullptr;
@@ -125,7 +128,7 @@ void release(gs_engine *e) {
         if (e->ev_kr[i]) (void)hipEventDestroy(e->ev_kr[i]);
     }
     if (e->cstream) (void)hipStreamDestroy(e->cstream);
-    void *bufs[] = {e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
+    void *bufs[] = {e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
                     e->partials, e->obs_state, e->obs_rec, e->obs_psize};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -145,6 +148,7 @@ gs_status reset_state(gs_engine *e) {
     GS_HIP(hipMemsetAsync(e->S[1], 0, sw * sizeof(u64), e->stream));
     GS_HIP(hipMemsetAsync(e->st32, 0, (size_t)4 * g.n * sizeof(uint32_t), e->stream));
     GS_HIP(hipMemsetAsync(e->st64, 0, (size_t)4 * g.n * sizeof(u64), e->stream));
+    if (e->offc) GS_HIP(hipMemsetAsync(e->offc, 0, (size_t)g.n * sizeof(uint32_t), e->stream));
     e->since_fold = 0;
     GS_HIP(hipMemsetAsync(e->flags, 0, 4 * sizeof(uint32_t), e->stream));
     e->cur = 0;
@@ -165,6 +169,9 @@ gs::RoundArgs base_args(gs_engine *e) {
         a.src = cur + e->spl.EP;
         a.spos_cur = cur + e->spl.SPOS;
         a.spos_next = nxt + e->spl.SPOS;
+        a.tg = cur + e->spl.tg_all + e->sp.lo;
+        a.node_lo = e->sp.lo;
+        a.tg_next = nxt + e->spl.tg_all + e->sp.lo;
         a.recvA = e->recvA;
         a.recvB = e->recvB;
         a.sendA = e->sendA;
@@ -178,6 +185,9 @@ gs::RoundArgs base_args(gs_engine *e) {
     }
     a.st32 = e->st32;
     a.st64 = e->st64;
+    a.f = e->faults;
+    a.pend = e->pend;
+    a.offc = e->offc;
     a.obs_rounds = e->round;
     a.flags = e->flags;
     a.g = e->g;
@@ -326,6 +336,11 @@ uint32_t gs_origin(uint64_t seed, uint32_t epoch, uint32_t rumor, uint32_t n) {
 uint32_t gs_coin(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node) {
     return gs::coin_of(seed, epoch, round, node);
 }
+uint32_t gs_fault(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node, uint32_t churn,
+                  uint32_t drop_push, uint32_t drop_pull) {
+    const gs::Ph4 w = gs::philox4(round, node, gs::kStreamFault, epoch, seed);
+    return (w.w0 < churn ? 1u : 0u) | (w.w1 < drop_push ? 2u : 0u) | (w.w2 < drop_pull ? 4u : 0u);
+}
 
 }  // extern "C"
 
@@ -356,6 +371,7 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
     e->sp = sp;
     e->seed = cfg->seed;
     e->epoch = cfg->epoch;
+    e->faults = gs::Faults{cfg->churn, cfg->drop_push, cfg->drop_pull};
     e->cmax = p[0];
     e->maxc = p[1];
     e->maxr = p[2];
@@ -421,6 +437,8 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
     ok = ok && dalloc(&e->S[0], sw) == hipSuccess && dalloc(&e->S[1], sw) == hipSuccess &&
          dalloc(&e->flags, 4) == hipSuccess && dalloc(&e->st32, (size_t)4 * n) == hipSuccess &&
          dalloc(&e->st64, (size_t)4 * n) == hipSuccess;
+    if (ok && e->faults.churn)
+        ok = dalloc(&e->pend, (size_t)n * 2 * g.W) == hipSuccess && dalloc(&e->offc, n) == hipSuccess;
     if (!ok) {
         hipError_t le = hipGetLastError();
         release(e);
@@ -435,7 +453,8 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
 }
 
 gs_status launch_plan(gs_engine *e, uint32_t r) {
-    GS_HIP(gs::launch_shard_plan(e->sp, e->spl, e->planw[r % 3], e->seed, e->epoch, r, e->cstream));
+    GS_HIP(gs::launch_shard_plan(e->sp, e->spl, e->planw[r % 3], e->seed, e->epoch, r, e->faults,
+                                 e->cstream));
     GS_HIP(hipEventRecord(e->ev_plan[r % 3], e->cstream));
     return GS_OK;
 }
@@ -617,6 +636,7 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
         la.seed = e->seed;
         la.epoch = e->epoch;
         la.round = e->round;
+        la.f = e->faults;
         GS_HIP(gs::launch_build_inlists(la, bs));
         GS_HIP(hipEventRecord(e->ev_built[ns], bs));
     }

@@ -43,8 +43,10 @@ constexpr uint32_t kInlThreads = 1024;
 constexpr uint32_t kBinnedMaxBins = 4096;         // n <= 2^26
 constexpr uint32_t kFlagLimit = 2u;               // flags[2] bit: a device limit was hit
 
+// Target word (target + delivery flags, gs_common.h); edges flagged kTgDead
+// carry no push batch and are left out of the lists.
 GS_DEV uint32_t target_of(const InListArgs &a, uint32_t x) {
-    return peer_of(a.seed, a.epoch, a.round, x, a.p.n);
+    return target_word(a.seed, a.epoch, a.round, x, a.p.n, a.f);
 }
 
 // Per-target record emission, shared by both paths.  `lst` holds y's k
@@ -89,7 +91,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
     for (uint32_t x = lo + threadIdx.x; x < hi; x += kInlThreads) {
         const uint32_t t = target_of(a, x);
         a.tg[x] = t;
-        atomicAdd(&cnt[t >> kBinLog], 1u);
+        if (!(t & kTgDead)) atomicAdd(&cnt[(t & kTgMask) >> kBinLog], 1u);
     }
     __syncthreads();
     // exclusive scan of the bin counts: thread i owns bins [i*per, i*per + per)
@@ -120,14 +122,15 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
     __syncthreads();
     for (uint32_t x = lo + threadIdx.x; x < hi; x += kInlThreads) {
         const uint32_t t = a.tg[x];  // written above by this thread
-        const uint32_t pos = atomicAdd(&cnt[t >> kBinLog], 1u);
+        if (t & kTgDead) continue;
+        const uint32_t pos = atomicAdd(&cnt[(t & kTgMask) >> kBinLog], 1u);
         stage[pos] = x;
         stage_lt[pos] = (uint16_t)(t & (kBin - 1u));
     }
     __syncthreads();
     // Consecutive stage entries of one bin go to consecutive region slots; the
     // bin of entry i is found by a binary search over the chunk-local starts.
-    for (uint32_t i = threadIdx.x; i < hi - lo; i += kInlThreads) {
+    for (uint32_t i = threadIdx.x; i < total; i += kInlThreads) {  // delivered edges of the chunk
         uint32_t lo_b = 0, hi_b = p.nb;  // last bin with off[b] <= i and a non-empty run
         while (hi_b - lo_b > 1) {
             const uint32_t mid = (lo_b + hi_b) >> 1;
@@ -248,7 +251,7 @@ __global__ __launch_bounds__(256) void csr_bin_count(InListArgs a) {
     for (u64 x = lo + threadIdx.x; x < hi; x += blockDim.x) {
         const uint32_t t = target_of(a, (uint32_t)x);
         a.tg[x] = t;
-        atomicAdd(&hist[t >> p.logbin], 1u);
+        if (!(t & kTgDead)) atomicAdd(&hist[(t & kTgMask) >> p.logbin], 1u);
     }
     __syncthreads();
     uint32_t *M = a.scratch;
@@ -300,7 +303,8 @@ __global__ __launch_bounds__(256) void csr_bin_scatter(InListArgs a) {
     const uint32_t lm = p.bin - 1u;
     for (u64 x = lo + threadIdx.x; x < hi; x += blockDim.x) {
         const uint32_t t = a.tg[x];
-        const uint32_t pos = atomicAdd(&cur[t >> p.logbin], 1u);
+        if (t & kTgDead) continue;
+        const uint32_t pos = atomicAdd(&cur[(t & kTgMask) >> p.logbin], 1u);
         pairs[pos] = ((u64)(t & lm) << 32) | (uint32_t)x;
     }
 }

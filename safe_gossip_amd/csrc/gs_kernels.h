@@ -11,7 +11,8 @@ struct RoundArgs {
     const SibRec *SIB8;       // round t, per source x: pushers of t(x) ahead of x
     const uint4 *IN;          // shard engine: per node {first edge, k | zi<<16, e0, e1}
     const uint32_t *src;      // round t in-list tails (shard engine: receive rows)
-    const uint32_t *tg;       // round t targets
+    const uint32_t *tg;       // round t target words (target_word: target + flags)
+    const uint32_t *tg_next;  // shard engine, faults: round t+1 target words
     uint32_t serial;          // build serial of the round-t lists (SIB validity)
     uint32_t *st32;           // [n][4] u32 Statistics deltas (empty_pull, empty_push,
                               //   full_sent, full_received)
@@ -34,6 +35,11 @@ struct RoundArgs {
     u64 *sendA;               // round-(t+1) push rows of this shard's nodes [pos][3][W]
     const uint32_t *spos_cur; // row of x in recvB (= its round-t push row position)
     const uint32_t *spos_next;// row of x in sendA for round t+1
+    // harness-injected faults (gs_common.h); pend/offc exist iff f.churn != 0
+    Faults f;
+    u64 *pend;                // [n][2][W]: votes (bump, anyC) of nodes frozen offline
+    uint32_t *offc;           // [n] rounds each node was offline (Statistics.rounds)
+    uint32_t node_lo;         // global id of local node 0 (shard engine; else 0)
     Geometry g;
     uint64_t seed;
     uint32_t epoch;
@@ -76,6 +82,7 @@ struct InListArgs {
     uint32_t serial;
     uint64_t seed;
     uint32_t epoch, round;
+    Faults f;           // edges that are not delivered are left out of the lists
 };
 // Peer choices of `round` (into tg) and their in-lists (IN8, SIB8 tagged with
 // `serial`).  Depends on nothing but the Philox stream, so it runs on its own
@@ -104,7 +111,8 @@ ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g);
 size_t shard_plan_words(const ShardPlan &P, ShardPlanLayout *L);
 // Plan of `round`: cnt = {m_in, overflow, scnt[G], rcnt[G]}, SPOS, IN, EP.
 hipError_t launch_shard_plan(const ShardPlan &P, const ShardPlanLayout &L, uint32_t *words,
-                             uint64_t seed, uint32_t epoch, uint32_t round, hipStream_t s);
+                             uint64_t seed, uint32_t epoch, uint32_t round, const Faults &f,
+                             hipStream_t s);
 
 struct PullArgs {
     const u64 *S;          // round-t planes of the owned nodes

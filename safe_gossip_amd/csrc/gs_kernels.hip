@@ -152,17 +152,20 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     InRec in8 = {};            // {first (tail), k, s0..s5}
     SibRec sb8 = {};           // {serial<<8 | rank of x in in(z), e0..e2}; stale unless rank >= 1
     uint32_t z = x, zi = 0xFFFFu, k = 0, r = 0;
+    uint32_t tgw = 0;  // round-t target word: t(x) + delivery flags (gs_common.h)
     if (DELIVER) {
         if (SHARD) {
             if (valid) {
                 in = a.IN[x];
                 zi = in.y >> 16;
                 k = in.y & 0xFFFFu;
+                if (faults_on(a.f)) tgw = a.tg[x];
             }
         } else {
             in8 = a.IN8[x];  // x = 0 on invalid lanes: a harmless valid address
             sb8 = a.SIB8[x];
-            z = a.tg[x];  // t_t(x)
+            tgw = a.tg[x];
+            z = tgw & kTgMask;  // t_t(x)
             k = valid ? in8.k : 0u;
             r = (valid && (sb8.tag >> 8) == (a.serial & kSerialMask)) ? (sb8.tag & 0xFFu) : 0u;
         }
@@ -193,10 +196,12 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             if (valid) {
                 if (k > 0) q[0] = L.load_row3(a.recvA, in.z);
                 if (k > 1) q[1] = L.load_row3(a.recvA, in.w);
-                const uint32_t sp = a.spos_cur[x];  // the pull row z returned to x
-                qz.c = a.recvB[L.row_index(sp, 2, 0)];
-                qz.a0 = a.recvB[L.row_index(sp, 2, 1)];
-                qz.a1 = 0;
+                if (!(tgw & kTgNoPull)) {
+                    const uint32_t sp = a.spos_cur[x];  // the pull row z returned to x
+                    qz.c = a.recvB[L.row_index(sp, 2, 0)];
+                    qz.a0 = a.recvB[L.row_index(sp, 2, 1)];
+                    qz.a1 = 0;
+                }
             }
         } else {
 #pragma unroll
@@ -229,6 +234,12 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     const u64 liveX = B | C;
 
     // ---- phases 1 and 2 of round t at x (Gossip::receive)
+    // Faults: a node offline in round t (off_t) has no pushers and no pull; its
+    // planes are the frozen pre-transition state of its last online round.  A
+    // dropped pull batch (!pulled) is neither absorbed nor counted, so t(x)'s
+    // own push copy, if any, stays recorded.
+    const bool off_t = DELIVER && (tgw & kTgOff);
+    const bool pulled = !(tgw & kTgNoPull);
     Recv<!TRANSITION> rv;
     rv.init(A, B, B & a0 & ~a1);
     uint32_t psize = 0;
@@ -239,9 +250,10 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         if (SHARD) {
             // zi = index of t(x) among x's pushers (0xFFFF: t(x) did not push to x)
             zin = zi != 0xFFFFu;
-            if (k > 0) rv.push(q[0], 0, k, zi != 0);
-            if (k > 1) rv.push(q[1], 1, k, zi != 1);
-            for (uint32_t i = 2; i < k; ++i) rv.push(L.load_row3(a.recvA, a.src[in.x + i]), i, k, zi != i);
+            const uint32_t zs = pulled ? zi : 0xFFFFu;  // push copy superseded by the pull copy
+            if (k > 0) rv.push(q[0], 0, k, zs != 0);
+            if (k > 1) rv.push(q[1], 1, k, zs != 1);
+            for (uint32_t i = 2; i < k; ++i) rv.push(L.load_row3(a.recvA, a.src[in.x + i]), i, k, zs != i);
             // pull row code (b0, b1): 01 counter 1, 10 counter 2, 11 counter 255
             pv2 = qz.a0 & ~qz.c;
             pvB = qz.c ^ qz.a0;
@@ -251,13 +263,13 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             for (uint32_t i = 0; i < kBatchK; ++i) {
                 if (i < k) {
                     zin |= in8.s[i] == z;
-                    rv.push(q[i], i, k, in8.s[i] != z);
+                    rv.push(q[i], i, k, !(pulled && in8.s[i] == z));
                 }
             }
             for (uint32_t i = kBatchK; i < k; ++i) {  // in-degree > kBatchK (1.9% of nodes)
                 const uint32_t s = i < kInline ? pick_inline(in8.s, i) : a.src[in8.first + (i - kInline)];
                 zin |= s == z;
-                rv.push(L.load_cls(S, s), i, k, s != z);
+                rv.push(L.load_cls(S, s), i, k, !(pulled && s == z));
             }
             // Pull batch from z: z's live set plus what z created from pushers
             // ahead of x.
@@ -267,7 +279,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
 #pragma unroll
             for (uint32_t i = 0; i < kBatchE; ++i)
                 if (i < r) sibling(e[i], pnot, pB, pC);
-            if (r > kBatchE && pnot) {  // rank > kBatchE (rare)
+            if (r > kBatchE && pnot && pulled) {  // rank > kBatchE (rare)
                 for (uint32_t i = kBatchE; i < min(r, kSibInline); ++i)
                     sibling(L.load_cls(S, pick_sib(sb8.e, i)), pnot, pB, pC);
                 if (r > kSibInline && pnot) {  // rank > 3: 0.2% of nodes
@@ -282,6 +294,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             pv2 = zB & qz.a1 & ~qz.a0;
             pvB = zB | pB;  // counter 1 (created entries: 1) or 2
             pCl = zC | pC;
+            if (!pulled) pv2 = pvB = pCl = 0;
         }
         const u64 pl = pvB | pCl;
         {
@@ -290,7 +303,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             rv.create(newc, pCl);
         }
         rv.recv += popc(pl);
-        psize = k + (zin ? 0u : 1u);  // |peers_in_this_round|
+        psize = k + ((pulled && !zin) ? 1u : 0u);  // |peers_in_this_round|
     }
     const u64 crB = rv.crB, crC = rv.crC, anyC = rv.anyC;
 
@@ -322,7 +335,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                 const uint4 d32 = reinterpret_cast<const uint4 *>(a.st32)[x];
                 const u64 *b64 = a.st64 + (u64)x * 4;
                 u64 *o = a.obs_stats + (u64)x * 5;
-                o[0] = a.obs_rounds;
+                o[0] = a.obs_rounds - (a.offc ? a.offc[x] : 0u);  // next_round calls
                 o[1] = b64[0] + d32.x + d_empty_pull;
                 o[2] = b64[1] + d32.y;
                 o[3] = b64[2] + d32.z + d_full_sent;
@@ -389,8 +402,20 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     const u64 oc1 = (Bold & a0 & ~a1) | cB | inj;
     const u64 oc2 = Bold & a1 & ~a0;
     const uint32_t thr = psize / 2u + 1u;
-    const u64 bump = ge_k<5>(rv.cv, thr) & (Bold | cB);  // cv counts only B entries' votes
-    const u64 anyCe = anyC & ninj;
+    // Churn: a node offline in round t+1 skips next_round; it keeps its
+    // pre-transition state (created entries folded in as B{0,1} / C{0,0}) and
+    // the two per-rumor votes next_round will use (bump, anyC) in `pend`.  A
+    // node returning from offline (off_t) takes its votes from there.
+    const bool on_next = !(a.f.churn && valid && offline_of(a.seed, a.epoch, a.round_new, a.node_lo + x, a.f.churn));
+    u64 bump, anyCe;
+    if (off_t && valid) {
+        const u64 pidx = ((u64)x * 2u) * g.W + L.j;
+        bump = a.pend[pidx] & Bold;
+        anyCe = a.pend[pidx + g.W] & ninj;
+    } else {
+        bump = ge_k<5>(rv.cv, thr) & (Bold | cB);  // cv counts only B entries' votes
+        anyCe = anyC & ninj;
+    }
     u64 nr[6];  // round + 1
     {
         u64 carry = ~0ull;
@@ -440,9 +465,19 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     N[2] = (Bn & oc2n) | (CC & d[1]) | Dn;
 #pragma unroll
     for (int i = 0; i < 5; ++i) N[3 + i] = ((Bn | BC) & nr[i]) | (CC & rib[i]);
+    if (!on_next) {  // frozen: pre-transition planes + votes (the lane is valid)
+        N[0] = (isC & ninj) | cC;
+        N[1] = (a0 & ninj) | cB | inj;
+        N[2] = a1 & ninj;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) N[3 + i] = P[3 + i] & ninj;
+        const u64 pidx = ((u64)x * 2u) * g.W + L.j;
+        a.pend[pidx] = bump;
+        a.pend[pidx + g.W] = anyCe & (Bold | cB);
+    }
 
     // ---- write round-(t+1) planes (through LDS, 16-byte coalesced stores)
-    uint32_t live_new = valid ? popc(Bn | Cn) : 0u;
+    uint32_t live_new = (valid && on_next) ? popc(Bn | Cn) : 0u;
     if (!SMALL) live_new = group_sum(live_new, g.W);
     const int blk_live = __syncthreads_or(live_new != 0u);  // also: every lane is done reading stage
     if (SMALL) {
@@ -463,7 +498,8 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         uint4 *dst4 = reinterpret_cast<uint4 *>(a.Snext + blk_base);
         for (uint32_t i = threadIdx.x; i < blk_v4; i += blockDim.x) dst4[i] = src4[i];
     }
-    if (SHARD && valid) {  // push row of round t+1: the class planes, to owner(t_{t+1}(x))
+    if (SHARD && valid && !(faults_on(a.f) && (a.tg_next[x] & kTgDead))) {
+        // push row of round t+1: the class planes, to owner(t_{t+1}(x))
         const uint32_t sp = a.spos_next[x];
 #pragma unroll
         for (int p = 0; p < kClsPlanes; ++p) a.sendA[L.row_index(sp, 3, p)] = N[p] & L.m;
@@ -485,10 +521,11 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         uint4 *st = reinterpret_cast<uint4 *>(a.st32) + x;
         uint4 v = *st;
         v.x += d_empty_pull;                       // empty_pull_sent
-        v.y += (live_new == 0u) ? 1u : 0u;         // empty_push_sent
+        v.y += (on_next && live_new == 0u) ? 1u : 0u;  // empty_push_sent
         v.z += live_new + d_full_sent;             // full_message_sent
         v.w += d_recv;                             // full_message_received
         *st = v;
+        if (!on_next) a.offc[x] += 1u;
 #endif
     }
 }

@@ -35,17 +35,23 @@ namespace gs {
 constexpr uint32_t kPlanBlock = 256;
 
 // ---------------------------------------------------------------- plan
+// Destination rank of a target word; edges that are not delivered (faults)
+// have none (G), so they get no row in either exchange.
+GS_DEV uint32_t dest_rank(const ShardPlan &P, uint32_t t) {
+    return (t & kTgDead) ? P.G : (t & kTgMask) / P.chunk;
+}
+
 __global__ __launch_bounds__(kPlanBlock) void plan_count(ShardPlan P, uint64_t seed, uint32_t epoch,
-                                                         uint32_t round, uint32_t *tg_all,
+                                                         uint32_t round, Faults f, uint32_t *tg_all,
                                                          uint32_t *bc_me, uint32_t *bc_d) {
     const uint32_t blk = blockIdx.x;
     const u64 x = (u64)blk * kPlanBlock + threadIdx.x;
     const bool valid = x < P.n;
-    uint32_t d = 0;
+    uint32_t d = P.G;
     if (valid) {
-        const uint32_t t = peer_of(seed, epoch, round, (uint32_t)x, P.n);
+        const uint32_t t = target_word(seed, epoch, round, (uint32_t)x, P.n, f);
         tg_all[x] = t;
-        d = t / P.chunk;
+        d = dest_rank(P, t);
     }
     const int me = __syncthreads_count(valid && d == P.g);
     if (threadIdx.x == 0) bc_me[blk] = (uint32_t)me;
@@ -123,13 +129,13 @@ __global__ __launch_bounds__(kPlanBlock) void plan_emit(ShardPlan P, const uint3
     const u64 x = (u64)blk * kPlanBlock + threadIdx.x;
     const bool valid = x < P.n;
     const uint32_t t = valid ? tg_all[x] : 0u;
-    const uint32_t d = t / P.chunk;
-    const bool me = valid && d == P.g;
+    const uint32_t d = valid ? dest_rank(P, t) : P.G;
+    const bool me = d == P.g;
     uint32_t tot;
     const uint32_t rpos = off_me[blk] + block_exclusive_scan(me ? 1u : 0u, lds, tot);
     if (me && rpos < P.cap_in) {
         E_id[rpos] = (uint32_t)x;
-        E_key[rpos] = t - P.lo;
+        E_key[rpos] = (t & kTgMask) - P.lo;
     }
     if (blk >= P.blk_lo && blk < P.blk_lo + P.nblk_own) {
         const bool own = valid && x >= P.lo && x < (u64)P.lo + P.m;
@@ -142,7 +148,7 @@ __global__ __launch_bounds__(kPlanBlock) void plan_emit(ShardPlan P, const uint3
             if (own && d == dd) myrank = (uint32_t)__popcll(mk & lt);
         }
         __syncthreads();
-        if (own) {
+        if (own && d < P.G) {  // a push row is sent (no row for an undelivered edge)
             uint32_t before = 0;
             for (uint32_t w = 0; w < wid; ++w) before += wcnt[d][w];
             SPOS[x - P.lo] = off_d[(u64)(blk - P.blk_lo) * P.G + d] + before + myrank;
@@ -255,7 +261,7 @@ __global__ __launch_bounds__(256) void edge_bin_sort(const u64 *__restrict__ pai
             EP[r] = v;
         }
         const uint32_t k = e - a;
-        const uint32_t tz = tg_all[lo + nb0 + i];  // t(z): did it push to z?
+        const uint32_t tz = tg_all[lo + nb0 + i] & kTgMask;  // t(z): did it push to z?
         uint32_t zi = 0xFFFFu;
         for (uint32_t q = a; q < e; ++q)
             if (E_id[EP[q]] == tz) zi = q - a;
@@ -321,13 +327,13 @@ size_t shard_plan_words(const ShardPlan &P, ShardPlanLayout *L) {
 }
 
 hipError_t launch_shard_plan(const ShardPlan &P, const ShardPlanLayout &L, uint32_t *w, uint64_t seed,
-                             uint32_t epoch, uint32_t round, hipStream_t s) {
+                             uint32_t epoch, uint32_t round, const Faults &f, hipStream_t s) {
     uint32_t *tg_all = w + L.tg_all, *bc_me = w + L.bc_me, *bc_d = w + L.bc_d, *cnt = w + L.cnt;
     uint32_t *E_id = w + L.E_id, *E_key = w + L.E_key, *SPOS = w + L.SPOS;
     uint32_t *M = w + L.M, *tot = w + L.tot, *base = w + L.base, *EP = w + L.EP;
     uint4 *IN = reinterpret_cast<uint4 *>(w + L.IN);
     u64 *pairs = reinterpret_cast<u64 *>(w + L.pairs);
-    hipLaunchKernelGGL(plan_count, dim3(P.nblk), dim3(kPlanBlock), 0, s, P, seed, epoch, round, tg_all,
+    hipLaunchKernelGGL(plan_count, dim3(P.nblk), dim3(kPlanBlock), 0, s, P, seed, epoch, round, f, tg_all,
                        bc_me, bc_d);
     hipLaunchKernelGGL(plan_scan, dim3(1), dim3(kScanBlock), 0, s, P, bc_me, bc_d, cnt);
     hipLaunchKernelGGL(plan_emit, dim3(P.nblk), dim3(kPlanBlock), 0, s, P, tg_all, bc_me, bc_d, E_id,

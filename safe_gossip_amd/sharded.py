@@ -25,7 +25,8 @@ from typing import Optional
 
 import numpy as np
 
-from . import DeviceError, GossipError, NoPeers, RoundReport, _check, _Config, _Report, load_library
+from . import (DeviceError, GossipError, NoPeers, RoundReport, _check, _Config, _Report,
+               fault_threshold, load_library)
 
 _P = ctypes.c_void_p
 _U32P = ctypes.POINTER(ctypes.c_uint32)
@@ -87,7 +88,7 @@ class ShardedNetwork:
 
     def __init__(self, n_nodes: int, n_rumors: int, world: int, seed: int = 0x5AFE6055,
                  epoch: int = 0, params=None, device: int = 0, transport: str = "local",
-                 group=None):
+                 group=None, churn: float = 0.0, drop_push: float = 0.0, drop_pull: float = 0.0):
         import torch
         self.torch = torch
         self.lib = _lib()
@@ -105,6 +106,8 @@ class ShardedNetwork:
         if params is not None:
             cfg.counter_max, cfg.max_c_rounds, cfg.max_rounds = params
         cfg.device = device
+        self.faults = (fault_threshold(churn), fault_threshold(drop_push), fault_threshold(drop_pull))
+        cfg.churn, cfg.drop_push, cfg.drop_pull = self.faults
         self._cfg = cfg
         if transport == "local":
             self.shards = [_Shard(self.lib, cfg, r, world, torch, device) for r in range(world)]

@@ -5,7 +5,13 @@ integers as R-bit rumor sets, so the 2P derivation (creation by the first
 carrier, records, z-dedupe, pull rows built from pushers ahead of x, median
 rule as 2*ge > |P|, C/D transitions, statistics) can be checked against the
 oracle on CPU independently of HIP.  Small sizes only.
+
+Harness-injected faults follow the kernel too: delivery flags per edge
+(dead push / dropped pull / offline), frozen pre-transition planes plus the
+two votes (bump, anyC) of offline nodes, and a per-node offline count.
 """
+
+OFF, DEAD, NOPULL = 1, 2, 4
 
 
 def popc(v):
@@ -13,7 +19,7 @@ def popc(v):
 
 
 class Model:
-    def __init__(self, n, R, seed, epoch, params, peer_fn):
+    def __init__(self, n, R, seed, epoch, params, peer_fn, fault_fn=None):
         self.n, self.R, self.seed, self.epoch = n, R, seed, epoch
         self.cmax, self.maxc, self.maxr = params
         self.M = (1 << R) - 1
@@ -24,7 +30,13 @@ class Model:
         self.round = 0
         self.pending = []
         self.peer_fn = peer_fn
+        self.fault_fn = fault_fn                 # (round, node) -> or_fault bits, or None
+        self.fl = [0] * n                        # delivery flags of the round (OFF/DEAD/NOPULL)
+        self.pend = [(0, 0)] * n                 # frozen votes (bump, anyC)
         self.deliver_pending = False
+
+    def offline(self, rnd, x):
+        return bool(self.fault_fn and self.fault_fn(rnd, x) & 1)
 
     def send_new(self, x, r):
         self.pending.append((x, r))
@@ -78,12 +90,13 @@ class Model:
         """Phases 1+2 of round t at x: returns the kernel's per-lane values."""
         z = self.tg[x]
         ins = [(s, self.cls(s)) for s in self.src[x]]
-        pull = self.pull_row(z, x, [(s, self.cls(s)) for s in self.src[z]])
-        return self.deliver_rows(x, z, ins, pull)
+        pulled = not self.fl[x] & NOPULL
+        pull = self.pull_row(z, x, [(s, self.cls(s)) for s in self.src[z]]) if pulled else (0, 0)
+        return self.deliver_rows(x, z, ins, pull, pulled)
 
-    def deliver_rows(self, x, z, ins, pull):
+    def deliver_rows(self, x, z, ins, pull, pulled=True):
         """`ins` = (source, class planes) of x's pushers ascending; `pull` = the
-        (b0, b1) code of the pull batch t(x) returned to x."""
+        (b0, b1) code of the pull batch t(x) returned to x (none: not pulled)."""
         M = self.M
         isC, a0, a1 = self.cls(x)
         A = ~isC & ~a0 & ~a1 & M
@@ -105,13 +118,12 @@ class Model:
             v2 = vB & q1 & ~q0 & M
             sl = vB | vC
             newc = notyet & sl
-            if s != z:
+            zin |= s == z
+            if not (pulled and s == z):  # t(x)'s push copy is superseded by its pull copy
                 rec = (B | crB) & sl
                 anyC |= rec & vC
                 self.add5(c1, rec & vB)
                 self.add5(c2, rec & v2)
-            else:
-                zin = True
             crB |= newc & ~vC & M
             crC |= newc & vC
             notyet &= ~sl & M
@@ -133,7 +145,7 @@ class Model:
         crB |= newc & ~pCl & M
         crC |= newc & pCl
         recv += popc(pl)
-        psize = k + (0 if zin else 1)
+        psize = k + (1 if pulled and not zin else 0)
         lc = popc(liveX)
         d_full = k * lc + part_cw
         d_empty_pull = 0
@@ -142,7 +154,7 @@ class Model:
         return dict(crB=crB, crC=crC, anyC=anyC, c1=c1, c2=c2, psize=psize, d_full=d_full,
                     d_empty_pull=d_empty_pull, d_recv=recv)
 
-    def transition(self, x, d, inj):
+    def transition(self, x, d, inj, off_t=False, on_next=True):
         M = self.M
         p = self.P[x]
         isC, a0, a1 = p[0], p[1], p[2]
@@ -160,8 +172,12 @@ class Model:
         oc1 = (Bold & a0 & ~a1 & M) | cB | inj
         oc2 = Bold & a1 & ~a0 & M
         thr = psize // 2 + 1
-        bump = ((oc1 & self.ge_k(c1, 5, thr)) | (oc2 & self.ge_k(c2, 5, thr))) & ninj
-        anyCe = anyC & ninj
+        if off_t:   # returning from offline: the votes frozen with the state
+            bump = self.pend[x][0] & Bold
+            anyCe = self.pend[x][1] & ninj
+        else:
+            bump = ((oc1 & self.ge_k(c1, 5, thr)) | (oc2 & self.ge_k(c2, 5, thr))) & ninj
+            anyCe = anyC & ninj
         nr = [0] * 6
         carry = M
         for i in range(5):
@@ -205,6 +221,10 @@ class Model:
         N[2] = (Bn & oc2n) | (CC & dd[1]) | Dn
         for i in range(5):
             N[3 + i] = ((Bn | BC) & nr[i]) | (CC & rib[i])
+        if not on_next:  # offline next round: pre-transition planes + votes
+            N = [(isC & ninj) | cC, (a0 & ninj) | cB | inj, a1 & ninj] + [v & ninj for v in b]
+            self.pend[x] = (bump, anyCe & (Bold | cB))
+            return [v & M for v in N], 0
         return [v & M for v in N], popc(Bn | Cn)
 
     def next_round(self):
@@ -222,21 +242,34 @@ class Model:
         newP = [None] * n
         live_any = False
         for x in range(n):
-            N, live = self.transition(x, dl[x], inj[x])
+            off_t = self.deliver_pending and bool(self.fl[x] & OFF)
+            on_next = not self.offline(rnd, x)
+            N, live = self.transition(x, dl[x], inj[x], off_t, on_next)
             newP[x] = N
             st = self.stats[x]
-            st[0] += 1
+            st[0] += 1 if on_next else 0
             st[1] += dl[x]["d_empty_pull"]
             st[4] += dl[x]["d_recv"]
-            st[2] += 1 if live == 0 else 0
+            st[2] += 1 if on_next and live == 0 else 0
             st[3] += live + dl[x]["d_full"]
             live_any |= live > 0
         self.P = newP
         self.round = rnd
         self.tg = [self.peer_fn(self.seed, self.epoch, rnd, x, n) for x in range(n)]
+        self.fl = [0] * n
+        if self.fault_fn:
+            fb = [self.fault_fn(rnd, x) for x in range(n)]
+            for x in range(n):
+                if fb[x] & 1:
+                    self.fl[x] = OFF | DEAD | NOPULL
+                elif fb[x] & 2 or fb[self.tg[x]] & 1:
+                    self.fl[x] = DEAD | NOPULL
+                elif fb[x] & 4:
+                    self.fl[x] = NOPULL
         self.src = [[] for _ in range(n)]
         for x in range(n):
-            self.src[self.tg[x]].append(x)
+            if not self.fl[x] & DEAD:
+                self.src[self.tg[x]].append(x)
         self.deliver_pending = True
         return live_any
 

@@ -60,6 +60,10 @@ _SIGS = {
                                     ctypes.c_uint32]),
     "or_coin": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.c_uint32]),
+    "or_fault": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                   ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                   ctypes.c_uint32]),
+    "or_set_faults": (None, [_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
     "or_derive_params": (None, [ctypes.c_uint32, _U8P]),
     "or_ms_step": (None, [_U8P, _U32P, _U8P, ctypes.c_uint32, _U32P, ctypes.c_uint32,
                           ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_int]),
@@ -104,6 +108,18 @@ def derive_params(n):
 
 TAGS = {"A": 0, "B": 1, "C": 2, "D": 3}
 
+FAULT_OFFLINE, FAULT_PUSH, FAULT_PULL = 1, 2, 4
+
+
+def fault_threshold(p):
+    """Probability -> threshold over 2^32 (the engine's and the oracle's unit)."""
+    return min(int(round(p * 2.0 ** 32)), 0xFFFFFFFF)
+
+
+def fault_bits(seed, epoch, rnd, node, faults):
+    """or_fault bits of (round, node) for faults = (churn, drop_push, drop_pull) thresholds."""
+    return lib().or_fault(seed, epoch, rnd, node, *faults)
+
 
 def ms_step(state, records, pir, params, next_round=True):
     """state = (tag, round, our_counter, rib); records = [(peer, counter)]."""
@@ -119,12 +135,21 @@ def ms_step(state, records, pir, params, next_round=True):
 class OracleNet:
     """One oracle network (per-node ordered maps, reference-faithful)."""
 
-    def __init__(self, n, R, seed=0x5AFE6055, epoch=0, params=None):
+    def __init__(self, n, R, seed=0x5AFE6055, epoch=0, params=None, faults=None):
+        """faults = (churn, drop_push, drop_pull) thresholds over 2^32 (fault_threshold)."""
         self._l = lib()
         self.h = self._l.or_create(n, R, seed, epoch)
         self.n, self.R, self.seed, self.epoch = n, R, seed, epoch
+        self.faults = tuple(faults) if faults else (0, 0, 0)
         if params is not None:
             self._l.or_set_params(self.h, *params)
+        if faults:
+            self._l.or_set_faults(self.h, *self.faults)
+
+    def offline(self, rnd):
+        """Boolean mask of the nodes offline in round `rnd` (churn)."""
+        return np.array([bool(fault_bits(self.seed, self.epoch, rnd, x, self.faults) & FAULT_OFFLINE)
+                         for x in range(self.n)])
 
     def close(self):
         if self.h:

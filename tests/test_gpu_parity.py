@@ -10,7 +10,7 @@ node, the known-rumor sets (Gossiper::messages) and the harness's
 import numpy as np
 import pytest
 
-from oracle_lib import SCHED_2P, OracleNet
+from oracle_lib import SCHED_2P, OracleNet, fault_threshold
 
 pytestmark = pytest.mark.gpu
 
@@ -55,12 +55,23 @@ def _first_diff(a, b):
 
 
 def run_parity(engine, n, R, kind, params=None, max_rounds=60, seed=SEED, epoch=0,
-               check_every=1, make_net=None):
+               check_every=1, make_net=None, faults=None):
+    """faults = (churn, drop_push, drop_pull) probabilities (harness-injected).
+
+    A node offline in the current round keeps the peer_counters and
+    peers_in_this_round of its last online round in the oracle; the engine
+    keeps only the two votes next_round derives from them, so records and |P|
+    are compared for online nodes (their effect on offline nodes is checked
+    through the state when they return)."""
+    fk = {}
+    if faults:
+        fk = dict(churn=faults[0], drop_push=faults[1], drop_pull=faults[2])
     if make_net is None:
-        net = engine.Network(n, R, seed=seed, epoch=epoch, params=params)
+        net = engine.Network(n, R, seed=seed, epoch=epoch, params=params, **fk)
     else:
-        net = make_net(n, R, seed=seed, epoch=epoch, params=params)
-    orc = OracleNet(n, R, seed=seed, epoch=epoch, params=params)
+        net = make_net(n, R, seed=seed, epoch=epoch, params=params, **fk)
+    orc = OracleNet(n, R, seed=seed, epoch=epoch, params=params,
+                    faults=[fault_threshold(p) for p in faults] if faults else None)
     assert net.params == orc.params
     rounds = 0
     try:
@@ -82,6 +93,10 @@ def run_parity(engine, n, R, kind, params=None, max_rounds=60, seed=SEED, epoch=
                                    f"gpu {gs[d]:#06x} oracle {os_[d]:#06x}")
                 grec, gps = net.dump_records()
                 orec, ops = orc.dump_records()
+                if faults and faults[0] > 0:
+                    off = orc.offline(rnd)
+                    grec[off] = orec[off] = 0
+                    gps[off] = ops[off] = 0
                 d = _first_diff(gps, ops)
                 assert d is None, f"round {rnd}: |P| differs at node {d}"
                 d = _first_diff(grec, orec)
@@ -127,6 +142,21 @@ def run_parity(engine, n, R, kind, params=None, max_rounds=60, seed=SEED, epoch=
 def test_round_parity(engine, n, R, kind, params):
     rounds = run_parity(engine, n, R, kind, params)
     assert rounds >= 1
+
+
+@pytest.mark.parametrize("n,R,kind,faults", [
+    (8, 3, "example", (0.2, 0.1, 0.1)),        # config 1 network under faults
+    (200, 1, "trickle", (0.1, 0.0, 0.0)),      # churn only
+    (300, 16, "origins", (0.0, 0.3, 0.0)),     # push drops only
+    (300, 16, "origins", (0.0, 0.0, 0.3)),     # pull drops only
+    (500, 16, "origins", (0.05, 0.05, 0.05)),  # config 5 shape (R=16, small segments)
+    (400, 64, "reinject", (0.3, 0.1, 0.1)),    # injections into frozen nodes
+    (130, 256, "origins", (0.1, 0.1, 0.2)),    # multi-word segments
+    (2000, 1, "trickle", (0.5, 0.2, 0.2)),
+    (64, 8, "origins", (1.0, 0.0, 0.0)),       # every node offline every round
+])
+def test_round_parity_faults(engine, n, R, kind, faults):
+    run_parity(engine, n, R, kind, faults=faults)
 
 
 @pytest.mark.parametrize("seed,epoch", [(1, 0), (0xDEADBEEF, 3), (2**63 + 5, 77)])

@@ -18,9 +18,9 @@ pytestmark = pytest.mark.gpu
 def _maker(world):
     from safe_gossip_amd.sharded import ShardedNetwork
 
-    def make(n, R, seed, epoch, params):
+    def make(n, R, seed, epoch, params, **faults):
         return ShardedNetwork(n, R, world, seed=seed, epoch=epoch, params=params,
-                              transport="local")
+                              transport="local", **faults)
     return make
 
 
@@ -45,6 +45,18 @@ def _maker(world):
 ])
 def test_sharded_parity(engine, world, n, R, kind, params):
     run_parity(engine, n, R, kind, params, make_net=_maker(world))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("n,R,kind,faults", [
+    (8, 3, "example", (0.2, 0.1, 0.1)),
+    (700, 3, "trickle", (0.1, 0.1, 0.1)),
+    (600, 16, "origins", (0.05, 0.05, 0.05)),   # config 5 shape
+    (520, 100, "reinject", (0.3, 0.2, 0.2)),
+    (1000, 256, "origins", (0.1, 0.0, 0.3)),
+])
+def test_sharded_parity_faults(engine, world, n, R, kind, faults):
+    run_parity(engine, n, R, kind, make_net=_maker(world), faults=faults)
 
 
 def test_sharded_larger(engine):

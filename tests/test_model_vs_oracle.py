@@ -9,10 +9,12 @@ from model_bitsliced import Model
 from oracle_lib import SCHED_2P, OracleNet
 
 
-def run(n, R, params=None, seed=0x5AFE6055, epoch=0, kind="origins", max_rounds=40):
-    orc = OracleNet(n, R, seed=seed, epoch=epoch, params=params)
+def run(n, R, params=None, seed=0x5AFE6055, epoch=0, kind="origins", max_rounds=40, faults=None):
+    thr = [oracle_lib.fault_threshold(p) for p in faults] if faults else None
+    orc = OracleNet(n, R, seed=seed, epoch=epoch, params=params, faults=thr)
     L = oracle_lib.lib()
-    mdl = Model(n, R, seed, epoch, orc.params, L.or_peer)
+    fault_fn = (lambda rnd, x: L.or_fault(seed, epoch, rnd, x, *thr)) if faults else None
+    mdl = Model(n, R, seed, epoch, orc.params, L.or_peer, fault_fn)
     rng = np.random.default_rng(n * 31 + R)
     for rnd in range(1, max_rounds + 1):
         inj = []
@@ -30,8 +32,13 @@ def run(n, R, params=None, seed=0x5AFE6055, epoch=0, kind="origins", max_rounds=
         np.testing.assert_array_equal(np.array(codes, np.uint16), orc.dump_state(),
                                       err_msg=f"state round {rnd}")
         orec, ops = orc.dump_records()
-        np.testing.assert_array_equal(np.array(psz, np.uint32), ops, err_msg=f"|P| round {rnd}")
-        np.testing.assert_array_equal(np.array(recs, np.uint16), orec,
+        psz, recs = np.array(psz, np.uint32), np.array(recs, np.uint16)
+        if faults:  # offline nodes: the oracle keeps stale records, the model only votes
+            off = orc.offline(rnd)
+            psz[off] = ops[off] = 0
+            recs[off] = orec[off] = 0
+        np.testing.assert_array_equal(psz, ops, err_msg=f"|P| round {rnd}")
+        np.testing.assert_array_equal(recs, orec,
                                       err_msg=f"records round {rnd}")
         np.testing.assert_array_equal(np.array(stats, np.uint64), orc.statistics(),
                                       err_msg=f"stats round {rnd}")
@@ -60,3 +67,16 @@ def run(n, R, params=None, seed=0x5AFE6055, epoch=0, kind="origins", max_rounds=
 ])
 def test_model_equals_oracle(oracle, n, R, params, kind):
     run(n, R, params, kind=kind)
+
+
+@pytest.mark.parametrize("n,R,kind,faults", [
+    (8, 3, "origins", (0.2, 0.1, 0.1)),
+    (60, 8, "origins", (0.1, 0.0, 0.0)),
+    (60, 8, "origins", (0.0, 0.3, 0.0)),
+    (60, 8, "origins", (0.0, 0.0, 0.3)),
+    (200, 5, "reinject", (0.3, 0.1, 0.1)),
+    (300, 6, "origins", (0.05, 0.05, 0.05)),
+    (150, 4, "reinject", (0.6, 0.2, 0.2)),
+])
+def test_model_equals_oracle_faults(oracle, n, R, kind, faults):
+    run(n, R, kind=kind, faults=faults)
