@@ -255,6 +255,13 @@ class Model:
             live_any |= live > 0
         self.P = newP
         self.round = rnd
+        self.plan_round(rnd)
+        self.deliver_pending = True
+        return live_any
+
+    def plan_round(self, rnd):
+        """Targets, delivery flags and in-lists of round `rnd` (the in-list build)."""
+        n = self.n
         self.tg = [self.peer_fn(self.seed, self.epoch, rnd, x, n) for x in range(n)]
         self.fl = [0] * n
         if self.fault_fn:
@@ -270,8 +277,6 @@ class Model:
         for x in range(n):
             if not self.fl[x] & DEAD:
                 self.src[self.tg[x]].append(x)
-        self.deliver_pending = True
-        return live_any
 
     def observe(self):
         """(state codes, records, psize, stats, known) after deliveries."""

@@ -5,18 +5,22 @@ ceil(n/G) rounded up to 256 nodes) and runs, per round, the same two row
 exchanges as the engine over a caller-supplied all-to-all
 ``a2a(rows_per_dest, width, recv_counts) -> rows_per_source``:
 
-  A  every owned node x sends (x, isC, a0, a1) to owner(t(x)), rows per
-     destination in ascending x, so each rank receives its pushers' rows in
-     ascending source order (rank order = node order);
+  A  every owned node x whose push batch is delivered sends (x, isC, a0, a1)
+     to owner(t(x)), rows per destination in ascending x, so each rank
+     receives its pushers' rows in ascending source order (rank order = node
+     order);
   B  the owner of z answers each received row, in the same order, with the pull
      batch z returned to that pusher (Model.pull_row: z's live set plus the
-     entries z created from earlier pushers, as a 2-plane class code).
+     entries z created from earlier pushers, as a 2-plane class code); a
+     receiver whose pull batch is dropped ignores it.
 
 Delivery and transition then use Model's bit-sliced algebra on the received
-rows only, so a rank never reads another rank's state directly.  Rumor sets are
-Python ints (R <= 62 so a plane fits one int64 of the gloo transport).
+rows only, so a rank never reads another rank's state directly.  Faults follow
+Model (flags of every edge derived locally from the Philox stream, like the
+engine's plan).  Rumor sets are Python ints (R <= 62 so a plane fits one int64
+of the gloo transport).
 """
-from model_bitsliced import Model
+from model_bitsliced import DEAD, NOPULL, OFF, Model
 
 
 def shard_range(n, G, g):
@@ -27,8 +31,8 @@ def shard_range(n, G, g):
 
 
 class ShardModel(Model):
-    def __init__(self, n, R, seed, epoch, params, peer_fn, rank, world, a2a):
-        super().__init__(n, R, seed, epoch, params, peer_fn)
+    def __init__(self, n, R, seed, epoch, params, peer_fn, rank, world, a2a, fault_fn=None):
+        super().__init__(n, R, seed, epoch, params, peer_fn, fault_fn)
         assert R <= 62
         self.rank, self.world, self.a2a = rank, world, a2a
         self.lo, self.m, self.chunk = shard_range(n, world, rank)
@@ -49,11 +53,12 @@ class ShardModel(Model):
         G = self.world
         sendA = [[] for _ in range(G)]
         for x in self.owned():
-            sendA[self.owner(self.tg[x])].append([x] + list(self.cls(x)))
+            if not self.fl[x] & DEAD:
+                sendA[self.owner(self.tg[x])].append([x] + list(self.cls(x)))
         # receive counts from the local plan (every rank knows all targets)
         rcA = [0] * G
         for x in range(self.n):
-            if self.owner(self.tg[x]) == self.rank:
+            if not self.fl[x] & DEAD and self.owner(self.tg[x]) == self.rank:
                 rcA[self.owner(x)] += 1
         recvA = self.a2a(sendA, 4, rcA)
         rows = [r for part in recvA for r in part]
@@ -76,11 +81,14 @@ class ShardModel(Model):
         self.exchanged = True
 
     def deliver(self, x):
-        return self.deliver_rows(x, self.tg[x], self.ins[x], self.pull[x])
+        pulled = not self.fl[x] & NOPULL
+        return self.deliver_rows(x, self.tg[x], self.ins[x], self.pull[x] if pulled else (0, 0),
+                                 pulled)
 
     def next_round(self):
         """Local part of the round; returns this shard's any-live flag."""
         self.exchange()
+        rnd = self.round + 1
         inj = {x: 0 for x in self.owned()}
         for x, r in self.pending:
             inj[x] |= 1 << r
@@ -91,20 +99,23 @@ class ShardModel(Model):
         live_any = False
         for x in self.owned():
             d = self.deliver(x) if self.deliver_pending else zero
-            N, live = self.transition(x, d, inj[x])
+            off_t = self.deliver_pending and bool(self.fl[x] & OFF)
+            on_next = not self.offline(rnd, x)
+            N, live = self.transition(x, d, inj[x], off_t, on_next)
             newP[x] = N
             st = self.stats[x]
-            st[0] += 1
+            st[0] += 1 if on_next else 0
             st[1] += d["d_empty_pull"]
             st[4] += d["d_recv"]
-            st[2] += 1 if live == 0 else 0
+            st[2] += 1 if on_next and live == 0 else 0
             st[3] += live + d["d_full"]
             live_any |= live > 0
         self.P = newP
-        self.round += 1
-        # every rank derives the whole round-(t+1) peer schedule (Philox): the
-        # plan's counts and send positions need the targets of all n sources
-        self.tg = [self.peer_fn(self.seed, self.epoch, self.round, x, self.n) for x in range(self.n)]
+        self.round = rnd
+        # every rank derives the whole round-(t+1) peer schedule and its
+        # delivery flags (Philox): the plan's counts and send positions need
+        # the targets of all n sources
+        self.plan_round(rnd)
         self.deliver_pending = True
         self.exchanged = False
         return live_any

@@ -43,7 +43,7 @@ def _a2a(send, width, recv_counts):
     return res
 
 
-def _worker(rank, world, port, n, R, params, kind, q):
+def _worker(rank, world, port, n, R, params, kind, q, faults=None):
     sys.path.insert(0, HERE)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -52,9 +52,11 @@ def _worker(rank, world, port, n, R, params, kind, q):
         from model_sharded import ShardModel
         from oracle_lib import SCHED_2P, OracleNet
         L = oracle_lib.lib()
-        orc = OracleNet(n, R, seed=SEED, params=params) if rank == 0 else None
+        thr = [oracle_lib.fault_threshold(p) for p in faults] if faults else None
+        orc = OracleNet(n, R, seed=SEED, params=params, faults=thr) if rank == 0 else None
         prm = params or oracle_lib.derive_params(n)
-        sm = ShardModel(n, R, SEED, 0, prm, L.or_peer, rank, world, _a2a)
+        fault_fn = (lambda rnd, x: L.or_fault(SEED, 0, rnd, x, *thr)) if faults else None
+        sm = ShardModel(n, R, SEED, 0, prm, L.or_peer, rank, world, _a2a, fault_fn)
         rng = np.random.default_rng(n)
         for rnd in range(1, 50):
             inj = []
@@ -80,8 +82,13 @@ def _worker(rank, world, port, n, R, params, kind, q):
                 np.testing.assert_array_equal(np.array(codes, np.uint16), orc.dump_state(),
                                               err_msg=f"state round {rnd}")
                 orec, ops = orc.dump_records()
-                np.testing.assert_array_equal(np.array(psz, np.uint32), ops)
-                np.testing.assert_array_equal(np.array(recs, np.uint16), orec)
+                psz, recs = np.array(psz, np.uint32), np.array(recs, np.uint16)
+                if faults:  # offline nodes: stale records in the oracle, votes only here
+                    off = orc.offline(rnd)
+                    psz[off] = ops[off] = 0
+                    recs[off] = orec[off] = 0
+                np.testing.assert_array_equal(psz, ops)
+                np.testing.assert_array_equal(recs, orec)
                 np.testing.assert_array_equal(np.array(stats, np.uint64), orc.statistics())
                 ok = orc.known_all()
                 assert known == [int(ok[x][0]) for x in range(n)]
@@ -97,16 +104,18 @@ def _worker(rank, world, port, n, R, params, kind, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n,R,params,kind", [
-    (2, 600, 16, None, "origins"),      # ranks own 512 / 88 nodes
-    (2, 700, 8, (3, 2, 9), "reinject"),
-    (3, 600, 12, None, "origins"),      # 256 / 256 / 88
+@pytest.mark.parametrize("world,n,R,params,kind,faults", [
+    (2, 600, 16, None, "origins", None),      # ranks own 512 / 88 nodes
+    (2, 700, 8, (3, 2, 9), "reinject", None),
+    (3, 600, 12, None, "origins", None),      # 256 / 256 / 88
+    (2, 600, 16, None, "origins", (0.1, 0.1, 0.1)),    # config 5 faults
+    (3, 600, 8, None, "reinject", (0.3, 0.2, 0.2)),
 ])
-def test_sharded_protocol_gloo(oracle, world, n, R, params, kind):
+def test_sharded_protocol_gloo(oracle, world, n, R, params, kind, faults):
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, R, params, kind, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, R, params, kind, q, faults))
              for r in range(world)]
     for p in procs:
         p.start()
