@@ -134,7 +134,7 @@ double      gs_round_kernel_bytes(const gs_engine *e);
 
 /* ---- Sharded network (multi-GPU): one engine per rank owns the node range
  * [lo, lo+m).  Per round t the caller moves two sets of rows between ranks
- * (DESIGN.md section 7): A = push rows (class planes of every node, sent to
+ * (DESIGN.md section 7): A = push rows (push-batch class codes, sent to
  * the owner of its target) and B = pull rows (returned in the reverse layout).
  * Sequence per round, after gs_next_round has produced round t:
  *   gs_shard_counts -> exchange A (sendA -> recvA) -> gs_shard_pull ->

@@ -133,20 +133,26 @@ struct Geometry {
 };
 
 // In-edge records of one round (gs_inlist.hip):
-//   InRec[y]  = {first, k, s0..s5} (32 B): y's k pushers in ascending index
-//               order (the order Gossip::receive sees them); pushers
-//               i >= kInline are at src[first + i - kInline].
+//   InRec[y]  = {first << 5 | k, s0, s1, s2} (16 B): y's k pushers in
+//               ascending index order (the order Gossip::receive sees them);
+//               pushers i >= kInline are at src[first + i - kInline] (tails of
+//               the 1.9% of nodes with in-degree > 3).  k <= kMaxIn: a larger
+//               in-degree (probability ~1e-34 per node) is a device limit.
 //   SibRec[x] = {serial << 8 | rank, e0, e1, e2} (16 B): x's rank among the
 //               pushers of t(x) and the first kSibInline pushers ahead of it
 //               (the rest are InRec[t(x)].s / its tail); valid iff the serial
 //               is the round build's (stale records are never cleared).
 // Both are read coalesced by the round kernel, so every gather of a node with
 // in-degree <= kInline is issued from one level of metadata reads.
-constexpr uint32_t kInline = 6;
+constexpr uint32_t kInline = 3;
 constexpr uint32_t kSibInline = 3;
 constexpr uint32_t kSerialMask = 0xFFFFFFu;
+constexpr uint32_t kMaxIn = 30;      // in-degree limit (5-bit k field)
+constexpr uint32_t kFirstShift = 5;  // tails: first < 2^27
 struct alignas(16) InRec {
-    uint32_t first, k, s[kInline];
+    uint32_t kf, s[kInline];
+    __host__ __device__ uint32_t k() const { return kf & ((1u << kFirstShift) - 1u); }
+    __host__ __device__ uint32_t first() const { return kf >> kFirstShift; }
 };
 struct alignas(16) SibRec {
     uint32_t tag, e[kSibInline];

@@ -86,12 +86,13 @@ struct Lane {
     GS_DEV u64 row_index(uint32_t e, uint32_t np, uint32_t p) const {
         return ((u64)e * np + p) * W + j;
     }
-    GS_DEV Cls load_row3(const u64 *__restrict__ rows, uint32_t e) const {
-        Cls r;
-        r.c = rows[row_index(e, 3, 0)];
-        r.a0 = rows[row_index(e, 3, 1)];
-        r.a1 = rows[row_index(e, 3, 2)];
-        return r;
+    // A push row: the 2-plane class code of the pusher's live entries (b0, b1):
+    // 01 counter 1, 10 counter 2, 11 counter 255 (C), 00 none.  Decoded into
+    // class planes that push()/sibling() read the same way (a C entry as
+    // C{round 0}, "none" as A: a pusher's A and D push nothing alike).
+    GS_DEV Cls load_push_row(const u64 *__restrict__ rows, uint32_t e) const {
+        const u64 b0 = rows[row_index(e, 2, 0)], b1 = rows[row_index(e, 2, 1)];
+        return Cls{b0 & b1, b0 & ~b1, b1 & ~b0};
     }
     // Class planes (isC, a0, a1) of node s for this lane's word.
     GS_DEV Cls load_cls(const u64 *__restrict__ S, uint32_t s) const {

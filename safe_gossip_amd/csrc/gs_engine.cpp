@@ -475,7 +475,7 @@ gs_status gs_shard_info(const gs_engine *e, uint32_t info[8]) {
     info[0] = e->sp.lo;
     info[1] = e->sp.m;
     info[2] = e->sp.cap_in;
-    info[3] = 3 * e->g.W;  // u64 words per push row
+    info[3] = 2 * e->g.W;  // u64 words per push row (2-plane class code)
     info[4] = 2 * e->g.W;  // u64 words per pull row
     info[5] = e->sp.G;
     info[6] = e->sp.g;
@@ -819,11 +819,11 @@ float gs_last_round_kernel_ms(gs_engine *e) {
 double gs_round_kernel_bytes(const gs_engine *e) {
     // DESIGN.md "Roofline": per (node, rumor slot) 1 B state read + 1 B state
     // write (8 bit-planes) + 3/8 B class planes of each pusher (mean in-degree
-    // 1) + 3/8 B class planes of t(x); per node 84 B: InRec 32 + SibRec 16 +
+    // 1) + 3/8 B class planes of t(x); per node 68 B: InRec 16 + SibRec 16 +
     // target 4 + Statistics deltas (16 r + 16 w).
     if (!e) return 0.0;
     const double n = e->g.n, rp = e->g.rpad;
-    return n * (2.75 * rp + 84.0);
+    return n * (2.75 * rp + 68.0);
 }
 
 }  // extern "C"

@@ -55,8 +55,11 @@ GS_DEV uint32_t target_of(const InListArgs &a, uint32_t x) {
 GS_DEV void emit_target(const InListArgs &a, uint32_t y, const uint32_t *lst, uint32_t k,
                         uint32_t first) {
     InRec r;
-    r.first = first;
-    r.k = k;
+    if (k > kMaxIn) {
+        atomicOr(&a.flags[2], kFlagLimit);
+        k = kMaxIn;
+    }
+    r.kf = (first << kFirstShift) | k;
 #pragma unroll
     for (uint32_t i = 0; i < kInline; ++i) r.s[i] = i < k ? lst[i] : 0u;
     a.IN8[y] = r;
@@ -67,6 +70,39 @@ GS_DEV void emit_target(const InListArgs &a, uint32_t y, const uint32_t *lst, ui
         for (uint32_t i = 0; i < kSibInline; ++i) sr.e[i] = i < j ? lst[i] : 0u;
         a.SIB8[lst[j]] = sr;
     }
+}
+
+// Pushers i >= kInline of a target go to the shared tail array.  A block
+// reserves the tail words of all its targets with ONE atomic (same-address
+// atomics serialise at the memory side): tail_len per target, a block scan,
+// then emit_tail at the thread's running cursor.
+GS_DEV uint32_t tail_len(uint32_t k) { return k > kInline ? min(k, kMaxIn) - kInline : 0u; }
+
+template <uint32_t NT>
+GS_DEV uint32_t reserve_tails(const InListArgs &a, uint32_t mine, uint32_t *tailcnt, uint32_t *lds_scan) {
+    __shared__ uint32_t blk_first;
+    uint32_t total;
+    const uint32_t off = block_exclusive_scan_t<NT>(mine, lds_scan, total);
+    if (threadIdx.x == 0) {
+        uint32_t f = total ? atomicAdd(tailcnt, total) : 0u;
+        if (f + total > a.p.tailcap) {
+            atomicOr(&a.flags[2], kFlagLimit);
+            f = kNone;  // no tails this round (reported as a device limit)
+        }
+        blk_first = f;
+    }
+    __syncthreads();
+    return blk_first == kNone ? kNone : blk_first + off;
+}
+
+// Writes a target's tail at *cur (kNone: none reserved); returns its start.
+GS_DEV uint32_t emit_tail(const InListArgs &a, const uint32_t *lst, uint32_t k, uint32_t &cur) {
+    const uint32_t m = tail_len(k);
+    if (m == 0 || cur == kNone) return 0u;
+    const uint32_t first = cur;
+    for (uint32_t j = 0; j < m; ++j) a.src[first + j] = lst[kInline + j];
+    cur += m;
+    return first;
 }
 
 // ------------------------------------------------------------ binned path
@@ -204,6 +240,10 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
     __syncthreads();
     // counters are now the ends of each target's run; lanes take consecutive
     // targets so the InRec stores are coalesced
+    uint32_t mine = 0;
+    for (uint32_t lt = threadIdx.x; lt < nodes; lt += kInlThreads)
+        mine += tail_len(half_of(h, lt) - (lt ? half_of(h, lt - 1) : 0u));
+    uint32_t cur = reserve_tails<kInlThreads>(a, mine, &a.scratch[p.nb], lds_scan);
     for (uint32_t lt = threadIdx.x; lt < nodes; lt += kInlThreads) {
         const uint32_t e = half_of(h, lt);
         const uint32_t s = lt ? half_of(h, lt - 1) : 0u;
@@ -218,17 +258,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
             }
             lst[r] = v;
         }
-        uint32_t first = 0;
-        if (k > kInline) {
-            first = atomicAdd(&a.scratch[p.nb], k - kInline);
-            if (first + (k - kInline) > p.tailcap) {
-                atomicOr(&a.flags[2], kFlagLimit);
-                first = 0;
-            } else {
-                for (uint32_t j = kInline; j < k; ++j) a.src[first + j - kInline] = lst[j];
-            }
-        }
-        emit_target(a, t0 + lt, lst, k, first);
+        emit_target(a, t0 + lt, lst, k, emit_tail(a, lst, k, cur));
     }
 }
 
@@ -256,6 +286,7 @@ __global__ __launch_bounds__(256) void csr_bin_count(InListArgs a) {
     __syncthreads();
     uint32_t *M = a.scratch;
     for (uint32_t i = threadIdx.x; i < p.nb; i += blockDim.x) M[(u64)blockIdx.x * p.nb + i] = hist[i];
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.scratch[(size_t)p.ba * p.nb + 2 * (size_t)p.nb] = 0u;  // tails
 }
 
 __global__ __launch_bounds__(256) void csr_col_scan(InListArgs a) {
@@ -313,8 +344,10 @@ __global__ __launch_bounds__(256) void csr_bin_sort(InListArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t h[];  // [bin] + 16 scan words
     const CsrPlan &p = a.p;
     const u64 *pairs = reinterpret_cast<const u64 *>(a.region);
+    uint32_t *csr = a.region + 2 * (size_t)p.n;  // exact CSR of the round's edges
     const uint32_t *tot = a.scratch + (size_t)p.ba * p.nb;
     const uint32_t *base = tot + p.nb;
+    uint32_t *tailcnt = a.scratch + (size_t)p.ba * p.nb + 2 * (size_t)p.nb;
     uint32_t *lds_scan = h + p.bin;
     const uint32_t b = blockIdx.x;
     const uint32_t start = base[b], cnt = tot[b];
@@ -339,12 +372,15 @@ __global__ __launch_bounds__(256) void csr_bin_sort(InListArgs a) {
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
         const u64 pr = pairs[start + i];
         const uint32_t pos = atomicAdd(&h[(uint32_t)(pr >> 32)], 1u);
-        a.src[start + pos] = (uint32_t)pr;
+        csr[start + pos] = (uint32_t)pr;
     }
     __syncthreads();
+    uint32_t mine = 0;
+    for (uint32_t i = threadIdx.x; i < nodes; i += blockDim.x) mine += tail_len(h[i] - (i ? h[i - 1] : 0u));
+    uint32_t cur = reserve_tails<256>(a, mine, tailcnt, lds_scan);
     for (uint32_t i = threadIdx.x; i < nodes; i += blockDim.x) {
         const uint32_t s = start + (i ? h[i - 1] : 0u), e = start + h[i];
-        uint32_t *lst = a.src + s;
+        uint32_t *lst = csr + s;
         const uint32_t k = e - s;
         for (uint32_t q = 1; q < k; ++q) {
             const uint32_t v = lst[q];
@@ -355,7 +391,7 @@ __global__ __launch_bounds__(256) void csr_bin_sort(InListArgs a) {
             }
             lst[r] = v;
         }
-        emit_target(a, nb0 + i, lst, k, s + kInline);  // src[first + i - kInline] = lst[i]
+        emit_target(a, nb0 + i, lst, k, emit_tail(a, lst, k, cur));
     }
 }
 
@@ -390,7 +426,7 @@ CsrPlan csr_plan(uint32_t n) {
     uint32_t ba = (uint32_t)(((u64)n + 4095) / 4096);
     p.ba = ba < 256u ? (ba ? ba : 1u) : 256u;
     p.chunk = (uint32_t)(((u64)n + p.ba - 1) / p.ba);
-    p.tailcap = 0;
+    p.tailcap = n / 32u + 1024u;
     return p;
 }
 
@@ -401,9 +437,9 @@ InListSizes inlist_sizes(const CsrPlan &p) {
         z.region_words = (size_t)p.nb * kBinCap * 3 / 2;  // sources (u32) + local targets (u16)
         z.scratch_words = (size_t)p.nb + 1;  // fill[nb], tailcnt
     } else {
-        z.src_words = p.n;
-        z.region_words = 2 * (size_t)p.n;  // u64 pairs
-        z.scratch_words = (size_t)p.ba * p.nb + 2 * (size_t)p.nb;
+        z.src_words = p.tailcap;
+        z.region_words = 3 * (size_t)p.n;  // u64 pairs + the CSR
+        z.scratch_words = (size_t)p.ba * p.nb + 2 * (size_t)p.nb + 1;  // M, tot, base, tail count
     }
     return z;
 }

@@ -30,9 +30,9 @@ struct RoundArgs {
     uint16_t *obs_rec;        // [n][R]
     uint32_t *obs_psize;      // [n]
     // shard engine only (null otherwise): exchange rows, see gs_shard.hip
-    const u64 *recvA;         // round-t push rows of this shard's pushers [e][3][W]
+    const u64 *recvA;         // round-t push rows of this shard's pushers [e][2][W]
     const u64 *recvB;         // round-t pull rows for this shard's nodes [pos][2][W]
-    u64 *sendA;               // round-(t+1) push rows of this shard's nodes [pos][3][W]
+    u64 *sendA;               // round-(t+1) push rows of this shard's nodes [pos][2][W]
     const uint32_t *spos_cur; // row of x in recvB (= its round-t push row position)
     const uint32_t *spos_next;// row of x in sendA for round t+1
     // harness-injected faults (gs_common.h); pend/offc exist iff f.churn != 0
@@ -118,7 +118,7 @@ struct PullArgs {
     const u64 *S;          // round-t planes of the owned nodes
     const uint4 *IN;       // round-t in-lists of receive rows
     const uint32_t *EP;
-    const u64 *recvA;      // round-t push rows received [e][3][W]
+    const u64 *recvA;      // round-t push rows received [e][2][W]
     u64 *sendB;            // pull rows out [e][2][W]
     Geometry g;            // local geometry (n = m)
 };

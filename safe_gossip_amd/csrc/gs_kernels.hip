@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
 
     // ---- coalesced per-node metadata (level 1)
     uint4 in = {0, 0, 0, 0};   // SHARD: {first, k|zi<<16, e0, e1}
-    InRec in8 = {};            // {first (tail), k, s0..s5}
+    InRec in8 = {};            // {first << 5 | k, s0..s2}
     SibRec sb8 = {};           // {serial<<8 | rank of x in in(z), e0..e2}; stale unless rank >= 1
     uint32_t z = x, zi = 0xFFFFu, k = 0, r = 0;
     uint32_t tgw = 0;  // round-t target word: t(x) + delivery flags (gs_common.h)
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             sb8 = a.SIB8[x];
             tgw = a.tg[x];
             z = tgw & kTgMask;  // t_t(x)
-            k = valid ? in8.k : 0u;
+            k = valid ? in8.k() : 0u;
             r = (valid && (sb8.tag >> 8) == (a.serial & kSerialMask)) ? (sb8.tag & 0xFFu) : 0u;
         }
 #ifdef GS_EXP_NO_PUSHERS
@@ -194,8 +194,8 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     if (DELIVER) {
         if (SHARD) {
             if (valid) {
-                if (k > 0) q[0] = L.load_row3(a.recvA, in.z);
-                if (k > 1) q[1] = L.load_row3(a.recvA, in.w);
+                if (k > 0) q[0] = L.load_push_row(a.recvA, in.z);
+                if (k > 1) q[1] = L.load_push_row(a.recvA, in.w);
                 if (!(tgw & kTgNoPull)) {
                     const uint32_t sp = a.spos_cur[x];  // the pull row z returned to x
                     qz.c = a.recvB[L.row_index(sp, 2, 0)];
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             const uint32_t zs = pulled ? zi : 0xFFFFu;  // push copy superseded by the pull copy
             if (k > 0) rv.push(q[0], 0, k, zs != 0);
             if (k > 1) rv.push(q[1], 1, k, zs != 1);
-            for (uint32_t i = 2; i < k; ++i) rv.push(L.load_row3(a.recvA, a.src[in.x + i]), i, k, zs != i);
+            for (uint32_t i = 2; i < k; ++i) rv.push(L.load_push_row(a.recvA, a.src[in.x + i]), i, k, zs != i);
             // pull row code (b0, b1): 01 counter 1, 10 counter 2, 11 counter 255
             pv2 = qz.a0 & ~qz.c;
             pvB = qz.c ^ qz.a0;
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                 }
             }
             for (uint32_t i = kBatchK; i < k; ++i) {  // in-degree > kBatchK (1.9% of nodes)
-                const uint32_t s = i < kInline ? pick_inline(in8.s, i) : a.src[in8.first + (i - kInline)];
+                const uint32_t s = i < kInline ? pick_inline(in8.s, i) : a.src[in8.first() + (i - kInline)];
                 zin |= s == z;
                 rv.push(L.load_cls(S, s), i, k, !(pulled && s == z));
             }
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                     const InRec zin8 = a.IN8[z];
                     for (uint32_t i = kSibInline; i < r && pnot; ++i) {
                         const uint32_t s = i < kInline ? pick_inline(zin8.s, i)
-                                                       : a.src[zin8.first + (i - kInline)];
+                                                       : a.src[zin8.first() + (i - kInline)];
                         sibling(L.load_cls(S, s), pnot, pB, pC);
                     }
                 }
@@ -499,10 +499,11 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         for (uint32_t i = threadIdx.x; i < blk_v4; i += blockDim.x) dst4[i] = src4[i];
     }
     if (SHARD && valid && !(faults_on(a.f) && (a.tg_next[x] & kTgDead))) {
-        // push row of round t+1: the class planes, to owner(t_{t+1}(x))
+        // push row of round t+1: the push batch's class code, to owner(t_{t+1}(x))
         const uint32_t sp = a.spos_next[x];
-#pragma unroll
-        for (int p = 0; p < kClsPlanes; ++p) a.sendA[L.row_index(sp, 3, p)] = N[p] & L.m;
+        const u64 vC = N[0] & ~(N[1] & N[2]), vB = ~N[0] & (N[1] | N[2]);
+        a.sendA[L.row_index(sp, 2, 0)] = ((vB & N[1] & ~N[2]) | vC) & L.m;  // code bit 0
+        a.sendA[L.row_index(sp, 2, 1)] = ((vB & N[2] & ~N[1]) | vC) & L.m;  // code bit 1
     }
 
     // ---- push list + Statistics (src/gossip.rs:80,103-111)

@@ -4,8 +4,9 @@
 // Per round t, rank g owns nodes [lo, lo+m).  Data movement between ranks is
 // two exchanges of rows (RCCL all-to-allv over xGMI, or device copies when the
 // shards share a GPU):
-//   A (push rows):  every node x sends its round-t class planes (isC, a0, a1;
-//                   3 x W words) to owner(t_t(x)).  Rank g's receive buffer
+//   A (push rows):  every node x sends its round-t push batch as a 2-plane
+//                   class code (2 x W words: 01 counter 1, 10 counter 2, 11
+//                   counter 255) to owner(t_t(x)).  Rank g's receive buffer
 //                   holds the rows of ALL sources targeting g in ascending
 //                   source order (ranks own ascending ranges and each sends its
 //                   rows for a destination in ascending order).
@@ -383,7 +384,7 @@ __global__ __launch_bounds__(256) void pull_kernel(PullArgs a) {
         const u64 pcl = zC | pC;
         a.sendB[L.row_index(e, 2, 0)] = zB1 | pB | pcl;  // code bit 0: counter 1 or 255
         a.sendB[L.row_index(e, 2, 1)] = zB2 | pcl;       // code bit 1: counter 2 or 255
-        if (i + 1 < k && pnot) sibling(L.load_row3(a.recvA, e), pnot, pB, pC);
+        if (i + 1 < k && pnot) sibling(L.load_push_row(a.recvA, e), pnot, pB, pC);
     }
 }
 
