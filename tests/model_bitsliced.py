@@ -19,7 +19,7 @@ def popc(v):
 
 
 class Model:
-    def __init__(self, n, R, seed, epoch, params, peer_fn, fault_fn=None):
+    def __init__(self, n, R, seed, epoch, params, peer_fn, fault_fn=None, schedule=0):
         self.n, self.R, self.seed, self.epoch = n, R, seed, epoch
         self.cmax, self.maxc, self.maxr = params
         self.M = (1 << R) - 1
@@ -34,6 +34,8 @@ class Model:
         self.fl = [0] * n                        # delivery flags of the round (OFF/DEAD/NOPULL)
         self.pend = [(0, 0)] * n                 # frozen votes (bump, anyC)
         self.deliver_pending = False
+        self.schedule = schedule                 # 0 = 2P, 1 = SEQ
+        self.W = None                            # SEQ: pull batch of every node
 
     def offline(self, rnd, x):
         return bool(self.fault_fn and self.fault_fn(rnd, x) & 1)
@@ -86,8 +88,113 @@ class Model:
         pcl = zC | pC
         return (zB & z0 & ~z1 & M) | pB | pcl, (zB & z1 & ~z0 & M) | pcl
 
+    # ------------------------------------------------------------------ SEQ
+    # The literal harness order (src/gossiper.rs:217-234): pair (x, t(x)) at
+    # "time" x; t(x) answers x's push with its CURRENT live set (before
+    # absorbing the push), which x absorbs at once.  So the pull x receives,
+    # W(x) = S(z) + what z created before time x, depends on W(z) when z < x:
+    # dependencies point to smaller ids, so ascending order (the engine: levels
+    # of the chain x -> t(x) -> ... while ids decrease) resolves them.
+    def got0(self, y):
+        return not self.fl[y] & NOPULL
+
+    def got(self, y):
+        """y receives a pull at time y: its push was delivered and answered
+        (t(y) had not heard from y already: the mutual pair processed second
+        gets none, src/gossip.rs:125-126) and the pull was not dropped."""
+        if not self.got0(y):
+            return False
+        z = self.tg[y]
+        return not (self.tg[z] == y and z < y and self.got0(z))
+
+    def seq_pulls(self):
+        M = self.M
+        W = [None] * self.n
+        for y in range(self.n):
+            if not self.got(y):
+                continue
+            z = self.tg[y]
+            zc, z0, z1 = self.cls(z)
+            notyet = ~zc & ~z0 & ~z1 & M
+            zB = ~zc & (z0 | z1) & M
+            zC = zc & ~(z0 & z1) & M
+            cB = cC = 0
+            ev = [(s, 0) for s in self.src[z] if s < y]
+            if z < y and self.got(z):
+                ev.append((z, 1))
+            for t_, kind in sorted(ev):
+                if kind == 0:
+                    qc, q0, q1 = self.cls(t_)
+                    vC = qc & ~(q0 & q1) & M
+                    sl = (~qc & (q0 | q1) & M) | vC
+                else:
+                    b0, b1 = W[z]
+                    vC = b0 & b1
+                    sl = (b0 | b1) & M
+                nc = notyet & sl
+                cB |= nc & ~vC & M
+                cC |= nc & vC
+                notyet &= ~sl & M
+            W[y] = ((zB & z0 & ~z1 & M) | cB | zC | cC, (zB & z1 & ~z0 & M) | zC | cC)
+        self.W = W
+
+    def deliver_seq(self, x):
+        M = self.M
+        isC, a0, a1 = self.cls(x)
+        A = ~isC & ~a0 & ~a1 & M
+        B = ~isC & (a0 | a1) & M
+        C = isC & ~(a0 & a1) & M
+        lc = popc(B | C)
+        z = self.tg[x]
+        gx = self.got(x)
+        ins = self.src[x]
+        zin = z in ins
+        ev = [(s, 0) for s in ins] + ([(x, 1)] if gx else [])
+        crB = crC = anyC = 0
+        c1, c2 = [0] * 5, [0] * 5
+        notyet = A
+        recv = full = empty = created = 0
+        for t_, kind in sorted(ev):
+            if kind == 0:
+                s = t_
+                if not (s == z and x < z and gx):      # x answers s's push
+                    if lc + created:
+                        full += lc + created
+                    else:
+                        empty += 1
+                qc, q0, q1 = self.cls(s)
+                vC = qc & ~(q0 & q1) & M
+                vB = ~qc & (q0 | q1) & M
+                v2 = vB & q1 & ~q0 & M
+                rec_on = not (s == z and gx and z < x)  # superseded by the later pull
+            else:
+                b0, b1 = self.W[x]
+                vC = b0 & b1
+                vB = (b0 ^ b1) & M
+                v2 = b1 & ~b0 & M
+                rec_on = not (zin and z > x)           # superseded by z's later push
+            sl = vB | vC
+            newc = notyet & sl
+            if rec_on:
+                rec = (B | crB) & sl
+                anyC |= rec & vC
+                self.add5(c1, rec & vB)
+                self.add5(c2, rec & v2)
+            crB |= newc & ~vC & M
+            crC |= newc & vC
+            notyet &= ~sl & M
+            created += popc(newc)
+            recv += popc(sl)
+        psize = len(ins) + (1 if gx and not zin else 0)
+        return dict(crB=crB, crC=crC, anyC=anyC, c1=c1, c2=c2, psize=psize, d_full=full,
+                    d_empty_pull=empty, d_recv=recv)
+
     def deliver(self, x):
         """Phases 1+2 of round t at x: returns the kernel's per-lane values."""
+        if self.schedule == 1:
+            if self.W is None:
+                self.seq_pulls()
+            return self.deliver_seq(x)
         z = self.tg[x]
         ins = [(s, self.cls(s)) for s in self.src[x]]
         pulled = not self.fl[x] & NOPULL
@@ -255,6 +362,7 @@ class Model:
             live_any |= live > 0
         self.P = newP
         self.round = rnd
+        self.W = None
         self.plan_round(rnd)
         self.deliver_pending = True
         return live_any

@@ -9,12 +9,13 @@ from model_bitsliced import Model
 from oracle_lib import SCHED_2P, OracleNet
 
 
-def run(n, R, params=None, seed=0x5AFE6055, epoch=0, kind="origins", max_rounds=40, faults=None):
+def run(n, R, params=None, seed=0x5AFE6055, epoch=0, kind="origins", max_rounds=40, faults=None,
+        schedule=SCHED_2P):
     thr = [oracle_lib.fault_threshold(p) for p in faults] if faults else None
     orc = OracleNet(n, R, seed=seed, epoch=epoch, params=params, faults=thr)
     L = oracle_lib.lib()
     fault_fn = (lambda rnd, x: L.or_fault(seed, epoch, rnd, x, *thr)) if faults else None
-    mdl = Model(n, R, seed, epoch, orc.params, L.or_peer, fault_fn)
+    mdl = Model(n, R, seed, epoch, orc.params, L.or_peer, fault_fn, schedule)
     rng = np.random.default_rng(n * 31 + R)
     for rnd in range(1, max_rounds + 1):
         inj = []
@@ -25,7 +26,7 @@ def run(n, R, params=None, seed=0x5AFE6055, epoch=0, kind="origins", max_rounds=
         for x, r in inj:
             orc.send_new(x, r)
             mdl.send_new(x, r)
-        _, olive = orc.next_round(SCHED_2P)
+        _, olive = orc.next_round(schedule)
         mlive = mdl.next_round()
         assert mlive == olive, rnd
         codes, recs, psz, stats, known = mdl.observe()
@@ -80,3 +81,23 @@ def test_model_equals_oracle(oracle, n, R, params, kind):
 ])
 def test_model_equals_oracle_faults(oracle, n, R, kind, faults):
     run(n, R, kind=kind, faults=faults)
+
+
+@pytest.mark.parametrize("n,R,kind,params,faults", [
+    (8, 3, "origins", None, None),
+    (2, 1, "origins", None, None),
+    (3, 2, "origins", None, None),
+    (20, 4, "reinject", None, None),
+    (60, 8, "origins", None, None),
+    (200, 5, "reinject", None, None),
+    (40, 7, "origins", (2, 3, 5), None),
+    (40, 7, "reinject", (1, 1, 3), None),
+    (300, 6, "origins", (3, 3, 14), None),
+    (1700, 3, "origins", None, None),
+    (60, 8, "origins", None, (0.1, 0.1, 0.1)),
+    (200, 5, "reinject", None, (0.3, 0.1, 0.2)),
+    (300, 6, "origins", None, (0.0, 0.0, 0.4)),
+])
+def test_model_equals_oracle_seq(oracle, n, R, kind, params, faults):
+    """The literal harness order (SEQ): pulls answered from the current state."""
+    run(n, R, params, kind=kind, faults=faults, schedule=oracle_lib.SCHED_SEQ)
