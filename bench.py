@@ -60,6 +60,8 @@ def parse():
     p.add_argument("--churn", type=float, default=None, help="P(node offline) per round")
     p.add_argument("--drop-push", type=float, default=None, help="P(push batch dropped)")
     p.add_argument("--drop-pull", type=float, default=None, help="P(pull batch dropped)")
+    p.add_argument("--schedule", default="2P", choices=["2P", "SEQ"],
+                   help="2P (default) or SEQ (the reference harness's literal order; 1 GPU)")
     p.add_argument("--seed", type=lambda s: int(s, 0), default=0x5AFE6055)
     p.add_argument("--cpu-seconds", type=float, default=15.0,
                    help="budget of the CPU-oracle sample")
@@ -109,7 +111,7 @@ def spread_run(net, epoch, max_rounds=200):
                 known_fraction=known / float(net.n * net.R))
 
 
-def cpu_baseline(R, seed, budget_s, faults=(0.0, 0.0, 0.0)):
+def cpu_baseline(R, seed, budget_s, faults=(0.0, 0.0, 0.0), schedule="2P"):
     """Time the CPU oracle (port) on a bounded sample: n_cpu nodes, same R."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib
@@ -123,7 +125,7 @@ def cpu_baseline(R, seed, budget_s, faults=(0.0, 0.0, 0.0)):
     t0 = time.perf_counter()
     rounds = 0
     while True:
-        _, live = net.next_round(oracle_lib.SCHED_2P)
+        _, live = net.next_round(oracle_lib.SCHED_SEQ if schedule == "SEQ" else oracle_lib.SCHED_2P)
         rounds += 1
         el = time.perf_counter() - t0
         if not live or el > budget_s:
@@ -131,7 +133,7 @@ def cpu_baseline(R, seed, budget_s, faults=(0.0, 0.0, 0.0)):
     net.close()
     return dict(value=n_cpu * R * rounds / el, unit="node-rumor updates/s", cores=1,
                 kind="port",
-                sample=f"CPU oracle (per-node ordered maps, 1 thread, 2P), n={n_cpu}, R={R}, "
+                sample=f"CPU oracle (per-node ordered maps, 1 thread, {schedule}), n={n_cpu}, R={R}, "
                        f"all rumors injected round 1, {rounds} rounds in {el:.1f}s"
                        + (f", faults {faults}" if thr else ""))
 
@@ -157,6 +159,8 @@ def main():
 
     n, R = args.nodes, args.rumors
     fk = dict(churn=args.faults[0], drop_push=args.faults[1], drop_pull=args.faults[2])
+    if args.schedule != "2P":
+        fk["schedule"] = args.schedule
     if world > 1:
         from safe_gossip_amd.sharded import ShardedNetwork
         net = ShardedNetwork(n, R, world, seed=args.seed, epoch=0, device=local,
@@ -215,7 +219,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(R, args.seed, args.cpu_seconds, args.faults)
+        cpu = cpu_baseline(R, args.seed, args.cpu_seconds, args.faults, args.schedule)
 
     if rank == 0:
         total_updates = float(n) * R * args.steps
@@ -234,7 +238,7 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": f"{args.config}: {n} nodes x {R} rumors, full mesh, all rumors injected in "
-                            f"round 1 at Philox origins, 2P schedule, {args.steps} rounds"
+                            f"round 1 at Philox origins, {args.schedule} schedule, {args.steps} rounds"
                             + (", faults churn/drop_push/drop_pull = %g/%g/%g per node-round"
                                % args.faults if any(args.faults) else ""),
                 "n_nodes": n, "n_rumors": R, "seed": hex(args.seed),

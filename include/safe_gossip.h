@@ -51,6 +51,12 @@ typedef enum {
                                      counter range (probability ~1e-34/node) */
 } gs_status;
 
+/* Delivery order of a round.  2P: the reference harness
+ * with each pull batch delivered after all push batches of the round.  SEQ:
+ * the harness's literal order (src/gossiper.rs:217-234), each pull answered
+ * from the responder's current state and delivered at once; single-GPU only. */
+typedef enum { GS_SCHED_2P = 0, GS_SCHED_SEQ = 1 } gs_schedule;
+
 typedef struct {
     uint32_t n_nodes;        /* network size n (full mesh)                   */
     uint32_t n_rumors;       /* R: rumor slots per node (1..4096)            */
@@ -59,7 +65,7 @@ typedef struct {
     uint8_t counter_max;     /* 0 = derive from n (src/gossip.rs:61)         */
     uint8_t max_c_rounds;    /* 0 = derive from n (src/gossip.rs:62)         */
     uint8_t max_rounds;      /* 0 = derive from n (src/gossip.rs:63)         */
-    uint8_t reserved0;
+    uint8_t schedule;        /* gs_schedule: delivery order of a round       */
     int32_t device;          /* HIP device ordinal, -1 = current             */
     /* Harness-injected faults (BASELINE config 5), thresholds over 2^32
      * (probability = value / 2^32), drawn per (round, node) from the Philox

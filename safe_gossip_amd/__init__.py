@@ -61,7 +61,7 @@ class _Config(ctypes.Structure):
         ("n_nodes", ctypes.c_uint32), ("n_rumors", ctypes.c_uint32),
         ("seed", ctypes.c_uint64), ("epoch", ctypes.c_uint32),
         ("counter_max", ctypes.c_uint8), ("max_c_rounds", ctypes.c_uint8),
-        ("max_rounds", ctypes.c_uint8), ("reserved0", ctypes.c_uint8),
+        ("max_rounds", ctypes.c_uint8), ("schedule", ctypes.c_uint8),
         ("device", ctypes.c_int32), ("churn", ctypes.c_uint32),
         ("drop_push", ctypes.c_uint32), ("drop_pull", ctypes.c_uint32),
         ("reserved1", ctypes.c_uint32 * 4),
@@ -248,6 +248,10 @@ def fault_threshold(p: float) -> int:
 
 FAULT_OFFLINE, FAULT_PUSH, FAULT_PULL = 1, 2, 4
 
+# gs_schedule: "2P" (pulls after all pushes) or "SEQ" (the reference harness's
+# literal order, src/gossiper.rs:217-234)
+SCHEDULES = {"2P": 0, "SEQ": 1}
+
 
 def fault_of(seed: int, epoch: int, rnd: int, node: int, faults) -> int:
     """Fault bits of (round, node); faults = (churn, drop_push, drop_pull) thresholds."""
@@ -270,9 +274,13 @@ class Network:
 
     def __init__(self, n_nodes: int, n_rumors: int, seed: int = 0x5AFE6055, epoch: int = 0,
                  params=None, device: int = 0, churn: float = 0.0, drop_push: float = 0.0,
-                 drop_pull: float = 0.0):
+                 drop_pull: float = 0.0, schedule: str = "2P"):
         self._lib = load_library()
         cfg = _Config()
+        if schedule not in SCHEDULES:
+            raise ValueError(f"schedule {schedule!r} not in {sorted(SCHEDULES)}")
+        cfg.schedule = SCHEDULES[schedule]
+        self.schedule = schedule
         # harness-injected faults (config 5): probabilities per (round, node)
         self.faults = (fault_threshold(churn), fault_threshold(drop_push), fault_threshold(drop_pull))
         cfg.churn, cfg.drop_push, cfg.drop_pull = self.faults

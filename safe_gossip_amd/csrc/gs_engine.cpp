@@ -23,6 +23,10 @@ struct gs_engine {
     uint64_t seed = 0;
     uint32_t epoch = 0;
     gs::Faults faults{};
+    bool seq = false;              // GS_SCHED_SEQ (gs_seq.hip)
+    u64 *Wb = nullptr;             // SEQ: pull batch of every node [n][2][W]
+    uint8_t *sinfo = nullptr;      // SEQ: got/dep/level per node
+    uint32_t seq_round = ~0u;      // round whose pull batches Wb holds
     u64 *pend = nullptr;       // churn: votes of frozen (offline) nodes [n][2][W]
     uint32_t *offc = nullptr;  // churn: rounds offline per node
     uint8_t cmax = 0, maxc = 0, maxr = 0;
@@ -128,7 +132,7 @@ void release(gs_engine *e) {
         if (e->ev_kr[i]) (void)hipEventDestroy(e->ev_kr[i]);
     }
     if (e->cstream) (void)hipStreamDestroy(e->cstream);
-    void *bufs[] = {e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
+    void *bufs[] = {e->Wb, e->sinfo, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
                     e->partials, e->obs_state, e->obs_rec, e->obs_psize};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -153,6 +157,7 @@ gs_status reset_state(gs_engine *e) {
     GS_HIP(hipMemsetAsync(e->flags, 0, 4 * sizeof(uint32_t), e->stream));
     e->cur = 0;
     e->round = 0;
+    e->seq_round = ~0u;
     e->deliver_pending = false;
     e->pending.clear();
     e->obs_valid = false;
@@ -188,6 +193,10 @@ gs::RoundArgs base_args(gs_engine *e) {
     a.f = e->faults;
     a.pend = e->pend;
     a.offc = e->offc;
+    if (e->seq) {
+        a.Wb = e->Wb;
+        a.sinfo = e->sinfo;
+    }
     a.obs_rounds = e->round;
     a.flags = e->flags;
     a.g = e->g;
@@ -260,6 +269,33 @@ gs_status ensure_obs(gs_engine *e, bool dumps) {
     return GS_OK;
 }
 
+// SEQ: the pull batches of the pending round (levels, then one pass per
+// level), once per round, on the engine stream.
+gs_status seq_prepare(gs_engine *e) {
+    if (!e->seq || !e->deliver_pending || e->seq_round == e->round) return GS_OK;
+    const auto &cs = e->csr[e->round & 1u];
+    GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
+    gs::SeqArgs sa{};
+    sa.S = e->S[e->cur];
+    sa.IN8 = cs.IN8;
+    sa.SIB8 = cs.SIB8;
+    sa.src = cs.src;
+    sa.tg = cs.tg;
+    sa.serial = cs.serial;
+    sa.sinfo = e->sinfo;
+    sa.Wb = e->Wb;
+    sa.flags = e->flags;
+    sa.g = e->g;
+    GS_HIP(hipMemsetAsync(e->flags + 3, 0, sizeof(uint32_t), e->stream));
+    GS_HIP(gs::launch_seq_levels(sa, e->stream));
+    uint32_t maxlev = 0;
+    GS_HIP(hipMemcpyAsync(&maxlev, e->flags + 3, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    GS_HIP(hipStreamSynchronize(e->stream));
+    for (uint32_t l = 0; l <= maxlev; ++l) GS_HIP(gs::launch_seq_pull_pass(sa, l, e->stream));
+    e->seq_round = e->round;
+    return GS_OK;
+}
+
 // Fill the observation buffers with the state after the last delivery.
 gs_status observe(gs_engine *e, bool dumps) {
     if (e->obs_valid && !dumps) return GS_OK;
@@ -276,6 +312,8 @@ gs_status observe(gs_engine *e, bool dumps) {
     if (e->deliver_pending) {
         if (e->shard) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[e->round % 3], 0));
         else GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
+        st = seq_prepare(e);
+        if (st != GS_OK) return st;
     }
     GS_HIP(gs::launch_round(a, e->deliver_pending ? 2 : 3, e->stream));
     uint32_t fl = 0;
@@ -364,6 +402,8 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
     if (cfg->max_rounds) p[2] = cfg->max_rounds;
     if (nglob >= 2 && (p[0] > 3 || p[1] > 3 || p[2] > 32 || !p[0] || !p[1] || !p[2]))
         return GS_ERR_UNSUPPORTED;
+    if (cfg->schedule > GS_SCHED_SEQ) return GS_ERR_INVALID_ARGUMENT;
+    if (world && cfg->schedule == GS_SCHED_SEQ) return GS_ERR_UNSUPPORTED;  // chains cross ranks
 
     gs_engine *e = new gs_engine();
     e->shard = world != 0;
@@ -372,6 +412,7 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
     e->seed = cfg->seed;
     e->epoch = cfg->epoch;
     e->faults = gs::Faults{cfg->churn, cfg->drop_push, cfg->drop_pull};
+    e->seq = cfg->schedule == GS_SCHED_SEQ;
     e->cmax = p[0];
     e->maxc = p[1];
     e->maxr = p[2];
@@ -437,6 +478,8 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
     ok = ok && dalloc(&e->S[0], sw) == hipSuccess && dalloc(&e->S[1], sw) == hipSuccess &&
          dalloc(&e->flags, 4) == hipSuccess && dalloc(&e->st32, (size_t)4 * n) == hipSuccess &&
          dalloc(&e->st64, (size_t)4 * n) == hipSuccess;
+    if (ok && e->seq)
+        ok = dalloc(&e->Wb, (size_t)n * 2 * g.W) == hipSuccess && dalloc(&e->sinfo, n) == hipSuccess;
     if (ok && e->faults.churn)
         ok = dalloc(&e->pend, (size_t)n * 2 * g.W) == hipSuccess && dalloc(&e->offc, n) == hipSuccess;
     if (!ok) {
@@ -583,6 +626,8 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
         if (e->deliver_pending) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[R0 % 3], 0));
     } else if (e->deliver_pending) {
         GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[rs], 0));
+        st = seq_prepare(e);  // SEQ: pull batches of round t (no-op for 2P)
+        if (st != GS_OK) return st;
     }
     if (e->timing) GS_HIP(hipEventRecord(t0, e->stream));
     GS_HIP(gs::launch_round(a, e->deliver_pending ? 1 : 0, e->stream));

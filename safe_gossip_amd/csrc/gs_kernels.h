@@ -40,6 +40,10 @@ struct RoundArgs {
     u64 *pend;                // [n][2][W]: votes (bump, anyC) of nodes frozen offline
     uint32_t *offc;           // [n] rounds each node was offline (Statistics.rounds)
     uint32_t node_lo;         // global id of local node 0 (shard engine; else 0)
+    // SEQ schedule (gs_seq.hip): pull batch of every node as a 2-plane class
+    // code [n][2][W], and per node got << 7 | dep << 6 | level
+    const u64 *Wb;
+    const uint8_t *sinfo;
     Geometry g;
     uint64_t seed;
     uint32_t epoch;
@@ -89,6 +93,26 @@ struct InListArgs {
 // stream concurrently with the round kernel of the round before.
 hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s);
 hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, hipStream_t s);
+
+// ---------------------------------------------------------------- SEQ
+// The literal harness order (gs_seq.hip): per round, seq_levels classifies
+// every node (does it get a pull, does its pull depend on t(x)'s, the depth of
+// that chain), then one pull pass per level builds W(x) for the nodes of that
+// level from W(t(x)) of the level before.
+struct SeqArgs {
+    const u64 *S;             // round-t planes
+    const InRec *IN8;
+    const SibRec *SIB8;
+    const uint32_t *src;
+    const uint32_t *tg;
+    uint32_t serial;
+    uint8_t *sinfo;           // [n] got << 7 | dep << 6 | level
+    u64 *Wb;                  // [n][2][W] pull batches (2-plane class code)
+    uint32_t *flags;          // flags[2] device limit, flags[3] deepest level
+    Geometry g;
+};
+hipError_t launch_seq_levels(const SeqArgs &a, hipStream_t s);
+hipError_t launch_seq_pull_pass(const SeqArgs &a, uint32_t level, hipStream_t s);
 
 // ---------------------------------------------------------------- shards
 // One rank's slice of a network sharded over G ranks (gs_shard.hip).

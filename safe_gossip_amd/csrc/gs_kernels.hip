@@ -93,8 +93,23 @@ struct Recv {
         oc1 |= newc & ~vC;
         notyet &= ~newc;
     }
-    // One push batch from pusher i of k (Gossip::receive, src/gossip.rs:153-163);
-    // `rec_on` is false for t(x)'s own push, superseded by its pull copy.
+    // One batch x absorbs (Gossip::receive, src/gossip.rs:153-163) with
+    // copies of class vB (counter < counter_max; v2: counter 2) or vC (255).
+    // `rafter` = pull rows x sends after it (they include what it creates),
+    // `ev` = its position among x's batches; `recm` masks out the rumors whose
+    // copy a later copy from the same peer overwrites (message_state.rs:79).
+    GS_DEV void absorb(u64 vB, u64 v2, u64 vC, uint32_t rafter, uint32_t ev, u64 recm) {
+        const u64 sl = vB | vC;                // the batch
+        const u64 newc = notyet & sl;          // new_from_peer: not recorded
+        record(recB & sl & recm, vB, v2, vC);  // MessageState::receive on B
+        create(newc, vC);
+        const uint32_t pc = popc(newc);
+        part_cw += rafter * pc;
+        if (pc && first_create == kNone) first_create = ev;
+        recv += popc(sl);
+    }
+    // Push batch of pusher i of k (2P: pushers in ascending order, all
+    // answered; `rec_on` is false for t(x)'s own push, superseded by its pull).
     GS_DEV void push(const Cls &q, uint32_t i, uint32_t k, bool rec_on) {
         const u64 vC = q.c & ~(q.a0 & q.a1);   // C: counter 255
         const u64 vB = ~q.c & (q.a0 | q.a1);   // B: counter = our_counter
@@ -108,6 +123,12 @@ struct Recv {
         if (pc && first_create == kNone) first_create = i;
         recv += popc(sl);
     }
+    GS_DEV void absorb_cls(const Cls &q, uint32_t rafter, uint32_t ev, bool rec_on) {
+        const u64 vC = q.c & ~(q.a0 & q.a1);   // C: counter 255
+        const u64 vB = ~q.c & (q.a0 | q.a1);   // B: counter = our_counter
+        const u64 v2 = vB & q.a1 & ~q.a0;      // B with our_counter 2
+        absorb(vB, v2, vC, rafter, ev, rec_on ? ~0ull : 0ull);
+    }
 };
 
 #ifndef GS_RK_MINW
@@ -119,7 +140,10 @@ struct Recv {
 // SHARD: this engine owns a node range of a sharded network; pusher class rows
 // and the pull row come from the exchange buffers (recvA, recvB) instead of
 // gathers, and the new class planes are also written as push rows (sendA).
-template <bool SMALL, int MODE, bool SHARD>
+// SEQ: the literal harness order (gs_seq.hip): x's pull batch W(x) was built
+// by the level passes, and it is absorbed at x's own position among its
+// pushers (time x), answered pushes included.
+template <bool SMALL, int MODE, bool SHARD, bool SEQ>
 __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     constexpr bool DELIVER = (MODE == 1 || MODE == 2);
     constexpr bool TRANSITION = (MODE == 0 || MODE == 1);
@@ -153,6 +177,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     SibRec sb8 = {};           // {serial<<8 | rank of x in in(z), e0..e2}; stale unless rank >= 1
     uint32_t z = x, zi = 0xFFFFu, k = 0, r = 0;
     uint32_t tgw = 0;  // round-t target word: t(x) + delivery flags (gs_common.h)
+    uint32_t sinf = 0;  // SEQ: got << 7 | ... (gs_seq.hip)
     if (DELIVER) {
         if (SHARD) {
             if (valid) {
@@ -163,11 +188,15 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             }
         } else {
             in8 = a.IN8[x];  // x = 0 on invalid lanes: a harmless valid address
-            sb8 = a.SIB8[x];
             tgw = a.tg[x];
             z = tgw & kTgMask;  // t_t(x)
             k = valid ? in8.k() : 0u;
-            r = (valid && (sb8.tag >> 8) == (a.serial & kSerialMask)) ? (sb8.tag & 0xFFu) : 0u;
+            if (SEQ) {
+                sinf = a.sinfo[x];
+            } else {
+                sb8 = a.SIB8[x];
+                r = (valid && (sb8.tag >> 8) == (a.serial & kSerialMask)) ? (sb8.tag & 0xFFu) : 0u;
+            }
         }
 #ifdef GS_EXP_NO_PUSHERS
         k = 0;
@@ -206,9 +235,17 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         } else {
 #pragma unroll
             for (uint32_t i = 0; i < kBatchK; ++i) q[i] = L.load_cls(S, i < k ? in8.s[i] : x);
-            qz = L.load_cls(S, z);
+            if (SEQ) {  // W(x), coalesced (qz holds its code planes)
+                if (valid && (sinf & kSeqGot)) {
+                    const u64 wi = ((u64)x * 2u) * g.W + L.j;
+                    qz.c = a.Wb[wi];
+                    qz.a0 = a.Wb[wi + g.W];
+                }
+            } else {
+                qz = L.load_cls(S, z);
 #pragma unroll
-            for (uint32_t i = 0; i < kBatchE; ++i) e[i] = L.load_cls(S, i < r ? sb8.e[i] : x);
+                for (uint32_t i = 0; i < kBatchE; ++i) e[i] = L.load_cls(S, i < r ? sb8.e[i] : x);
+            }
         }
     }
     {
@@ -243,6 +280,8 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     Recv<!TRANSITION> rv;
     rv.init(A, B, B & a0 & ~a1);
     uint32_t psize = 0;
+    bool seq_gx = false, seq_skip = false;
+    uint32_t seq_px = 0, seq_jz = kNone;
     if (DELIVER && valid) {
         if (k > 30u) atomicOr(&a.flags[2], 1u);
         bool zin = false;
@@ -258,6 +297,55 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             pv2 = qz.a0 & ~qz.c;
             pvB = qz.c ^ qz.a0;
             pCl = qz.c & qz.a0;
+        } else if (SEQ) {
+            // Events at x in time order: pushes from s < x, x's own pair (its
+            // pull W(x), if it gets one), pushes from s > x.  x answers every
+            // push except z's when x already heard from z (x < z, pulled);
+            // of two copies from z the later one is recorded.
+            const bool gx = (sinf & kSeqGot) != 0;
+            uint32_t px = 0, jz = kNone;
+            for (uint32_t i = 0; i < k; ++i) {
+                const uint32_t s = i < kInline ? pick_inline(in8.s, i) : a.src[in8.first() + (i - kInline)];
+                px += s < x ? 1u : 0u;
+                if (s == z) jz = i;
+            }
+            zin = jz != kNone;
+            const bool skip = gx && zin && z > x;
+            const uint32_t sk = skip ? 1u : 0u;
+            // z's later push (z > x) overwrites the pull's records of the
+            // rumors it carries (the pull may also carry entries z created)
+            u64 precm = ~0ull;
+            if (zin && z > x) {
+                Cls qj = L.load_cls(S, z);
+                const u64 vCj = qj.c & ~(qj.a0 & qj.a1);
+                precm = ~((~qj.c & (qj.a0 | qj.a1)) | vCj);
+            }
+            pv2 = qz.a0 & ~qz.c;  // W(x) code (b0, b1) = (qz.c, qz.a0)
+            pvB = qz.c ^ qz.a0;
+            pCl = qz.c & qz.a0;
+            bool pdone = !gx;
+            for (uint32_t i = 0; i < k; ++i) {
+                if (!pdone && i == px) {
+                    rv.absorb(pvB, pv2, pCl, k - px - sk, px, precm);
+                    pdone = true;
+                }
+                Cls qi;
+                if (i < kBatchK) {
+                    qi = q[0];
+#pragma unroll
+                    for (uint32_t b = 1; b < kBatchK; ++b) qi = (i == b) ? q[b] : qi;
+                } else {
+                    qi = L.load_cls(S, a.src[in8.first() + (i - kInline)]);
+                }
+                const uint32_t rafter = (k - 1u - i) - ((skip && jz > i) ? 1u : 0u);
+                rv.absorb_cls(qi, rafter, i + ((gx && i >= px) ? 1u : 0u), !(i == jz && gx && z < x));
+            }
+            if (!pdone) rv.absorb(pvB, pv2, pCl, 0u, px, precm);
+            seq_gx = gx;
+            seq_px = px;
+            seq_jz = jz;
+            seq_skip = skip;
+            pv2 = pvB = pCl = 0;  // absorbed above
         } else {
 #pragma unroll
             for (uint32_t i = 0; i < kBatchK; ++i) {
@@ -303,7 +391,8 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             rv.create(newc, pCl);
         }
         rv.recv += popc(pl);
-        psize = k + ((pulled && !zin) ? 1u : 0u);  // |peers_in_this_round|
+        const bool gets = SEQ ? seq_gx : pulled;
+        psize = k + ((gets && !zin) ? 1u : 0u);  // |peers_in_this_round|
     }
     const u64 crB = rv.crB, crC = rv.crC, anyC = rv.anyC;
 
@@ -317,7 +406,23 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         first_create = group_min(first_create, g.W);
     }
     uint32_t d_full_sent = 0, d_empty_pull = 0, d_recv = 0;
-    if (DELIVER) {
+    if (DELIVER && SEQ) {
+        // pull rows x sends: every answered push gets x's live set plus what x
+        // created before it; empty ones until the first creating batch
+        const uint32_t nresp = k - (seq_skip ? 1u : 0u);
+        d_full_sent = nresp * lc + part_cw;
+        if (nresp > 0 && lc == 0) {
+            if (first_create == kNone) {
+                d_empty_pull = nresp;
+            } else {
+                uint32_t c = (!seq_gx || first_create < seq_px) ? first_create + 1u : first_create;
+                c = min(c, k);
+                if (seq_skip && seq_jz + 1u <= first_create) c -= 1u;
+                d_empty_pull = c;
+            }
+        }
+        d_recv = recv;
+    } else if (DELIVER) {
         d_full_sent = k * lc + part_cw;  // pull rows sent by x
         if (k > 0 && lc == 0) d_empty_pull = (first_create == kNone) ? k : first_create + 1u;
         d_recv = recv;
@@ -531,24 +636,26 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     }
 }
 
-template <bool SMALL, bool SHARD>
+template <bool SMALL, bool SHARD, bool SEQ>
 static hipError_t launch_mode(const RoundArgs &a, int mode, hipStream_t s) {
     const uint32_t block = 256;
     const u64 grid = (a.g.nseg + block - 1) / block;
     if (grid == 0) return hipSuccess;
     switch (mode) {
-    case 0: hipLaunchKernelGGL((round_kernel<SMALL, 0, SHARD>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
-    case 1: hipLaunchKernelGGL((round_kernel<SMALL, 1, SHARD>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((round_kernel<SMALL, 2, SHARD>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
-    default: hipLaunchKernelGGL((round_kernel<SMALL, 3, SHARD>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
+    case 0: hipLaunchKernelGGL((round_kernel<SMALL, 0, SHARD, SEQ>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((round_kernel<SMALL, 1, SHARD, SEQ>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((round_kernel<SMALL, 2, SHARD, SEQ>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
+    default: hipLaunchKernelGGL((round_kernel<SMALL, 3, SHARD, SEQ>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
     }
     return hipGetLastError();
 }
 
 hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s) {
-    if (a.recvA)  // shard engine
-        return a.g.small ? launch_mode<true, true>(a, mode, s) : launch_mode<false, true>(a, mode, s);
-    return a.g.small ? launch_mode<true, false>(a, mode, s) : launch_mode<false, false>(a, mode, s);
+    if (a.recvA)  // shard engine (2P only)
+        return a.g.small ? launch_mode<true, true, false>(a, mode, s) : launch_mode<false, true, false>(a, mode, s);
+    if (a.Wb)     // SEQ schedule
+        return a.g.small ? launch_mode<true, false, true>(a, mode, s) : launch_mode<false, false, true>(a, mode, s);
+    return a.g.small ? launch_mode<true, false, false>(a, mode, s) : launch_mode<false, false, false>(a, mode, s);
 }
 
 // Fold the u32 statistics deltas into the u64 totals (before they can wrap).

@@ -155,6 +155,7 @@ class Model:
         notyet = A
         recv = full = empty = created = 0
         for t_, kind in sorted(ev):
+            rec_mask = M
             if kind == 0:
                 s = t_
                 if not (s == z and x < z and gx):      # x answers s's push
@@ -172,11 +173,14 @@ class Model:
                 vC = b0 & b1
                 vB = (b0 ^ b1) & M
                 v2 = b1 & ~b0 & M
-                rec_on = not (zin and z > x)           # superseded by z's later push
+                rec_on = True
+                if zin and z > x:  # z's later push overwrites the rumors it carries
+                    qc, q0, q1 = self.cls(z)
+                    rec_mask = ~((~qc & (q0 | q1)) | (qc & ~(q0 & q1))) & M
             sl = vB | vC
             newc = notyet & sl
             if rec_on:
-                rec = (B | crB) & sl
+                rec = (B | crB) & sl & rec_mask
                 anyC |= rec & vC
                 self.add5(c1, rec & vB)
                 self.add5(c2, rec & v2)

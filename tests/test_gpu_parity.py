@@ -10,7 +10,7 @@ node, the known-rumor sets (Gossiper::messages) and the harness's
 import numpy as np
 import pytest
 
-from oracle_lib import SCHED_2P, OracleNet, fault_threshold
+from oracle_lib import SCHED_2P, SCHED_SEQ, OracleNet, fault_threshold
 
 pytestmark = pytest.mark.gpu
 
@@ -55,7 +55,7 @@ def _first_diff(a, b):
 
 
 def run_parity(engine, n, R, kind, params=None, max_rounds=60, seed=SEED, epoch=0,
-               check_every=1, make_net=None, faults=None):
+               check_every=1, make_net=None, faults=None, schedule="2P"):
     """faults = (churn, drop_push, drop_pull) probabilities (harness-injected).
 
     A node offline in the current round keeps the peer_counters and
@@ -66,6 +66,9 @@ def run_parity(engine, n, R, kind, params=None, max_rounds=60, seed=SEED, epoch=
     fk = {}
     if faults:
         fk = dict(churn=faults[0], drop_push=faults[1], drop_pull=faults[2])
+    if schedule != "2P":
+        fk["schedule"] = schedule
+    osched = SCHED_SEQ if schedule == "SEQ" else SCHED_2P
     if make_net is None:
         net = engine.Network(n, R, seed=seed, epoch=epoch, params=params, **fk)
     else:
@@ -80,7 +83,7 @@ def run_parity(engine, n, R, kind, params=None, max_rounds=60, seed=SEED, epoch=
                 net.send_new(x, r)
                 orc.send_new(x, r)
             rep = net.next_round()
-            rc, olive = orc.next_round(SCHED_2P)
+            rc, olive = orc.next_round(osched)
             assert rc == 0
             assert rep.round == rnd == orc.round
             assert rep.any_live == olive, f"round {rnd}: any_live"
@@ -157,6 +160,35 @@ def test_round_parity(engine, n, R, kind, params):
 ])
 def test_round_parity_faults(engine, n, R, kind, faults):
     run_parity(engine, n, R, kind, faults=faults)
+
+
+@pytest.mark.parametrize("n,R,kind,params,faults", [
+    (8, 3, "example", None, None),       # config 1 under the literal harness order
+    (2, 1, "origins", None, None),
+    (3, 2, "origins", None, None),
+    (5, 3, "trickle", None, None),
+    (20, 1, "trickle", None, None),      # README rows under SEQ: the published harness
+    (200, 1, "trickle", None, None),
+    (2000, 1, "trickle", None, None),
+    (97, 16, "origins", None, None),
+    (101, 32, "reinject", None, None),
+    (300, 64, "trickle", None, None),
+    (77, 100, "origins", None, None),
+    (130, 256, "reinject", None, None),
+    (40, 7, "origins", (1, 1, 3), None),
+    (40, 7, "origins", (2, 3, 5), None),
+    (500, 8, "reinject", (3, 2, 9), None),
+    (300, 16, "origins", None, (0.05, 0.05, 0.1)),
+    (400, 64, "reinject", None, (0.3, 0.1, 0.1)),
+    (130, 256, "origins", None, (0.1, 0.2, 0.2)),
+])
+def test_round_parity_seq(engine, n, R, kind, params, faults):
+    run_parity(engine, n, R, kind, params, faults=faults, schedule="SEQ")
+
+
+def test_parity_seq_larger(engine):
+    # 20k nodes: pull chains of depth ~7 (levels of the SEQ pull passes)
+    run_parity(engine, 20000, 64, "origins", check_every=4, schedule="SEQ")
 
 
 @pytest.mark.parametrize("seed,epoch", [(1, 0), (0xDEADBEEF, 3), (2**63 + 5, 77)])

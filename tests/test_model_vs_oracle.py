@@ -17,10 +17,22 @@ def run(n, R, params=None, seed=0x5AFE6055, epoch=0, kind="origins", max_rounds=
     fault_fn = (lambda rnd, x: L.or_fault(seed, epoch, rnd, x, *thr)) if faults else None
     mdl = Model(n, R, seed, epoch, orc.params, L.or_peer, fault_fn, schedule)
     rng = np.random.default_rng(n * 31 + R)
+    injected = []
     for rnd in range(1, max_rounds + 1):
         inj = []
         if kind == "origins" and rnd == 1:
             inj = [(L.or_origin(seed, epoch, r, n), r) for r in range(R)]
+        if kind == "trickle":  # harness: first rumor at a Philox origin, then 50%/node/round
+            if rnd == 1:
+                inj.append((L.or_origin(seed, epoch, 0, n), 0))
+            nxt = len(injected) + len(inj)
+            for x in range(n):
+                if nxt >= R:
+                    break
+                if L.or_coin(seed, epoch, rnd, x):
+                    inj.append((x, nxt))
+                    nxt += 1
+            injected.extend(inj)
         if kind == "reinject" and rnd in (1, 2, 4, 5):
             inj = [(int(rng.integers(n)), int(rng.integers(R))) for _ in range(max(1, R // 2))]
         for x, r in inj:
@@ -65,6 +77,7 @@ def run(n, R, params=None, seed=0x5AFE6055, epoch=0, kind="origins", max_rounds=
     (300, 6, (3, 3, 14), "origins"),
     (400, 6, (3, 2, 9), "reinject"),
     (1700, 3, None, "origins"),
+    (300, 64, None, "trickle"),
 ])
 def test_model_equals_oracle(oracle, n, R, params, kind):
     run(n, R, params, kind=kind)
@@ -94,6 +107,8 @@ def test_model_equals_oracle_faults(oracle, n, R, kind, faults):
     (40, 7, "reinject", (1, 1, 3), None),
     (300, 6, "origins", (3, 3, 14), None),
     (1700, 3, "origins", None, None),
+    (300, 64, "trickle", None, None),   # mutual pairs: a pull overwritten per rumor
+    (1000, 32, "trickle", None, None),
     (60, 8, "origins", None, (0.1, 0.1, 0.1)),
     (200, 5, "reinject", None, (0.3, 0.1, 0.2)),
     (300, 6, "origins", None, (0.0, 0.0, 0.4)),
