@@ -1,14 +1,17 @@
 // one_message_test -- the reference's convergence experiment
 // (src/gossiper.rs:173-323: send_messages / one_message_test / print_metric)
-// driven through the C++ host API on the MI355X engine (2P schedule).
+// driven through the C++ host API on the MI355X engine.  The default schedule
+// is SEQ, the reference harness's literal delivery order, whose averages are
+// the published table (README.md:5); "2P" buffers pulls after all pushes.
 //
-//   ./examples/one_message_test [nodes=2000] [iterations=1000] [messages=1]
+//   ./examples/one_message_test [nodes=2000] [iterations=1000] [messages=1] [SEQ|2P]
 //
 // Prints the AVERAGE / MIN / MAX lines in the reference's format.
 #include <cinttypes>
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <string>
 #include <tuple>
 #include <vector>
 
@@ -74,9 +77,10 @@ int main(int argc, char **argv) {
     const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 2000;
     const uint32_t iterations = argc > 2 ? (uint32_t)atoi(argv[2]) : 1000;
     const uint32_t msgs = argc > 3 ? (uint32_t)atoi(argv[3]) : 1;
+    const bool two_phase = argc > 4 && std::string(argv[4]) == "2P";
     try {
-        Network net(n, msgs);
-        printf("Network of %u nodes:\n", n);
+        Network net(n, msgs, 0x5AFE6055ull, 0, 0, two_phase ? GS_SCHED_2P : GS_SCHED_SEQ);
+        printf("Network of %u nodes (%s schedule):\n", n, two_phase ? "2P" : "SEQ");
         Statistics avg, mx, mn = Statistics::new_max();
         double nm_avg = 0, mm_avg = 0;
         uint64_t nm_max = 0, nm_min = UINT64_MAX, mm_max = 0, mm_min = UINT64_MAX;

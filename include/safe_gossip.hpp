@@ -100,13 +100,14 @@ class Gossiper {
 class Network {
   public:
     Network(uint32_t n_nodes, uint32_t n_rumors, uint64_t seed = 0x5AFE6055ull, uint32_t epoch = 0,
-            int device = 0) {
+            int device = 0, gs_schedule schedule = GS_SCHED_2P) {
         gs_config cfg{};
         cfg.n_nodes = n_nodes;
         cfg.n_rumors = n_rumors;
         cfg.seed = seed;
         cfg.epoch = epoch;
         cfg.device = device;
+        cfg.schedule = (uint8_t)schedule;
         check(gs_create(&cfg, &e_));
         n_ = n_nodes;
         r_ = n_rumors;
