@@ -40,7 +40,7 @@ constexpr uint32_t kBin = 1u << kBinLog;          // targets per bin
 constexpr uint32_t kBinCap = kBin + kBin / 4;     // region capacity per bin
 constexpr uint32_t kChunk = 16384;                // sources per inl_bin block
 constexpr uint32_t kInlThreads = 1024;
-constexpr uint32_t kBinnedMaxBins = 4096;         // n <= 2^26
+constexpr uint32_t kBinnedMaxBins = 8192;         // n <= 2^27 (per-bin LDS state is 6 B)
 constexpr uint32_t kFlagLimit = 2u;               // flags[2] bit: a device limit was hit
 
 // Target word (target + delivery flags, gs_common.h); edges flagged kTgDead
@@ -113,21 +113,28 @@ GS_DEV uint32_t emit_tail(const InListArgs &a, const uint32_t *lst, uint32_t k, 
 __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     const CsrPlan &p = a.p;
+    // Per-bin state is 16-bit (every count, start and cursor is <= kChunk,
+    // every reserved slot <= kBinCap): counts / cursors packed two per word for
+    // LDS atomics, so 8192 bins fit beside the stage.
     uint32_t *stage = sh;                                      // [kChunk] sources by bin
     uint16_t *stage_lt = reinterpret_cast<uint16_t *>(sh + kChunk);  // [kChunk]
-    uint32_t *cnt = sh + kChunk + kChunk / 2;  // [nb] counts, then cursors
-    uint32_t *off = cnt + p.nb;                // [nb] chunk-local bin starts
-    uint32_t *res = off + p.nb;                // [nb] reserved start in the bin's region
+    uint32_t *cnt = sh + kChunk + kChunk / 2;  // [nb/2] counts, then cursors (2 x u16 per word)
+    uint16_t *cnt16 = reinterpret_cast<uint16_t *>(cnt);
+    uint16_t *off = reinterpret_cast<uint16_t *>(cnt + (p.nb + 1) / 2);  // [nb] chunk-local bin starts
+    uint16_t *res = off + p.nb;                // [nb] reserved start in the bin's region
     __shared__ uint32_t lds_scan[kInlThreads / 64];
     if (blockIdx.x == 0 && threadIdx.x == 0) a.scratch[p.nb] = 0u;  // tail count; inl_sort runs after
-    for (uint32_t i = threadIdx.x; i < p.nb; i += kInlThreads) cnt[i] = 0u;
+    for (uint32_t i = threadIdx.x; i < (p.nb + 1) / 2; i += kInlThreads) cnt[i] = 0u;
     __syncthreads();
     const uint32_t lo = blockIdx.x * kChunk;
     const uint32_t hi = min(p.n, lo + kChunk);
     for (uint32_t x = lo + threadIdx.x; x < hi; x += kInlThreads) {
         const uint32_t t = target_of(a, x);
         a.tg[x] = t;
-        if (!(t & kTgDead)) atomicAdd(&cnt[(t & kTgMask) >> kBinLog], 1u);
+        if (!(t & kTgDead)) {
+            const uint32_t b = (t & kTgMask) >> kBinLog;
+            atomicAdd(&cnt[b >> 1], 1u << ((b & 1u) << 4));
+        }
     }
     __syncthreads();
     // exclusive scan of the bin counts: thread i owns bins [i*per, i*per + per)
@@ -135,14 +142,14 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
     const uint32_t b0 = threadIdx.x * per;
     uint32_t sum = 0;
     for (uint32_t q = 0; q < per; ++q)
-        if (b0 + q < p.nb) sum += cnt[b0 + q];
+        if (b0 + q < p.nb) sum += cnt16[b0 + q];
     uint32_t total;
     uint32_t run = block_exclusive_scan_t<kInlThreads>(sum, lds_scan, total);
     for (uint32_t q = 0; q < per; ++q) {
         const uint32_t b = b0 + q;
         if (b >= p.nb) break;
-        const uint32_t c = cnt[b];
-        off[b] = run;
+        const uint32_t c = cnt16[b];
+        off[b] = (uint16_t)run;
         uint32_t r0 = 0;
         if (c) {
             r0 = atomicAdd(&a.scratch[b], c);
@@ -151,15 +158,16 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
                 r0 = kBinCap;  // drop this run; the round reports the limit
             }
         }
-        res[b] = r0;
-        cnt[b] = run;  // cursor
+        res[b] = (uint16_t)r0;
+        cnt16[b] = (uint16_t)run;  // cursor
         run += c;
     }
     __syncthreads();
     for (uint32_t x = lo + threadIdx.x; x < hi; x += kInlThreads) {
         const uint32_t t = a.tg[x];  // written above by this thread
         if (t & kTgDead) continue;
-        const uint32_t pos = atomicAdd(&cnt[(t & kTgMask) >> kBinLog], 1u);
+        const uint32_t b = (t & kTgMask) >> kBinLog, sh16 = (b & 1u) << 4;
+        const uint32_t pos = (atomicAdd(&cnt[b >> 1], 1u << sh16) >> sh16) & 0xFFFFu;
         stage[pos] = x;
         stage_lt[pos] = (uint16_t)(t & (kBin - 1u));
     }
@@ -448,7 +456,8 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
     const CsrPlan &p = a.p;
     if (p.n == 0) return hipSuccess;
     if (p.binned) {
-        const size_t lds_bin = ((size_t)3 * p.nb + kChunk + kChunk / 2) * sizeof(uint32_t);
+        const size_t lds_bin = ((size_t)kChunk + kChunk / 2 + (p.nb + 1) / 2) * sizeof(uint32_t) +
+                               (size_t)2 * p.nb * sizeof(uint16_t);
         const size_t lds_sort = ((size_t)kBin / 2 + kBinCap) * sizeof(uint32_t);
         hipError_t e = hipFuncSetAttribute((const void *)inl_bin, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)lds_bin);
