@@ -671,6 +671,12 @@ void or_messages(const or_net *net, uint32_t node, uint64_t *words)
     }
 }
 
+void or_known_all(const or_net *net, uint64_t *words)
+{
+    const uint32_t nw = (net->R + 63) / 64;
+    for (uint32_t x = 0; x < net->n; ++x) or_messages(net, x, words + (size_t)x * nw);
+}
+
 uint64_t or_known_total(const or_net *net)
 {
     uint64_t t = 0;

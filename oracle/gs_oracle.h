@@ -89,6 +89,7 @@ void     or_dump_records(const or_net *net, uint16_t *rec, uint32_t *psize);
 void     or_statistics(const or_net *net, uint64_t *out);         /* n*5  */
 void     or_messages(const or_net *net, uint32_t node, uint64_t *words);
 uint64_t or_known_total(const or_net *net);
+void     or_known_all(const or_net *net, uint64_t *words);   /* n*ceil(R/64) */
 
 /* send_messages(gossipers, num_of_msgs) restated (src/gossiper.rs:173-259):
  * Philox-chosen first origin, then 50% per node per round while rumors remain,

@@ -51,6 +51,7 @@ _SIGS = {
     "or_statistics": (None, [_P, _U64P]),
     "or_messages": (None, [_P, ctypes.c_uint32, _U64P]),
     "or_known_total": (ctypes.c_uint64, [_P]),
+    "or_known_all": (None, [_P, _U64P]),
     "or_send_messages": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_int,
                                          ctypes.POINTER(OrMetrics)]),
     "or_philox": (None, [_U32P, _U32P, _U32P]),
@@ -203,8 +204,7 @@ class OracleNet:
     def known_all(self):
         kw = (self.R + 63) // 64
         out = np.zeros((self.n, kw), dtype=np.uint64)
-        for x in range(self.n):
-            self._l.or_messages(self.h, x, out[x].ctypes.data_as(_U64P))
+        self._l.or_known_all(self.h, out.ctypes.data_as(_U64P))
         return out
 
     def known_total(self):

@@ -263,3 +263,21 @@ def test_parity_many_bins(engine):
     known, _ = net.known_counts()
     assert known > 1
     net.close()
+
+
+@pytest.mark.parametrize("n,R,kind", [
+    (40, 4096, "origins"),      # the largest R (64 words per node)
+    (60, 1000, "reinject"),     # R padded to 1024
+    (50, 65, "origins"),        # one bit past a word
+    (90, 33, "trickle"),        # small-R segments of 64 bits holding one node
+])
+def test_round_parity_wide_and_ragged(engine, n, R, kind):
+    run_parity(engine, n, R, kind)
+
+
+def test_config2_full_size(engine):
+    # BASELINE config 2 at its full size: 10^6 nodes x 1 rumor to termination,
+    # every round bit-exact against the oracle (state, records, |P|,
+    # Statistics, known sets); the dissemination takes O(ln n) rounds.
+    rounds = run_parity(engine, 1_000_000, 1, "origins")
+    assert 14 <= rounds <= 30
