@@ -26,6 +26,7 @@ struct gs_engine {
     bool seq = false;              // GS_SCHED_SEQ (gs_seq.hip)
     u64 *Wb = nullptr;             // SEQ: pull batch of every node [n][2][W]
     uint8_t *sinfo = nullptr;      // SEQ: got/dep/level per node
+    uint32_t *seqw = nullptr;      // SEQ: block counts, list sizes, level lists
     uint32_t seq_round = ~0u;      // round whose pull batches Wb holds
     u64 *pend = nullptr;       // churn: votes of frozen (offline) nodes [n][2][W]
     uint32_t *offc = nullptr;  // churn: rounds offline per node
@@ -132,7 +133,7 @@ void release(gs_engine *e) {
         if (e->ev_kr[i]) (void)hipEventDestroy(e->ev_kr[i]);
     }
     if (e->cstream) (void)hipStreamDestroy(e->cstream);
-    void *bufs[] = {e->Wb, e->sinfo, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
+    void *bufs[] = {e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
                     e->partials, e->obs_state, e->obs_rec, e->obs_psize};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -286,12 +287,25 @@ gs_status seq_prepare(gs_engine *e) {
     sa.Wb = e->Wb;
     sa.flags = e->flags;
     sa.g = e->g;
+    const size_t nb = (size_t)gs::seq_blocks(e->g.n) * gs::kSeqLists;
+    sa.bcnt = e->seqw;
+    sa.ltot = e->seqw + nb;
+    sa.lists = e->seqw + nb + gs::kSeqLists;
     GS_HIP(hipMemsetAsync(e->flags + 3, 0, sizeof(uint32_t), e->stream));
     GS_HIP(gs::launch_seq_levels(sa, e->stream));
-    uint32_t maxlev = 0;
+    uint32_t maxlev = 0, ltot[gs::kSeqLists];
     GS_HIP(hipMemcpyAsync(&maxlev, e->flags + 3, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    GS_HIP(hipMemcpyAsync(ltot, sa.ltot, sizeof(ltot), hipMemcpyDeviceToHost, e->stream));
     GS_HIP(hipStreamSynchronize(e->stream));
-    for (uint32_t l = 0; l <= maxlev; ++l) GS_HIP(gs::launch_seq_pull_pass(sa, l, e->stream));
+    uint32_t lstart[gs::kSeqLists], run = 0;
+    for (uint32_t l = 0; l < gs::kSeqLists; ++l) {
+        lstart[l] = run;
+        run += ltot[l];
+    }
+    for (uint32_t l = 0; l <= maxlev; ++l) {
+        const uint32_t li = std::min(l, gs::kSeqLists - 1u);
+        GS_HIP(gs::launch_seq_pull_pass(sa, l, lstart[li], ltot[li], e->stream));
+    }
     e->seq_round = e->round;
     return GS_OK;
 }
@@ -479,7 +493,8 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
          dalloc(&e->flags, 4) == hipSuccess && dalloc(&e->st32, (size_t)4 * n) == hipSuccess &&
          dalloc(&e->st64, (size_t)4 * n) == hipSuccess;
     if (ok && e->seq)
-        ok = dalloc(&e->Wb, (size_t)n * 2 * g.W) == hipSuccess && dalloc(&e->sinfo, n) == hipSuccess;
+        ok = dalloc(&e->Wb, (size_t)n * 2 * g.W) == hipSuccess && dalloc(&e->sinfo, n) == hipSuccess &&
+             dalloc(&e->seqw, (size_t)gs::seq_blocks(n) * gs::kSeqLists + gs::kSeqLists + n) == hipSuccess;
     if (ok && e->faults.churn)
         ok = dalloc(&e->pend, (size_t)n * 2 * g.W) == hipSuccess && dalloc(&e->offc, n) == hipSuccess;
     if (!ok) {

@@ -110,9 +110,17 @@ struct SeqArgs {
     u64 *Wb;                  // [n][2][W] pull batches (2-plane class code)
     uint32_t *flags;          // flags[2] device limit, flags[3] deepest level
     Geometry g;
+    // per-level node lists: bcnt [blocks][kSeqLists] counts -> offsets,
+    // ltot [kSeqLists] list sizes, lists [n] node ids grouped by level
+    uint32_t *bcnt, *ltot, *lists;
 };
+constexpr uint32_t kSeqLists = 16;  // levels >= 15 share the last list
+inline uint32_t seq_blocks(uint32_t n) { return (n + 255u) / 256u; }
+// seq_levels + the per-level lists (ltot read back by the caller)
 hipError_t launch_seq_levels(const SeqArgs &a, hipStream_t s);
-hipError_t launch_seq_pull_pass(const SeqArgs &a, uint32_t level, hipStream_t s);
+// pass `level` over the `count` nodes listed from `start` of lists
+hipError_t launch_seq_pull_pass(const SeqArgs &a, uint32_t level, uint32_t start, uint32_t count,
+                                hipStream_t s);
 
 // ---------------------------------------------------------------- shards
 // One rank's slice of a network sharded over G ranks (gs_shard.hip).

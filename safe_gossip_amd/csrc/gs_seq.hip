@@ -30,8 +30,9 @@ constexpr uint32_t kMaxSeqLevel = 62;
 GS_DEV bool got0(uint32_t tw) { return !(tw & kTgNoPull); }
 
 __global__ __launch_bounds__(256) void seq_levels(SeqArgs a) {
-    __shared__ uint32_t bmax;
+    __shared__ uint32_t bmax, hist[kSeqLists];
     if (threadIdx.x == 0) bmax = 0;
+    if (threadIdx.x < kSeqLists) hist[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t y = blockIdx.x * blockDim.x + threadIdx.x;
     if (y < a.g.n) {
@@ -64,23 +65,66 @@ __global__ __launch_bounds__(256) void seq_levels(SeqArgs a) {
         }
         a.sinfo[y] = (uint8_t)((gy ? kSeqGot : 0u) | (dep ? kSeqDep : 0u) | min(lev, kMaxSeqLevel));
         if (lev) atomicMax(&bmax, lev);
+        if (gy) atomicAdd(&hist[min(lev, kSeqLists - 1u)], 1u);
     }
     __syncthreads();
+    if (threadIdx.x < kSeqLists) a.bcnt[(u64)blockIdx.x * kSeqLists + threadIdx.x] = hist[threadIdx.x];
     if (threadIdx.x == 0 && bmax &&
         __hip_atomic_load(&a.flags[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < bmax)
         atomicMax(&a.flags[3], bmax);
 }
 
+// Per level list, exclusive prefix of the block counts (one block per list).
+__global__ __launch_bounds__(kScanBlock) void seq_scan(SeqArgs a, uint32_t nblk) {
+    __shared__ uint32_t lds[kScanBlock / 64];
+    const uint32_t l = blockIdx.x;
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nblk; base += kScanBlock) {
+        const uint32_t i = base + threadIdx.x;
+        const u64 idx = (u64)i * kSeqLists + l;
+        const uint32_t v = i < nblk ? a.bcnt[idx] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_exclusive_scan(v, lds, tot);
+        if (i < nblk) a.bcnt[idx] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) a.ltot[l] = carry;
+}
+
+// Every node that gets a pull into its level's list (order inside a list
+// is irrelevant: each W(x) is computed on its own).
+__global__ __launch_bounds__(256) void seq_scatter(SeqArgs a) {
+    __shared__ uint32_t cur[kSeqLists], lstart[kSeqLists];
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (uint32_t l = 0; l < kSeqLists; ++l) {
+            lstart[l] = run;
+            run += a.ltot[l];
+        }
+    }
+    if (threadIdx.x < kSeqLists) cur[threadIdx.x] = a.bcnt[(u64)blockIdx.x * kSeqLists + threadIdx.x];
+    __syncthreads();
+    const uint32_t y = blockIdx.x * blockDim.x + threadIdx.x;
+    if (y >= a.g.n) return;
+    const uint32_t si = a.sinfo[y];
+    if (!(si & kSeqGot)) return;
+    const uint32_t l = min(si & kSeqLevelMask, kSeqLists - 1u);
+    a.lists[lstart[l] + atomicAdd(&cur[l], 1u)] = y;
+}
+
 template <bool SMALL>
-__global__ __launch_bounds__(256) void seq_pull_pass(SeqArgs a, uint32_t level) {
+__global__ __launch_bounds__(256) void seq_pull_pass(SeqArgs a, uint32_t level, uint32_t start,
+                                                     uint32_t count) {
     const Geometry &g = a.g;
-    const u64 seg = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (seg >= g.nseg) return;
+    const u64 lane = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t W = SMALL ? 1u : g.W;
+    if (lane >= (u64)count * W) return;
+    const uint32_t y0 = a.lists[start + (uint32_t)(lane / W)];
     Lane<SMALL> L;
-    L.init(g, seg);
+    L.init(g, SMALL ? (u64)y0 : (u64)y0 * W + (uint32_t)(lane % W));
     const uint32_t y = L.x;
     const uint32_t si = a.sinfo[y];
-    if (!(si & kSeqGot) || (si & kSeqLevelMask) != level) return;
+    if ((si & kSeqLevelMask) != level) return;  // the last list holds every level >= 15
     const uint32_t z = a.tg[y] & kTgMask;
     const SibRec sb = a.SIB8[y];
     const uint32_t r = ((sb.tag >> 8) == (a.serial & kSerialMask)) ? (sb.tag & 0xFFu) : 0u;
@@ -119,15 +163,20 @@ __global__ __launch_bounds__(256) void seq_pull_pass(SeqArgs a, uint32_t level) 
 
 hipError_t launch_seq_levels(const SeqArgs &a, hipStream_t s) {
     if (a.g.n == 0) return hipSuccess;
-    hipLaunchKernelGGL(seq_levels, dim3((a.g.n + 255) / 256), dim3(256), 0, s, a);
+    const uint32_t nblk = seq_blocks(a.g.n);
+    hipLaunchKernelGGL(seq_levels, dim3(nblk), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(seq_scan, dim3(kSeqLists), dim3(kScanBlock), 0, s, a, nblk);
+    hipLaunchKernelGGL(seq_scatter, dim3(nblk), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_seq_pull_pass(const SeqArgs &a, uint32_t level, hipStream_t s) {
-    const u64 grid = (a.g.nseg + 255) / 256;
-    if (grid == 0) return hipSuccess;
-    if (a.g.small) hipLaunchKernelGGL(seq_pull_pass<true>, dim3((uint32_t)grid), dim3(256), 0, s, a, level);
-    else hipLaunchKernelGGL(seq_pull_pass<false>, dim3((uint32_t)grid), dim3(256), 0, s, a, level);
+hipError_t launch_seq_pull_pass(const SeqArgs &a, uint32_t level, uint32_t start, uint32_t count,
+                                hipStream_t s) {
+    const u64 lanes = (u64)count * (a.g.small ? 1u : a.g.W);
+    if (lanes == 0) return hipSuccess;
+    const uint32_t grid = (uint32_t)((lanes + 255) / 256);
+    if (a.g.small) hipLaunchKernelGGL(seq_pull_pass<true>, dim3(grid), dim3(256), 0, s, a, level, start, count);
+    else hipLaunchKernelGGL(seq_pull_pass<false>, dim3(grid), dim3(256), 0, s, a, level, start, count);
     return hipGetLastError();
 }
 
