@@ -138,6 +138,33 @@ def cpu_baseline(R, seed, budget_s, faults=(0.0, 0.0, 0.0), schedule="2P"):
                        + (f", faults {faults}" if thr else ""))
 
 
+def cpu_best(R, seed, budget_s):
+    """The dense bit-sliced OpenMP CPU program (oracle/gs_dense.c, checked
+    against the oracle in tests/test_dense_cpu.py) on all its threads: the
+    secondary "best CPU" line of SURVEY.md section 8d (2P, no faults)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib
+    oracle_lib.build_oracle()
+    L = oracle_lib.lib()
+    n_cpu = 1 << 20
+    net = oracle_lib.DenseNet(n_cpu, R, seed=seed)
+    for r in range(R):
+        net.send_new(L.or_origin(seed, 0, r, n_cpu), r)
+    t0 = time.perf_counter()
+    rounds = 0
+    while True:
+        live = net.next_round()
+        rounds += 1
+        el = time.perf_counter() - t0
+        if not live or el > budget_s:
+            break
+    net.close()
+    return dict(value=n_cpu * R * rounds / el, unit="node-rumor updates/s", cores=L.dn_threads(),
+                kind="port (dense bit-sliced, OpenMP)",
+                sample=f"oracle/gs_dense.c, n={n_cpu}, R={R}, all rumors injected round 1, "
+                       f"{rounds} rounds in {el:.1f}s")
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -217,9 +244,11 @@ def main():
         except Exception:
             traffic = None
 
-    cpu = None
+    cpu = best = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(R, args.seed, args.cpu_seconds, args.faults, args.schedule)
+        if args.schedule == "2P" and not any(args.faults):
+            best = cpu_best(R, args.seed, args.cpu_seconds)
 
     if rank == 0:
         total_updates = float(n) * R * args.steps
@@ -257,6 +286,7 @@ def main():
                 "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": bytes_per,
             },
             "cpu_baseline": cpu,
+            "cpu_best": best,
             "spread": spread,
         }
         print(json.dumps(line), flush=True)

@@ -116,6 +116,15 @@ void     or_ms_step(uint8_t io[4], const uint32_t *peers, const uint8_t *vals,
 void     or_ms_new(uint8_t io[4]);
 int      or_ms_our_counter(const uint8_t io[4]);
 
+/* gs_dense.c: the 2P round as a dense bit-sliced OpenMP CPU program (the
+ * secondary "best CPU" baseline); checked against the oracle in tests/. */
+void    *dn_create(uint32_t n, uint32_t R, uint64_t seed, uint32_t epoch);
+void     dn_destroy(void *d);
+void     dn_send_new(void *d, uint32_t node, uint32_t rumor);
+int      dn_next_round(void *d, uint32_t *any_live);
+void     dn_dump_state(void *d, uint16_t *codes /* n*R */, uint64_t *stats /* n*5 */);
+int      dn_threads(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -66,6 +66,13 @@ _SIGS = {
                                    ctypes.c_uint32]),
     "or_set_faults": (None, [_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
     "or_derive_params": (None, [ctypes.c_uint32, _U8P]),
+    # gs_dense.c: the dense bit-sliced OpenMP CPU line
+    "dn_create": (_P, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32]),
+    "dn_destroy": (None, [_P]),
+    "dn_send_new": (None, [_P, ctypes.c_uint32, ctypes.c_uint32]),
+    "dn_next_round": (ctypes.c_int, [_P, _U32P]),
+    "dn_dump_state": (None, [_P, _U16P, _U64P]),
+    "dn_threads": (ctypes.c_int, []),
     "or_ms_step": (None, [_U8P, _U32P, _U8P, ctypes.c_uint32, _U32P, ctypes.c_uint32,
                           ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_int]),
     "or_ms_new": (None, [_U8P]),
@@ -215,3 +222,38 @@ class OracleNet:
         rc = self._l.or_send_messages(self.h, num_msgs, schedule, ctypes.byref(m))
         assert rc == 0
         return m
+
+
+class DenseNet:
+    """The dense bit-sliced OpenMP CPU program (oracle/gs_dense.c), 2P only."""
+
+    def __init__(self, n, R, seed=0x5AFE6055, epoch=0):
+        self._l = lib()
+        self.h = self._l.dn_create(n, R, seed, epoch)
+        assert self.h
+        self.n, self.R = n, R
+
+    def close(self):
+        if self.h:
+            self._l.dn_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def send_new(self, node, rumor):
+        self._l.dn_send_new(self.h, node, rumor)
+
+    def next_round(self):
+        live = ctypes.c_uint32()
+        self._l.dn_next_round(self.h, ctypes.byref(live))
+        return bool(live.value)
+
+    def dump(self):
+        codes = np.zeros((self.n, self.R), dtype=np.uint16)
+        st = np.zeros((self.n, 5), dtype=np.uint64)
+        self._l.dn_dump_state(self.h, codes.ctypes.data_as(_U16P), st.ctypes.data_as(_U64P))
+        return codes, st
