@@ -1,0 +1,28 @@
+"""Per-kernel profile of the sharded engine: `world` shards on one GPU, local
+(device-copy) transport, config 4 sizes.  Run under rocprofv3 --kernel-trace."""
+import sys
+import time
+
+import os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import safe_gossip_amd as sg  # noqa: E402
+from safe_gossip_amd.sharded import ShardedNetwork  # noqa: E402
+
+world = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+n, R = 1 << 24, 256
+torch.cuda.set_device(0)
+net = ShardedNetwork(n, R, world, transport="local")
+for r in range(R):
+    x = sg.origin_of(net.seed, 0, r, n)
+    net.send_new(x, r)
+for _ in range(3):
+    net.next_round(report=False)
+net.sync()
+t0 = time.perf_counter()
+K = 10
+for _ in range(K):
+    net.next_round(report=False)
+net.sync()
+print("world", world, "ms/round", (time.perf_counter() - t0) / K * 1e3)
+net.close()

@@ -172,6 +172,7 @@ gs::RoundArgs base_args(gs_engine *e) {
     if (e->shard) {
         uint32_t *cur = e->planw[e->round % 3], *nxt = e->planw[(e->round + 1) % 3];
         a.IN = reinterpret_cast<const uint4 *>(cur + e->spl.IN);
+        a.IN2 = cur + e->spl.IN2;
         a.src = cur + e->spl.EP;
         a.spos_cur = cur + e->spl.SPOS;
         a.spos_next = nxt + e->spl.SPOS;
@@ -576,6 +577,7 @@ gs_status gs_shard_pull(gs_engine *e) {
     gs::PullArgs a{};
     a.S = e->S[e->cur];
     a.IN = reinterpret_cast<const uint4 *>(pw + e->spl.IN);
+    a.IN2 = pw + e->spl.IN2;
     a.EP = pw + e->spl.EP;
     a.recvA = e->recvA;
     a.sendB = e->sendB;

@@ -35,7 +35,10 @@ namespace gs {
 
 namespace {
 
-constexpr uint32_t kBinLog = 14;
+#ifndef GS_INL_BINLOG
+#define GS_INL_BINLOG 14
+#endif
+constexpr uint32_t kBinLog = GS_INL_BINLOG;
 constexpr uint32_t kBin = 1u << kBinLog;          // targets per bin
 constexpr uint32_t kBinCap = kBin + kBin / 4;     // region capacity per bin
 constexpr uint32_t kChunk = 16384;                // sources per inl_bin block

@@ -10,6 +10,7 @@ struct RoundArgs {
     const InRec *IN8;         // round t, per node y: in-list record (gs_common.h)
     const SibRec *SIB8;       // round t, per source x: pushers of t(x) ahead of x
     const uint4 *IN;          // shard engine: per node {first edge, k | zi<<16, e0, e1}
+    const uint32_t *IN2;      // shard engine: per node e2 (third pusher's receive row)
     const uint32_t *src;      // round t in-list tails (shard engine: receive rows)
     const uint32_t *tg;       // round t target words (target_word: target + flags)
     const uint32_t *tg_next;  // shard engine, faults: round t+1 target words
@@ -137,7 +138,7 @@ struct ShardPlan {
 };
 // u32-word offsets of one plan's buffers inside a single allocation.
 struct ShardPlanLayout {
-    size_t tg_all, bc_me, bc_d, cnt, E_id, E_key, SPOS, M, tot, base, EP, IN, pairs;
+    size_t tg_all, bc_me, bc_d, cnt, E_id, E_key, SPOS, M, tot, base, EP, IN, IN2, pairs;
 };
 ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g);
 size_t shard_plan_words(const ShardPlan &P, ShardPlanLayout *L);
@@ -149,6 +150,7 @@ hipError_t launch_shard_plan(const ShardPlan &P, const ShardPlanLayout &L, uint3
 struct PullArgs {
     const u64 *S;          // round-t planes of the owned nodes
     const uint4 *IN;       // round-t in-lists of receive rows
+    const uint32_t *IN2;   // their third pushers
     const uint32_t *EP;
     const u64 *recvA;      // round-t push rows received [e][2][W]
     u64 *sendB;            // pull rows out [e][2][W]

@@ -223,8 +223,12 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     if (DELIVER) {
         if (SHARD) {
             if (valid) {
-                if (k > 0) q[0] = L.load_push_row(a.recvA, in.z);
-                if (k > 1) q[1] = L.load_push_row(a.recvA, in.w);
+                static_assert(kBatchK == 3, "shard rows: three batched pushers");
+                // the first three pushers' rows together (unconditional: row 0
+                // stands in for a missing pusher)
+                q[0] = L.load_push_row(a.recvA, in.z);
+                q[1] = L.load_push_row(a.recvA, in.w);
+                q[2] = L.load_push_row(a.recvA, a.IN2[x]);
                 if (!(tgw & kTgNoPull)) {
                     const uint32_t sp = a.spos_cur[x];  // the pull row z returned to x
                     qz.c = a.recvB[L.row_index(sp, 2, 0)];
@@ -290,9 +294,10 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             // zi = index of t(x) among x's pushers (0xFFFF: t(x) did not push to x)
             zin = zi != 0xFFFFu;
             const uint32_t zs = pulled ? zi : 0xFFFFu;  // push copy superseded by the pull copy
-            if (k > 0) rv.push(q[0], 0, k, zs != 0);
-            if (k > 1) rv.push(q[1], 1, k, zs != 1);
-            for (uint32_t i = 2; i < k; ++i) rv.push(L.load_push_row(a.recvA, a.src[in.x + i]), i, k, zs != i);
+#pragma unroll
+            for (uint32_t i = 0; i < kBatchK; ++i)
+                if (i < k) rv.push(q[i], i, k, zs != i);
+            for (uint32_t i = kBatchK; i < k; ++i) rv.push(L.load_push_row(a.recvA, a.src[in.x + i]), i, k, zs != i);
             // pull row code (b0, b1): 01 counter 1, 10 counter 2, 11 counter 255
             pv2 = qz.a0 & ~qz.c;
             pvB = qz.c ^ qz.a0;

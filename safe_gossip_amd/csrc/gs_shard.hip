@@ -65,20 +65,45 @@ __global__ __launch_bounds__(kPlanBlock) void plan_count(ShardPlan P, uint64_t s
     }
 }
 
-// Exclusive scans in place; cnt = {m_in, overflow, scnt[G], rcnt[G]}.
-__global__ __launch_bounds__(kScanBlock) void plan_scan(ShardPlan P, uint32_t *bc_me, uint32_t *bc_d,
-                                                        uint32_t *cnt) {
-    __shared__ uint32_t lds[kScanBlock / 64];
-    __shared__ uint32_t sdbase[64];
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < P.nblk; base += kScanBlock) {
-        const uint32_t i = base + threadIdx.x;
-        const uint32_t v = i < P.nblk ? bc_me[i] : 0u;
-        uint32_t tot;
-        const uint32_t ex = block_exclusive_scan(v, lds, tot);
-        if (i < P.nblk) bc_me[i] = carry + ex;
-        carry += tot;
+// In-place exclusive scan of v[i * stride] for i < count by one block of
+// kPlanScanThreads: each thread scans a contiguous chunk serially around a
+// single block-wide scan of the chunk sums; returns the total.
+constexpr uint32_t kPlanScanThreads = 1024;
+GS_DEV uint32_t chunked_scan(uint32_t *v, uint32_t count, uint32_t stride, uint32_t *lds) {
+    constexpr uint32_t kBatch = 16;  // loads in flight per thread
+    const uint32_t per = (count + kPlanScanThreads - 1) / kPlanScanThreads;
+    const uint32_t i0 = threadIdx.x * per;
+    uint32_t sum = 0;
+    for (uint32_t q0 = 0; q0 < per; q0 += kBatch) {
+        uint32_t t[kBatch];
+#pragma unroll
+        for (uint32_t q = 0; q < kBatch; ++q)
+            t[q] = (q0 + q < per && i0 + q0 + q < count) ? v[(u64)(i0 + q0 + q) * stride] : 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < kBatch; ++q) sum += t[q];
     }
+    uint32_t tot;
+    uint32_t run = block_exclusive_scan_t<kPlanScanThreads>(sum, lds, tot);
+    for (uint32_t q0 = 0; q0 < per; q0 += kBatch) {
+        uint32_t t[kBatch];
+#pragma unroll
+        for (uint32_t q = 0; q < kBatch; ++q)
+            t[q] = (q0 + q < per && i0 + q0 + q < count) ? v[(u64)(i0 + q0 + q) * stride] : 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < kBatch; ++q) {
+            if (q0 + q < per && i0 + q0 + q < count) v[(u64)(i0 + q0 + q) * stride] = run;
+            run += t[q];
+        }
+    }
+    return tot;
+}
+
+// Exclusive scans in place; cnt = {m_in, overflow, scnt[G], rcnt[G]}.
+__global__ __launch_bounds__(kPlanScanThreads) void plan_scan(ShardPlan P, uint32_t *bc_me,
+                                                              uint32_t *bc_d, uint32_t *cnt) {
+    __shared__ uint32_t lds[kPlanScanThreads / 64];
+    __shared__ uint32_t sdbase[64];
+    const uint32_t carry = chunked_scan(bc_me, P.nblk, 1u, lds);
     __syncthreads();
     if (threadIdx.x == 0) {
         cnt[0] = carry;  // m_in: sources targeting this rank
@@ -93,16 +118,7 @@ __global__ __launch_bounds__(kScanBlock) void plan_scan(ShardPlan P, uint32_t *b
     }
     // per destination: exclusive prefix over owned blocks, then + base of d
     for (uint32_t dd = 0; dd < P.G; ++dd) {
-        uint32_t c2 = 0;
-        for (uint32_t base = 0; base < P.nblk_own; base += kScanBlock) {
-            const uint32_t i = base + threadIdx.x;
-            const u64 idx = (u64)i * P.G + dd;
-            const uint32_t v = i < P.nblk_own ? bc_d[idx] : 0u;
-            uint32_t tot;
-            const uint32_t ex = block_exclusive_scan(v, lds, tot);
-            if (i < P.nblk_own) bc_d[idx] = c2 + ex;
-            c2 += tot;
-        }
+        const uint32_t c2 = chunked_scan(bc_d + dd, P.nblk_own, P.G, lds);
         if (threadIdx.x == 0) sdbase[dd] = c2;  // scnt[dd]
         __syncthreads();
     }
@@ -220,7 +236,8 @@ __global__ __launch_bounds__(256) void edge_bin_sort(const u64 *__restrict__ pai
                                                      uint32_t nodes_total,
                                                      const uint32_t *__restrict__ base,
                                                      const uint32_t *__restrict__ tot, uint32_t *EP,
-                                                     uint4 *IN, const uint32_t *__restrict__ E_id,
+                                                     uint4 *IN, uint32_t *IN2,
+                                                     const uint32_t *__restrict__ E_id,
                                                      const uint32_t *__restrict__ tg_all, uint32_t lo) {
     extern __shared__ __attribute__((aligned(16))) uint32_t h[];
     uint32_t *lds_scan = h + p.bin;
@@ -267,6 +284,7 @@ __global__ __launch_bounds__(256) void edge_bin_sort(const u64 *__restrict__ pai
         for (uint32_t q = a; q < e; ++q)
             if (E_id[EP[q]] == tz) zi = q - a;
         IN[nb0 + i] = make_uint4(a, k | (zi << 16), k > 0 ? EP[a] : 0u, k > 1 ? EP[a + 1] : 0u);
+        IN2[nb0 + i] = k > 2 ? EP[a + 2] : 0u;
     }
 }
 
@@ -323,6 +341,7 @@ size_t shard_plan_words(const ShardPlan &P, ShardPlanLayout *L) {
     L->base = take(P.edges.nb);
     L->EP = take(P.cap_in);
     L->IN = take(4 * (size_t)P.m);
+    L->IN2 = take(P.m);
     L->pairs = take(2 * (size_t)P.cap_in);
     return off;
 }
@@ -333,10 +352,11 @@ hipError_t launch_shard_plan(const ShardPlan &P, const ShardPlanLayout &L, uint3
     uint32_t *E_id = w + L.E_id, *E_key = w + L.E_key, *SPOS = w + L.SPOS;
     uint32_t *M = w + L.M, *tot = w + L.tot, *base = w + L.base, *EP = w + L.EP;
     uint4 *IN = reinterpret_cast<uint4 *>(w + L.IN);
+    uint32_t *IN2 = w + L.IN2;
     u64 *pairs = reinterpret_cast<u64 *>(w + L.pairs);
     hipLaunchKernelGGL(plan_count, dim3(P.nblk), dim3(kPlanBlock), 0, s, P, seed, epoch, round, f, tg_all,
                        bc_me, bc_d);
-    hipLaunchKernelGGL(plan_scan, dim3(1), dim3(kScanBlock), 0, s, P, bc_me, bc_d, cnt);
+    hipLaunchKernelGGL(plan_scan, dim3(1), dim3(kPlanScanThreads), 0, s, P, bc_me, bc_d, cnt);
     hipLaunchKernelGGL(plan_emit, dim3(P.nblk), dim3(kPlanBlock), 0, s, P, tg_all, bc_me, bc_d, E_id,
                        E_key, SPOS);
     if (P.m == 0) return hipGetLastError();
@@ -353,7 +373,7 @@ hipError_t launch_shard_plan(const ShardPlan &P, const ShardPlanLayout &L, uint3
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(edge_bin_sort, dim3(c.nb), dim3(256), lds_sort, s, pairs, c, P.m, base, tot, EP,
-                       IN, E_id, tg_all, P.lo);
+                       IN, IN2, E_id, tg_all, P.lo);
     return hipGetLastError();
 }
 
@@ -378,12 +398,14 @@ __global__ __launch_bounds__(256) void pull_kernel(PullArgs a) {
     const u64 zC = c & ~(q0 & q1);
     u64 pnot = ~c & ~q0 & ~q1 & L.m, pB = 0, pC = 0;
     const uint4 in = a.IN[z];
+    const uint32_t e2 = a.IN2[z];
     const uint32_t k = in.y & 0xFFFFu;
     for (uint32_t i = 0; i < k; ++i) {
-        const uint32_t e = i == 0 ? in.z : (i == 1 ? in.w : a.EP[in.x + i]);
+        const uint32_t e = i == 0 ? in.z : (i == 1 ? in.w : (i == 2 ? e2 : a.EP[in.x + i]));
         const u64 pcl = zC | pC;
         a.sendB[L.row_index(e, 2, 0)] = zB1 | pB | pcl;  // code bit 0: counter 1 or 255
         a.sendB[L.row_index(e, 2, 1)] = zB2 | pcl;       // code bit 1: counter 2 or 255
+        // a pusher's row matters to the later pull rows only while z lacks rumors
         if (i + 1 < k && pnot) sibling(L.load_push_row(a.recvA, e), pnot, pB, pC);
     }
 }
