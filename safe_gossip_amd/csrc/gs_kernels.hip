@@ -178,6 +178,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     uint32_t z = x, zi = 0xFFFFu, k = 0, r = 0;
     uint32_t tgw = 0;  // round-t target word: t(x) + delivery flags (gs_common.h)
     uint32_t sinf = 0;  // SEQ: got << 7 | ... (gs_seq.hip)
+    bool seq_inl = false;  // SEQ: W(x) built here, not by a pull pass (kSeqInline)
     if (DELIVER) {
         if (SHARD) {
             if (valid) {
@@ -191,11 +192,12 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             tgw = a.tg[x];
             z = tgw & kTgMask;  // t_t(x)
             k = valid ? in8.k() : 0u;
+            if (SEQ) sinf = a.sinfo[x];
+            sb8 = a.SIB8[x];
+            r = (valid && (sb8.tag >> 8) == (a.serial & kSerialMask)) ? (sb8.tag & 0xFFu) : 0u;
             if (SEQ) {
-                sinf = a.sinfo[x];
-            } else {
-                sb8 = a.SIB8[x];
-                r = (valid && (sb8.tag >> 8) == (a.serial & kSerialMask)) ? (sb8.tag & 0xFFu) : 0u;
+                seq_inl = valid && (sinf & kSeqGot) && (sinf & kSeqLevelMask) == kSeqInline;
+                if (!seq_inl) r = 0;
             }
         }
 #ifdef GS_EXP_NO_PUSHERS
@@ -239,14 +241,16 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         } else {
 #pragma unroll
             for (uint32_t i = 0; i < kBatchK; ++i) q[i] = L.load_cls(S, i < k ? in8.s[i] : x);
-            if (SEQ) {  // W(x), coalesced (qz holds its code planes)
+            if (SEQ && !seq_inl) {  // W(x), coalesced (qz holds its code planes)
                 if (valid && (sinf & kSeqGot)) {
                     const u64 wi = ((u64)x * 2u) * g.W + L.j;
                     qz.c = a.Wb[wi];
                     qz.a0 = a.Wb[wi + g.W];
                 }
-            } else {
+            } else {  // 2P, and SEQ level 0 without a reader of W(x)
                 qz = L.load_cls(S, z);
+            }
+            if (!SEQ || seq_inl) {
 #pragma unroll
                 for (uint32_t i = 0; i < kBatchE; ++i) e[i] = L.load_cls(S, i < r ? sb8.e[i] : x);
             }
@@ -315,6 +319,30 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                 if (s == z) jz = i;
             }
             zin = jz != kNone;
+            if (seq_inl) {  // W(x) = S(z) + what z created from its pushers s < x
+                const u64 zB = ~qz.c & (qz.a0 | qz.a1);
+                const u64 zC = qz.c & ~(qz.a0 & qz.a1);
+                u64 pnot = ~qz.c & ~qz.a0 & ~qz.a1 & L.m, pB = 0, pC = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < kBatchE; ++i)
+                    if (i < r) sibling(e[i], pnot, pB, pC);
+                if (r > kBatchE && pnot) {
+                    for (uint32_t i = kBatchE; i < min(r, kSibInline); ++i)
+                        sibling(L.load_cls(S, pick_sib(sb8.e, i)), pnot, pB, pC);
+                    if (r > kSibInline && pnot) {
+                        const InRec zin8 = a.IN8[z];
+                        for (uint32_t i = kSibInline; i < r && pnot; ++i) {
+                            const uint32_t s = i < kInline ? pick_inline(zin8.s, i)
+                                                           : a.src[zin8.first() + (i - kInline)];
+                            sibling(L.load_cls(S, s), pnot, pB, pC);
+                        }
+                    }
+                }
+                const u64 pcl = zC | pC;  // the 2-plane code seq_pull_pass writes
+                const u64 b0 = ((zB & qz.a0 & ~qz.a1) | pB | pcl) & L.m;
+                const u64 b1 = ((zB & qz.a1 & ~qz.a0) | pcl) & L.m;
+                qz = Cls{b0, b1, 0};
+            }
             const bool skip = gx && zin && z > x;
             const uint32_t sk = skip ? 1u : 0u;
             // z's later push (z > x) overwrites the pull's records of the

@@ -63,32 +63,71 @@ __global__ __launch_bounds__(256) void seq_levels(SeqArgs a) {
                 tc = tz;
             }
         }
-        a.sinfo[y] = (uint8_t)((gy ? kSeqGot : 0u) | (dep ? kSeqDep : 0u) | min(lev, kMaxSeqLevel));
+        // A level-0 W(y) is read only by a later w > y with t(w) = y that gets
+        // a pull, and every such w is in y's in-list (ascending): without a
+        // pusher above y, no pass builds W(y) and the round kernel makes it
+        // inline from t(y)'s planes and t(y)'s pushers ahead of y, as in 2P.
+        bool inl = false;
+#ifndef GS_SEQ_NO_INLINE
+        if (gy && lev == 0) {
+            const InRec r = a.IN8[y];
+            const uint32_t k = r.k();
+            const uint32_t top = k == 0 ? 0u
+                                        : (k <= kInline ? pick_inline(r.s, k - 1u)
+                                                        : a.src[r.first() + (k - 1u - kInline)]);
+            inl = k == 0 || top < y;
+        }
+#endif
+        a.sinfo[y] = (uint8_t)((gy ? kSeqGot : 0u) | (dep ? kSeqDep : 0u) |
+                               (inl ? kSeqInline : min(lev, kMaxSeqLevel)));
         if (lev) atomicMax(&bmax, lev);
-        if (gy) atomicAdd(&hist[min(lev, kSeqLists - 1u)], 1u);
+        if (gy && !inl) atomicAdd(&hist[min(lev, kSeqLists - 1u)], 1u);
     }
     __syncthreads();
-    if (threadIdx.x < kSeqLists) a.bcnt[(u64)blockIdx.x * kSeqLists + threadIdx.x] = hist[threadIdx.x];
+    if (threadIdx.x < kSeqLists) a.bcnt[(u64)threadIdx.x * gridDim.x + blockIdx.x] = hist[threadIdx.x];
     if (threadIdx.x == 0 && bmax &&
         __hip_atomic_load(&a.flags[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < bmax)
         atomicMax(&a.flags[3], bmax);
 }
 
-// Per level list, exclusive prefix of the block counts (one block per list).
-__global__ __launch_bounds__(kScanBlock) void seq_scan(SeqArgs a, uint32_t nblk) {
-    __shared__ uint32_t lds[kScanBlock / 64];
-    const uint32_t l = blockIdx.x;
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < nblk; base += kScanBlock) {
-        const uint32_t i = base + threadIdx.x;
-        const u64 idx = (u64)i * kSeqLists + l;
-        const uint32_t v = i < nblk ? a.bcnt[idx] : 0u;
-        uint32_t tot;
-        const uint32_t ex = block_exclusive_scan(v, lds, tot);
-        if (i < nblk) a.bcnt[idx] = carry + ex;
-        carry += tot;
+// Per level list, exclusive prefix of its block counts (bcnt[list][block]):
+// one 1024-thread block per list, each thread scanning a contiguous chunk
+// (sum, block scan of the sums, rewrite), instead of a serial walk in steps
+// of one block width (0.22 ms at 2^16 blocks).
+constexpr uint32_t kSeqScanThreads = 1024;
+__global__ __launch_bounds__(kSeqScanThreads) void seq_scan(SeqArgs a, uint32_t nblk) {
+    __shared__ uint32_t lds[kSeqScanThreads / 64];
+    uint32_t *c = a.bcnt + (u64)blockIdx.x * nblk;
+    const uint32_t chunk = (nblk + kSeqScanThreads - 1u) / kSeqScanThreads;
+    const uint32_t lo = min(threadIdx.x * chunk, nblk), hi = min(lo + chunk, nblk);
+    constexpr uint32_t U = 16;  // loads in flight per thread
+    uint32_t sum = 0, i = lo;
+    for (; i + U <= hi; i += U) {
+        uint32_t v[U];
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j) v[j] = c[i + j];
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j) sum += v[j];
     }
-    if (threadIdx.x == 0) a.ltot[l] = carry;
+    for (; i < hi; ++i) sum += c[i];
+    uint32_t tot;
+    uint32_t run = block_exclusive_scan_t<kSeqScanThreads>(sum, lds, tot);
+    for (i = lo; i + U <= hi; i += U) {
+        uint32_t v[U];
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j) v[j] = c[i + j];
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j) {
+            c[i + j] = run;
+            run += v[j];
+        }
+    }
+    for (; i < hi; ++i) {
+        const uint32_t v = c[i];
+        c[i] = run;
+        run += v;
+    }
+    if (threadIdx.x == 0) a.ltot[blockIdx.x] = tot;
 }
 
 // Every node that gets a pull into its level's list (order inside a list
@@ -102,12 +141,12 @@ __global__ __launch_bounds__(256) void seq_scatter(SeqArgs a) {
             run += a.ltot[l];
         }
     }
-    if (threadIdx.x < kSeqLists) cur[threadIdx.x] = a.bcnt[(u64)blockIdx.x * kSeqLists + threadIdx.x];
+    if (threadIdx.x < kSeqLists) cur[threadIdx.x] = a.bcnt[(u64)threadIdx.x * gridDim.x + blockIdx.x];
     __syncthreads();
     const uint32_t y = blockIdx.x * blockDim.x + threadIdx.x;
     if (y >= a.g.n) return;
     const uint32_t si = a.sinfo[y];
-    if (!(si & kSeqGot)) return;
+    if (!(si & kSeqGot) || (si & kSeqLevelMask) == kSeqInline) return;
     const uint32_t l = min(si & kSeqLevelMask, kSeqLists - 1u);
     a.lists[lstart[l] + atomicAdd(&cur[l], 1u)] = y;
 }
@@ -165,7 +204,7 @@ hipError_t launch_seq_levels(const SeqArgs &a, hipStream_t s) {
     if (a.g.n == 0) return hipSuccess;
     const uint32_t nblk = seq_blocks(a.g.n);
     hipLaunchKernelGGL(seq_levels, dim3(nblk), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(seq_scan, dim3(kSeqLists), dim3(kScanBlock), 0, s, a, nblk);
+    hipLaunchKernelGGL(seq_scan, dim3(kSeqLists), dim3(kSeqScanThreads), 0, s, a, nblk);
     hipLaunchKernelGGL(seq_scatter, dim3(nblk), dim3(256), 0, s, a);
     return hipGetLastError();
 }
