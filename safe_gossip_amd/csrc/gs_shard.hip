@@ -67,73 +67,86 @@ __global__ __launch_bounds__(kPlanBlock) void plan_count(ShardPlan P, uint64_t s
 
 // In-place exclusive scan of v[i * stride] for i < count by one block of
 // kPlanScanThreads: each thread scans a contiguous chunk serially around a
-// single block-wide scan of the chunk sums; returns the total.
+// single block-wide scan of the chunk sums; returns the total.  The chunk is
+// read in unconditional batches of kBatch loads (a bounds test per load made
+// the compiler issue them one at a time: 0.2 ms per 2^16-entry scan).
 constexpr uint32_t kPlanScanThreads = 1024;
 GS_DEV uint32_t chunked_scan(uint32_t *v, uint32_t count, uint32_t stride, uint32_t *lds) {
     constexpr uint32_t kBatch = 16;  // loads in flight per thread
     const uint32_t per = (count + kPlanScanThreads - 1) / kPlanScanThreads;
-    const uint32_t i0 = threadIdx.x * per;
-    uint32_t sum = 0;
-    for (uint32_t q0 = 0; q0 < per; q0 += kBatch) {
+    const uint32_t lo = min(threadIdx.x * per, count), hi = min(lo + per, count);
+    uint32_t sum = 0, i = lo;
+    for (; i + kBatch <= hi; i += kBatch) {
         uint32_t t[kBatch];
 #pragma unroll
-        for (uint32_t q = 0; q < kBatch; ++q)
-            t[q] = (q0 + q < per && i0 + q0 + q < count) ? v[(u64)(i0 + q0 + q) * stride] : 0u;
+        for (uint32_t q = 0; q < kBatch; ++q) t[q] = v[(u64)(i + q) * stride];
 #pragma unroll
         for (uint32_t q = 0; q < kBatch; ++q) sum += t[q];
     }
+    for (; i < hi; ++i) sum += v[(u64)i * stride];
     uint32_t tot;
     uint32_t run = block_exclusive_scan_t<kPlanScanThreads>(sum, lds, tot);
-    for (uint32_t q0 = 0; q0 < per; q0 += kBatch) {
+    for (i = lo; i + kBatch <= hi; i += kBatch) {
         uint32_t t[kBatch];
 #pragma unroll
-        for (uint32_t q = 0; q < kBatch; ++q)
-            t[q] = (q0 + q < per && i0 + q0 + q < count) ? v[(u64)(i0 + q0 + q) * stride] : 0u;
+        for (uint32_t q = 0; q < kBatch; ++q) t[q] = v[(u64)(i + q) * stride];
 #pragma unroll
         for (uint32_t q = 0; q < kBatch; ++q) {
-            if (q0 + q < per && i0 + q0 + q < count) v[(u64)(i0 + q0 + q) * stride] = run;
+            v[(u64)(i + q) * stride] = run;
             run += t[q];
         }
+    }
+    for (; i < hi; ++i) {
+        const uint32_t t = v[(u64)i * stride];
+        v[(u64)i * stride] = run;
+        run += t;
     }
     return tot;
 }
 
-// Exclusive scans in place; cnt = {m_in, overflow, scnt[G], rcnt[G]}.
+// Exclusive scans in place, one block per scan (G + 1 blocks, independent);
+// cnt = {m_in, overflow, scnt[G], rcnt[G]}.
+//   block 0     : bc_me (sources targeting this rank, per block of all n) ->
+//                 m_in and the receive count from every source rank
+//   block 1 + d : bc_d[.][d] over the owned blocks -> scnt[d]
+// plan_scan_fix then adds the base of d (prefix of scnt) to bc_d[.][d].
 __global__ __launch_bounds__(kPlanScanThreads) void plan_scan(ShardPlan P, uint32_t *bc_me,
                                                               uint32_t *bc_d, uint32_t *cnt) {
     __shared__ uint32_t lds[kPlanScanThreads / 64];
-    __shared__ uint32_t sdbase[64];
+    if (blockIdx.x > 0) {
+        const uint32_t dd = blockIdx.x - 1u;
+        const uint32_t c2 = chunked_scan(bc_d + dd, P.nblk_own, P.G, lds);
+        if (threadIdx.x == 0) cnt[2 + dd] = c2;  // scnt[dd]
+        return;
+    }
     const uint32_t carry = chunked_scan(bc_me, P.nblk, 1u, lds);
     __syncthreads();
     if (threadIdx.x == 0) {
         cnt[0] = carry;  // m_in: sources targeting this rank
         cnt[1] = carry > P.cap_in ? 1u : 0u;
-        // recv counts per source rank: difference of the prefix at rank boundaries
-        for (uint32_t s = 0; s < P.G; ++s) {
-            const u64 b0 = (u64)s * P.chunk / kPlanBlock, b1 = (u64)(s + 1) * P.chunk / kPlanBlock;
-            const uint32_t p0 = b0 < P.nblk ? bc_me[b0] : carry;
-            const uint32_t p1 = b1 < P.nblk ? bc_me[b1] : carry;
-            cnt[2 + P.G + s] = p1 - p0;
-        }
     }
-    // per destination: exclusive prefix over owned blocks, then + base of d
-    for (uint32_t dd = 0; dd < P.G; ++dd) {
-        const uint32_t c2 = chunked_scan(bc_d + dd, P.nblk_own, P.G, lds);
-        if (threadIdx.x == 0) sdbase[dd] = c2;  // scnt[dd]
-        __syncthreads();
+    // recv counts per source rank: difference of the prefix at rank boundaries
+    for (uint32_t s = threadIdx.x; s < P.G; s += blockDim.x) {
+        const u64 b0 = (u64)s * P.chunk / kPlanBlock, b1 = (u64)(s + 1) * P.chunk / kPlanBlock;
+        const uint32_t p0 = b0 < P.nblk ? bc_me[b0] : carry;
+        const uint32_t p1 = b1 < P.nblk ? bc_me[b1] : carry;
+        cnt[2 + P.G + s] = p1 - p0;
     }
+}
+
+__global__ __launch_bounds__(256) void plan_scan_fix(ShardPlan P, uint32_t *bc_d, const uint32_t *cnt) {
+    __shared__ uint32_t sdbase[64];
     if (threadIdx.x == 0) {
         uint32_t run = 0;
         for (uint32_t dd = 0; dd < P.G; ++dd) {
-            cnt[2 + dd] = sdbase[dd];
-            const uint32_t c = sdbase[dd];
             sdbase[dd] = run;
-            run += c;
+            run += cnt[2 + dd];
         }
     }
     __syncthreads();
-    for (uint32_t dd = 0; dd < P.G; ++dd)
-        for (uint32_t i = threadIdx.x; i < P.nblk_own; i += blockDim.x) bc_d[(u64)i * P.G + dd] += sdbase[dd];
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (u64)P.nblk_own * P.G) return;
+    bc_d[i] += sdbase[(uint32_t)(i % P.G)];
 }
 
 __global__ __launch_bounds__(kPlanBlock) void plan_emit(ShardPlan P, const uint32_t *__restrict__ tg_all,
@@ -356,7 +369,11 @@ hipError_t launch_shard_plan(const ShardPlan &P, const ShardPlanLayout &L, uint3
     u64 *pairs = reinterpret_cast<u64 *>(w + L.pairs);
     hipLaunchKernelGGL(plan_count, dim3(P.nblk), dim3(kPlanBlock), 0, s, P, seed, epoch, round, f, tg_all,
                        bc_me, bc_d);
-    hipLaunchKernelGGL(plan_scan, dim3(1), dim3(kPlanScanThreads), 0, s, P, bc_me, bc_d, cnt);
+    hipLaunchKernelGGL(plan_scan, dim3(P.G + 1), dim3(kPlanScanThreads), 0, s, P, bc_me, bc_d, cnt);
+    if (P.nblk_own) {
+        const u64 nfix = (u64)P.nblk_own * P.G;
+        hipLaunchKernelGGL(plan_scan_fix, dim3((uint32_t)((nfix + 255) / 256)), dim3(256), 0, s, P, bc_d, cnt);
+    }
     hipLaunchKernelGGL(plan_emit, dim3(P.nblk), dim3(kPlanBlock), 0, s, P, tg_all, bc_me, bc_d, E_id,
                        E_key, SPOS);
     if (P.m == 0) return hipGetLastError();
