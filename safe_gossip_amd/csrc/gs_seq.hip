@@ -36,31 +36,28 @@ __global__ __launch_bounds__(256) void seq_levels(SeqArgs a) {
     __syncthreads();
     const uint32_t y = blockIdx.x * blockDim.x + threadIdx.x;
     if (y < a.g.n) {
-        // got(w) = got0(w) and not (t(t(w)) = w, t(w) < w, got0(t(w)))
-        auto got = [&](uint32_t w, uint32_t tw) -> bool {
-            if (!got0(tw)) return false;
-            const uint32_t v = tw & kTgMask;
-            const uint32_t tv = a.tg[v];
-            return !((tv & kTgMask) == w && v < w && got0(tv));
-        };
+        // got(w) = got0(w) and not (t(t(w)) = w, t(w) < w, got0(t(w))).
+        // Walk y -> z = t(y) -> t(z) ... while ids decrease, carrying each
+        // loaded target word so every level costs one dependent random read;
+        // y's in-list record is read up front, beside tg[y].
         const uint32_t ty = a.tg[y];
-        const bool gy = got(y, ty);
+        const InRec iy = a.IN8[y];
+        bool gy = false, dep = false;
         uint32_t lev = 0;
-        bool dep = false;
-        if (gy) {
-            uint32_t cur = y, tc = ty;
-            for (;;) {
-                const uint32_t zc = tc & kTgMask;
-                if (zc >= cur) break;
-                const uint32_t tz = a.tg[zc];
-                if (!got(zc, tz)) break;
-                if (lev == 0) dep = true;
+        if (got0(ty)) {
+            uint32_t zc = ty & kTgMask, tz = a.tg[zc];  // z = t(y) and its target word
+            gy = !((tz & kTgMask) == y && zc < y && got0(tz));
+            for (uint32_t cur = y; gy && zc < cur && got0(tz);) {
+                const uint32_t w = tz & kTgMask, tw = a.tg[w];
+                if ((tw & kTgMask) == zc && w < zc && got0(tw)) break;  // zc gets no pull
+                dep = true;
                 if (++lev > kMaxSeqLevel) {
                     atomicOr(&a.flags[2], 4u);  // device limit (probability ~n/64!)
                     break;
                 }
                 cur = zc;
-                tc = tz;
+                zc = w;
+                tz = tw;
             }
         }
         // A level-0 W(y) is read only by a later w > y with t(w) = y that gets
@@ -70,11 +67,10 @@ __global__ __launch_bounds__(256) void seq_levels(SeqArgs a) {
         bool inl = false;
 #ifndef GS_SEQ_NO_INLINE
         if (gy && lev == 0) {
-            const InRec r = a.IN8[y];
-            const uint32_t k = r.k();
+            const uint32_t k = iy.k();
             const uint32_t top = k == 0 ? 0u
-                                        : (k <= kInline ? pick_inline(r.s, k - 1u)
-                                                        : a.src[r.first() + (k - 1u - kInline)]);
+                                        : (k <= kInline ? pick_inline(iy.s, k - 1u)
+                                                        : a.src[iy.first() + (k - 1u - kInline)]);
             inl = k == 0 || top < y;
         }
 #endif
