@@ -191,6 +191,14 @@ def test_parity_seq_larger(engine):
     run_parity(engine, 20000, 64, "origins", check_every=4, schedule="SEQ")
 
 
+def test_parity_seq_larger_small_words(engine):
+    # 20k nodes x 16 rumors (four nodes per 64-bit word): level-0 pulls built
+    # inline by the round kernel next to listed ones, with t(x)'s deeper
+    # pusher walks (rank > 3) and in-list tails, under faults
+    run_parity(engine, 20000, 16, "reinject", check_every=3, schedule="SEQ",
+               faults=(0.02, 0.05, 0.05))
+
+
 @pytest.mark.parametrize("seed,epoch", [(1, 0), (0xDEADBEEF, 3), (2**63 + 5, 77)])
 def test_round_parity_seeds(engine, seed, epoch):
     run_parity(engine, 600, 48, "origins", seed=seed, epoch=epoch)
