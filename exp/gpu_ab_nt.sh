@@ -1,0 +1,10 @@
+set -o pipefail
+mkdir -p gpurun_out
+L=safe_gossip_amd/libsafe_gossip_amd.so
+for rep in 1 2 3; do
+for v in base nts ntl ntb; do
+  cp exp/ab/$v.so $L
+  echo "== $v" >> gpurun_out/ab_nt.log
+  timeout -k 10 120 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-spread >> gpurun_out/ab_nt.log 2>&1 || exit 1
+done
+done

@@ -1,0 +1,11 @@
+set -o pipefail
+mkdir -p gpurun_out
+L=safe_gossip_amd/libsafe_gossip_amd.so
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || exit 1
+for rep in 1 2 3; do
+for v in base nst ninl; do
+  cp exp/ab/$v.so $L
+  echo "== $v" >> gpurun_out/ab_nt2.log
+  timeout -k 10 120 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-spread >> gpurun_out/ab_nt2.log 2>&1 || exit 1
+done
+done

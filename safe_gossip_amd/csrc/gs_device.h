@@ -160,6 +160,14 @@ GS_DEV uint32_t pick_sib(const uint32_t (&v)[kSibInline], uint32_t i) {
     return r;
 }
 
+// 16-byte streaming (nontemporal) store, for outputs nobody reads again
+// while they could still be cached (the next round's planes, 4.3 GB at config 4).
+typedef unsigned int gs_u32x4 __attribute__((ext_vector_type(4)));
+GS_DEV void nt_store4(const uint4 &v, uint4 *p) {
+    const gs_u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<gs_u32x4 *>(p));
+}
+
 constexpr uint32_t kScanBlock = 256;
 
 // Block-wide exclusive scan of one value per thread; returns the block total.
