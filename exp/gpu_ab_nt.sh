@@ -1,4 +1,6 @@
 set -o pipefail
+# A/B of library variants: exp/ab/<variant>.so are built beforehand on the CPU host
+# (build.py's hipcc line plus the variant's -D switch) and swapped in per run.
 mkdir -p gpurun_out
 L=safe_gossip_amd/libsafe_gossip_amd.so
 for rep in 1 2 3; do

@@ -1,4 +1,6 @@
 set -o pipefail
+# A/B of library variants: exp/ab/<variant>.so are built beforehand on the CPU host
+# (build.py's hipcc line plus the variant's -D switch) and swapped in per run.
 mkdir -p gpurun_out
 L=safe_gossip_amd/libsafe_gossip_amd.so
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || exit 1
