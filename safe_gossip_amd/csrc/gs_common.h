@@ -102,8 +102,8 @@ constexpr uint32_t kTgMask = kTgOff - 1u;
 // SEQ schedule, per-node info byte (gs_seq.hip): x receives a pull at time x,
 // its pull depends on t(x)'s pull (t(x) < x), and the level of that chain.
 constexpr uint32_t kSeqGot = 0x80u, kSeqDep = 0x40u, kSeqLevelMask = 0x3Fu;
-// Level code of a level-0 node whose pull no later node reads (no pusher above
-// it): the round kernel builds its pull inline, so it is in no pass list.
+// Level code of a node whose pull no later node reads (no pusher above it):
+// the round kernel builds its pull inline, so it is in no pass list.
 constexpr uint32_t kSeqInline = kSeqLevelMask;
 
 __host__ __device__ __forceinline__ uint32_t target_word(uint64_t seed, uint32_t epoch,

@@ -179,6 +179,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     uint32_t tgw = 0;  // round-t target word: t(x) + delivery flags (gs_common.h)
     uint32_t sinf = 0;  // SEQ: got << 7 | ... (gs_seq.hip)
     bool seq_inl = false;  // SEQ: W(x) built here, not by a pull pass (kSeqInline)
+    bool seq_dep = false;  // SEQ: W(x) includes W(t(x)) (kSeqDep)
     if (DELIVER) {
         if (SHARD) {
             if (valid) {
@@ -197,6 +198,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             r = (valid && (sb8.tag >> 8) == (a.serial & kSerialMask)) ? (sb8.tag & 0xFFu) : 0u;
             if (SEQ) {
                 seq_inl = valid && (sinf & kSeqGot) && (sinf & kSeqLevelMask) == kSeqInline;
+                seq_dep = seq_inl && (sinf & kSeqDep);
                 if (!seq_inl) r = 0;
             }
         }
@@ -217,7 +219,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     // barrier: the first kBatchK pushers, t(x), and the first kBatchE pushers
     // of t(x) ahead of x.  Slots past k / r load x's own row (an L2 hit) so no
     // load is conditional.  Rarer deeper in-lists are walked afterwards.
-    Cls q[kBatchK], e[kBatchE], qz = {0, 0, 0};
+    Cls q[kBatchK], e[kBatchE], qz = {0, 0, 0}, wz = {0, 0, 0};
 #pragma unroll
     for (uint32_t i = 0; i < kBatchK; ++i) q[i] = {0, 0, 0};
 #pragma unroll
@@ -247,8 +249,13 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                     qz.c = a.Wb[wi];
                     qz.a0 = a.Wb[wi + g.W];
                 }
-            } else {  // 2P, and SEQ level 0 without a reader of W(x)
+            } else {  // 2P, and SEQ nodes without a reader of W(x)
                 qz = L.load_cls(S, z);
+                if (SEQ && seq_dep) {  // W(z), built by z's pass (z < x has reader x)
+                    const u64 wi = ((u64)z * 2u) * g.W + L.j;
+                    const u64 b0 = a.Wb[wi], b1 = a.Wb[wi + g.W];
+                    wz = Cls{b0 & b1, b0 & ~b1, b1 & ~b0};
+                }
             }
             if (!SEQ || seq_inl) {
 #pragma unroll
@@ -319,25 +326,41 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                 if (s == z) jz = i;
             }
             zin = jz != kNone;
-            if (seq_inl) {  // W(x) = S(z) + what z created from its pushers s < x
+            if (seq_inl) {  // W(x) = S(z) + what z created before time x: from
+                            // its pushers s < x and (dep) from W(z) at time z
                 const u64 zB = ~qz.c & (qz.a0 | qz.a1);
                 const u64 zC = qz.c & ~(qz.a0 & qz.a1);
                 u64 pnot = ~qz.c & ~qz.a0 & ~qz.a1 & L.m, pB = 0, pC = 0;
+                bool wdone = !seq_dep;
+                auto put_w = [&](uint32_t s) {  // W(z) lands between z's pushers < z and > z
+                    if (!wdone && s > z) {
+                        sibling(wz, pnot, pB, pC);
+                        wdone = true;
+                    }
+                };
 #pragma unroll
                 for (uint32_t i = 0; i < kBatchE; ++i)
-                    if (i < r) sibling(e[i], pnot, pB, pC);
-                if (r > kBatchE && pnot) {
-                    for (uint32_t i = kBatchE; i < min(r, kSibInline); ++i)
-                        sibling(L.load_cls(S, pick_sib(sb8.e, i)), pnot, pB, pC);
-                    if (r > kSibInline && pnot) {
+                    if (i < r) {
+                        put_w(sb8.e[i]);
+                        sibling(e[i], pnot, pB, pC);
+                    }
+                if (r > kBatchE && (pnot || !wdone)) {
+                    for (uint32_t i = kBatchE; i < min(r, kSibInline); ++i) {
+                        const uint32_t s = pick_sib(sb8.e, i);
+                        put_w(s);
+                        sibling(L.load_cls(S, s), pnot, pB, pC);
+                    }
+                    if (r > kSibInline && (pnot || !wdone)) {
                         const InRec zin8 = a.IN8[z];
-                        for (uint32_t i = kSibInline; i < r && pnot; ++i) {
+                        for (uint32_t i = kSibInline; i < r && (pnot || !wdone); ++i) {
                             const uint32_t s = i < kInline ? pick_inline(zin8.s, i)
                                                            : a.src[zin8.first() + (i - kInline)];
+                            put_w(s);
                             sibling(L.load_cls(S, s), pnot, pB, pC);
                         }
                     }
                 }
+                if (!wdone) sibling(wz, pnot, pB, pC);
                 const u64 pcl = zC | pC;  // the 2-plane code seq_pull_pass writes
                 const u64 b0 = ((zB & qz.a0 & ~qz.a1) | pB | pcl) & L.m;
                 const u64 b1 = ((zB & qz.a1 & ~qz.a0) | pcl) & L.m;

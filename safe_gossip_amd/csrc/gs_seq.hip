@@ -60,13 +60,14 @@ __global__ __launch_bounds__(256) void seq_levels(SeqArgs a) {
                 tz = tw;
             }
         }
-        // A level-0 W(y) is read only by a later w > y with t(w) = y that gets
-        // a pull, and every such w is in y's in-list (ascending): without a
-        // pusher above y, no pass builds W(y) and the round kernel makes it
-        // inline from t(y)'s planes and t(y)'s pushers ahead of y, as in 2P.
+        // W(y) is read by a pass only for a later w > y with t(w) = y that
+        // gets a pull, and every such w is in y's in-list (ascending): without
+        // a pusher above y, no pass builds W(y) and the round kernel makes it
+        // inline from t(y)'s planes, t(y)'s pushers ahead of y and (dep) the
+        // W(t(y)) its own pass wrote, t(y) having reader y.
         bool inl = false;
 #ifndef GS_SEQ_NO_INLINE
-        if (gy && lev == 0) {
+        if (gy) {
             const uint32_t k = iy.k();
             const uint32_t top = k == 0 ? 0u
                                         : (k <= kInline ? pick_inline(iy.s, k - 1u)
