@@ -1,0 +1,8 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 &&
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
+timeout -k 10 400 python -u bench.py > gpurun_out/bench_default.log 2>&1 &&
+timeout -k 10 300 python -u bench.py --schedule SEQ --no-cpu-baseline > gpurun_out/bench_seq.log 2>&1 &&
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 --no-spread --dist-backend gloo --nodes 4194304 > gpurun_out/bench2_gloo.log 2>&1 &&
+bash profiles/rocprof_r1.sh r1h
