@@ -20,7 +20,8 @@ cfg5 (10^8 x 16 with harness-injected faults: 1% churn, 1% push-batch drop, 1%
 pull-batch drop per node per round, Philox stream 3).  The default line is
 cfg4, the configuration the metric is quoted on that fits one GPU.
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): ONE network
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N, or plain
+`python bench.py --gpus N`, which starts that launcher itself): ONE network
 of the same n x R sharded by node range over the N ranks (safe_gossip_amd.sharded,
 DESIGN.md section 7): every round exchanges push rows and pull rows with RCCL
 all_to_all_single over xGMI on the engine's stream.  Total work is fixed, so
@@ -165,9 +166,29 @@ def cpu_best(R, seed, budget_s):
                        f"{rounds} rounds in {el:.1f}s")
 
 
+def self_launch(args):
+    """`bench.py --gpus N` without a launcher: run torch.distributed.run with
+    N ranks as a child process (before anything touches the GPU), relay its
+    output and exit with its status."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.run(cmd).returncode)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        self_launch(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -178,6 +199,10 @@ def main():
             local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
         dist.init_process_group(args.dist_backend)
+        if dist.get_world_size() != args.gpus:
+            print(f"bench.py: process group of {dist.get_world_size()} ranks, --gpus {args.gpus}",
+                  file=sys.stderr)
+            sys.exit(2)
     else:
         torch.cuda.set_device(0)
 
@@ -215,7 +240,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         net.next_round(report=False)
-    barrier_sync()
+    barrier_sync()   # net.sync() raises DeviceError if a device limit was hit
     elapsed = time.perf_counter() - t0
     ktimes = net.round_kernel_times()
     net.set_timing(False)
@@ -274,7 +299,7 @@ def main():
                 "faults": {"churn": args.faults[0], "drop_push": args.faults[1],
                            "drop_pull": args.faults[2]},
                 "params": list(net.params),
-                "parallelism": (f"node-range shards x{world}, "
+                "parallelism": (f"node-range shards x{dist.get_world_size()}, "
                                 + ("RCCL" if args.dist_backend == "nccl" else args.dist_backend)
                                 + " all-to-all push/pull rows") if world > 1 else "single-gpu",
             },

@@ -39,21 +39,13 @@ static Metric send_messages(Network &net, uint32_t num_msgs) {
             if (gs_coin(net.seed(), net.epoch(), rnd, x)) net.send_new(x, next++);
         processed = net.next_round();
     }
-    const std::vector<uint64_t> st = net.statistics_all();
-    const std::vector<uint64_t> known = net.known_all();
-    const uint32_t kw = (net.rumors() + 63) / 64;
-    Metric m{0, 0, Statistics()};
+    // Statistics::add over every gossiper, rounds = the last one's (:241-245),
+    // as device reductions; messages().len() per node as a device popcount
+    Metric m{0, 0, net.statistics_reduce(GS_REDUCE_SUM)};
+    m.stats.rounds = net.statistics(n - 1).rounds;
+    const std::vector<uint32_t> counts = net.known_popcounts();
     for (uint32_t x = 0; x < n; ++x) {
-        Statistics s;
-        s.rounds = st[5 * (size_t)x];
-        s.empty_pull_sent = st[5 * (size_t)x + 1];
-        s.empty_push_sent = st[5 * (size_t)x + 2];
-        s.full_message_sent = st[5 * (size_t)x + 3];
-        s.full_message_received = st[5 * (size_t)x + 4];
-        m.stats.add(s);
-        m.stats.rounds = s.rounds;
-        uint32_t c = 0;
-        for (uint32_t w = 0; w < kw; ++w) c += (uint32_t)__builtin_popcountll(known[(size_t)x * kw + w]);
+        const uint32_t c = counts[x];
         if (c != num_msgs) {
             m.nodes_missed += 1;
             m.msgs_missed += num_msgs - c;

@@ -19,6 +19,9 @@
  *   gs_messages        <- Gossiper::messages      (src/gossiper.rs:102-104)
  *   gs_statistics      <- Gossiper::statistics    (src/gossiper.rs:107-109)
  *   gs_statistics_reduce <- Statistics::add/min/max (src/gossip.rs:225-263)
+ *   gs_set_params      <- Gossiper::add_peer's AlreadyStarted rule and
+ *                         Gossip::add_peer's parameters (src/gossiper.rs:45-52,
+ *                         src/gossip.rs:59-64)
  *   gs_clear           <- Gossiper::clear (cfg(test), src/gossiper.rs:111-115)
  *   status codes       <- enum Error               (src/error.rs:23-51)
  *
@@ -101,8 +104,15 @@ void        gs_destroy(gs_engine *e);
 gs_status   gs_get_params(const gs_engine *e, uint8_t out[3]);
 
 /* Queue Gossiper::send_new(rumor) on `node`; applied in the next round's phase
- * 0 right before that node's next_round (src/gossiper.rs:203-208). */
+ * 0 right before that node's next_round (src/gossiper.rs:203-208).  Observers
+ * see it at once, as Gossip::new_message inserts it (src/gossip.rs:71-75). */
 gs_status   gs_send_new(gs_engine *e, uint32_t node, uint32_t rumor);
+
+/* Gossiper::add_peer's parameter update (src/gossiper.rs:45-52 ->
+ * src/gossip.rs:59-64): params[i] = 0 derives from the network size.  Fails
+ * with GS_ERR_ALREADY_STARTED once any send_new happened since the last
+ * clear, like add_peer once a gossiper holds a message. */
+gs_status   gs_set_params(gs_engine *e, const uint8_t params[3]);
 
 /* One round for the whole population.  `report` may be NULL (no host sync). */
 gs_status   gs_next_round(gs_engine *e, gs_round_report *report);
@@ -114,6 +124,12 @@ gs_status   gs_statistics_reduce(gs_engine *e, gs_reduce_op op, gs_statistics_t 
 gs_status   gs_messages(gs_engine *e, uint32_t node, uint64_t *words /* ceil(R/64) */);
 gs_status   gs_known_all(gs_engine *e, uint64_t *words /* n*ceil(R/64) */);
 gs_status   gs_known_counts(gs_engine *e, uint64_t *known_total, uint64_t *nodes_complete);
+/* As gs_known_counts, with "complete" = knows at least `min_known` rumors
+ * (the harness's messages().len() == num_of_msgs, src/gossiper.rs:246). */
+gs_status   gs_known_counts_min(gs_engine *e, uint32_t min_known, uint64_t *known_total,
+                                uint64_t *nodes_complete);
+/* |Gossiper::messages()| of every node (n u32). */
+gs_status   gs_known_popcounts(gs_engine *e, uint32_t *counts);
 
 /* Parity dumps (u16 codes identical to the oracle's):
  *   state: tag<<14 | f2<<7 | f1  (B: f1 round, f2 our_counter; C: f1
@@ -122,7 +138,11 @@ gs_status   gs_known_counts(gs_engine *e, uint64_t *known_total, uint64_t *nodes
 gs_status   gs_dump_state(gs_engine *e, uint16_t *out);
 gs_status   gs_dump_records(gs_engine *e, uint16_t *rec, uint32_t *psize);
 
+/* Gossiper::clear for every node.  Returns GS_ERR_DEVICE_LIMIT (after
+ * clearing) when a device limit was hit since the previous clear. */
 gs_status   gs_clear(gs_engine *e, uint32_t epoch);
+/* Wait for every queued round; GS_ERR_DEVICE_LIMIT when a device limit was hit
+ * since the last clear (gs_next_round with report == NULL does not check). */
 gs_status   gs_sync(gs_engine *e);
 uint32_t    gs_round(const gs_engine *e);
 

@@ -156,6 +156,30 @@ class Network {
         check(gs_known_all(e_, w.data()));
         return w;
     }
+    // |Gossiper::messages()| of every node (device popcount)
+    std::vector<uint32_t> known_popcounts() {
+        std::vector<uint32_t> c(n_);
+        check(gs_known_popcounts(e_, c.data()));
+        return c;
+    }
+    // Statistics::add / min / max over every node (device reduction)
+    Statistics statistics_reduce(gs_reduce_op op) {
+        gs_statistics_t s{};
+        check(gs_statistics_reduce(e_, op, &s));
+        return Statistics::from(s);
+    }
+    // Gossiper::add_peer's parameter update: throws AlreadyStarted once a
+    // message was sent (src/gossiper.rs:45-52); 0 = derive from n
+    void set_params(uint8_t counter_max, uint8_t max_c_rounds, uint8_t max_rounds) {
+        const uint8_t p[3] = {counter_max, max_c_rounds, max_rounds};
+        check(gs_set_params(e_, p));
+    }
+    std::vector<uint8_t> params() const {
+        std::vector<uint8_t> p(3);
+        check(gs_get_params(e_, p.data()));
+        return p;
+    }
+    void sync() { check(gs_sync(e_)); }
     void clear(uint32_t epoch) {
         check(gs_clear(e_, epoch));
         epoch_ = epoch;

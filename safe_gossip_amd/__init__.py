@@ -97,6 +97,9 @@ SYMBOLS = {
     "gs_messages": (ctypes.c_int, [_P, ctypes.c_uint32, _U64P]),
     "gs_known_all": (ctypes.c_int, [_P, _U64P]),
     "gs_known_counts": (ctypes.c_int, [_P, _U64P, _U64P]),
+    "gs_known_counts_min": (ctypes.c_int, [_P, ctypes.c_uint32, _U64P, _U64P]),
+    "gs_known_popcounts": (ctypes.c_int, [_P, _U32P]),
+    "gs_set_params": (ctypes.c_int, [_P, _U8P]),
     "gs_dump_state": (ctypes.c_int, [_P, _U16P]),
     "gs_dump_records": (ctypes.c_int, [_P, _U16P, _U32P]),
     "gs_clear": (ctypes.c_int, [_P, ctypes.c_uint32]),
@@ -337,6 +340,13 @@ class Network:
     def send_new(self, node: int, rumor: int) -> None:
         _check(self._lib.gs_send_new(self._h, node, rumor))
 
+    def set_params(self, params=(0, 0, 0)) -> None:
+        """``Gossiper::add_peer``'s parameter update (src/gossiper.rs:45-52):
+        0 entries derive from n; raises :class:`AlreadyStarted` once a message
+        was sent since the last clear."""
+        p = (ctypes.c_uint8 * 3)(*params)
+        _check(self._lib.gs_set_params(self._h, p))
+
     def next_round(self, report: bool = True) -> Optional[RoundReport]:
         if not report:
             _check(self._lib.gs_next_round(self._h, None))
@@ -372,11 +382,19 @@ class Network:
         _check(self._lib.gs_known_all(self._h, out.ctypes.data_as(_U64P)))
         return out
 
-    def known_counts(self):
+    def known_counts(self, min_known: Optional[int] = None):
+        """(known node-rumor pairs, nodes knowing >= min_known rumors; default R)."""
         t = ctypes.c_uint64()
         c = ctypes.c_uint64()
-        _check(self._lib.gs_known_counts(self._h, ctypes.byref(t), ctypes.byref(c)))
+        mk = self.R if min_known is None else min_known
+        _check(self._lib.gs_known_counts_min(self._h, mk, ctypes.byref(t), ctypes.byref(c)))
         return int(t.value), int(c.value)
+
+    def known_popcounts(self) -> np.ndarray:
+        """``Gossiper::messages().len()`` of every node (device popcount)."""
+        out = np.zeros(self.n, dtype=np.uint32)
+        _check(self._lib.gs_known_popcounts(self._h, out.ctypes.data_as(_U32P)))
+        return out
 
     def dump_state(self) -> np.ndarray:
         out = np.zeros((self.n, self.R), dtype=np.uint16)
@@ -448,6 +466,8 @@ def send_messages(net: Network, num_of_msgs: int):
     and clears the network (next epoch), like the reference.
     """
     assert num_of_msgs >= 1
+    if num_of_msgs > net.R:
+        raise ValueError(f"num_of_msgs {num_of_msgs} > rumor slots {net.R}")
     n = net.n
     next_rumor = 0
     net.send_new(origin_of(net.seed, net.epoch, 0, n), next_rumor)
@@ -467,17 +487,18 @@ def send_messages(net: Network, num_of_msgs: int):
         rep = net.next_round()
         processed = rep.any_live
         rounds_run += 1
-        if not round_full:
-            _, complete = net.known_counts()
-            if complete == n and next_rumor == num_of_msgs and num_of_msgs <= net.R:
+        if not round_full and next_rumor == num_of_msgs:
+            # every node's messages().len() == num_of_msgs (only rumors
+            # 0..num_of_msgs-1 are ever sent, so ">=" is "==")
+            _, complete = net.known_counts(num_of_msgs)
+            if complete == n:
                 round_full = net.round
-    st_all = net.statistics_all().astype(np.int64)
-    known = net.known_all()
-    counts = np.array([sum(bin(int(w)).count("1") for w in row) for row in known]) \
-        if net.kw > 1 else np.array([bin(int(w)).count("1") for w in known[:, 0]])
-    stats = Statistics(int(st_all[-1, 0]), int(st_all[:, 1].sum()) - n,
-                       int(st_all[:, 2].sum()) - n, int(st_all[:, 3].sum()),
-                       int(st_all[:, 4].sum()))
+    # device reductions (src/gossiper.rs:241-256): Statistics::add over all
+    # nodes, rounds = the last gossiper's, the final empty round subtracted
+    tot = net.statistics_reduce("sum")
+    stats = Statistics(net.statistics(n - 1).rounds, tot.empty_pull_sent - n,
+                       tot.empty_push_sent - n, tot.full_message_sent, tot.full_message_received)
+    counts = net.known_popcounts().astype(np.int64)
     missed = counts < num_of_msgs
     nodes_missed = int(missed.sum())
     msgs_missed = int((num_of_msgs - counts[missed]).sum())

@@ -74,7 +74,10 @@ struct gs_engine {
     u64 *obs_known = nullptr, *obs_stats = nullptr, *partials = nullptr;
     uint16_t *obs_state = nullptr, *obs_rec = nullptr;
     uint32_t *obs_psize = nullptr;
+    u64 *obs_pend = nullptr;       // queued send_new (node << 32 | rumor) shown to observers
+    uint32_t obs_pend_cap = 0;
     bool obs_valid = false;
+    bool started = false;          // some send_new since the last clear (Error::AlreadyStarted)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timing = false, timed = false;
     // per-round kernel timing ring (gs_round_kernel_times)
@@ -134,7 +137,7 @@ void release(gs_engine *e) {
     }
     if (e->cstream) (void)hipStreamDestroy(e->cstream);
     void *bufs[] = {e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
-                    e->partials, e->obs_state, e->obs_rec, e->obs_psize};
+                    e->partials, e->obs_state, e->obs_rec, e->obs_psize, e->obs_pend};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (e->inj_host) (void)hipHostFree(e->inj_host);
@@ -162,7 +165,18 @@ gs_status reset_state(gs_engine *e) {
     e->deliver_pending = false;
     e->pending.clear();
     e->obs_valid = false;
+    e->started = false;
     return GS_OK;
+}
+
+// flags[2]: a device limit was hit since the last clear (in-degree > kMaxIn,
+// in-list bin / tail overflow, SEQ level overflow, shard receive capacity).
+gs_status device_limit(gs_engine *e) {
+    uint32_t fl = 0;
+    GS_HIP(hipStreamSynchronize(e->cstream));  // in-list builds may run there
+    GS_HIP(hipMemcpyAsync(&fl, e->flags + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    GS_HIP(hipStreamSynchronize(e->stream));
+    return fl ? GS_ERR_DEVICE_LIMIT : GS_OK;
 }
 
 gs::RoundArgs base_args(gs_engine *e) {
@@ -331,10 +345,27 @@ gs_status observe(gs_engine *e, bool dumps) {
         if (st != GS_OK) return st;
     }
     GS_HIP(gs::launch_round(a, e->deliver_pending ? 2 : 3, e->stream));
-    uint32_t fl = 0;
-    GS_HIP(hipMemcpyAsync(&fl, e->flags + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
-    GS_HIP(hipStreamSynchronize(e->stream));
-    if (fl) return GS_ERR_DEVICE_LIMIT;
+    if (!e->pending.empty()) {
+        // Queued send_new calls: Gossip::new_message inserts MessageState::new
+        // into the map at once (src/gossip.rs:71-75), so observers show the
+        // rumor as known, in state B{round 0, our_counter 1}, records dropped.
+        const uint32_t m = (uint32_t)e->pending.size();
+        if (m > e->obs_pend_cap) {
+            if (e->obs_pend) (void)hipFree(e->obs_pend);
+            e->obs_pend = nullptr;
+            e->obs_pend_cap = 0;
+            GS_HIP(dalloc(&e->obs_pend, m));
+            e->obs_pend_cap = m;
+        }
+        std::vector<u64> pv(m);
+        for (uint32_t i = 0; i < m; ++i) pv[i] = ((u64)e->pending[i].first << 32) | e->pending[i].second;
+        GS_HIP(hipMemcpyAsync(e->obs_pend, pv.data(), m * sizeof(u64), hipMemcpyHostToDevice, e->stream));
+        GS_HIP(gs::launch_obs_pending(e->obs_pend, m, e->g.R, e->obs_known, a.obs_state, a.obs_rec,
+                                      e->stream));
+        GS_HIP(hipStreamSynchronize(e->stream));  // pv is a host temporary
+    }
+    gs_status st2 = device_limit(e);
+    if (st2 != GS_OK) return st2;
     e->obs_valid = true;
     return GS_OK;
 }
@@ -355,7 +386,7 @@ const char *gs_status_string(gs_status s) {
     case GS_ERR_UNSUPPORTED: return "parameters outside the packed state layout (counter_max<=3, max_c_rounds<=3, max_rounds<=32, R<=4096)";
     case GS_ERR_HIP: return "HIP runtime error (no usable MI355X device?)";
     case GS_ERR_OUT_OF_MEMORY: return "out of device memory";
-    case GS_ERR_DEVICE_LIMIT: return "in-degree beyond the packed counter range";
+    case GS_ERR_DEVICE_LIMIT: return "device limit hit (in-degree > 30, in-list or receive-row capacity, SEQ depth)";
     }
     return "unknown";
 }
@@ -407,6 +438,9 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
     const uint32_t nglob = cfg->n_nodes, R = cfg->n_rumors;
     if (nglob == 0 || nglob == 0xffffffffu || R == 0 || R > 4096) return GS_ERR_INVALID_ARGUMENT;
     if (world && (rank >= world || world > 64)) return GS_ERR_INVALID_ARGUMENT;
+    // Target words pack t(x) into 29 bits below the delivery flags
+    // (gs_common.h kTgMask), whatever the parameters.
+    if (nglob > gs::kTgMask + 1u) return GS_ERR_UNSUPPORTED;
     gs::ShardPlan sp{};
     if (world) sp = gs::shard_plan(nglob, world, rank);
     const uint32_t n = world ? sp.m : nglob;  // nodes owned by this engine
@@ -610,6 +644,25 @@ gs_status gs_send_new(gs_engine *e, uint32_t node, uint32_t rumor) {
     if (node >= e->g.n || rumor >= e->g.R) return GS_ERR_INVALID_ARGUMENT;
     e->pending.emplace_back(node, rumor);
     e->obs_valid = false;
+    e->started = true;
+    return GS_OK;
+}
+
+gs_status gs_set_params(gs_engine *e, const uint8_t params[3]) {
+    if (!e || !params) return GS_ERR_INVALID_ARGUMENT;
+    // Gossiper::add_peer (src/gossiper.rs:45-52): the parameters may only
+    // change before any message exists.
+    if (e->started) return GS_ERR_ALREADY_STARTED;
+    uint8_t p[3];
+    gs_derive_params(e->shard ? e->n_global : e->g.n, p);
+    for (int i = 0; i < 3; ++i)
+        if (params[i]) p[i] = params[i];
+    if ((e->shard ? e->n_global : e->g.n) >= 2 && (p[0] > 3 || p[1] > 3 || p[2] > 32 || !p[0] || !p[1] || !p[2]))
+        return GS_ERR_UNSUPPORTED;
+    e->cmax = p[0];
+    e->maxc = p[1];
+    e->maxr = p[2];
+    e->obs_valid = false;
     return GS_OK;
 }
 
@@ -783,12 +836,17 @@ gs_status gs_known_all(gs_engine *e, uint64_t *words) {
 }
 
 gs_status gs_known_counts(gs_engine *e, uint64_t *known_total, uint64_t *nodes_complete) {
+    return gs_known_counts_min(e, e ? e->g.R : 0, known_total, nodes_complete);
+}
+
+gs_status gs_known_counts_min(gs_engine *e, uint32_t min_known, uint64_t *known_total,
+                              uint64_t *nodes_complete) {
     if (!e) return GS_ERR_INVALID_ARGUMENT;
     gs_status st = set_device(e);
     if (st == GS_OK) st = observe(e, false);
     if (st != GS_OK) return st;
     const uint32_t KW = (e->g.R + 63) / 64;
-    GS_HIP(gs::launch_known_reduce(e->obs_known, e->g.n, KW, e->g.R, e->partials, kReduceBlocks / 2,
+    GS_HIP(gs::launch_known_reduce(e->obs_known, e->g.n, KW, min_known, e->partials, kReduceBlocks / 2,
                                    e->stream));
     std::vector<u64> part(kReduceBlocks);
     GS_HIP(hipMemcpyAsync(part.data(), e->partials, part.size() * sizeof(u64), hipMemcpyDeviceToHost,
@@ -801,6 +859,21 @@ gs_status gs_known_counts(gs_engine *e, uint64_t *known_total, uint64_t *nodes_c
     }
     if (known_total) *known_total = t;
     if (nodes_complete) *nodes_complete = c;
+    return GS_OK;
+}
+
+gs_status gs_known_popcounts(gs_engine *e, uint32_t *counts) {
+    if (!e || !counts) return GS_ERR_INVALID_ARGUMENT;
+    gs_status st = set_device(e);
+    if (st == GS_OK) st = observe(e, false);
+    if (st != GS_OK) return st;
+    const uint32_t KW = (e->g.R + 63) / 64;
+    // obs_psize is free scratch here ([n] u32; rewritten by the next observe)
+    GS_HIP(gs::launch_known_popc(e->obs_known, e->g.n, KW, e->obs_psize, e->stream));
+    GS_HIP(hipMemcpyAsync(counts, e->obs_psize, (size_t)e->g.n * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                          e->stream));
+    GS_HIP(hipStreamSynchronize(e->stream));
+    e->obs_valid = false;  // obs_psize overwritten
     return GS_OK;
 }
 
@@ -828,18 +901,24 @@ gs_status gs_clear(gs_engine *e, uint32_t epoch) {
     if (!e) return GS_ERR_INVALID_ARGUMENT;
     gs_status st = set_device(e);
     if (st != GS_OK) return st;
+    // A device limit hit since the last clear is reported here rather than
+    // dropped with the flags (gs_next_round(e, NULL) never reads them).
+    const gs_status lim = device_limit(e);
+    if (lim != GS_OK && lim != GS_ERR_DEVICE_LIMIT) return lim;
     e->epoch = epoch;
     st = reset_state(e);
     if (st != GS_OK) return st;
     GS_HIP(hipStreamSynchronize(e->stream));
-    return GS_OK;
+    return lim;
 }
 
 gs_status gs_sync(gs_engine *e) {
     if (!e) return GS_ERR_INVALID_ARGUMENT;
+    gs_status st = set_device(e);
+    if (st != GS_OK) return st;
     GS_HIP(hipStreamSynchronize(e->stream));
     GS_HIP(hipStreamSynchronize(e->cstream));
-    return GS_OK;
+    return device_limit(e);
 }
 
 void gs_set_timing(gs_engine *e, int enable) {

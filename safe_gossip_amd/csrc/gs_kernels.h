@@ -159,9 +159,16 @@ struct PullArgs {
 hipError_t launch_pull(const PullArgs &a, hipStream_t s);
 
 // Reductions for observers.
-hipError_t launch_known_reduce(const u64 *known, uint32_t n, uint32_t KW, uint32_t R,
+// nodes_complete counts nodes knowing >= min_known rumors.
+hipError_t launch_known_reduce(const u64 *known, uint32_t n, uint32_t KW, uint32_t min_known,
                                u64 *partials /* [2*blocks] */, uint32_t blocks,
                                hipStream_t s);
+// Per node: |known| (popcount over KW words) into counts[n].
+hipError_t launch_known_popc(const u64 *known, uint32_t n, uint32_t KW, uint32_t *counts, hipStream_t s);
+// Observation of queued injections (node << 32 | rumor): known bit set, state
+// B{0,1}, records dropped; state/rec may be null.
+hipError_t launch_obs_pending(const u64 *pairs, uint32_t m, uint32_t R, u64 *known, uint16_t *state,
+                              uint16_t *rec, hipStream_t s);
 hipError_t launch_stats_reduce(const u64 *stats, uint32_t n, int op,
                                u64 *partials /* [5*blocks] */, uint32_t blocks,
                                hipStream_t s);

@@ -734,14 +734,14 @@ hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, hipStream_t 
 
 // ------------------------------------------------------------ reductions
 __global__ __launch_bounds__(256) void known_reduce(const u64 *__restrict__ known, uint32_t n,
-                                                    uint32_t KW, uint32_t R, u64 *partials) {
+                                                    uint32_t KW, uint32_t min_known, u64 *partials) {
     __shared__ u64 s_tot[256], s_cmp[256];
     u64 tot = 0, cmp = 0;
     for (u64 x = (u64)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (u64)gridDim.x * blockDim.x) {
         uint32_t c = 0;
         for (uint32_t w = 0; w < KW; ++w) c += popc(known[x * KW + w]);
         tot += c;
-        cmp += (c == R) ? 1u : 0u;
+        cmp += (c >= min_known) ? 1u : 0u;
     }
     s_tot[threadIdx.x] = tot;
     s_cmp[threadIdx.x] = cmp;
@@ -759,9 +759,42 @@ __global__ __launch_bounds__(256) void known_reduce(const u64 *__restrict__ know
     }
 }
 
-hipError_t launch_known_reduce(const u64 *known, uint32_t n, uint32_t KW, uint32_t R,
+hipError_t launch_known_reduce(const u64 *known, uint32_t n, uint32_t KW, uint32_t min_known,
                                u64 *partials, uint32_t blocks, hipStream_t s) {
-    hipLaunchKernelGGL(known_reduce, dim3(blocks), dim3(256), 0, s, known, n, KW, R, partials);
+    hipLaunchKernelGGL(known_reduce, dim3(blocks), dim3(256), 0, s, known, n, KW, min_known, partials);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void known_popc(const u64 *__restrict__ known, uint32_t n, uint32_t KW,
+                                                  uint32_t *counts) {
+    const u64 x = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= n) return;
+    uint32_t c = 0;
+    for (uint32_t w = 0; w < KW; ++w) c += popc(known[x * KW + w]);
+    counts[x] = c;
+}
+
+hipError_t launch_known_popc(const u64 *known, uint32_t n, uint32_t KW, uint32_t *counts, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(known_popc, dim3((n + 255) / 256), dim3(256), 0, s, known, n, KW, counts);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void obs_pending(const u64 *__restrict__ pairs, uint32_t m, uint32_t R,
+                                                   u64 *known, uint16_t *state, uint16_t *rec) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t x = (uint32_t)(pairs[i] >> 32), r = (uint32_t)pairs[i];
+    const uint32_t KW = (R + 63u) >> 6;
+    atomicOr(&known[(u64)x * KW + (r >> 6)], 1ull << (r & 63u));
+    if (state) state[(u64)x * R + r] = (uint16_t)((1u << 14) | (1u << 7));  // B{round 0, counter 1}
+    if (rec) rec[(u64)x * R + r] = 0;
+}
+
+hipError_t launch_obs_pending(const u64 *pairs, uint32_t m, uint32_t R, u64 *known, uint16_t *state,
+                              uint16_t *rec, hipStream_t s) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(obs_pending, dim3((m + 255) / 256), dim3(256), 0, s, pairs, m, R, known, state, rec);
     return hipGetLastError();
 }
 

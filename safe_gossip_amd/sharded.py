@@ -320,12 +320,14 @@ class ShardedNetwork:
         both = self._gather_rows(self._per_shard(f))
         return both[:, :-1].astype(np.uint16), both[:, -1].astype(np.uint32)
 
-    def known_counts(self):
+    def known_counts(self, min_known: Optional[int] = None):
+        mk = self.R if min_known is None else min_known
+
         def f(s):
             if not s.m:
                 return (0, 0)
             t, c = ctypes.c_uint64(), ctypes.c_uint64()
-            _check(self.lib.gs_known_counts(s.h, ctypes.byref(t), ctypes.byref(c)))
+            _check(self.lib.gs_known_counts_min(s.h, mk, ctypes.byref(t), ctypes.byref(c)))
             return (int(t.value), int(c.value))
         parts = self._per_shard(f)
         tot = sum(p[0] for p in parts)

@@ -76,3 +76,13 @@ def test_invalid_config_rejected(engine):
     assert lib.gs_create(ctypes.byref(cfg), ctypes.byref(h)) == -2   # unsupported layout
     cfg.counter_max, cfg.max_c_rounds, cfg.max_rounds = 3, 3, 33
     assert lib.gs_create(ctypes.byref(cfg), ctypes.byref(h)) == -2
+
+
+def test_node_ids_beyond_target_word_rejected(engine):
+    # t(x) is packed into 29 bits of the target word (gs_common.h kTgMask):
+    # a network above 2^29 nodes is refused whatever the parameters, before
+    # any device call (so this runs without a GPU).
+    with pytest.raises(engine.DeviceError, match="status -2"):
+        engine.Network((1 << 29) + 1, 1, params=(3, 3, 21))
+    with pytest.raises(engine.DeviceError, match="status -2"):
+        engine.Network(0xFFFFFFFE, 1, params=(3, 3, 21))

@@ -102,3 +102,30 @@ def test_peer_choice_is_uniform_over_others(engine):
     off = cnt[~np.eye(n, dtype=bool)]
     expect = trials / n / (n - 1)
     assert np.all(np.abs(off - expect) < 6 * np.sqrt(expect))
+
+
+def test_torch_philox_matches_oracle():
+    # the vectorised torch Philox (tests/philox_torch.py) used by the
+    # full-size property tests equals the oracle's on KATs and random counters
+    import numpy as np
+    import torch
+    import philox_torch as pt
+    import oracle_lib
+    L = oracle_lib.lib()
+    rng = np.random.default_rng(5)
+    for seed in (0, 0x5AFE6055, 0xFFFFFFFFFFFFFFFF, 2**63 + 5):
+        ctr = rng.integers(0, 2**32, size=(64, 4), dtype=np.uint64)
+        got = pt.philox4x32(*(torch.tensor(ctr[:, i].astype(np.int64)) for i in range(4)), seed)
+        for i in range(64):
+            exp = oracle_lib.philox([int(v) for v in ctr[i]], [seed & 0xFFFFFFFF, seed >> 32])
+            assert [int(g[i]) for g in got] == list(exp)
+    nodes = torch.arange(0, 5000, dtype=torch.int64)
+    for n in (5000, 2**24):
+        nn = nodes if n == 5000 else nodes * 3355
+        peers = pt.peer_of(0x5AFE6055, 3, 7, nn, n)
+        for x in range(0, 5000, 97):
+            assert int(peers[x]) == L.or_peer(0x5AFE6055, 3, 7, int(nn[x]), n)
+    thr = [oracle_lib.fault_threshold(p) for p in (0.3, 0.2, 0.1)]
+    fb = pt.fault_bits(0x5AFE6055, 1, 4, nodes, *thr)
+    for x in range(0, 5000, 13):
+        assert int(fb[x]) == L.or_fault(0x5AFE6055, 1, 4, x, *thr)
