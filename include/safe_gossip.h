@@ -160,25 +160,30 @@ double      gs_round_kernel_bytes(const gs_engine *e);
 
 /* ---- Sharded network (multi-GPU): one engine per rank owns the node range
  * [lo, lo+m).  Per round t the caller moves two sets of rows between ranks
- * (DESIGN.md section 7): A = push rows (push-batch class codes, sent to
- * the owner of its target) and B = pull rows (returned in the reverse layout).
- * Sequence per round, after gs_next_round has produced round t:
- *   gs_shard_counts -> exchange A (sendA -> recvA) -> gs_shard_pull ->
- *   exchange B (sendB -> recvB, counts swapped) -> gs_next_round (round t+1).
- * Rows are u64 words: push row = info[3] words, pull row = info[4] words;
- * row counts per peer rank come from gs_shard_counts.  gs_send_new takes global
- * node ids owned by this rank; observers report the owned nodes only. */
+ *  with FIXED-SIZE all-to-all exchanges (equal splits:
+ * no row count ever reaches the host, a round needs no host synchronisation):
+ *   A(t): exchange-A buffer set t % 2, block d of sendA -> block g of rank d's
+ *         recvA (block = info[8] u64 words: push rows of round t and the
+ *         source ids of round t+1 for the in-lists, built one round ahead);
+ *   B(t): block d of sendB -> block g of rank d's recvB (info[9] words).
+ * Sequence per round t >= 1, after gs_next_round has produced round t:
+ *   [t == 1: A(0) on set 0] -> A(t) on set t % 2 -> gs_shard_pull -> B(t)
+ *   -> gs_next_round (round t+1).
+ * Exchanges must be ordered on the engine stream (gs_stream).  gs_send_new
+ * takes global node ids owned by this rank; observers report the owned nodes
+ * only.  A capacity overflow (probability < 1e-50 per round) is reported as
+ * GS_ERR_DEVICE_LIMIT by gs_sync / gs_clear / the observers. */
 gs_status   gs_shard_create(const gs_config *cfg, uint32_t rank, uint32_t world, gs_engine **out);
-/* info = {lo, m, recv capacity (rows), push row words, pull row words, world,
- *         rank, nodes per rank} */
-gs_status   gs_shard_info(const gs_engine *e, uint32_t info[8]);
-/* Device buffers (u64 words): sendA m*info[3], recvA cap*info[3],
- * sendB cap*info[4], recvB m*info[4]. */
-gs_status   gs_shard_bind(gs_engine *e, void *sendA, void *recvA, void *sendB, void *recvB);
-/* Rows this rank sends to / receives from each rank in the exchanges of the
- * current round (A; B is the reverse). */
-gs_status   gs_shard_counts(gs_engine *e, uint32_t *send_rows, uint32_t *recv_rows);
-/* Pull rows of the current round (after exchange A). */
+/* info = {lo, m, cap (row slots per block of B), capA (row slots per block
+ *         of A), row words, world, rank, nodes per rank, u64 words per block
+ *         of A, u64 words per block of B, 0, 0} */
+gs_status   gs_shard_info(const gs_engine *e, uint32_t info[12]);
+/* Device buffers of world blocks each: sendA[2], recvA[2] (info[8] words per
+ * block), sendB, recvB (info[9] words per block). */
+gs_status   gs_shard_bind(gs_engine *e, void *sendA0, void *sendA1, void *recvA0, void *recvA1,
+                          void *sendB, void *recvB);
+/* After exchange A of the current round: the pull rows (into sendB), and the
+ * next round's in-lists on the side stream. */
 gs_status   gs_shard_pull(gs_engine *e);
 /* The engine's HIP stream (hipStream_t), to order collectives on it. */
 uint64_t    gs_stream(const gs_engine *e);

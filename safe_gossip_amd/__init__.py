@@ -124,8 +124,7 @@ SYMBOLS = {
     "gs_shard_create": (ctypes.c_int, [ctypes.POINTER(_Config), ctypes.c_uint32, ctypes.c_uint32,
                                        ctypes.POINTER(_P)]),
     "gs_shard_info": (ctypes.c_int, [_P, _U32P]),
-    "gs_shard_bind": (ctypes.c_int, [_P, _P, _P, _P, _P]),
-    "gs_shard_counts": (ctypes.c_int, [_P, _U32P, _U32P]),
+    "gs_shard_bind": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P]),
     "gs_shard_pull": (ctypes.c_int, [_P]),
     "gs_stream": (ctypes.c_uint64, [_P]),
 }

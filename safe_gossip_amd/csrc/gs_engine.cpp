@@ -52,15 +52,23 @@ struct gs_engine {
     uint32_t *flags = nullptr;
     gs::CsrPlan plan{};
     // Shard engine (gs_shard_create): this rank's node range of a network
-    // sharded over `world` ranks; plans of rounds r live in set r % 3.
+    // sharded over `world` ranks.  The plan of round r (owned targets, send
+    // slots) lives in set r % 3, the in-lists of round r in set r % 2, and
+    // exchange A of round t (rows of round t + ids of round t+1) in buffer
+    // set t % 2 (gs_shard.hip).
     bool shard = false;
     uint32_t n_global = 0;
     gs::ShardPlan sp{};
     gs::ShardPlanLayout spl{};
+    gs::ShardEdgeLayout sel{};
     uint32_t *planw[3] = {nullptr, nullptr, nullptr};
-    hipEvent_t ev_plan[3] = {nullptr, nullptr, nullptr};  // plan of set i built
-    hipEvent_t ev_kr[3] = {nullptr, nullptr, nullptr};    // round kernel r (set r%3) done
-    u64 *sendA = nullptr, *recvA = nullptr, *sendB = nullptr, *recvB = nullptr;
+    uint32_t *edgew[2] = {nullptr, nullptr};
+    hipEvent_t ev_plan[3] = {nullptr, nullptr, nullptr};  // plan set i built
+    hipEvent_t ev_edges[2] = {nullptr, nullptr};          // in-list set i built
+    hipEvent_t ev_main = nullptr;                          // engine stream position (cstream waits)
+    u64 *sendA[2] = {nullptr, nullptr}, *recvA[2] = {nullptr, nullptr};
+    u64 *sendB = nullptr, *recvB = nullptr;
+    uint32_t pulled_round = 0;  // round whose gs_shard_pull ran (its plan of t+2 is launched)
     uint32_t *st32 = nullptr;  // [n][4] u32 deltas
     u64 *st64 = nullptr;       // [n][4] folded totals
     uint32_t fold_every = 1, since_fold = 0;
@@ -133,8 +141,12 @@ void release(gs_engine *e) {
     for (int i = 0; i < 3; ++i) {
         if (e->planw[i]) (void)hipFree(e->planw[i]);
         if (e->ev_plan[i]) (void)hipEventDestroy(e->ev_plan[i]);
-        if (e->ev_kr[i]) (void)hipEventDestroy(e->ev_kr[i]);
     }
+    for (int i = 0; i < 2; ++i) {
+        if (e->edgew[i]) (void)hipFree(e->edgew[i]);
+        if (e->ev_edges[i]) (void)hipEventDestroy(e->ev_edges[i]);
+    }
+    if (e->ev_main) (void)hipEventDestroy(e->ev_main);
     if (e->cstream) (void)hipStreamDestroy(e->cstream);
     void *bufs[] = {e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
                     e->partials, e->obs_state, e->obs_rec, e->obs_psize, e->obs_pend};
@@ -162,6 +174,7 @@ gs_status reset_state(gs_engine *e) {
     e->cur = 0;
     e->round = 0;
     e->seq_round = ~0u;
+    e->pulled_round = 0;
     e->deliver_pending = false;
     e->pending.clear();
     e->obs_valid = false;
@@ -184,18 +197,19 @@ gs::RoundArgs base_args(gs_engine *e) {
     a.Scur = e->S[e->cur];
     a.Snext = e->S[e->cur ^ 1];
     if (e->shard) {
-        uint32_t *cur = e->planw[e->round % 3], *nxt = e->planw[(e->round + 1) % 3];
-        a.IN = reinterpret_cast<const uint4 *>(cur + e->spl.IN);
-        a.IN2 = cur + e->spl.IN2;
-        a.src = cur + e->spl.EP;
-        a.spos_cur = cur + e->spl.SPOS;
-        a.spos_next = nxt + e->spl.SPOS;
-        a.tg = cur + e->spl.tg_all + e->sp.lo;
+        const uint32_t t = e->round;
+        uint32_t *cur = e->planw[t % 3], *nxt = e->planw[(t + 1) % 3], *ed = e->edgew[t % 2];
+        a.IN = reinterpret_cast<const uint4 *>(ed + e->sel.IN);
+        a.IN2 = ed + e->sel.IN2;
+        a.src = ed + e->sel.EP;
+        a.spos_cur = cur + e->spl.SPOSB;
+        a.spos_next = nxt + e->spl.SPOSA;
+        a.tg = cur + e->spl.tg;
         a.node_lo = e->sp.lo;
-        a.tg_next = nxt + e->spl.tg_all + e->sp.lo;
-        a.recvA = e->recvA;
+        a.tg_next = nxt + e->spl.tg;
+        a.recvA = e->recvA[t % 2];
         a.recvB = e->recvB;
-        a.sendA = e->sendA;
+        a.sendA = e->sendA[(t + 1) % 2];
     } else {
         const auto &cs = e->csr[e->round & 1u];  // round-t lists (t = e->round)
         a.IN8 = cs.IN8;
@@ -339,7 +353,7 @@ gs_status observe(gs_engine *e, bool dumps) {
         a.obs_rec = e->obs_rec;
     }
     if (e->deliver_pending) {
-        if (e->shard) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[e->round % 3], 0));
+        if (e->shard) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_edges[e->round % 2], 0));
         else GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
         st = seq_prepare(e);
         if (st != GS_OK) return st;
@@ -437,12 +451,12 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
     *out = nullptr;
     const uint32_t nglob = cfg->n_nodes, R = cfg->n_rumors;
     if (nglob == 0 || nglob == 0xffffffffu || R == 0 || R > 4096) return GS_ERR_INVALID_ARGUMENT;
-    if (world && (rank >= world || world > 64)) return GS_ERR_INVALID_ARGUMENT;
+    if (world && (rank >= world || world > gs::kMaxShards)) return GS_ERR_INVALID_ARGUMENT;
     // Target words pack t(x) into 29 bits below the delivery flags
     // (gs_common.h kTgMask), whatever the parameters.
     if (nglob > gs::kTgMask + 1u) return GS_ERR_UNSUPPORTED;
     gs::ShardPlan sp{};
-    if (world) sp = gs::shard_plan(nglob, world, rank);
+    if (world) sp = gs::shard_plan(nglob, world, rank, R >= 64 ? (next_pow2(R) / 64) : 1u);
     const uint32_t n = world ? sp.m : nglob;  // nodes owned by this engine
     uint8_t p[3];
     gs_derive_params(nglob, p);
@@ -509,9 +523,14 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
     for (int i = 0; i < 3 && ok && e->shard; ++i) {
         const size_t words = gs::shard_plan_words(e->sp, &e->spl);
         ok = hipEventCreateWithFlags(&e->ev_plan[i], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&e->ev_kr[i], hipEventDisableTiming) == hipSuccess &&
              dalloc(&e->planw[i], words) == hipSuccess;
     }
+    for (int i = 0; i < 2 && ok && e->shard; ++i) {
+        const size_t words = gs::shard_edge_words(e->sp, &e->sel);
+        ok = hipEventCreateWithFlags(&e->ev_edges[i], hipEventDisableTiming) == hipSuccess &&
+             dalloc(&e->edgew[i], words) == hipSuccess;
+    }
+    if (ok && e->shard) ok = hipEventCreateWithFlags(&e->ev_main, hipEventDisableTiming) == hipSuccess;
     const gs::InListSizes isz = gs::inlist_sizes(e->plan);
     for (int i = 0; i < 2 && ok && !e->shard; ++i) {
         auto &c = e->csr[i];
@@ -545,10 +564,22 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
     return GS_OK;
 }
 
+// Plan of round r on the side stream: owned targets and send slots (set
+// r % 3), and the ids exchange A of round r-1 carries (buffer set (r-1) % 2).
 gs_status launch_plan(gs_engine *e, uint32_t r) {
-    GS_HIP(gs::launch_shard_plan(e->sp, e->spl, e->planw[r % 3], e->seed, e->epoch, r, e->faults,
-                                 e->cstream));
+    GS_HIP(gs::launch_shard_plan(e->sp, e->spl, e->planw[r % 3], e->sendA[(r + 1) % 2], e->seed, e->epoch, r,
+                                 e->faults, e->flags, e->cstream));
     GS_HIP(hipEventRecord(e->ev_plan[r % 3], e->cstream));
+    return GS_OK;
+}
+
+// In-lists of round r from the ids received by exchange A of round r-1
+// (buffer set (r-1) % 2), on the side stream.
+gs_status launch_edges(gs_engine *e, uint32_t r) {
+    GS_HIP(gs::launch_shard_edges(e->sp, e->sel, e->edgew[r % 2], e->recvA[(r + 1) % 2],
+                                  e->planw[r % 3] + e->spl.tg, e->seed, e->epoch, r, e->faults, e->flags,
+                                  e->cstream));
+    GS_HIP(hipEventRecord(e->ev_edges[r % 2], e->cstream));
     return GS_OK;
 }
 
@@ -563,58 +594,70 @@ gs_status gs_shard_create(const gs_config *cfg, uint32_t rank, uint32_t world, g
     return create_engine(cfg, rank, world, out);
 }
 
-gs_status gs_shard_info(const gs_engine *e, uint32_t info[8]) {
+gs_status gs_shard_info(const gs_engine *e, uint32_t info[12]) {
     if (!e || !info || !e->shard) return GS_ERR_INVALID_ARGUMENT;
+    const uint32_t wa = 2 * e->g.W;  // u64 words per row (2-plane class code)
     info[0] = e->sp.lo;
     info[1] = e->sp.m;
-    info[2] = e->sp.cap_in;
-    info[3] = 2 * e->g.W;  // u64 words per push row (2-plane class code)
-    info[4] = 2 * e->g.W;  // u64 words per pull row
+    info[2] = e->sp.cap;
+    info[3] = e->sp.capA;
+    info[4] = wa;
     info[5] = e->sp.G;
     info[6] = e->sp.g;
     info[7] = e->sp.chunk;
+    info[8] = e->sp.capA * wa;  // u64 words per exchange-A block
+    info[9] = e->sp.cap * wa;   // u64 words per exchange-B block
+    info[10] = info[11] = 0;
     return GS_OK;
 }
 
-gs_status gs_shard_bind(gs_engine *e, void *sendA, void *recvA, void *sendB, void *recvB) {
-    if (!e || !e->shard || !sendA || !recvA || !sendB || !recvB) return GS_ERR_INVALID_ARGUMENT;
-    e->sendA = (u64 *)sendA;
-    e->recvA = (u64 *)recvA;
+gs_status gs_shard_bind(gs_engine *e, void *sendA0, void *sendA1, void *recvA0, void *recvA1, void *sendB,
+                        void *recvB) {
+    if (!e || !e->shard || !sendA0 || !sendA1 || !recvA0 || !recvA1 || !sendB || !recvB)
+        return GS_ERR_INVALID_ARGUMENT;
+    e->sendA[0] = (u64 *)sendA0;
+    e->sendA[1] = (u64 *)sendA1;
+    e->recvA[0] = (u64 *)recvA0;
+    e->recvA[1] = (u64 *)recvA1;
     e->sendB = (u64 *)sendB;
     e->recvB = (u64 *)recvB;
     return GS_OK;
 }
 
-gs_status gs_shard_counts(gs_engine *e, uint32_t *send_rows, uint32_t *recv_rows) {
-    if (!e || !e->shard || e->round == 0 || !send_rows || !recv_rows) return GS_ERR_INVALID_ARGUMENT;
-    gs_status st = set_device(e);
-    if (st != GS_OK) return st;
-    GS_HIP(hipEventSynchronize(e->ev_plan[e->round % 3]));
-    const uint32_t G = e->sp.G;
-    std::vector<uint32_t> c(2 + 2 * (size_t)G);
-    GS_HIP(hipMemcpy(c.data(), e->planw[e->round % 3] + e->spl.cnt, c.size() * sizeof(uint32_t),
-                     hipMemcpyDeviceToHost));
-    if (c[1]) return GS_ERR_DEVICE_LIMIT;  // more sources than receive rows
-    for (uint32_t i = 0; i < G; ++i) {
-        send_rows[i] = c[2 + i];
-        recv_rows[i] = c[2 + G + i];
-    }
-    return GS_OK;
-}
-
 gs_status gs_shard_pull(gs_engine *e) {
-    if (!e || !e->shard || e->round == 0 || !e->recvA) return GS_ERR_INVALID_ARGUMENT;
+    if (!e || !e->shard || e->round == 0 || !e->recvB) return GS_ERR_INVALID_ARGUMENT;
     gs_status st = set_device(e);
     if (st != GS_OK) return st;
-    uint32_t *pw = e->planw[e->round % 3];
-    GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[e->round % 3], 0));
+    const uint32_t t = e->round;
+    // Exchange A of round t (and, in round 1, the ids-only exchange A of
+    // round 0) is complete on the engine stream: build the in-lists of round
+    // t+1 (and of round 1) on the side stream, behind this round's work.
+    GS_HIP(hipEventRecord(e->ev_main, e->stream));
+    GS_HIP(hipStreamWaitEvent(e->cstream, e->ev_main, 0));
+    if (t == 1) {
+        st = launch_edges(e, 1);
+        if (st != GS_OK) return st;
+    }
+    GS_HIP(hipStreamWaitEvent(e->stream, e->ev_edges[t % 2], 0));
+    st = launch_edges(e, t + 1);
+    if (st != GS_OK) return st;
+    // Plan of round t+2 into set (t+2)%3 (last read by the round kernel of
+    // round t-1) and its ids into exchange-A buffer (t+1)%2 (last sent by
+    // exchange A of round t-1): it has this round's pull rows, exchange B and
+    // round kernel to finish before exchange A of round t+1 needs it.
+    st = launch_plan(e, t + 2);
+    if (st != GS_OK) return st;
+    e->pulled_round = t;
+    uint32_t *ed = e->edgew[t % 2];
     gs::PullArgs a{};
     a.S = e->S[e->cur];
-    a.IN = reinterpret_cast<const uint4 *>(pw + e->spl.IN);
-    a.IN2 = pw + e->spl.IN2;
-    a.EP = pw + e->spl.EP;
-    a.recvA = e->recvA;
+    a.IN = reinterpret_cast<const uint4 *>(ed + e->sel.IN);
+    a.IN2 = ed + e->sel.IN2;
+    a.EP = ed + e->sel.EP;
+    a.recvA = e->recvA[t % 2];
     a.sendB = e->sendB;
+    a.cap = e->sp.cap;
+    a.capA = e->sp.capA;
     a.g = e->g;
     GS_HIP(gs::launch_pull(a, e->stream));
     return GS_OK;
@@ -669,12 +712,19 @@ gs_status gs_set_params(gs_engine *e, const uint8_t params[3]) {
 gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
     if (!e) return GS_ERR_INVALID_ARGUMENT;
     if ((e->shard ? e->n_global : e->g.n) < 2) return GS_ERR_NO_PEERS;  // src/gossiper.rs:71-74
-    if (e->shard && !e->sendA) return GS_ERR_INVALID_ARGUMENT;  // gs_shard_bind first
+    if (e->shard && !e->sendB) return GS_ERR_INVALID_ARGUMENT;  // gs_shard_bind first
+    // a shard delivers round t only after its exchanges (gs_shard_pull)
+    if (e->shard && e->round > 0 && e->pulled_round != e->round) return GS_ERR_INVALID_ARGUMENT;
     gs_status st = set_device(e);
     if (st != GS_OK) return st;
-    if (e->shard && e->round == 0) {
-        st = launch_plan(e, 1);  // send rows of round 1's push rows
-        if (st != GS_OK) return st;
+    if (e->shard) {
+        // cstream work launched below may reuse buffers read before this point
+        GS_HIP(hipEventRecord(e->ev_main, e->stream));
+        GS_HIP(hipStreamWaitEvent(e->cstream, e->ev_main, 0));
+        if (e->round == 0) {
+            st = launch_plan(e, 1);  // send slots of round 1's push rows, ids for exchange A(0)
+            if (st != GS_OK) return st;
+        }
     }
     uint32_t n_inj = 0;
     st = upload_injections(e, &n_inj);
@@ -693,7 +743,7 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
     const uint32_t rs = R0 & 1u;  // set holding round t = e->round
     if (e->shard) {
         GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[(R0 + 1) % 3], 0));
-        if (e->deliver_pending) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[R0 % 3], 0));
+        if (e->deliver_pending) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_edges[R0 % 2], 0));
     } else if (e->deliver_pending) {
         GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[rs], 0));
         st = seq_prepare(e);  // SEQ: pull batches of round t (no-op for 2P)
@@ -702,8 +752,7 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
     if (e->timing) GS_HIP(hipEventRecord(t0, e->stream));
     GS_HIP(gs::launch_round(a, e->deliver_pending ? 1 : 0, e->stream));
     if (e->timing) GS_HIP(hipEventRecord(t1, e->stream));
-    if (e->shard) GS_HIP(hipEventRecord(e->ev_kr[(R0 + 1) % 3], e->stream));
-    else GS_HIP(hipEventRecord(e->ev_read[rs], e->stream));
+    if (!e->shard) GS_HIP(hipEventRecord(e->ev_read[rs], e->stream));
     e->ev0 = t0;
     e->ev1 = t1;
     e->timed = e->timing;
@@ -716,11 +765,14 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
         e->since_fold = 0;
     }
     if (e->shard) {
-        // Plan of round t+2 into set (t+2)%3, last read by the round kernel
-        // of round t (and the pull kernel before it).
-        GS_HIP(hipStreamWaitEvent(e->cstream, e->ev_kr[R0 % 3], 0));
-        st = launch_plan(e, R0 + 2);
-        if (st != GS_OK) return st;
+        // Exchange A of round t+1 (next on the engine stream) carries the ids
+        // of the plan of round t+2, launched by gs_shard_pull (or, for round
+        // 2, here); the in-lists of round t+1 are built by then.
+        if (R0 == 0) {
+            st = launch_plan(e, 2);
+            if (st != GS_OK) return st;
+        }
+        GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[(R0 + 2) % 3], 0));
     } else {
         // Lists of the new round t+1 into the other set, whose last reader
         // was the round kernel before this one; runs beside this round's kernel.

@@ -13,7 +13,7 @@ struct RoundArgs {
     const uint32_t *IN2;      // shard engine: per node e2 (third pusher's receive row)
     const uint32_t *src;      // round t in-list tails (shard engine: receive rows)
     const uint32_t *tg;       // round t target words (target_word: target + flags)
-    const uint32_t *tg_next;  // shard engine, faults: round t+1 target words
+    const uint32_t *tg_next;  // shard engine: round t+1 target words of the owned nodes
     uint32_t serial;          // build serial of the round-t lists (SIB validity)
     uint32_t *st32;           // [n][4] u32 Statistics deltas (empty_pull, empty_push,
                               //   full_sent, full_received)
@@ -31,11 +31,11 @@ struct RoundArgs {
     uint16_t *obs_rec;        // [n][R]
     uint32_t *obs_psize;      // [n]
     // shard engine only (null otherwise): exchange rows, see gs_shard.hip
-    const u64 *recvA;         // round-t push rows of this shard's pushers [e][2][W]
-    const u64 *recvB;         // round-t pull rows for this shard's nodes [pos][2][W]
-    u64 *sendA;               // round-(t+1) push rows of this shard's nodes [pos][2][W]
-    const uint32_t *spos_cur; // row of x in recvB (= its round-t push row position)
-    const uint32_t *spos_next;// row of x in sendA for round t+1
+    const u64 *recvA;         // round-t push rows of this shard's pushers [slot][2][W]
+    const u64 *recvB;         // round-t pull rows for this shard's nodes [slot][2][W]
+    u64 *sendA;               // round-(t+1) push rows of this shard's nodes [slot][2][W]
+    const uint32_t *spos_cur; // slot of x in recvB (exchange B of round t)
+    const uint32_t *spos_next;// slot of x in sendA (exchange A of round t+1)
     // harness-injected faults (gs_common.h); pend/offc exist iff f.churn != 0
     Faults f;
     u64 *pend;                // [n][2][W]: votes (bump, anyC) of nodes frozen offline
@@ -125,35 +125,47 @@ hipError_t launch_seq_pull_pass(const SeqArgs &a, uint32_t level, uint32_t start
 
 // ---------------------------------------------------------------- shards
 // One rank's slice of a network sharded over G ranks (gs_shard.hip).
+constexpr uint32_t kMaxShards = 64;
 struct ShardPlan {
     uint32_t n;         // global nodes
     uint32_t G, g;      // ranks, this rank
     uint32_t chunk;     // nodes per rank (multiple of 256)
     uint32_t lo, m;     // owned range [lo, lo+m)
-    uint32_t nblk;      // 256-source plan blocks over all n
-    uint32_t blk_lo;    // first owned plan block
-    uint32_t nblk_own;  // owned plan blocks
-    uint32_t cap_in;    // capacity of the receive rows (sources targeting g)
-    CsrPlan edges;      // counting sort of the received edges over the m targets
+    uint32_t nblk_own;  // 256-source plan blocks over the owned range
+    uint32_t W;         // words per plane of a row (rows are 2W words)
+    uint32_t cap;       // row slots per (source rank, destination rank) block
+    uint32_t capA;      // row slots per exchange-A block: cap rows + cap u32 ids
+    CsrPlan edges;      // counting sort of the G*capA receive slots over the m targets
 };
-// u32-word offsets of one plan's buffers inside a single allocation.
+// u32-word offsets inside one plan set (round r: targets and send slots of
+// the owned sources) and one in-list set (round r: receive-slot in-lists).
 struct ShardPlanLayout {
-    size_t tg_all, bc_me, bc_d, cnt, E_id, E_key, SPOS, M, tot, base, EP, IN, IN2, pairs;
+    size_t tg, SPOSA, SPOSB, bc_d, cnt;
 };
-ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g);
+struct ShardEdgeLayout {
+    size_t E_id, E_key, M, tot, base, EP, IN, IN2, pairs;
+};
+ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W);
 size_t shard_plan_words(const ShardPlan &P, ShardPlanLayout *L);
-// Plan of `round`: cnt = {m_in, overflow, scnt[G], rcnt[G]}, SPOS, IN, EP.
-hipError_t launch_shard_plan(const ShardPlan &P, const ShardPlanLayout &L, uint32_t *words,
+size_t shard_edge_words(const ShardPlan &P, ShardEdgeLayout *L);
+// Plan of `round`: owned targets, send slots, and the ids of every block of
+// the exchange-A buffer bufA (which carries them one round ahead).
+hipError_t launch_shard_plan(const ShardPlan &P, const ShardPlanLayout &L, uint32_t *words, u64 *bufA,
                              uint64_t seed, uint32_t epoch, uint32_t round, const Faults &f,
-                             hipStream_t s);
+                             uint32_t *flags, hipStream_t s);
+// In-lists of `round` from the ids received in recvA; tg = the plan's owned targets.
+hipError_t launch_shard_edges(const ShardPlan &P, const ShardEdgeLayout &L, uint32_t *words,
+                              const u64 *recvA, const uint32_t *tg, uint64_t seed, uint32_t epoch,
+                              uint32_t round, const Faults &f, uint32_t *flags, hipStream_t s);
 
 struct PullArgs {
     const u64 *S;          // round-t planes of the owned nodes
-    const uint4 *IN;       // round-t in-lists of receive rows
+    const uint4 *IN;       // round-t in-lists of receive slots
     const uint32_t *IN2;   // their third pushers
     const uint32_t *EP;
-    const u64 *recvA;      // round-t push rows received [e][2][W]
-    u64 *sendB;            // pull rows out [e][2][W]
+    const u64 *recvA;      // round-t push rows received (slots of 2W words)
+    u64 *sendB;            // pull rows out (exchange-B slots)
+    uint32_t cap, capA;    // slot e of A (block e / capA) is slot e - (e / capA)(capA - cap) of B
     Geometry g;            // local geometry (n = m)
 };
 hipError_t launch_pull(const PullArgs &a, hipStream_t s);

@@ -233,8 +233,8 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                 q[0] = L.load_push_row(a.recvA, in.z);
                 q[1] = L.load_push_row(a.recvA, in.w);
                 q[2] = L.load_push_row(a.recvA, a.IN2[x]);
-                if (!(tgw & kTgNoPull)) {
-                    const uint32_t sp = a.spos_cur[x];  // the pull row z returned to x
+                const uint32_t sp = a.spos_cur[x];  // the slot of x's pull row (z's answer)
+                if (!(tgw & kTgNoPull) && sp != 0xFFFFFFFFu) {  // no slot: capacity overflow (flagged)
                     qz.c = a.recvB[L.row_index(sp, 2, 0)];
                     qz.a0 = a.recvB[L.row_index(sp, 2, 1)];
                     qz.a1 = 0;
@@ -661,8 +661,9 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         // config 4 (nontemporal plane loads measured slower: 3.27 ms)
         for (uint32_t i = threadIdx.x; i < blk_v4; i += blockDim.x) nt_store4(src4[i], &dst4[i]);
     }
-    if (SHARD && valid && !(faults_on(a.f) && (a.tg_next[x] & kTgDead))) {
+    if (SHARD && valid && a.spos_next[x] != 0xFFFFFFFFu) {
         // push row of round t+1: the push batch's class code, to owner(t_{t+1}(x))
+        // (no slot: an undelivered edge, or a capacity overflow, flagged)
         const uint32_t sp = a.spos_next[x];
         const u64 vC = N[0] & ~(N[1] & N[2]), vB = ~N[0] & (N[1] | N[2]);
         a.sendA[L.row_index(sp, 2, 0)] = ((vB & N[1] & ~N[2]) | vC) & L.m;  // code bit 0

@@ -1,9 +1,13 @@
 """Sharded network: the node-id space split across ranks.
 
 Each rank's engine (``gs_shard_create``) owns a contiguous node range.  Every
-round moves two sets of rows between ranks:
+round moves two sets of rows between ranks, each as ONE fixed-size all-to-all
+(equal splits: the engine sizes every block for the binomial row counts, so
+no count is read back and a round runs without a host synchronisation):
 
-* A -- push rows: the class planes of each node go to the owner of its target;
+* A -- push rows: the class code of each node's push batch goes to the owner
+  of its target, plus the source ids of next round's edges (the receiver
+  builds next round's in-lists from them on its side stream);
 * B -- pull rows: the owner of each target returns, per pusher, the pull batch
   ``Gossip::receive`` built (``src/gossip.rs:124-151``), in the reverse layout.
 
@@ -46,33 +50,27 @@ class _Shard:
         h = _P()
         _check(lib.gs_shard_create(ctypes.byref(cfg), rank, world, ctypes.byref(h)))
         self.h = h
-        info = (ctypes.c_uint32 * 8)()
+        info = (ctypes.c_uint32 * 12)()
         _check(lib.gs_shard_info(h, info))
-        self.lo, self.m, self.cap, self.wa, self.wb, self.world, self.rank, self.chunk = list(info)
+        (self.lo, self.m, self.cap, self.capA, self.wa, self.world, self.rank, self.chunk,
+         self.blockA, self.blockB) = list(info)[:10]
         dev = torch.device("cuda", device)
         i64 = torch.int64
-        self.sendA = torch.zeros(max(1, self.m) * self.wa, dtype=i64, device=dev)
-        self.recvA = torch.zeros(max(1, self.cap) * self.wa, dtype=i64, device=dev)
-        self.sendB = torch.zeros(max(1, self.cap) * self.wb, dtype=i64, device=dev)
-        self.recvB = torch.zeros(max(1, self.m) * self.wb, dtype=i64, device=dev)
-        _check(lib.gs_shard_bind(h, self.sendA.data_ptr(), self.recvA.data_ptr(),
+        G = self.world
+        # exchange A: two buffer sets (round parity); B: one
+        self.sendA = [torch.zeros(G * self.blockA, dtype=i64, device=dev) for _ in range(2)]
+        self.recvA = [torch.zeros(G * self.blockA, dtype=i64, device=dev) for _ in range(2)]
+        self.sendB = torch.zeros(G * self.blockB, dtype=i64, device=dev)
+        self.recvB = torch.zeros(G * self.blockB, dtype=i64, device=dev)
+        _check(lib.gs_shard_bind(h, self.sendA[0].data_ptr(), self.sendA[1].data_ptr(),
+                                 self.recvA[0].data_ptr(), self.recvA[1].data_ptr(),
                                  self.sendB.data_ptr(), self.recvB.data_ptr()))
         self.stream = torch.cuda.ExternalStream(lib.gs_stream(h), device=dev)
-
-    def counts(self):
-        s = (ctypes.c_uint32 * self.world)()
-        r = (ctypes.c_uint32 * self.world)()
-        _check(self.lib.gs_shard_counts(self.h, s, r))
-        return list(s), list(r)
 
     def close(self):
         if self.h:
             self.lib.gs_destroy(self.h)
             self.h = None
-
-
-def _displ(c):
-    return [0] + list(np.cumsum(c)[:-1]) if len(c) else []
 
 
 class ShardedNetwork:
@@ -159,69 +157,57 @@ class ShardedNetwork:
             _check(self.lib.gs_sync(s.h))
 
     def _deliver(self):
-        """Exchange A, pull rows, exchange B for the current round."""
+        """Exchange A (and A(0)'s ids in round 1), pull rows, exchange B of the
+        current round, all ordered on the engine stream(s)."""
         if self._delivered or self.round == 0:
             return
-        counts = [s.counts() for s in self.shards]
+        t = self.round
+        sets = [0, 1] if t == 1 else [t % 2]
         if self.transport == "local":
             self._sync_all()
-            self._local_exchange(counts, "A")
-            self._sync_all()
+            for k in sets:
+                self._local_exchange("A", k)
             for s in self.shards:
                 _check(self.lib.gs_shard_pull(s.h))
             self._sync_all()
-            self._local_exchange(counts, "B")
-            self._sync_all()
+            self._local_exchange("B")
         else:
             s = self.shards[0]
-            scnt, rcnt = counts[0]
-            self._dist_exchange(s, s.sendA, s.recvA, scnt, rcnt, s.wa)
+            for k in sets:
+                self._dist_exchange(s, s.sendA[k], s.recvA[k])
             _check(self.lib.gs_shard_pull(s.h))
-            self._dist_exchange(s, s.sendB, s.recvB, rcnt, scnt, s.wb)
+            self._dist_exchange(s, s.sendB, s.recvB)
         self._delivered = True
 
-    def _local_exchange(self, counts, which):
-        torch = self.torch
+    def _local_exchange(self, which, k=0):
+        """Block d of every shard's send buffer -> block (its rank) of shard d's
+        receive buffer (device copies; the shards share this GPU)."""
         G = self.world
         for d in range(G):
             dst = self.shards[d]
-            rcnt_d = counts[d][1]
-            rdis_d = _displ(rcnt_d)
-            for src_rank in range(G):
-                s = self.shards[src_rank]
-                scnt_s = counts[src_rank][0]
-                sdis_s = _displ(scnt_s)
-                rows = scnt_s[d]
-                assert rows == rcnt_d[src_rank], "send/recv counts disagree"
-                if rows == 0:
-                    continue
-                if which == "A":      # s.sendA[sdis_s[d]] -> dst.recvA[rdis_d[src]]
-                    w = s.wa
-                    dst.recvA[rdis_d[src_rank] * w:(rdis_d[src_rank] + rows) * w].copy_(
-                        s.sendA[sdis_s[d] * w:(sdis_s[d] + rows) * w])
-                else:                 # dst.sendB[rdis_d[src]] -> s.recvB[sdis_s[d]]
-                    w = s.wb
-                    s.recvB[sdis_s[d] * w:(sdis_s[d] + rows) * w].copy_(
-                        dst.sendB[rdis_d[src_rank] * w:(rdis_d[src_rank] + rows) * w])
-        torch.cuda.synchronize(self.device)
+            for r in range(G):
+                src = self.shards[r]
+                if which == "A":
+                    w = src.blockA
+                    dst.recvA[k][r * w:(r + 1) * w].copy_(src.sendA[k][d * w:(d + 1) * w])
+                else:
+                    w = src.blockB
+                    dst.recvB[r * w:(r + 1) * w].copy_(src.sendB[d * w:(d + 1) * w])
+        self.torch.cuda.synchronize(self.device)
 
-    def _dist_exchange(self, s, send, recv, scnt, rcnt, w):
+    def _dist_exchange(self, s, send, recv):
+        """One equal-split all_to_all on the engine stream (RCCL), or staged
+        through host memory (gloo)."""
         torch, dist = self.torch, self.dist
-        ss = [int(c) * w for c in scnt]
-        rs = [int(c) * w for c in rcnt]
-        out = recv[:sum(rs)]
-        inp = send[:sum(ss)]
         if self.host_staged:
             _check(self.lib.gs_sync(s.h))
-            hout = torch.empty(sum(rs), dtype=torch.int64)
-            dist.all_to_all_single(hout, inp.cpu(), output_split_sizes=rs, input_split_sizes=ss,
-                                   group=self.group)
-            out.copy_(hout.to(out.device))
+            hout = torch.empty(recv.numel(), dtype=torch.int64)
+            dist.all_to_all_single(hout, send.cpu(), group=self.group)
+            recv.copy_(hout.to(recv.device))
             torch.cuda.synchronize(self.device)
         else:
             with torch.cuda.stream(s.stream):
-                dist.all_to_all_single(out, inp, output_split_sizes=rs, input_split_sizes=ss,
-                                       group=self.group)
+                dist.all_to_all_single(recv, send, group=self.group)
 
     def next_round(self, report: bool = True) -> Optional[RoundReport]:
         self._deliver()

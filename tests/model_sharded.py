@@ -2,13 +2,17 @@
 
 Each rank owns the node range [lo, lo+m) (shard_plan in gs_shard.hip: chunk =
 ceil(n/G) rounded up to 256 nodes) and runs, per round, the same two row
-exchanges as the engine over a caller-supplied all-to-all
-``a2a(rows_per_dest, width, recv_counts) -> rows_per_source``:
+exchanges as the engine over a caller-supplied all-to-all of FIXED-SIZE
+blocks ``a2a(blocks_per_dest, width) -> blocks_per_source`` (every block holds
+``cap`` rows, the engine's capacity; empty slots carry id -1), so no row count
+is exchanged or derived from other ranks' schedules:
 
   A  every owned node x whose push batch is delivered sends (x, isC, a0, a1)
      to owner(t(x)), rows per destination in ascending x, so each rank
      receives its pushers' rows in ascending source order (rank order = node
-     order);
+     order); the receiver recomputes each received source's target from the
+     Philox stream (the engine's edge_keys) -- a rank computes the targets of
+     its own sources only;
   B  the owner of z answers each received row, in the same order, with the pull
      batch z returned to that pusher (Model.pull_row: z's live set plus the
      entries z created from earlier pushers, as a 2-plane class code); a
@@ -30,12 +34,24 @@ def shard_range(n, G, g):
     return lo, min(lo + chunk, n) - lo, chunk
 
 
+def shard_cap(n, G, W=1):
+    """Row slots per (source rank, destination rank) block (shard_plan)."""
+    import math
+    chunk = shard_range(n, G, 0)[2]
+    mean = chunk * chunk / max(1.0, n - 1.0)
+    cap = min(float(chunk), mean + 16.0 * math.sqrt(mean + 1.0) + 64.0)
+    q = max(64, 4 * W)
+    return -(-math.ceil(cap) // q) * q
+
+
 class ShardModel(Model):
     def __init__(self, n, R, seed, epoch, params, peer_fn, rank, world, a2a, fault_fn=None):
         super().__init__(n, R, seed, epoch, params, peer_fn, fault_fn)
         assert R <= 62
         self.rank, self.world, self.a2a = rank, world, a2a
         self.lo, self.m, self.chunk = shard_range(n, world, rank)
+        self.cap = shard_cap(n, world)
+        self.tg, self.fl = {}, {}
         self.P = {x: [0] * 8 for x in self.owned()}
         self.stats = {x: [0] * 5 for x in self.owned()}
         self.exchanged = False
@@ -50,33 +66,36 @@ class ShardModel(Model):
         """Exchanges A and B of the current round (needs self.tg of round t)."""
         if self.exchanged or not self.deliver_pending:
             return
-        G = self.world
+        G, cap = self.world, self.cap
         sendA = [[] for _ in range(G)]
         for x in self.owned():
             if not self.fl[x] & DEAD:
                 sendA[self.owner(self.tg[x])].append([x] + list(self.cls(x)))
-        # receive counts from the local plan (every rank knows all targets)
-        rcA = [0] * G
-        for x in range(self.n):
-            if not self.fl[x] & DEAD and self.owner(self.tg[x]) == self.rank:
-                rcA[self.owner(x)] += 1
-        recvA = self.a2a(sendA, 4, rcA)
-        rows = [r for part in recvA for r in part]
+        for part in sendA:
+            assert len(part) <= cap, "block capacity exceeded (the engine flags a device limit)"
+            part.extend([[-1, 0, 0, 0]] * (cap - len(part)))
+        recvA = self.a2a(sendA, 4)
+        rows = [r for part in recvA for r in part if r[0] >= 0]
         srcs = [r[0] for r in rows]
         assert srcs == sorted(srcs), "receive rows must be in ascending source order"
+        # the receiver's own view of each source's target (Philox, edge_keys)
+        rnd = self.round
+        tgt = {s: self.peer_fn(self.seed, self.epoch, rnd, s, self.n) for s in srcs}
         ins = {z: [] for z in self.owned()}
         for s, qc, q0, q1 in rows:
-            ins[self.tg[s]].append((s, (qc, q0, q1)))
+            assert self.lo <= tgt[s] < self.lo + self.m, "row sent to a rank that does not own its target"
+            ins[tgt[s]].append((s, (qc, q0, q1)))
         sendB = []
         for part in recvA:
-            sendB.append([[r[0]] + list(self.pull_row(self.tg[r[0]], r[0], ins[self.tg[r[0]]]))
-                          for r in part])
-        recvB = self.a2a(sendB, 3, [len(p) for p in sendA])
+            sendB.append([[r[0]] + list(self.pull_row(tgt[r[0]], r[0], ins[tgt[r[0]]]))
+                          if r[0] >= 0 else [-1, 0, 0] for r in part])
+        recvB = self.a2a(sendB, 3)
         pull = {}
         for d in range(G):
             assert [r[0] for r in recvB[d]] == [r[0] for r in sendA[d]], "B order = A order"
             for x, b0, b1 in recvB[d]:
-                pull[x] = (b0, b1)
+                if x >= 0:
+                    pull[x] = (b0, b1)
         self.ins, self.pull = ins, pull
         self.exchanged = True
 
@@ -112,13 +131,28 @@ class ShardModel(Model):
             live_any |= live > 0
         self.P = newP
         self.round = rnd
-        # every rank derives the whole round-(t+1) peer schedule and its
-        # delivery flags (Philox): the plan's counts and send positions need
-        # the targets of all n sources
+        # the plan of round t+1: targets and delivery flags of the OWNED
+        # sources only (the engine's plan_count)
         self.plan_round(rnd)
         self.deliver_pending = True
         self.exchanged = False
         return live_any
+
+    def plan_round(self, rnd):
+        self.tg, self.fl = {}, {}
+        for x in self.owned():
+            t = self.peer_fn(self.seed, self.epoch, rnd, x, self.n)
+            self.tg[x] = t
+            f = 0
+            if self.fault_fn:
+                fb = self.fault_fn(rnd, x)
+                if fb & 1:
+                    f = OFF | DEAD | NOPULL
+                elif fb & 2 or self.fault_fn(rnd, t) & 1:
+                    f = DEAD | NOPULL
+                elif fb & 4:
+                    f = NOPULL
+            self.fl[x] = f
 
     def observe_local(self):
         """(codes, records, psize, stats, known) rows of the owned nodes."""

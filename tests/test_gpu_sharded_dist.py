@@ -2,7 +2,9 @@
 the box's one GPU, each one rank of a network sharded over 2 ranks; every rank
 checks the all-gathered state against the oracle each round (bit-exact).  The
 RCCL transport differs only in where the all_to_all_single runs (on the
-engine's stream); it needs one GPU per rank and runs in bench.py --gpus N.
+engine's stream, no host synchronisation); RCCL refuses two ranks on one GPU,
+so here it runs as a single rank (the exchanges are then the collective's
+self-copies through RCCL) and across GPUs in bench.py --gpus N.
 """
 import os
 import socket
@@ -20,12 +22,15 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, cases, q):
+def _worker(rank, world, port, cases, q, backend="gloo"):
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
     import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         import safe_gossip_amd as sg
         from safe_gossip_amd.sharded import ShardedNetwork
@@ -63,3 +68,21 @@ def test_sharded_dist_gloo_two_ranks(engine):
     while not q.empty():
         msgs.append(q.get())
     assert len(msgs) == world and all(m[0] == "ok" for m in msgs), msgs
+
+
+def test_sharded_dist_rccl_single_rank(engine):
+    # the RCCL transport end to end: equal-split all_to_all_single of the
+    # exchange buffers on the engine's stream, no host synchronisation per round
+    import torch.multiprocessing as mp
+    cases = [(600, 48, "origins"), (700, 256, "reinject"), (1000, 3, "trickle")]
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    p = ctx.Process(target=_worker, args=(0, 1, _free_port(), cases, q, "nccl"))
+    p.start()
+    p.join(timeout=200)
+    if p.is_alive():
+        p.kill()
+    msgs = []
+    while not q.empty():
+        msgs.append(q.get())
+    assert msgs == [("ok", 0)], msgs

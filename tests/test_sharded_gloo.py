@@ -2,8 +2,8 @@
 
 Each process is one rank of tests/model_sharded.py: it owns a node range, moves
 push rows to the owners of their targets and pull rows back with
-all_to_all_single (receive counts derived locally from the Philox schedule,
-as the engine's plan does), ORs any-live with all_reduce, and rank 0 checks the
+equal-split all_to_all_single of fixed-size blocks (as the engine does: no
+row counts are exchanged, each rank computes only its own sources' targets), ORs any-live with all_reduce, and rank 0 checks the
 gathered per-node state, records, |P|, Statistics and known sets against the
 reference-faithful oracle every round (bit-exact).
 """
@@ -27,20 +27,18 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _a2a(send, width, recv_counts):
+def _a2a(send, width):
+    """Equal-split all-to-all of fixed-size blocks (the engine's exchanges)."""
     G = len(send)
+    cap = len(send[0])
+    assert all(len(p) == cap for p in send)
     flat = [v for part in send for row in part for v in row]
     inp = torch.tensor(flat, dtype=torch.int64) if flat else torch.zeros(0, dtype=torch.int64)
-    out = torch.empty(sum(recv_counts) * width, dtype=torch.int64)
-    dist.all_to_all_single(out, inp, output_split_sizes=[c * width for c in recv_counts],
-                           input_split_sizes=[len(p) * width for p in send])
+    out = torch.empty(G * cap * width, dtype=torch.int64)
+    dist.all_to_all_single(out, inp)
     vals = out.tolist()
-    res, o = [], 0
-    for s in range(G):
-        c = recv_counts[s]
-        res.append([vals[o + i * width:o + (i + 1) * width] for i in range(c)])
-        o += c * width
-    return res
+    return [[vals[(s * cap + i) * width:(s * cap + i + 1) * width] for i in range(cap)]
+            for s in range(G)]
 
 
 def _worker(rank, world, port, n, R, params, kind, q, faults=None):
