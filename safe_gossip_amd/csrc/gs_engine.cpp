@@ -42,8 +42,11 @@ struct gs_engine {
         uint32_t *src = nullptr, *tg = nullptr, *scratch = nullptr, *region = nullptr;
         gs::InRec *IN8 = nullptr;
         gs::SibRec *SIB8 = nullptr;
+        gs::DlvRec *DR = nullptr;  // DLV path: delivery records (src holds {id, code} tails)
         uint32_t serial = 0;
     } csr[2];
+    bool dlv = false;  // delivery-record path (2P, R_pad <= 16, binned in-lists)
+    uint32_t *pc = nullptr;  // DLV: push codes of the current round [n]
     hipStream_t cstream = nullptr;
     hipEvent_t ev_built[2] = {nullptr, nullptr};  // set i complete
     hipEvent_t ev_read[2] = {nullptr, nullptr};   // last reader of set i done
@@ -130,7 +133,7 @@ void release(gs_engine *e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->cstream) (void)hipStreamSynchronize(e->cstream);
     for (auto &c : e->csr) {
-        void *cb[] = {c.src, c.tg, c.scratch, c.region, c.IN8, c.SIB8};
+        void *cb[] = {c.src, c.tg, c.scratch, c.region, c.IN8, c.SIB8, c.DR};
         for (void *b : cb)
             if (b) (void)hipFree(b);
     }
@@ -148,7 +151,7 @@ void release(gs_engine *e) {
     }
     if (e->ev_main) (void)hipEventDestroy(e->ev_main);
     if (e->cstream) (void)hipStreamDestroy(e->cstream);
-    void *bufs[] = {e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
+    void *bufs[] = {e->pc, e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
                     e->partials, e->obs_state, e->obs_rec, e->obs_psize, e->obs_pend};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -214,6 +217,9 @@ gs::RoundArgs base_args(gs_engine *e) {
         const auto &cs = e->csr[e->round & 1u];  // round-t lists (t = e->round)
         a.IN8 = cs.IN8;
         a.SIB8 = cs.SIB8;
+        a.DR = cs.DR;
+        a.dtail = e->dlv ? reinterpret_cast<const uint2 *>(cs.src) : nullptr;
+        a.pc_out = e->pc;
         a.src = cs.src;
         a.tg = cs.tg;
         a.serial = cs.serial;
@@ -509,7 +515,15 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
         g.nseg = n;
     }
     const size_t sw = (size_t)g.units * gs::kPlanes * g.W;
-    e->plan = gs::csr_plan(n);
+    {
+        // Delivery records (DLV) for small R in the 2P schedule: every
+        // class-plane gather but one is replaced by records of the in-list
+        // build.  SAFE_GOSSIP_AMD_NO_DLV=1 forces gathers.
+        const char *v = std::getenv("SAFE_GOSSIP_AMD_NO_DLV");
+        const bool off = v && *v && *v != '0';
+        e->dlv = !off && !e->seq && !e->shard && g.small && g.rpad <= 16 && gs::dlv_plan(n).binned;
+    }
+    e->plan = e->dlv ? gs::dlv_plan(n) : gs::csr_plan(n);
     {
         const char *v = std::getenv("SAFE_GOSSIP_AMD_CONCURRENT_INLISTS");
         e->concurrent_inlists = v && *v && *v != '0';
@@ -536,16 +550,21 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
         auto &c = e->csr[i];
         ok = hipEventCreateWithFlags(&e->ev_built[i], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&e->ev_read[i], hipEventDisableTiming) == hipSuccess &&
-             dalloc(&c.IN8, n) == hipSuccess && dalloc(&c.SIB8, n) == hipSuccess &&
              dalloc(&c.src, isz.src_words) == hipSuccess && dalloc(&c.tg, n) == hipSuccess &&
              dalloc(&c.region, isz.region_words) == hipSuccess &&
              dalloc(&c.scratch, isz.scratch_words) == hipSuccess &&
-             hipMemset(c.scratch, 0, std::max<size_t>(isz.scratch_words, 1) * sizeof(uint32_t)) == hipSuccess &&
-             hipMemset(c.SIB8, 0, std::max<size_t>(n, 1) * sizeof(gs::SibRec)) == hipSuccess;
+             hipMemset(c.scratch, 0, std::max<size_t>(isz.scratch_words, 1) * sizeof(uint32_t)) == hipSuccess;
+        if (ok && e->dlv) {
+            ok = dalloc(&c.DR, n) == hipSuccess;
+        } else if (ok) {
+            ok = dalloc(&c.IN8, n) == hipSuccess && dalloc(&c.SIB8, n) == hipSuccess &&
+                 hipMemset(c.SIB8, 0, std::max<size_t>(n, 1) * sizeof(gs::SibRec)) == hipSuccess;
+        }
     }
     ok = ok && dalloc(&e->S[0], sw) == hipSuccess && dalloc(&e->S[1], sw) == hipSuccess &&
          dalloc(&e->flags, 4) == hipSuccess && dalloc(&e->st32, (size_t)4 * n) == hipSuccess &&
          dalloc(&e->st64, (size_t)4 * n) == hipSuccess;
+    if (ok && e->dlv) ok = dalloc(&e->pc, n) == hipSuccess;
     if (ok && e->seq)
         ok = dalloc(&e->Wb, (size_t)n * 2 * g.W) == hipSuccess && dalloc(&e->sinfo, n) == hipSuccess &&
              dalloc(&e->seqw, (size_t)gs::seq_blocks(n) * gs::kSeqLists + gs::kSeqLists + n) == hipSuccess;
@@ -782,12 +801,14 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
         // both are HBM-bound, and the in-list kernels hold whole CUs (1024
         // threads, >100 KiB LDS), so running them beside the round kernel
         // measured slower than in sequence.
-        hipStream_t bs = e->concurrent_inlists ? e->cstream : e->stream;
+        // (DLV: the build reads the planes this round kernel writes: in sequence)
+        hipStream_t bs = (e->concurrent_inlists && !e->dlv) ? e->cstream : e->stream;
         GS_HIP(hipStreamWaitEvent(bs, e->ev_read[ns], 0));
         c.serial = ++e->build_serial & gs::kSerialMask;
         if (c.serial == 0) {  // 24-bit serial wrapped: no stale SibRec may match a new serial
             GS_HIP(hipStreamSynchronize(e->stream));
-            for (auto &cc : e->csr) GS_HIP(hipMemsetAsync(cc.SIB8, 0, (size_t)e->g.n * sizeof(gs::SibRec), bs));
+            for (auto &cc : e->csr)
+                if (cc.SIB8) GS_HIP(hipMemsetAsync(cc.SIB8, 0, (size_t)e->g.n * sizeof(gs::SibRec), bs));
             c.serial = ++e->build_serial & gs::kSerialMask;
         }
         gs::InListArgs la{};
@@ -804,6 +825,14 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
         la.epoch = e->epoch;
         la.round = e->round;
         la.f = e->faults;
+        if (e->dlv) {  // records carry the push codes of the new round's planes
+            la.dlv = 1;
+            la.S = e->S[e->cur];
+            la.PC = e->pc;
+            la.g = e->g;
+            la.DR = c.DR;
+            la.dtail = reinterpret_cast<uint2 *>(c.src);
+        }
         GS_HIP(gs::launch_build_inlists(la, bs));
         GS_HIP(hipEventRecord(e->ev_built[ns], bs));
     }
@@ -1016,6 +1045,10 @@ double gs_round_kernel_bytes(const gs_engine *e) {
     // target 4 + Statistics deltas (16 r + 16 w).
     if (!e) return 0.0;
     const double n = e->g.n, rp = e->g.rpad;
+    // DLV path: per slot 1 B planes read + 1 B written; per node its own
+    // delivery record 32 + t(x)'s record 32 + target word 4 + Statistics
+    // deltas 16 r + 16 w + the next push code 4.
+    if (e->dlv) return n * (2.0 * rp + 104.0);
     return n * (2.75 * rp + 68.0);
 }
 

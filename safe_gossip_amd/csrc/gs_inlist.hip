@@ -79,7 +79,8 @@ GS_DEV void emit_target(const InListArgs &a, uint32_t y, const uint32_t *lst, ui
 // reserves the tail words of all its targets with ONE atomic (same-address
 // atomics serialise at the memory side): tail_len per target, a block scan,
 // then emit_tail at the thread's running cursor.
-GS_DEV uint32_t tail_len(uint32_t k) { return k > kInline ? min(k, kMaxIn) - kInline : 0u; }
+template <uint32_t INL = kInline>
+GS_DEV uint32_t tail_len(uint32_t k) { return k > INL ? min(k, kMaxIn) - INL : 0u; }
 
 template <uint32_t NT>
 GS_DEV uint32_t reserve_tails(const InListArgs &a, uint32_t mine, uint32_t *tailcnt, uint32_t *lds_scan) {
@@ -100,7 +101,7 @@ GS_DEV uint32_t reserve_tails(const InListArgs &a, uint32_t mine, uint32_t *tail
 
 // Writes a target's tail at *cur (kNone: none reserved); returns its start.
 GS_DEV uint32_t emit_tail(const InListArgs &a, const uint32_t *lst, uint32_t k, uint32_t &cur) {
-    const uint32_t m = tail_len(k);
+    const uint32_t m = tail_len<>(k);
     if (m == 0 || cur == kNone) return 0u;
     const uint32_t first = cur;
     for (uint32_t j = 0; j < m; ++j) a.src[first + j] = lst[kInline + j];
@@ -113,6 +114,7 @@ GS_DEV uint32_t emit_tail(const InListArgs &a, const uint32_t *lst, uint32_t k, 
 // the bin (u16) at region_lt[b*kBinCap ...].  Each target is drawn once, here:
 // a Philox4x32-10 draw is ~40 quarter-rate multiplies, so redrawing it in
 // inl_sort would cost more than carrying 2 bytes.
+template <bool DLV>
 __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     const CsrPlan &p = a.p;
@@ -177,19 +179,37 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
     __syncthreads();
     // Consecutive stage entries of one bin go to consecutive region slots; the
     // bin of entry i is found by a binary search over the chunk-local starts.
-    for (uint32_t i = threadIdx.x; i < total; i += kInlThreads) {  // delivered edges of the chunk
-        uint32_t lo_b = 0, hi_b = p.nb;  // last bin with off[b] <= i and a non-empty run
-        while (hi_b - lo_b > 1) {
-            const uint32_t mid = (lo_b + hi_b) >> 1;
-            if (off[mid] <= i) lo_b = mid; else hi_b = mid;
+    // DLV: each entry also carries its source's push code, read from the
+    // chunk's 64 KB window of the push codes the round kernel wrote (L2
+    // resident); the loads of kBatchW entries are issued together.
+    constexpr uint32_t kBatchW = DLV ? 4u : 1u;
+    for (uint32_t i0 = threadIdx.x; i0 < total; i0 += kBatchW * kInlThreads) {  // delivered edges
+        uint32_t code[kBatchW];
+        if (DLV) {
+#pragma unroll
+            for (uint32_t j = 0; j < kBatchW; ++j) {
+                const uint32_t i = i0 + j * kInlThreads;
+                code[j] = a.PC[i < total ? stage[i] : lo];
+            }
         }
-        // (empty bins share their start with the next bin, so the last bin
-        // whose start is <= i is the one whose run holds entry i)
-        const uint32_t b = lo_b;
-        const uint32_t slot = res[b] + (i - off[b]);
-        if (slot < kBinCap) {
-            a.region[(u64)b * kBinCap + slot] = stage[i];
-            a.region_lt[(u64)b * kBinCap + slot] = stage_lt[i];
+#pragma unroll
+        for (uint32_t j = 0; j < kBatchW; ++j) {
+            const uint32_t i = i0 + j * kInlThreads;
+            if (i >= total) break;
+            uint32_t lo_b = 0, hi_b = p.nb;  // last bin with off[b] <= i and a non-empty run
+            while (hi_b - lo_b > 1) {
+                const uint32_t mid = (lo_b + hi_b) >> 1;
+                if (off[mid] <= i) lo_b = mid; else hi_b = mid;
+            }
+            // (empty bins share their start with the next bin, so the last bin
+            // whose start is <= i is the one whose run holds entry i)
+            const uint32_t b = lo_b;
+            const uint32_t slot = res[b] + (i - off[b]);
+            if (slot < kBinCap) {
+                a.region[(u64)b * kBinCap + slot] = stage[i];
+                a.region_lt[(u64)b * kBinCap + slot] = stage_lt[i];
+                if (DLV) a.region_code[(u64)b * kBinCap + slot] = code[j];
+            }
         }
     }
 }
@@ -245,6 +265,8 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
         if (el[q] != kNone) {
             const uint32_t shf = (el[q] & 1u) << 4;
             const uint32_t old = atomicAdd(&h[el[q] >> 1], 1u << shf);
+            // DLV: the entry's index in the region (its id and code are
+            // re-read from there, an L2-resident window)
             sorted[(old >> shf) & 0xFFFFu] = ex[q];
         }
     }
@@ -253,7 +275,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
     // targets so the InRec stores are coalesced
     uint32_t mine = 0;
     for (uint32_t lt = threadIdx.x; lt < nodes; lt += kInlThreads)
-        mine += tail_len(half_of(h, lt) - (lt ? half_of(h, lt - 1) : 0u));
+        mine += tail_len<>(half_of(h, lt) - (lt ? half_of(h, lt - 1) : 0u));
     uint32_t cur = reserve_tails<kInlThreads>(a, mine, &a.scratch[p.nb], lds_scan);
     for (uint32_t lt = threadIdx.x; lt < nodes; lt += kInlThreads) {
         const uint32_t e = half_of(h, lt);
@@ -270,6 +292,135 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
             lst[r] = v;
         }
         emit_target(a, t0 + lt, lst, k, emit_tail(a, lst, k, cur));
+    }
+}
+
+// DLV: the records of one HALF of a bin (kHalf targets; blockIdx.y picks the
+// half) from the bin's region: an LDS counting sort of (id, push code) pairs
+// by target, per target an insertion sort by id, then the DlvRec with the
+// target's class planes and the tails.  Halving the bin keeps ids and codes in
+// LDS (no global re-reads inside the per-target loop).
+constexpr uint32_t kHalfLog = kBinLog - 1;
+constexpr uint32_t kHalf = 1u << kHalfLog;
+constexpr uint32_t kHalfCap = kBinCap / 2;
+constexpr uint32_t kHalfPer = kHalf / kInlThreads;  // targets per thread
+
+__global__ __launch_bounds__(kInlThreads) void inl_sort_dlv(InListArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
+    const CsrPlan &p = a.p;
+    uint32_t *h = sh;                   // [kHalf/2] packed per-target counters
+    uint32_t *sid = sh + kHalf / 2;     // [kHalfCap] source ids by target
+    uint32_t *scd = sid + kHalfCap;     // [kHalfCap] their push codes
+    __shared__ uint32_t lds_scan[kInlThreads / 64];
+    const uint32_t b = blockIdx.x, hh = blockIdx.y;
+    const uint32_t cnt = min(a.scratch[b], kBinCap);
+    const uint32_t t0 = (b << kBinLog) + (hh << kHalfLog);
+    const uint32_t nodes = t0 < p.n ? min(kHalf, p.n - t0) : 0u;
+    uint32_t ex[kSortPer], ec[kSortPer], el[kSortPer];
+#pragma unroll
+    for (uint32_t q = 0; q < kSortPer; ++q) {
+        const uint32_t i = threadIdx.x + q * kInlThreads;
+        const bool ok = i < cnt;
+        const u64 ri = (u64)b * kBinCap + (ok ? i : 0u);
+        const uint32_t lt = ok ? (uint32_t)a.region_lt[ri] : kNone;
+        ex[q] = a.region[ri];
+        ec[q] = a.region_code[ri];
+        el[q] = (ok && (lt >> kHalfLog) == hh) ? (lt & (kHalf - 1u)) : kNone;
+    }
+    for (uint32_t i = threadIdx.x; i < kHalf / 2; i += kInlThreads) h[i] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < kSortPer; ++q)
+        if (el[q] != kNone) atomicAdd(&h[el[q] >> 1], 1u << ((el[q] & 1u) << 4));
+    __syncthreads();
+    const uint32_t i0 = threadIdx.x * kHalfPer;
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kHalfPer; ++q) sum += half_of(h, i0 + q);
+    uint32_t total;
+    uint32_t run = block_exclusive_scan_t<kInlThreads>(sum, lds_scan, total);
+#pragma unroll
+    for (uint32_t q = 0; q < kHalfPer; q += 2) {
+        const uint32_t c0 = half_of(h, i0 + q), c1 = half_of(h, i0 + q + 1);
+        h[(i0 + q) >> 1] = run | ((run + c0) << 16);
+        run += c0 + c1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && total > kHalfCap) atomicOr(&a.flags[2], kFlagLimit);
+#pragma unroll
+    for (uint32_t q = 0; q < kSortPer; ++q) {
+        if (el[q] != kNone) {
+            const uint32_t shf = (el[q] & 1u) << 4;
+            const uint32_t pos = (atomicAdd(&h[el[q] >> 1], 1u << shf) >> shf) & 0xFFFFu;
+            if (pos < kHalfCap) {
+                sid[pos] = ex[q];
+                scd[pos] = ec[q];
+            }
+        }
+    }
+    __syncthreads();
+    // the targets' own target words and class planes, loads issued together
+    uint32_t tgv[kHalfPer];
+    u64 w0[kHalfPer], w1[kHalfPer], w2[kHalfPer];
+#pragma unroll
+    for (uint32_t q = 0; q < kHalfPer; ++q) {
+        const uint32_t lt = threadIdx.x + q * kInlThreads;
+        const uint32_t y = t0 + (lt < nodes ? lt : 0u);
+        const u64 rb = (u64)(y >> a.g.lognpu) * kPlanes;
+        tgv[q] = a.tg[y];
+        w0[q] = a.S[rb];
+        w1[q] = a.S[rb + 1];
+        w2[q] = a.S[rb + 2];
+    }
+    uint32_t mine = 0;
+    for (uint32_t lt = threadIdx.x; lt < nodes; lt += kInlThreads)
+        mine += tail_len<kDlvInline>(min(half_of(h, lt), kHalfCap) - (lt ? min(half_of(h, lt - 1), kHalfCap) : 0u));
+    uint32_t cur = reserve_tails<kInlThreads>(a, mine, &a.scratch[p.nb], lds_scan);
+    const u64 m = (1ull << a.g.rpad) - 1ull;
+#pragma unroll
+    for (uint32_t q = 0; q < kHalfPer; ++q) {
+        const uint32_t lt = threadIdx.x + q * kInlThreads;
+        if (lt >= nodes) break;
+        const uint32_t e = min(half_of(h, lt), kHalfCap);
+        const uint32_t s = lt ? min(half_of(h, lt - 1), kHalfCap) : 0u;
+        uint32_t k = e - s;
+        for (uint32_t j = s + 1; j < e; ++j) {  // insertion sort of (id, code) by id
+            const uint32_t v = sid[j], vc = scd[j];
+            uint32_t r = j;
+            while (r > s && sid[r - 1] > v) {
+                sid[r] = sid[r - 1];
+                scd[r] = scd[r - 1];
+                --r;
+            }
+            sid[r] = v;
+            scd[r] = vc;
+        }
+        if (k > kMaxIn) {
+            atomicOr(&a.flags[2], kFlagLimit);
+            k = kMaxIn;
+        }
+        const uint32_t tz = tgv[q] & kTgMask;  // t(y): did it push to y?
+        const uint32_t mt = tail_len<kDlvInline>(k);
+        const uint32_t first = (mt && cur != kNone) ? cur : 0u;
+        uint32_t zi = kDlvNoZ;
+        for (uint32_t j = 0; j < k; ++j) {
+            if (sid[s + j] == tz) zi = j;
+            if (j >= kDlvInline && cur != kNone) a.dtail[first + j - kDlvInline] = make_uint2(sid[s + j], scd[s + j]);
+        }
+        if (mt && cur != kNone) cur += mt;
+        const uint32_t ysh = ((t0 + lt) & ((1u << a.g.lognpu) - 1u)) << a.g.logr;
+        const uint32_t c = (uint32_t)((w0[q] >> ysh) & m), a0 = (uint32_t)((w1[q] >> ysh) & m),
+                       a1 = (uint32_t)((w2[q] >> ysh) & m);
+        DlvRec r;
+        r.meta = k | (zi << 5);
+        r.cls01 = c | (a0 << 16);
+        r.cls2 = a1;
+        r.pad = first;
+        r.s[0] = k > 0 ? sid[s] : 0u;
+        r.c[0] = k > 0 ? scd[s] : 0u;
+        r.s[1] = k > 1 ? sid[s + 1] : 0u;
+        r.c[1] = k > 1 ? scd[s + 1] : 0u;
+        a.DR[t0 + lt] = r;
     }
 }
 
@@ -387,7 +538,7 @@ __global__ __launch_bounds__(256) void csr_bin_sort(InListArgs a) {
     }
     __syncthreads();
     uint32_t mine = 0;
-    for (uint32_t i = threadIdx.x; i < nodes; i += blockDim.x) mine += tail_len(h[i] - (i ? h[i - 1] : 0u));
+    for (uint32_t i = threadIdx.x; i < nodes; i += blockDim.x) mine += tail_len<>(h[i] - (i ? h[i - 1] : 0u));
     uint32_t cur = reserve_tails<256>(a, mine, tailcnt, lds_scan);
     for (uint32_t i = threadIdx.x; i < nodes; i += blockDim.x) {
         const uint32_t s = start + (i ? h[i - 1] : 0u), e = start + h[i];
@@ -413,6 +564,23 @@ bool getenv_generic_inlists() {
 }
 
 }  // namespace
+
+CsrPlan dlv_plan(uint32_t n) {
+    CsrPlan p{};
+    p.n = n;
+    const uint32_t nb_binned = (uint32_t)(((u64)n + kBin - 1) / kBin);
+    if (nb_binned > kBinnedMaxBins || getenv_generic_inlists()) return p;  // binned == 0: no DLV path
+    p.binned = 1;
+    p.dlv = 1;
+    p.bin = kBin;
+    p.logbin = kBinLog;
+    p.nb = nb_binned;
+    p.ba = (uint32_t)(((u64)n + kChunk - 1) / kChunk);
+    p.chunk = kChunk;
+    // pushers beyond kDlvInline: E[max(k - 2, 0)] = 3/e - 1 = 10.4 % of n
+    p.tailcap = n / 8u + 4096u;
+    return p;
+}
 
 CsrPlan csr_plan(uint32_t n) {
     CsrPlan p{};
@@ -444,8 +612,9 @@ CsrPlan csr_plan(uint32_t n) {
 InListSizes inlist_sizes(const CsrPlan &p) {
     InListSizes z{};
     if (p.binned) {
-        z.src_words = p.tailcap;
-        z.region_words = (size_t)p.nb * kBinCap * 3 / 2;  // sources (u32) + local targets (u16)
+        z.src_words = p.dlv ? 2 * (size_t)p.tailcap : p.tailcap;  // DLV: {id, code} pairs
+        // sources (u32) + local targets (u16) [+ push codes (u32)]
+        z.region_words = (size_t)p.nb * kBinCap * (p.dlv ? 5 : 3) / 2;
         z.scratch_words = (size_t)p.nb + 1;  // fill[nb], tailcnt
     } else {
         z.src_words = p.tailcap;
@@ -462,16 +631,27 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
         const size_t lds_bin = ((size_t)kChunk + kChunk / 2 + (p.nb + 1) / 2) * sizeof(uint32_t) +
                                (size_t)2 * p.nb * sizeof(uint16_t);
         const size_t lds_sort = ((size_t)kBin / 2 + kBinCap) * sizeof(uint32_t);
-        hipError_t e = hipFuncSetAttribute((const void *)inl_bin, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)lds_bin);
+        const size_t lds_dlv = ((size_t)kHalf / 2 + 2 * (size_t)kHalfCap) * sizeof(uint32_t);
+        const void *kb = p.dlv ? (const void *)inl_bin<true> : (const void *)inl_bin<false>;
+        const void *ks = p.dlv ? (const void *)inl_sort_dlv : (const void *)inl_sort;
+        hipError_t e = hipFuncSetAttribute(kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bin);
         if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void *)inl_sort, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds_sort);
+            e = hipFuncSetAttribute(ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(p.dlv ? lds_dlv : lds_sort));
         if (e != hipSuccess) return e;
         InListArgs ab = a;
         ab.region_lt = reinterpret_cast<uint16_t *>(a.region + (size_t)p.nb * kBinCap);
-        hipLaunchKernelGGL(inl_bin, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
-        hipLaunchKernelGGL(inl_sort, dim3(p.nb), dim3(kInlThreads), lds_sort, s, ab);
+        ab.region_code = a.region + (size_t)p.nb * kBinCap * 3 / 2;
+        if (p.dlv) {
+            // the two half-bin blocks of a bin both read its fill count, so it
+            // is cleared here rather than by the sort
+            e = hipMemsetAsync(a.scratch, 0, (size_t)p.nb * sizeof(uint32_t), s);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(inl_bin<true>, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
+            hipLaunchKernelGGL(inl_sort_dlv, dim3(p.nb, 2), dim3(kInlThreads), lds_dlv, s, ab);
+        } else {
+            hipLaunchKernelGGL(inl_bin<false>, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
+            hipLaunchKernelGGL(inl_sort, dim3(p.nb), dim3(kInlThreads), lds_sort, s, ab);
+        }
         return hipGetLastError();
     }
     const size_t lds_nb = (size_t)p.nb * sizeof(uint32_t);

@@ -9,6 +9,9 @@ struct RoundArgs {
     u64 *Snext;               // state planes, round t+1 (post phase 0)
     const InRec *IN8;         // round t, per node y: in-list record (gs_common.h)
     const SibRec *SIB8;       // round t, per source x: pushers of t(x) ahead of x
+    const DlvRec *DR;         // round t delivery records (DLV path; IN8/SIB8 unused)
+    const uint2 *dtail;       //   their pushers >= kDlvInline: {id, push code}
+    uint32_t *pc_out;         // DLV: push code of every node's round-(t+1) push batch
     const uint4 *IN;          // shard engine: per node {first edge, k | zi<<16, e0, e1}
     const uint32_t *IN2;      // shard engine: per node e2 (third pusher's receive row)
     const uint32_t *src;      // round t in-list tails (shard engine: receive rows)
@@ -67,8 +70,12 @@ struct CsrPlan {
     uint32_t ba;      // source chunks
     uint32_t chunk;   // sources per chunk
     uint32_t tailcap; // binned: capacity of the in-degree > kInline tail list
+    uint32_t dlv;     // delivery records (DlvRec) instead of InRec / SibRec
 };
 CsrPlan csr_plan(uint32_t n);
+// The plan of the DLV path (binned only; tails sized for kDlvInline), or one
+// with binned == 0 when n is too large for it.
+CsrPlan dlv_plan(uint32_t n);
 struct InListSizes {
     size_t src_words, region_words, scratch_words;  // u32 words
 };
@@ -77,6 +84,15 @@ InListSizes inlist_sizes(const CsrPlan &p);
 struct InListArgs {
     CsrPlan p;
     uint32_t *tg;       // [n] targets of the round
+    // DLV path (dlv != 0, binned, R_pad <= 16): records carry push codes read
+    // from the round's planes S (small-segment geometry g)
+    uint32_t dlv;
+    const u64 *S;
+    const uint32_t *PC;     // push codes of the round (written by the round kernel)
+    Geometry g;
+    DlvRec *DR;         // [n]
+    uint2 *dtail;       // [tailcap] {id, code} of pushers >= kDlvInline
+    uint32_t *region_code;  // binned: [nb][cap] push codes of the region's sources (set internally)
     InRec *IN8;         // [n]
     SibRec *SIB8;       // [n]
     uint32_t *src;      // tails (binned) or the full CSR (generic)

@@ -143,7 +143,16 @@ struct Recv {
 // SEQ: the literal harness order (gs_seq.hip): x's pull batch W(x) was built
 // by the level passes, and it is absorbed at x's own position among its
 // pushers (time x), answered pushes included.
-template <bool SMALL, int MODE, bool SHARD, bool SEQ>
+// DLV (R_pad <= 16, 2P): a push code (b0 | b1 << 16) as class planes.
+GS_DEV Cls decode16(uint32_t code) {
+    const u64 b0 = code & 0xFFFFu, b1 = code >> 16;
+    return Cls{b0 & b1, b0 & ~b1, b1 & ~b0};
+}
+
+// DLV: delivery records (gs_common.h DlvRec) replace every class-plane gather
+// but t(x)'s record: a lane's pushers and their push codes are in its own
+// record (coalesced), t(x)'s class and t(x)'s pushers ahead of x in t(x)'s.
+template <bool SMALL, int MODE, bool SHARD, bool SEQ, bool DLV>
 __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     constexpr bool DELIVER = (MODE == 1 || MODE == 2);
     constexpr bool TRANSITION = (MODE == 0 || MODE == 1);
@@ -180,8 +189,14 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     uint32_t sinf = 0;  // SEQ: got << 7 | ... (gs_seq.hip)
     bool seq_inl = false;  // SEQ: W(x) built here, not by a pull pass (kSeqInline)
     bool seq_dep = false;  // SEQ: W(x) includes W(t(x)) (kSeqDep)
+    DlvRec dr = {}, dz = {};  // DLV: x's record, t(x)'s record
     if (DELIVER) {
-        if (SHARD) {
+        if (DLV) {
+            dr = a.DR[x];  // x = 0 on invalid lanes: a harmless valid address
+            tgw = a.tg[x];
+            z = tgw & kTgMask;
+            k = valid ? (dr.meta & 31u) : 0u;
+        } else if (SHARD) {
             if (valid) {
                 in = a.IN[x];
                 zi = in.y >> 16;
@@ -225,7 +240,9 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
 #pragma unroll
     for (uint32_t i = 0; i < kBatchE; ++i) e[i] = {0, 0, 0};
     if (DELIVER) {
-        if (SHARD) {
+        if (DLV) {
+            dz = a.DR[z];  // the one random access of the lane
+        } else if (SHARD) {
             if (valid) {
                 static_assert(kBatchK == 3, "shard rows: three batched pushers");
                 // the first three pushers' rows together (unconditional: row 0
@@ -301,7 +318,35 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         if (k > 30u) atomicOr(&a.flags[2], 1u);
         bool zin = false;
         u64 pv2, pvB, pCl;
-        if (SHARD) {
+        if (DLV) {
+            static_assert(kDlvInline == 2, "inline pushers are read by hand");
+            const uint32_t dzi = (dr.meta >> 5) & 31u;  // t(x)'s index among x's pushers
+            zin = dzi != kDlvNoZ;
+            for (uint32_t i = 0; i < k; ++i) {
+                const uint32_t code = i == 0 ? dr.c[0] : (i == 1 ? dr.c[1] : a.dtail[dr.pad + i - kDlvInline].y);
+                rv.push(decode16(code), i, k, !(pulled && i == dzi));
+            }
+            // Pull batch from z: z's live set plus what z created from its
+            // pushers ahead of x (ascending ids, x's own entry ends the scan).
+            const u64 zc = dz.cls01 & 0xFFFFu, za0 = dz.cls01 >> 16, za1 = dz.cls2 & 0xFFFFu;
+            const u64 zB = ~zc & (za0 | za1);
+            const u64 zC = zc & ~(za0 & za1);
+            u64 pnot = ~zc & ~za0 & ~za1 & L.m, pB = 0, pC = 0;
+            if (pulled) {
+                const uint32_t kz = dz.meta & 31u;
+                for (uint32_t j = 0; j < kz && pnot; ++j) {
+                    const uint2 sc = j == 0 ? make_uint2(dz.s[0], dz.c[0])
+                                            : (j == 1 ? make_uint2(dz.s[1], dz.c[1])
+                                                      : a.dtail[dz.pad + j - kDlvInline]);
+                    if (sc.x >= x) break;
+                    sibling(decode16(sc.y), pnot, pB, pC);
+                }
+            }
+            pv2 = zB & za1 & ~za0;
+            pvB = zB | pB;  // counter 1 (created entries: 1) or 2
+            pCl = zC | pC;
+            if (!pulled) pv2 = pvB = pCl = 0;
+        } else if (SHARD) {
             // zi = index of t(x) among x's pushers (0xFFFF: t(x) did not push to x)
             zin = zi != 0xFFFFu;
             const uint32_t zs = pulled ? zi : 0xFFFFu;  // push copy superseded by the pull copy
@@ -637,6 +682,14 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         a.pend[pidx + g.W] = anyCe & (Bold | cB);
     }
 
+    // DLV: the push code of round t+1 (b0 | b1 << 16), which the in-list
+    // build carries to the receivers (coalesced, 4 B per node)
+    if (DLV && valid) {
+        const u64 vC = N[0] & ~(N[1] & N[2]), vB = ~N[0] & (N[1] | N[2]);
+        const u64 b0 = ((vB & N[1] & ~N[2]) | vC) & L.m, b1 = ((vB & N[2] & ~N[1]) | vC) & L.m;
+        a.pc_out[x] = (uint32_t)b0 | ((uint32_t)b1 << 16);
+    }
+
     // ---- write round-(t+1) planes (through LDS, 16-byte coalesced stores)
     uint32_t live_new = (valid && on_next) ? popc(Bn | Cn) : 0u;
     if (!SMALL) live_new = group_sum(live_new, g.W);
@@ -695,16 +748,16 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     }
 }
 
-template <bool SMALL, bool SHARD, bool SEQ>
+template <bool SMALL, bool SHARD, bool SEQ, bool DLV = false>
 static hipError_t launch_mode(const RoundArgs &a, int mode, hipStream_t s) {
     const uint32_t block = 256;
     const u64 grid = (a.g.nseg + block - 1) / block;
     if (grid == 0) return hipSuccess;
     switch (mode) {
-    case 0: hipLaunchKernelGGL((round_kernel<SMALL, 0, SHARD, SEQ>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
-    case 1: hipLaunchKernelGGL((round_kernel<SMALL, 1, SHARD, SEQ>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((round_kernel<SMALL, 2, SHARD, SEQ>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
-    default: hipLaunchKernelGGL((round_kernel<SMALL, 3, SHARD, SEQ>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
+    case 0: hipLaunchKernelGGL((round_kernel<SMALL, 0, SHARD, SEQ, DLV>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((round_kernel<SMALL, 1, SHARD, SEQ, DLV>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((round_kernel<SMALL, 2, SHARD, SEQ, DLV>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
+    default: hipLaunchKernelGGL((round_kernel<SMALL, 3, SHARD, SEQ, DLV>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
     }
     return hipGetLastError();
 }
@@ -714,6 +767,10 @@ hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s) {
         return a.g.small ? launch_mode<true, true, false>(a, mode, s) : launch_mode<false, true, false>(a, mode, s);
     if (a.Wb)     // SEQ schedule
         return a.g.small ? launch_mode<true, false, true>(a, mode, s) : launch_mode<false, false, true>(a, mode, s);
+    if (a.DR) {   // delivery records (2P, R_pad <= 16)
+        if (!a.g.small || a.g.rpad > 16) return hipErrorInvalidValue;
+        return launch_mode<true, false, false, true>(a, mode, s);
+    }
     return a.g.small ? launch_mode<true, false, false>(a, mode, s) : launch_mode<false, false, false>(a, mode, s);
 }
 

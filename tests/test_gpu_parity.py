@@ -289,3 +289,21 @@ def test_config2_full_size(engine):
     # Statistics, known sets); the dissemination takes O(ln n) rounds.
     rounds = run_parity(engine, 1_000_000, 1, "origins")
     assert 14 <= rounds <= 30
+
+
+@pytest.mark.parametrize("n,R,kind,faults", [
+    (300, 16, "origins", None),
+    (2000, 1, "trickle", (0.1, 0.05, 0.05)),
+    (500, 8, "reinject", (0.05, 0.1, 0.1)),
+])
+def test_parity_small_gather_path(engine, monkeypatch, n, R, kind, faults):
+    # R_pad <= 16 runs on delivery records by default; the class-plane gather
+    # path stays bit-exact too (SAFE_GOSSIP_AMD_NO_DLV=1)
+    monkeypatch.setenv("SAFE_GOSSIP_AMD_NO_DLV", "1")
+    run_parity(engine, n, R, kind, faults=faults)
+
+
+def test_parity_delivery_records_larger(engine):
+    # delivery records at 20k nodes: many in-list tails (in-degree > 2) and
+    # pull scans through t(x)'s tail, with faults, every 3rd round checked
+    run_parity(engine, 20000, 16, "reinject", check_every=3, faults=(0.02, 0.05, 0.05))
