@@ -114,7 +114,6 @@ GS_DEV uint32_t emit_tail(const InListArgs &a, const uint32_t *lst, uint32_t k, 
 // the bin (u16) at region_lt[b*kBinCap ...].  Each target is drawn once, here:
 // a Philox4x32-10 draw is ~40 quarter-rate multiplies, so redrawing it in
 // inl_sort would cost more than carrying 2 bytes.
-template <bool DLV>
 __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     const CsrPlan &p = a.p;
@@ -179,37 +178,19 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
     __syncthreads();
     // Consecutive stage entries of one bin go to consecutive region slots; the
     // bin of entry i is found by a binary search over the chunk-local starts.
-    // DLV: each entry also carries its source's push code, read from the
-    // chunk's 64 KB window of the push codes the round kernel wrote (L2
-    // resident); the loads of kBatchW entries are issued together.
-    constexpr uint32_t kBatchW = DLV ? 4u : 1u;
-    for (uint32_t i0 = threadIdx.x; i0 < total; i0 += kBatchW * kInlThreads) {  // delivered edges
-        uint32_t code[kBatchW];
-        if (DLV) {
-#pragma unroll
-            for (uint32_t j = 0; j < kBatchW; ++j) {
-                const uint32_t i = i0 + j * kInlThreads;
-                code[j] = a.PC[i < total ? stage[i] : lo];
-            }
+    for (uint32_t i = threadIdx.x; i < total; i += kInlThreads) {  // delivered edges of the chunk
+        uint32_t lo_b = 0, hi_b = p.nb;  // last bin with off[b] <= i and a non-empty run
+        while (hi_b - lo_b > 1) {
+            const uint32_t mid = (lo_b + hi_b) >> 1;
+            if (off[mid] <= i) lo_b = mid; else hi_b = mid;
         }
-#pragma unroll
-        for (uint32_t j = 0; j < kBatchW; ++j) {
-            const uint32_t i = i0 + j * kInlThreads;
-            if (i >= total) break;
-            uint32_t lo_b = 0, hi_b = p.nb;  // last bin with off[b] <= i and a non-empty run
-            while (hi_b - lo_b > 1) {
-                const uint32_t mid = (lo_b + hi_b) >> 1;
-                if (off[mid] <= i) lo_b = mid; else hi_b = mid;
-            }
-            // (empty bins share their start with the next bin, so the last bin
-            // whose start is <= i is the one whose run holds entry i)
-            const uint32_t b = lo_b;
-            const uint32_t slot = res[b] + (i - off[b]);
-            if (slot < kBinCap) {
-                a.region[(u64)b * kBinCap + slot] = stage[i];
-                a.region_lt[(u64)b * kBinCap + slot] = stage_lt[i];
-                if (DLV) a.region_code[(u64)b * kBinCap + slot] = code[j];
-            }
+        // (empty bins share their start with the next bin, so the last bin
+        // whose start is <= i is the one whose run holds entry i)
+        const uint32_t b = lo_b;
+        const uint32_t slot = res[b] + (i - off[b]);
+        if (slot < kBinCap) {
+            a.region[(u64)b * kBinCap + slot] = stage[i];
+            a.region_lt[(u64)b * kBinCap + slot] = stage_lt[i];
         }
     }
 }
@@ -295,6 +276,173 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
     }
 }
 
+// ------------------------------------------------------------ DLV path
+// The delivery-record build partitions (source, local target, push code)
+// entries in two levels, so every partition writes long runs (a single level
+// over ~6000 bins of 16 K targets wrote ~3-entry runs, twice the bytes):
+//   dl_coarse : per chunk of kPartChunk sources: Philox targets (-> tg), push
+//               codes (coalesced), an LDS counting sort into coarse buckets of
+//               2^kCoarseLog targets (kCoarseBins bins each), runs of ~170
+//   dl_fine   : per chunk of a coarse bucket: an LDS counting sort into its
+//               kCoarseBins bins of kBin targets, runs of ~64, into the bin
+//               regions inl_sort_dlv reads
+constexpr uint32_t kCoarseBins = 128;
+constexpr uint32_t kCoarseLog = kBinLog + 7;
+constexpr uint32_t kCoarseCap = (1u << kCoarseLog) + (1u << (kCoarseLog - 4));
+constexpr uint32_t kPartChunk = 8192;
+constexpr uint32_t kPartPer = kPartChunk / kInlThreads;
+constexpr uint32_t kMaxCoarse = 64;  // n <= 2^27
+
+GS_DEV uint32_t n_coarse(uint32_t nb) { return (nb + kCoarseBins - 1) / kCoarseBins; }
+
+// Coarse-bucket arrays inside the region buffer, after the bin regions.
+struct CoarseArrays {
+    uint32_t *x, *t, *c;
+};
+__host__ __device__ inline CoarseArrays coarse_arrays(uint32_t *region, uint32_t nb) {
+    const size_t base = (size_t)nb * kBinCap * 5 / 2;
+    const size_t cap = (size_t)((nb + kCoarseBins - 1) / kCoarseBins) * kCoarseCap;
+    return CoarseArrays{region + base, region + base + cap, region + base + 2 * cap};
+}
+
+__global__ __launch_bounds__(kInlThreads) void dl_coarse(InListArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
+    uint32_t *sx = sh, *st = sh + kPartChunk, *sc = sh + 2 * kPartChunk;
+    __shared__ uint32_t cnt[kMaxCoarse], off[kMaxCoarse], res[kMaxCoarse + 1];
+    const CsrPlan &p = a.p;
+    const uint32_t nc = n_coarse(p.nb);
+    uint32_t *cfill = a.scratch + p.nb + 1;
+    const CoarseArrays ca = coarse_arrays(a.region, p.nb);
+    for (uint32_t i = threadIdx.x; i < nc; i += kInlThreads) cnt[i] = 0u;
+    __syncthreads();
+    const uint32_t lo = blockIdx.x * kPartChunk;
+    uint32_t tv[kPartPer], cv[kPartPer];
+#pragma unroll
+    for (uint32_t q = 0; q < kPartPer; ++q) {
+        const uint32_t x = lo + threadIdx.x + q * kInlThreads;
+        tv[q] = kTgDead;
+        cv[q] = 0u;
+        if (x < p.n) {
+            const uint32_t t = target_of(a, x);
+            a.tg[x] = t;
+            tv[q] = t;
+            cv[q] = a.PC[x];
+            if (!(t & kTgDead)) atomicAdd(&cnt[(t & kTgMask) >> kCoarseLog], 1u);
+        }
+    }
+    __syncthreads();
+    {  // exclusive scan of the nc <= 64 bucket counts; one reservation per bucket
+        __shared__ uint32_t lds_scan[kInlThreads / 64];
+        const uint32_t c = threadIdx.x < nc ? cnt[threadIdx.x] : 0u;
+        uint32_t total;
+        const uint32_t ex = block_exclusive_scan_t<kInlThreads>(c, lds_scan, total);
+        if (threadIdx.x < nc) {
+            off[threadIdx.x] = ex;
+            uint32_t r0 = c ? atomicAdd(&cfill[threadIdx.x], c) : 0u;
+            if (r0 + c > kCoarseCap) {
+                atomicOr(&a.flags[2], kFlagLimit);
+                r0 = kCoarseCap;
+            }
+            res[threadIdx.x] = r0;
+            cnt[threadIdx.x] = ex;  // cursor
+        }
+        if (threadIdx.x == 0) res[kMaxCoarse] = total;  // entries of the chunk
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < kPartPer; ++q) {
+        if (tv[q] & kTgDead) continue;
+        const uint32_t t = tv[q] & kTgMask;
+        const uint32_t pos = atomicAdd(&cnt[t >> kCoarseLog], 1u);
+        sx[pos] = lo + threadIdx.x + q * kInlThreads;
+        st[pos] = t;
+        sc[pos] = cv[q];
+    }
+    __syncthreads();
+    const uint32_t total = res[kMaxCoarse];
+    for (uint32_t i = threadIdx.x; i < total; i += kInlThreads) {
+        const uint32_t b = st[i] >> kCoarseLog;
+        const uint32_t slot = res[b] + (i - off[b]);
+        if (slot < kCoarseCap) {
+            const u64 o = (u64)b * kCoarseCap + slot;
+            ca.x[o] = sx[i];
+            ca.t[o] = st[i];
+            ca.c[o] = sc[i];
+        }
+    }
+}
+
+__global__ __launch_bounds__(kInlThreads) void dl_fine(InListArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
+    uint32_t *sx = sh, *sc = sh + kPartChunk;
+    uint16_t *slt = reinterpret_cast<uint16_t *>(sh + 2 * kPartChunk);
+    __shared__ uint32_t cnt[kCoarseBins], off[kCoarseBins], res[kCoarseBins];
+    __shared__ uint32_t lds_scan[kInlThreads / 64];
+    const CsrPlan &p = a.p;
+    const uint32_t cb = blockIdx.y;
+    const uint32_t fill = min(a.scratch[p.nb + 1 + cb], kCoarseCap);
+    const uint32_t lo = blockIdx.x * kPartChunk;
+    if (lo >= fill) return;  // uniform per block
+    const uint32_t hi = min(fill, lo + kPartChunk);
+    const CoarseArrays ca = coarse_arrays(a.region, p.nb);
+    if (threadIdx.x < kCoarseBins) cnt[threadIdx.x] = 0u;
+    __syncthreads();
+    uint32_t xv[kPartPer], tv[kPartPer], cv[kPartPer];
+#pragma unroll
+    for (uint32_t q = 0; q < kPartPer; ++q) {
+        const uint32_t i = lo + threadIdx.x + q * kInlThreads;
+        const bool ok = i < hi;
+        const u64 o = (u64)cb * kCoarseCap + (ok ? i : lo);
+        xv[q] = ca.x[o];
+        tv[q] = ok ? ca.t[o] : kNone;
+        cv[q] = ca.c[o];
+        if (ok) atomicAdd(&cnt[(tv[q] >> kBinLog) & (kCoarseBins - 1u)], 1u);
+    }
+    __syncthreads();
+    {  // exclusive scan of the kCoarseBins counts, reservations in the bin regions
+        const uint32_t c = threadIdx.x < kCoarseBins ? cnt[threadIdx.x] : 0u;
+        uint32_t total;
+        const uint32_t ex = block_exclusive_scan_t<kInlThreads>(c, lds_scan, total);
+        if (threadIdx.x < kCoarseBins) {
+            const uint32_t b = cb * kCoarseBins + threadIdx.x;
+            off[threadIdx.x] = ex;
+            uint32_t r0 = c ? atomicAdd(&a.scratch[b], c) : 0u;
+            if (r0 + c > kBinCap) {
+                atomicOr(&a.flags[2], kFlagLimit);
+                r0 = kBinCap;
+            }
+            res[threadIdx.x] = r0;
+            cnt[threadIdx.x] = ex;  // cursor
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < kPartPer; ++q) {
+        if (tv[q] == kNone) continue;
+        const uint32_t fb = (tv[q] >> kBinLog) & (kCoarseBins - 1u);
+        const uint32_t pos = atomicAdd(&cnt[fb], 1u);
+        sx[pos] = xv[q];
+        sc[pos] = cv[q];
+        slt[pos] = (uint16_t)(tv[q] & (kBin - 1u));  // (its fine bin is found from off[] below)
+    }
+    __syncthreads();
+    const uint32_t n_here = hi - lo;
+    for (uint32_t i = threadIdx.x; i < n_here; i += kInlThreads) {
+        uint32_t lo_b = 0, hi_b = kCoarseBins;  // last bin whose run starts at or before i
+        while (hi_b - lo_b > 1) {
+            const uint32_t mid = (lo_b + hi_b) >> 1;
+            if (off[mid] <= i) lo_b = mid; else hi_b = mid;
+        }
+        const uint32_t slot = res[lo_b] + (i - off[lo_b]);
+        if (slot < kBinCap) {
+            const u64 o = (u64)(cb * kCoarseBins + lo_b) * kBinCap + slot;
+            a.region[o] = sx[i];
+            a.region_lt[o] = slt[i];
+            a.region_code[o] = sc[i];
+        }
+    }
+}
+
 // DLV: the records of one HALF of a bin (kHalf targets; blockIdx.y picks the
 // half) from the bin's region: an LDS counting sort of (id, push code) pairs
 // by target, per target an insertion sort by id, then the DlvRec with the
@@ -316,6 +464,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort_dlv(InListArgs a) {
     const uint32_t cnt = min(a.scratch[b], kBinCap);
     const uint32_t t0 = (b << kBinLog) + (hh << kHalfLog);
     const uint32_t nodes = t0 < p.n ? min(kHalf, p.n - t0) : 0u;
+    if (nodes == 0) return;  // a half past the last node (uniform per block)
     uint32_t ex[kSortPer], ec[kSortPer], el[kSortPer];
 #pragma unroll
     for (uint32_t q = 0; q < kSortPer; ++q) {
@@ -575,8 +724,8 @@ CsrPlan dlv_plan(uint32_t n) {
     p.bin = kBin;
     p.logbin = kBinLog;
     p.nb = nb_binned;
-    p.ba = (uint32_t)(((u64)n + kChunk - 1) / kChunk);
-    p.chunk = kChunk;
+    p.ba = (uint32_t)(((u64)n + kPartChunk - 1) / kPartChunk);  // dl_coarse blocks
+    p.chunk = kPartChunk;
     // pushers beyond kDlvInline: E[max(k - 2, 0)] = 3/e - 1 = 10.4 % of n
     p.tailcap = n / 8u + 4096u;
     return p;
@@ -613,9 +762,11 @@ InListSizes inlist_sizes(const CsrPlan &p) {
     InListSizes z{};
     if (p.binned) {
         z.src_words = p.dlv ? 2 * (size_t)p.tailcap : p.tailcap;  // DLV: {id, code} pairs
-        // sources (u32) + local targets (u16) [+ push codes (u32)]
+        // sources (u32) + local targets (u16) [+ push codes (u32) + the coarse buckets]
         z.region_words = (size_t)p.nb * kBinCap * (p.dlv ? 5 : 3) / 2;
-        z.scratch_words = (size_t)p.nb + 1;  // fill[nb], tailcnt
+        const size_t nc = (p.nb + kCoarseBins - 1) / kCoarseBins;
+        if (p.dlv) z.region_words += 3 * nc * kCoarseCap;
+        z.scratch_words = (size_t)p.nb + 1 + (p.dlv ? nc : 0);  // fill[nb], tailcnt[, coarse fill]
     } else {
         z.src_words = p.tailcap;
         z.region_words = 3 * (size_t)p.n;  // u64 pairs + the CSR
@@ -632,9 +783,9 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
                                (size_t)2 * p.nb * sizeof(uint16_t);
         const size_t lds_sort = ((size_t)kBin / 2 + kBinCap) * sizeof(uint32_t);
         const size_t lds_dlv = ((size_t)kHalf / 2 + 2 * (size_t)kHalfCap) * sizeof(uint32_t);
-        const void *kb = p.dlv ? (const void *)inl_bin<true> : (const void *)inl_bin<false>;
         const void *ks = p.dlv ? (const void *)inl_sort_dlv : (const void *)inl_sort;
-        hipError_t e = hipFuncSetAttribute(kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bin);
+        hipError_t e = hipFuncSetAttribute((const void *)inl_bin, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds_bin);
         if (e == hipSuccess)
             e = hipFuncSetAttribute(ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(p.dlv ? lds_dlv : lds_sort));
         if (e != hipSuccess) return e;
@@ -642,14 +793,25 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
         ab.region_lt = reinterpret_cast<uint16_t *>(a.region + (size_t)p.nb * kBinCap);
         ab.region_code = a.region + (size_t)p.nb * kBinCap * 3 / 2;
         if (p.dlv) {
-            // the two half-bin blocks of a bin both read its fill count, so it
-            // is cleared here rather than by the sort
-            e = hipMemsetAsync(a.scratch, 0, (size_t)p.nb * sizeof(uint32_t), s);
+            // fill counts (both half-bin blocks of a bin read them, so they are
+            // cleared here rather than by the sort), tail count, coarse fills
+            const uint32_t nc = (p.nb + kCoarseBins - 1) / kCoarseBins;
+            e = hipMemsetAsync(a.scratch, 0, ((size_t)p.nb + 1 + nc) * sizeof(uint32_t), s);
+            const size_t lds_c = 3 * (size_t)kPartChunk * sizeof(uint32_t);
+            const size_t lds_f = (2 * (size_t)kPartChunk + kPartChunk / 2) * sizeof(uint32_t);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void *)dl_coarse, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)lds_c);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void *)dl_fine, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)lds_f);
             if (e != hipSuccess) return e;
-            hipLaunchKernelGGL(inl_bin<true>, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
+            hipLaunchKernelGGL(dl_coarse, dim3(p.ba), dim3(kInlThreads), lds_c, s, ab);
+            hipLaunchKernelGGL(dl_fine, dim3((kCoarseCap + kPartChunk - 1) / kPartChunk, nc), dim3(kInlThreads),
+                               lds_f, s, ab);
             hipLaunchKernelGGL(inl_sort_dlv, dim3(p.nb, 2), dim3(kInlThreads), lds_dlv, s, ab);
         } else {
-            hipLaunchKernelGGL(inl_bin<false>, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
+            hipLaunchKernelGGL(inl_bin, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
             hipLaunchKernelGGL(inl_sort, dim3(p.nb), dim3(kInlThreads), lds_sort, s, ab);
         }
         return hipGetLastError();
