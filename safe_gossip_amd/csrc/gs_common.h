@@ -166,23 +166,21 @@ struct alignas(16) SibRec {
 };
 
 // Delivery records (R_pad <= 16, 2P, binned in-lists; gs_inlist.hip): the
-// in-list build also carries every pusher's push code, so a round kernel
-// lane reads its own record coalesced and ONE random record -- that of t(x) --
-// instead of gathering the class planes of its pushers, of t(x) and of t(x)'s
-// earlier pushers (three random 128-B lines per node in the gather path).
-//   meta = k (5 bits) | zi << 5 (index of t(y) among y's pushers, 31 = none)
-//          | first << 10 (pushers i >= kDlvInline at dtail[first + i - kDlvInline])
-//   cls  = y's round-t class planes isC | a0 << 16, a1 (16 bits each)
-//   s, c = the first kDlvInline pushers (ascending ids) and their push codes
-//          (b0 | b1 << 16: 01 counter 1, 10 counter 2, 11 counter 255)
+// in-list build carries every pusher's push code to its receiver and returns
+// every pull batch to its pusher, both in node order, so a round kernel lane
+// reads only coalesced per-node data -- no class-plane gathers (the gather
+// path fetches three random 128-B lines per node: pushers, t(x), t(x)'s
+// earlier pushers).
+//   DlvRec[y] = {meta = k | zi << 5 (index of t(y) among y's pushers, 31 =
+//               none), first, c[0], c[1]}: the push codes (b0 | b1 << 16: 01
+//               counter 1, 10 counter 2, 11 counter 255) of y's pushers in
+//               ascending order, pushers i >= kDlvInline at dtail[first + i - 2]
+//   PULL[x]   = the pull batch t(x) returned to x, the same 2-plane code
 constexpr uint32_t kDlvInline = 2;
 constexpr uint32_t kDlvNoZ = 31u;
-constexpr uint32_t kDlvFirstShift = 10;
-constexpr uint32_t kDlvMaxTail = 1u << (32 - kDlvFirstShift);
-struct alignas(32) DlvRec {
-    uint32_t meta, cls01, cls2, pad;
-    uint32_t s[kDlvInline], c[kDlvInline];
+struct alignas(16) DlvRec {
+    uint32_t meta, first, c[kDlvInline];
 };
-static_assert(sizeof(DlvRec) == 32, "one delivery record is 32 bytes");
+static_assert(sizeof(DlvRec) == 16, "one delivery record is 16 bytes");
 
 }  // namespace gs

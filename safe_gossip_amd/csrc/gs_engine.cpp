@@ -42,7 +42,8 @@ struct gs_engine {
         uint32_t *src = nullptr, *tg = nullptr, *scratch = nullptr, *region = nullptr;
         gs::InRec *IN8 = nullptr;
         gs::SibRec *SIB8 = nullptr;
-        gs::DlvRec *DR = nullptr;  // DLV path: delivery records (src holds {id, code} tails)
+        gs::DlvRec *DR = nullptr;  // DLV path: delivery records (src holds the tails' codes)
+        uint32_t *pull = nullptr;  // DLV path: PULL[x]
         uint32_t serial = 0;
     } csr[2];
     bool dlv = false;  // delivery-record path (2P, R_pad <= 16, binned in-lists)
@@ -133,7 +134,7 @@ void release(gs_engine *e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->cstream) (void)hipStreamSynchronize(e->cstream);
     for (auto &c : e->csr) {
-        void *cb[] = {c.src, c.tg, c.scratch, c.region, c.IN8, c.SIB8, c.DR};
+        void *cb[] = {c.src, c.tg, c.scratch, c.region, c.IN8, c.SIB8, c.DR, c.pull};
         for (void *b : cb)
             if (b) (void)hipFree(b);
     }
@@ -218,7 +219,8 @@ gs::RoundArgs base_args(gs_engine *e) {
         a.IN8 = cs.IN8;
         a.SIB8 = cs.SIB8;
         a.DR = cs.DR;
-        a.dtail = e->dlv ? reinterpret_cast<const uint2 *>(cs.src) : nullptr;
+        a.dtail = e->dlv ? cs.src : nullptr;
+        a.pull = cs.pull;
         a.pc_out = e->pc;
         a.src = cs.src;
         a.tg = cs.tg;
@@ -555,7 +557,7 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
              dalloc(&c.scratch, isz.scratch_words) == hipSuccess &&
              hipMemset(c.scratch, 0, std::max<size_t>(isz.scratch_words, 1) * sizeof(uint32_t)) == hipSuccess;
         if (ok && e->dlv) {
-            ok = dalloc(&c.DR, n) == hipSuccess;
+            ok = dalloc(&c.DR, n) == hipSuccess && dalloc(&c.pull, n) == hipSuccess;
         } else if (ok) {
             ok = dalloc(&c.IN8, n) == hipSuccess && dalloc(&c.SIB8, n) == hipSuccess &&
                  hipMemset(c.SIB8, 0, std::max<size_t>(n, 1) * sizeof(gs::SibRec)) == hipSuccess;
@@ -831,7 +833,8 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
             la.PC = e->pc;
             la.g = e->g;
             la.DR = c.DR;
-            la.dtail = reinterpret_cast<uint2 *>(c.src);
+            la.dtail = c.src;
+            la.pull = c.pull;
         }
         GS_HIP(gs::launch_build_inlists(la, bs));
         GS_HIP(hipEventRecord(e->ev_built[ns], bs));
@@ -1045,10 +1048,10 @@ double gs_round_kernel_bytes(const gs_engine *e) {
     // target 4 + Statistics deltas (16 r + 16 w).
     if (!e) return 0.0;
     const double n = e->g.n, rp = e->g.rpad;
-    // DLV path: per slot 1 B planes read + 1 B written; per node its own
-    // delivery record 32 + t(x)'s record 32 + target word 4 + Statistics
-    // deltas 16 r + 16 w + the next push code 4.
-    if (e->dlv) return n * (2.0 * rp + 104.0);
+    // DLV path: per slot 1 B planes read + 1 B written; per node its delivery
+    // record 16 + its pull batch 4 + target word 4 + Statistics deltas 16 r +
+    // 16 w + the next round's push code 4.
+    if (e->dlv) return n * (2.0 * rp + 60.0);
     return n * (2.75 * rp + 68.0);
 }
 

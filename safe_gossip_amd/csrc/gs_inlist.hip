@@ -305,6 +305,26 @@ __host__ __device__ inline CoarseArrays coarse_arrays(uint32_t *region, uint32_t
     return CoarseArrays{region + base, region + base + cap, region + base + 2 * cap};
 }
 
+// Pull pass-back arrays, after the coarse buckets: per coarse source bucket
+// 2^kCoarseLog (pusher, pull) slots (a source appears at most once), then per
+// source bin kBin (local pusher u16, pull) slots.
+struct PullArrays {
+    uint32_t *x, *v;
+    uint16_t *fx;
+    uint32_t *fv;
+};
+__host__ __device__ inline size_t pull_words(uint32_t nb) {
+    const size_t nc = (nb + kCoarseBins - 1) / kCoarseBins;
+    return 2 * (nc << kCoarseLog) + (size_t)nb * kBin * 3 / 2;
+}
+__host__ __device__ inline PullArrays pull_arrays(uint32_t *region, uint32_t nb) {
+    const size_t nc = (nb + kCoarseBins - 1) / kCoarseBins;
+    uint32_t *base = region + (size_t)nb * kBinCap * 5 / 2 + 3 * nc * kCoarseCap;
+    const size_t pc = nc << kCoarseLog;
+    return PullArrays{base, base + pc, reinterpret_cast<uint16_t *>(base + 2 * pc),
+                      base + 2 * pc + (size_t)nb * kBin / 2};
+}
+
 __global__ __launch_bounds__(kInlThreads) void dl_coarse(InListArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     uint32_t *sx = sh, *st = sh + kPartChunk, *sc = sh + 2 * kPartChunk;
@@ -445,9 +465,12 @@ __global__ __launch_bounds__(kInlThreads) void dl_fine(InListArgs a) {
 
 // DLV: the records of one HALF of a bin (kHalf targets; blockIdx.y picks the
 // half) from the bin's region: an LDS counting sort of (id, push code) pairs
-// by target, per target an insertion sort by id, then the DlvRec with the
-// target's class planes and the tails.  Halving the bin keeps ids and codes in
-// LDS (no global re-reads inside the per-target loop).
+// by target, per target an insertion sort by id, the DlvRec and its tails;
+// then, per pusher in order, the pull batch the target returns
+// (Gossip::receive, src/gossip.rs:124-151: the target's live set plus what it
+// created from the pushers ahead), partitioned by the pusher's coarse source
+// bucket for the pull pass-back (pb_fine, pb_place).  Halving the bin keeps
+// ids and codes in LDS.
 constexpr uint32_t kHalfLog = kBinLog - 1;
 constexpr uint32_t kHalf = 1u << kHalfLog;
 constexpr uint32_t kHalfCap = kBinCap / 2;
@@ -458,13 +481,17 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort_dlv(InListArgs a) {
     const CsrPlan &p = a.p;
     uint32_t *h = sh;                   // [kHalf/2] packed per-target counters
     uint32_t *sid = sh + kHalf / 2;     // [kHalfCap] source ids by target
-    uint32_t *scd = sid + kHalfCap;     // [kHalfCap] their push codes
+    uint32_t *scd = sid + kHalfCap;     // [kHalfCap] their push codes, then their pulls
     __shared__ uint32_t lds_scan[kInlThreads / 64];
+    __shared__ uint32_t pcnt[kMaxCoarse], pres[kMaxCoarse];
     const uint32_t b = blockIdx.x, hh = blockIdx.y;
     const uint32_t cnt = min(a.scratch[b], kBinCap);
     const uint32_t t0 = (b << kBinLog) + (hh << kHalfLog);
     const uint32_t nodes = t0 < p.n ? min(kHalf, p.n - t0) : 0u;
     if (nodes == 0) return;  // a half past the last node (uniform per block)
+    const uint32_t nc = n_coarse(p.nb);
+    uint32_t *pcfill = a.scratch + p.nb + 1 + nc;
+    const PullArrays pa = pull_arrays(a.region, p.nb);
     uint32_t ex[kSortPer], ec[kSortPer], el[kSortPer];
 #pragma unroll
     for (uint32_t q = 0; q < kSortPer; ++q) {
@@ -477,6 +504,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort_dlv(InListArgs a) {
         el[q] = (ok && (lt >> kHalfLog) == hh) ? (lt & (kHalf - 1u)) : kNone;
     }
     for (uint32_t i = threadIdx.x; i < kHalf / 2; i += kInlThreads) h[i] = 0u;
+    if (threadIdx.x < kMaxCoarse) pcnt[threadIdx.x] = 0u;
     __syncthreads();
 #pragma unroll
     for (uint32_t q = 0; q < kSortPer; ++q)
@@ -525,7 +553,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort_dlv(InListArgs a) {
     for (uint32_t lt = threadIdx.x; lt < nodes; lt += kInlThreads)
         mine += tail_len<kDlvInline>(min(half_of(h, lt), kHalfCap) - (lt ? min(half_of(h, lt - 1), kHalfCap) : 0u));
     uint32_t cur = reserve_tails<kInlThreads>(a, mine, &a.scratch[p.nb], lds_scan);
-    const u64 m = (1ull << a.g.rpad) - 1ull;
+    const uint32_t m = (uint32_t)((1ull << a.g.rpad) - 1ull);
 #pragma unroll
     for (uint32_t q = 0; q < kHalfPer; ++q) {
         const uint32_t lt = threadIdx.x + q * kInlThreads;
@@ -554,23 +582,134 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort_dlv(InListArgs a) {
         uint32_t zi = kDlvNoZ;
         for (uint32_t j = 0; j < k; ++j) {
             if (sid[s + j] == tz) zi = j;
-            if (j >= kDlvInline && cur != kNone) a.dtail[first + j - kDlvInline] = make_uint2(sid[s + j], scd[s + j]);
+            if (j >= kDlvInline && cur != kNone) a.dtail[first + j - kDlvInline] = scd[s + j];
         }
         if (mt && cur != kNone) cur += mt;
-        const uint32_t ysh = ((t0 + lt) & ((1u << a.g.lognpu) - 1u)) << a.g.logr;
-        const uint32_t c = (uint32_t)((w0[q] >> ysh) & m), a0 = (uint32_t)((w1[q] >> ysh) & m),
-                       a1 = (uint32_t)((w2[q] >> ysh) & m);
         DlvRec r;
         r.meta = k | (zi << 5);
-        r.cls01 = c | (a0 << 16);
-        r.cls2 = a1;
-        r.pad = first;
-        r.s[0] = k > 0 ? sid[s] : 0u;
+        r.first = first;
         r.c[0] = k > 0 ? scd[s] : 0u;
-        r.s[1] = k > 1 ? sid[s + 1] : 0u;
         r.c[1] = k > 1 ? scd[s + 1] : 0u;
         a.DR[t0 + lt] = r;
+        // the pull batch of each pusher, in place of its push code: y's live
+        // set (B with our_counter, C as 255) plus the entries y created from
+        // the pushers ahead of it (first carrier B -> counter 1, C -> 255)
+        const uint32_t ysh = ((t0 + lt) & ((1u << a.g.lognpu) - 1u)) << a.g.logr;
+        const uint32_t c = (uint32_t)(w0[q] >> ysh) & m, a0 = (uint32_t)(w1[q] >> ysh) & m,
+                       a1 = (uint32_t)(w2[q] >> ysh) & m;
+        const uint32_t zB = ~c & (a0 | a1), zC = c & ~(a0 & a1);
+        const uint32_t zB1 = zB & a0 & ~a1, zB2 = zB & a1 & ~a0;
+        uint32_t pnot = ~c & ~a0 & ~a1 & m, pB = 0, pC = 0;
+        for (uint32_t j = s; j < e; ++j) {  // (entries past kMaxIn keep the clamped pulls)
+            const uint32_t code = scd[j];
+            const uint32_t pcl = zC | pC;
+            scd[j] = ((zB1 | pB | pcl) & 0xFFFFu) | ((zB2 | pcl) << 16);
+            const uint32_t b0 = code & 0xFFFFu, b1 = code >> 16;
+            const uint32_t vC = b0 & b1, sl = b0 | b1;  // the pusher's batch; C carries 255
+            const uint32_t nw = pnot & sl;
+            pB |= nw & ~vC;
+            pC |= nw & vC;
+            pnot &= ~sl;
+            atomicAdd(&pcnt[sid[j] >> kCoarseLog], 1u);
+        }
     }
+    __syncthreads();
+    // the (pusher, pull) pairs into the pushers' coarse source buckets
+    if (threadIdx.x < nc) {
+        const uint32_t c = pcnt[threadIdx.x];
+        pres[threadIdx.x] = c ? atomicAdd(&pcfill[threadIdx.x], c) : 0u;
+        pcnt[threadIdx.x] = 0u;  // cursor
+    }
+    __syncthreads();
+    const uint32_t placed = min(total, kHalfCap);
+    for (uint32_t j = threadIdx.x; j < placed; j += kInlThreads) {
+        const uint32_t x = sid[j], cb = x >> kCoarseLog;
+        const uint32_t slot = pres[cb] + atomicAdd(&pcnt[cb], 1u);  // < 2^kCoarseLog: one per source
+        const u64 o = ((u64)cb << kCoarseLog) + slot;
+        pa.x[o] = x;
+        pa.v[o] = scd[j];
+    }
+}
+
+// Pull pass-back, level 2: per chunk of a coarse source bucket, an LDS
+// counting sort of (pusher, pull) pairs into its kCoarseBins source bins.
+__global__ __launch_bounds__(kInlThreads) void pb_fine(InListArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
+    uint32_t *sv = sh;
+    uint16_t *sx = reinterpret_cast<uint16_t *>(sh + kPartChunk);
+    uint8_t *sb = reinterpret_cast<uint8_t *>(sh + kPartChunk + kPartChunk / 2);
+    __shared__ uint32_t cnt[kCoarseBins], off[kCoarseBins], res[kCoarseBins];
+    __shared__ uint32_t lds_scan[kInlThreads / 64];
+    const CsrPlan &p = a.p;
+    const uint32_t nc = n_coarse(p.nb);
+    const uint32_t cb = blockIdx.y;
+    const uint32_t fill = min(a.scratch[p.nb + 1 + nc + cb], 1u << kCoarseLog);
+    const uint32_t lo = blockIdx.x * kPartChunk;
+    if (lo >= fill) return;  // uniform per block
+    const uint32_t hi = min(fill, lo + kPartChunk);
+    const PullArrays pa = pull_arrays(a.region, p.nb);
+    uint32_t *pffill = a.scratch + p.nb + 1 + 2 * nc;
+    if (threadIdx.x < kCoarseBins) cnt[threadIdx.x] = 0u;
+    __syncthreads();
+    uint32_t xv[kPartPer], vv[kPartPer];
+#pragma unroll
+    for (uint32_t q = 0; q < kPartPer; ++q) {
+        const uint32_t i = lo + threadIdx.x + q * kInlThreads;
+        const bool ok = i < hi;
+        const u64 o = ((u64)cb << kCoarseLog) + (ok ? i : lo);
+        xv[q] = ok ? pa.x[o] : kNone;
+        vv[q] = pa.v[o];
+        if (ok) atomicAdd(&cnt[(xv[q] >> kBinLog) & (kCoarseBins - 1u)], 1u);
+    }
+    __syncthreads();
+    {
+        const uint32_t c = threadIdx.x < kCoarseBins ? cnt[threadIdx.x] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_exclusive_scan_t<kInlThreads>(c, lds_scan, tot);
+        if (threadIdx.x < kCoarseBins) {
+            off[threadIdx.x] = ex;
+            res[threadIdx.x] = c ? atomicAdd(&pffill[cb * kCoarseBins + threadIdx.x], c) : 0u;  // < kBin
+            cnt[threadIdx.x] = ex;  // cursor
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < kPartPer; ++q) {
+        if (xv[q] == kNone) continue;
+        const uint32_t fb = (xv[q] >> kBinLog) & (kCoarseBins - 1u);
+        const uint32_t pos = atomicAdd(&cnt[fb], 1u);
+        sv[pos] = vv[q];
+        sx[pos] = (uint16_t)(xv[q] & (kBin - 1u));
+        sb[pos] = (uint8_t)fb;
+    }
+    __syncthreads();
+    const uint32_t n_here = hi - lo;
+    for (uint32_t i = threadIdx.x; i < n_here; i += kInlThreads) {
+        const uint32_t fb = sb[i];
+        const u64 o = (u64)(cb * kCoarseBins + fb) * kBin + res[fb] + (i - off[fb]);
+        pa.fx[o] = sx[i];
+        pa.fv[o] = sv[i];
+    }
+}
+
+// Pull pass-back, level 3: per source bin, the pulls into an LDS image of
+// PULL[bin], written out coalesced.  A slot nobody wrote belongs to a node
+// whose pull is not delivered this round; the round kernel ignores it.
+__global__ __launch_bounds__(kInlThreads) void pb_place(InListArgs a) {
+    __shared__ uint32_t img[kBin];
+    const CsrPlan &p = a.p;
+    const uint32_t nc = n_coarse(p.nb);
+    const uint32_t b = blockIdx.x;
+    const uint32_t cnt = min(a.scratch[p.nb + 1 + 2 * nc + b], kBin);
+    const PullArrays pa = pull_arrays(a.region, p.nb);
+    for (uint32_t i = threadIdx.x; i < cnt; i += kInlThreads) {
+        const u64 o = (u64)b * kBin + i;
+        img[pa.fx[o]] = pa.fv[o];
+    }
+    __syncthreads();
+    const uint32_t x0 = b << kBinLog;
+    const uint32_t nodes = min(kBin, p.n - x0);
+    for (uint32_t i = threadIdx.x; i < nodes; i += kInlThreads) a.pull[x0 + i] = img[i];
 }
 
 // ------------------------------------------------------------ generic path
@@ -727,7 +866,7 @@ CsrPlan dlv_plan(uint32_t n) {
     p.ba = (uint32_t)(((u64)n + kPartChunk - 1) / kPartChunk);  // dl_coarse blocks
     p.chunk = kPartChunk;
     // pushers beyond kDlvInline: E[max(k - 2, 0)] = 3/e - 1 = 10.4 % of n
-    p.tailcap = n / 8u + 4096u;
+    p.tailcap = n / 8u + 4096u;  // (the tails hold push codes only: src_words = tailcap)
     return p;
 }
 
@@ -761,12 +900,13 @@ CsrPlan csr_plan(uint32_t n) {
 InListSizes inlist_sizes(const CsrPlan &p) {
     InListSizes z{};
     if (p.binned) {
-        z.src_words = p.dlv ? 2 * (size_t)p.tailcap : p.tailcap;  // DLV: {id, code} pairs
+        z.src_words = p.tailcap;  // ids (or DLV: push codes) of the in-list tails
         // sources (u32) + local targets (u16) [+ push codes (u32) + the coarse buckets]
         z.region_words = (size_t)p.nb * kBinCap * (p.dlv ? 5 : 3) / 2;
         const size_t nc = (p.nb + kCoarseBins - 1) / kCoarseBins;
-        if (p.dlv) z.region_words += 3 * nc * kCoarseCap;
-        z.scratch_words = (size_t)p.nb + 1 + (p.dlv ? nc : 0);  // fill[nb], tailcnt[, coarse fill]
+        if (p.dlv) z.region_words += 3 * nc * kCoarseCap + pull_words(p.nb);
+        // fill[nb], tailcnt[, coarse fill[nc], pull coarse fill[nc], pull bin fill[nb]]
+        z.scratch_words = (size_t)p.nb + 1 + (p.dlv ? 2 * nc + p.nb : 0);
     } else {
         z.src_words = p.tailcap;
         z.region_words = 3 * (size_t)p.n;  // u64 pairs + the CSR
@@ -796,7 +936,7 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
             // fill counts (both half-bin blocks of a bin read them, so they are
             // cleared here rather than by the sort), tail count, coarse fills
             const uint32_t nc = (p.nb + kCoarseBins - 1) / kCoarseBins;
-            e = hipMemsetAsync(a.scratch, 0, ((size_t)p.nb + 1 + nc) * sizeof(uint32_t), s);
+            e = hipMemsetAsync(a.scratch, 0, ((size_t)2 * p.nb + 1 + 2 * nc) * sizeof(uint32_t), s);
             const size_t lds_c = 3 * (size_t)kPartChunk * sizeof(uint32_t);
             const size_t lds_f = (2 * (size_t)kPartChunk + kPartChunk / 2) * sizeof(uint32_t);
             if (e == hipSuccess)
@@ -810,6 +950,11 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
             hipLaunchKernelGGL(dl_fine, dim3((kCoarseCap + kPartChunk - 1) / kPartChunk, nc), dim3(kInlThreads),
                                lds_f, s, ab);
             hipLaunchKernelGGL(inl_sort_dlv, dim3(p.nb, 2), dim3(kInlThreads), lds_dlv, s, ab);
+            const size_t lds_pb = ((size_t)kPartChunk + kPartChunk / 2 + kPartChunk / 4) * sizeof(uint32_t);
+            e = hipFuncSetAttribute((const void *)pb_fine, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_pb);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(pb_fine, dim3((1u << kCoarseLog) / kPartChunk, nc), dim3(kInlThreads), lds_pb, s, ab);
+            hipLaunchKernelGGL(pb_place, dim3(p.nb), dim3(kInlThreads), 0, s, ab);
         } else {
             hipLaunchKernelGGL(inl_bin, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
             hipLaunchKernelGGL(inl_sort, dim3(p.nb), dim3(kInlThreads), lds_sort, s, ab);

@@ -10,7 +10,8 @@ struct RoundArgs {
     const InRec *IN8;         // round t, per node y: in-list record (gs_common.h)
     const SibRec *SIB8;       // round t, per source x: pushers of t(x) ahead of x
     const DlvRec *DR;         // round t delivery records (DLV path; IN8/SIB8 unused)
-    const uint2 *dtail;       //   their pushers >= kDlvInline: {id, push code}
+    const uint32_t *dtail;    //   push codes of pushers >= kDlvInline
+    const uint32_t *pull;     //   PULL[x]: the pull batch t(x) returned to x
     uint32_t *pc_out;         // DLV: push code of every node's round-(t+1) push batch
     const uint4 *IN;          // shard engine: per node {first edge, k | zi<<16, e0, e1}
     const uint32_t *IN2;      // shard engine: per node e2 (third pusher's receive row)
@@ -91,7 +92,8 @@ struct InListArgs {
     const uint32_t *PC;     // push codes of the round (written by the round kernel)
     Geometry g;
     DlvRec *DR;         // [n]
-    uint2 *dtail;       // [tailcap] {id, code} of pushers >= kDlvInline
+    uint32_t *dtail;    // [tailcap] push codes of pushers >= kDlvInline
+    uint32_t *pull;     // [n] PULL: pull batch of every pusher
     uint32_t *region_code;  // binned: [nb][cap] push codes of the region's sources (set internally)
     InRec *IN8;         // [n]
     SibRec *SIB8;       // [n]

@@ -149,9 +149,9 @@ GS_DEV Cls decode16(uint32_t code) {
     return Cls{b0 & b1, b0 & ~b1, b1 & ~b0};
 }
 
-// DLV: delivery records (gs_common.h DlvRec) replace every class-plane gather
-// but t(x)'s record: a lane's pushers and their push codes are in its own
-// record (coalesced), t(x)'s class and t(x)'s pushers ahead of x in t(x)'s.
+// DLV: delivery records (gs_common.h DlvRec) replace every class-plane
+// gather: a lane's pushers' push codes are in its own record and its pull
+// batch in PULL[x], both read coalesced.
 template <bool SMALL, int MODE, bool SHARD, bool SEQ, bool DLV>
 __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     constexpr bool DELIVER = (MODE == 1 || MODE == 2);
@@ -189,11 +189,13 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     uint32_t sinf = 0;  // SEQ: got << 7 | ... (gs_seq.hip)
     bool seq_inl = false;  // SEQ: W(x) built here, not by a pull pass (kSeqInline)
     bool seq_dep = false;  // SEQ: W(x) includes W(t(x)) (kSeqDep)
-    DlvRec dr = {}, dz = {};  // DLV: x's record, t(x)'s record
+    DlvRec dr = {};     // DLV: x's record
+    uint32_t dpull = 0;  // DLV: x's pull batch
     if (DELIVER) {
         if (DLV) {
             dr = a.DR[x];  // x = 0 on invalid lanes: a harmless valid address
             tgw = a.tg[x];
+            dpull = a.pull[x];
             z = tgw & kTgMask;
             k = valid ? (dr.meta & 31u) : 0u;
         } else if (SHARD) {
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     for (uint32_t i = 0; i < kBatchE; ++i) e[i] = {0, 0, 0};
     if (DELIVER) {
         if (DLV) {
-            dz = a.DR[z];  // the one random access of the lane
+            // nothing to gather
         } else if (SHARD) {
             if (valid) {
                 static_assert(kBatchK == 3, "shard rows: three batched pushers");
@@ -323,28 +325,15 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             const uint32_t dzi = (dr.meta >> 5) & 31u;  // t(x)'s index among x's pushers
             zin = dzi != kDlvNoZ;
             for (uint32_t i = 0; i < k; ++i) {
-                const uint32_t code = i == 0 ? dr.c[0] : (i == 1 ? dr.c[1] : a.dtail[dr.pad + i - kDlvInline].y);
+                const uint32_t code = i == 0 ? dr.c[0] : (i == 1 ? dr.c[1] : a.dtail[dr.first + i - kDlvInline]);
                 rv.push(decode16(code), i, k, !(pulled && i == dzi));
             }
-            // Pull batch from z: z's live set plus what z created from its
-            // pushers ahead of x (ascending ids, x's own entry ends the scan).
-            const u64 zc = dz.cls01 & 0xFFFFu, za0 = dz.cls01 >> 16, za1 = dz.cls2 & 0xFFFFu;
-            const u64 zB = ~zc & (za0 | za1);
-            const u64 zC = zc & ~(za0 & za1);
-            u64 pnot = ~zc & ~za0 & ~za1 & L.m, pB = 0, pC = 0;
-            if (pulled) {
-                const uint32_t kz = dz.meta & 31u;
-                for (uint32_t j = 0; j < kz && pnot; ++j) {
-                    const uint2 sc = j == 0 ? make_uint2(dz.s[0], dz.c[0])
-                                            : (j == 1 ? make_uint2(dz.s[1], dz.c[1])
-                                                      : a.dtail[dz.pad + j - kDlvInline]);
-                    if (sc.x >= x) break;
-                    sibling(decode16(sc.y), pnot, pB, pC);
-                }
-            }
-            pv2 = zB & za1 & ~za0;
-            pvB = zB | pB;  // counter 1 (created entries: 1) or 2
-            pCl = zC | pC;
+            // the pull batch z returned (built by the in-list build): code
+            // (b0, b1) = 01 counter 1, 10 counter 2, 11 counter 255
+            const u64 b0 = dpull & 0xFFFFu, b1 = dpull >> 16;
+            pv2 = b1 & ~b0;
+            pvB = b0 ^ b1;
+            pCl = b0 & b1;
             if (!pulled) pv2 = pvB = pCl = 0;
         } else if (SHARD) {
             // zi = index of t(x) among x's pushers (0xFFFF: t(x) did not push to x)
