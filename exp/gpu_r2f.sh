@@ -1,0 +1,7 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
+timeout -k 10 400 python -u bench.py > gpurun_out/bench_default.log 2>&1 &&
+timeout -k 10 400 python -u bench.py --config cfg5 --steps 10 --warmup 2 > gpurun_out/bench_cfg5.log 2>&1 &&
+bash profiles/rocprof_r2.sh r2 &&
+bash profiles/rocprof_r2.sh r2_cfg5 --config cfg5

@@ -1,12 +1,15 @@
 """Summarise a rocprofv3 run of bench.py (profiles/rocprof_r1.sh) into profiles/<tag>/.
 
-Writes kernel_stats.csv (copied), summary.json and pmc_latest.json (traffic of
-the dominant kernel per launch).  HBM bytes = 2*FETCH_SIZE + WRITE_SIZE (KiB
-units): on gfx950 FETCH_SIZE reports half of a wide coalesced streaming read
-(MI355X_MICROARCH.md section HBM); WRITE_SIZE is exact for our stores (it
-equals the algorithmic write bytes of the round kernel to 0.1%).
+Writes kernel_stats.csv (copied), summary.json and (for the default config 4
+workload) pmc_latest.json (traffic of the dominant kernel per launch).
+HBM bytes = 2*FETCH_SIZE + WRITE_SIZE (KiB units): FETCH_SIZE counts 64 B per
+memory-side read request (TCC_EA0_RDREQ) and every request of the round
+kernel moves a 128-B line -- calibrated with exp/gather_calib.hip on the
+state's own layouts (coalesced 16-B streaming reads, and random 32-/96-B
+class-row gathers: one request per gather, profiles/r2/pmc_calib_and_cfg5.json);
+WRITE_SIZE is exact for our stores.
 
-    python profiles/summarize.py gpurun_out/prof_r1c r1 --nodes 16777216 --rumors 256
+    python profiles/summarize.py gpurun_out/prof_r2 r2 --nodes 16777216 --rumors 256
 """
 import argparse
 import collections
@@ -25,6 +28,8 @@ def main():
     ap.add_argument("tag")
     ap.add_argument("--nodes", type=int, default=1 << 24)
     ap.add_argument("--rumors", type=int, default=256)
+    ap.add_argument("--dominant", default=DOMINANT, help="substring of the dominant kernel's name")
+    ap.add_argument("--no-latest", action="store_true", help="do not update profiles/pmc_latest.json")
     a = ap.parse_args()
     out = os.path.join(HERE, a.tag)
     os.makedirs(out, exist_ok=True)
@@ -44,20 +49,22 @@ def main():
             vals[x["Kernel_Name"]].append(float(x["Counter_Value"]))
         for k, v in vals.items():
             pmc[k][counter + "_KiB_mean"] = sum(v) / len(v)
-    dom = next((k for k in pmc if DOMINANT in k), None)
+    dom = next((k for k in pmc if a.dominant in k), None)
     summary = dict(kernels=kernels, pmc=pmc)
     if dom and "FETCH_SIZE_KiB_mean" in pmc[dom] and "WRITE_SIZE_KiB_mean" in pmc[dom]:
         f = pmc[dom]["FETCH_SIZE_KiB_mean"] * 1024
         w = pmc[dom]["WRITE_SIZE_KiB_mean"] * 1024
-        dom_ms = next(k["avg_ms"] for k in kernels if DOMINANT in k["name"])
+        dom_ms = next(k["avg_ms"] for k in kernels if a.dominant in k["name"])
         latest = dict(tag=a.tag, kernel=dom, nodes=a.nodes, rumors=a.rumors,
                       fetch_bytes_raw=f, write_bytes=w, hbm_bytes_per_launch=2 * f + w,
                       kernel_avg_ms_rocprof=dom_ms,
                       hbm_gbs=(2 * f + w) / (dom_ms * 1e-3) / 1e9,
-                      note="hbm_bytes = 2*FETCH_SIZE + WRITE_SIZE per launch (gfx950 FETCH_SIZE "
-                           "under-reports wide streaming reads by 2x)")
+                      note="hbm_bytes = 2*FETCH_SIZE + WRITE_SIZE per launch (FETCH_SIZE = 64 B per "
+                           "read request; each request moves a 128-B line, calibrated in "
+                           "profiles/r2/pmc_calib_and_cfg5.json)")
         summary["dominant"] = latest
-        json.dump(latest, open(os.path.join(HERE, "pmc_latest.json"), "w"), indent=1)
+        if not a.no_latest:
+            json.dump(latest, open(os.path.join(HERE, "pmc_latest.json"), "w"), indent=1)
     json.dump(summary, open(os.path.join(out, "summary.json"), "w"), indent=1)
     print(json.dumps(summary.get("dominant", {}), indent=1))
 
