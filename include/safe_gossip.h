@@ -19,6 +19,11 @@
  *   gs_messages        <- Gossiper::messages      (src/gossiper.rs:102-104)
  *   gs_statistics      <- Gossiper::statistics    (src/gossiper.rs:107-109)
  *   gs_statistics_reduce <- Statistics::add/min/max (src/gossip.rs:225-263)
+ *   gs_push_batch      <- Gossiper::next_round's serialised Push RPCs
+ *                         (src/gossiper.rs:70-79, src/messages.rs:57-64)
+ *   gs_handle_received <- Gossiper::handle_received_message (src/gossiper.rs:82-99)
+ *                         for peers outside the simulated network
+ *   gs_rpc_encode/decode <- Message::serialise/deserialise (src/messages.rs:46-55)
  *   gs_set_params      <- Gossiper::add_peer's AlreadyStarted rule and
  *                         Gossip::add_peer's parameters (src/gossiper.rs:45-52,
  *                         src/gossip.rs:59-64)
@@ -43,9 +48,9 @@ typedef enum {
     GS_OK = 0,
     GS_ERR_NO_PEERS = 1,          /* Error::NoPeers         */
     GS_ERR_ALREADY_STARTED = 2,   /* Error::AlreadyStarted  */
-    GS_ERR_SIG_FAILURE = 3,       /* Error::SigFailure (reserved: no wire format) */
+    GS_ERR_SIG_FAILURE = 3,       /* Error::SigFailure (reserved: signatures are not verified) */
     GS_ERR_IO = 4,                /* Error::Io (reserved)   */
-    GS_ERR_SERIALISATION = 5,     /* Error::Serialisation (reserved) */
+    GS_ERR_SERIALISATION = 5,     /* Error::Serialisation: undecodable RPC bytes, buffer too small */
     GS_ERR_INVALID_ARGUMENT = -1,
     GS_ERR_UNSUPPORTED = -2,      /* parameters outside the packed state layout */
     GS_ERR_HIP = -3,
@@ -187,6 +192,48 @@ gs_status   gs_shard_bind(gs_engine *e, void *sendA0, void *sendA1, void *recvA0
 gs_status   gs_shard_pull(gs_engine *e);
 /* The engine's HIP stream (hipStream_t), to order collectives on it. */
 uint64_t    gs_stream(const gs_engine *e);
+
+/* ---- Wire format (src/messages.rs) ----------------------------------------
+ * GossipRpc as maidsafe_utilities::serialisation (bincode, fixed-width little
+ * endian) writes it: u32 variant (0 Push, 1 Pull) | u64 msg length | msg |
+ * u8 counter.  The signed Message(Vec<u8>, Signature) wrapper used outside
+ * cfg(test) (src/messages.rs:26-44) is framed but NOT signed or verified
+ * (ed25519 over SHA3-512 is parity-unpinned here): callers pass frames
+ * through, as the reference's own cfg(test) simulation does (:46-55).
+ * Size errors return GS_ERR_SERIALISATION with *out_len = the size needed. */
+gs_status   gs_rpc_encode(int pull, const uint8_t *msg, uint32_t msg_len, uint8_t counter, uint8_t *out,
+                          uint32_t cap, uint32_t *out_len);
+gs_status   gs_rpc_decode(const uint8_t *buf, uint32_t len, int *pull, uint32_t *msg_off, uint32_t *msg_len,
+                          uint8_t *counter);
+gs_status   gs_message_wrap(const uint8_t *payload, uint32_t len, const uint8_t signature[64], uint8_t *out,
+                            uint32_t cap, uint32_t *out_len);
+gs_status   gs_message_unwrap(const uint8_t *buf, uint32_t len, uint32_t *payload_off, uint32_t *payload_len,
+                              uint32_t *signature_off);
+/* The message bytes (Gossip's BTreeMap<Vec<u8>, _> key) of rumor slot `rumor`;
+ * default: bincode of the 4-byte big-endian slot number (u64 length 4 + bytes).
+ * Keys must be distinct; a push list is in key (byte) order. */
+gs_status   gs_set_rumor_key(gs_engine *e, uint32_t rumor, const uint8_t *key, uint32_t len);
+gs_status   gs_rumor_key(const gs_engine *e, uint32_t rumor, uint8_t *out, uint32_t cap, uint32_t *len);
+/* Gossiper::next_round's return value for `node` in the current round
+ * (src/gossiper.rs:70-79, src/gossip.rs:79-113): the Push RPCs as frames
+ * (u32 LE length + bincode GossipRpc), key order; one empty Push if none;
+ * no frame for a node the harness skipped (churn). */
+gs_status   gs_push_batch(gs_engine *e, uint32_t node, uint8_t *out, uint32_t cap, uint32_t *len,
+                          uint32_t *count);
+/* Gossiper::handle_received_message(peer, bytes) on `node` for a peer
+ * OUTSIDE the simulated network (peer >= n_nodes), after the current round's
+ * internal deliveries (src/gossiper.rs:82-99 -> src/gossip.rs:118-166): a
+ * first Push from the peer this round is answered with the node's live
+ * entries as Pull frames (or one empty Pull); the copy is absorbed (a new
+ * entry is created, or recorded on a B entry); peers_in_this_round and the
+ * Statistics count it.  2P schedule, unsharded; after a gs_next_round.
+ * Messages whose bytes are no rumor slot's key: GS_ERR_INVALID_ARGUMENT.
+ * A node offline this round (churn) drops the RPC: GS_OK, no frames, no
+ * effect.  Undecodable bytes: GS_ERR_SERIALISATION, nothing applied; so is a
+ * response list larger than `cap` (*out_len = the size needed; call again). */
+gs_status   gs_handle_received(gs_engine *e, uint32_t node, uint32_t peer, const uint8_t *msg,
+                               uint32_t msg_len, uint8_t *out, uint32_t cap, uint32_t *out_len,
+                               uint32_t *out_count);
 
 /* Injected peer schedule: the peer node `node` chooses in `round`. */
 uint32_t    gs_peer(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node, uint32_t n);

@@ -684,6 +684,41 @@ uint64_t or_known_total(const or_net *net)
     return t;
 }
 
+/* ------------------------------------------------------- byte-level RPCs */
+/* Gossiper::next_round's push list of `node` in the current round
+ * (src/gossip.rs:93-111): rumors (-1 = the empty Push) and counters in map
+ * order; *n = 0 for a node the harness skipped (churn). */
+void or_push_list(const or_net *net, uint32_t node, int32_t *rumors, uint8_t *counters, uint32_t *n)
+{
+    const rpc_vec *pv = &net->push[node];
+    *n = net->round ? pv->n : 0u;
+    for (uint32_t i = 0; i < *n; ++i) {
+        rumors[i] = pv->v[i].msg;
+        counters[i] = pv->v[i].counter;
+    }
+}
+
+/* Gossiper::handle_received_message from `peer` on `node`, now (after the
+ * round's deliveries): Gossip::receive (src/gossip.rs:118-166) with the RPC
+ * {push, rumor (-1 = empty message), counter}; the responses (Pull RPCs) into
+ * rumors/counters (rumor -1 = the empty Pull), *n of them. */
+void or_receive(or_net *net, uint32_t node, uint32_t peer, int push, int32_t rumor, uint8_t counter,
+                int32_t *rumors, uint8_t *counters, uint32_t *n)
+{
+    or_rpc rpc;
+    rpc.push = (uint8_t)(push != 0);
+    rpc.msg = rumor;
+    rpc.counter = counter;
+    rpc_vec resp = {0, 0, 0};
+    gossip_receive(&net->g[node], peer, &rpc, &resp);
+    *n = resp.n;
+    for (uint32_t i = 0; i < resp.n; ++i) {
+        rumors[i] = resp.v[i].msg;
+        counters[i] = resp.v[i].counter;
+    }
+    free(resp.v);
+}
+
 /* --------------------------------------------------------------- harness */
 /* send_messages, src/gossiper.rs:173-259. */
 int or_send_messages(or_net *net, uint32_t num_msgs, int schedule, or_metrics *out)

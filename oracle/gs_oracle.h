@@ -91,6 +91,14 @@ void     or_messages(const or_net *net, uint32_t node, uint64_t *words);
 uint64_t or_known_total(const or_net *net);
 void     or_known_all(const or_net *net, uint64_t *words);   /* n*ceil(R/64) */
 
+/* Byte-level RPC hooks (the wire-format tests): the push list of `node` this
+ * round, and Gossip::receive of one RPC from `peer` on `node` now, after the
+ * round's deliveries (rumor -1 = the empty message). */
+void     or_push_list(const or_net *net, uint32_t node, int32_t *rumors, uint8_t *counters,
+                      uint32_t *n);
+void     or_receive(or_net *net, uint32_t node, uint32_t peer, int push, int32_t rumor,
+                    uint8_t counter, int32_t *rumors, uint8_t *counters, uint32_t *n);
+
 /* send_messages(gossipers, num_of_msgs) restated (src/gossiper.rs:173-259):
  * Philox-chosen first origin, then 50% per node per round while rumors remain,
  * termination after a round with no live push; clears the network at the end. */

@@ -27,7 +27,8 @@ from .build import LIB_PATH
 __all__ = [
     "Network", "Gossiper", "Statistics", "RoundReport", "GossipError", "NoPeers",
     "AlreadyStarted", "DeviceError", "derive_params", "peer_of", "origin_of", "coin_of",
-    "send_messages", "load_library", "SYMBOLS",
+    "send_messages", "load_library", "SYMBOLS", "rpc_encode", "rpc_decode", "message_wrap",
+    "message_unwrap", "split_frames",
 ]
 
 # ----------------------------------------------------------------- errors
@@ -100,6 +101,17 @@ SYMBOLS = {
     "gs_known_counts_min": (ctypes.c_int, [_P, ctypes.c_uint32, _U64P, _U64P]),
     "gs_known_popcounts": (ctypes.c_int, [_P, _U32P]),
     "gs_set_params": (ctypes.c_int, [_P, _U8P]),
+    "gs_rpc_encode": (ctypes.c_int, [ctypes.c_int, _U8P, ctypes.c_uint32, ctypes.c_uint8, _U8P,
+                                     ctypes.c_uint32, _U32P]),
+    "gs_rpc_decode": (ctypes.c_int, [_U8P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int), _U32P, _U32P,
+                                     _U8P]),
+    "gs_message_wrap": (ctypes.c_int, [_U8P, ctypes.c_uint32, _U8P, _U8P, ctypes.c_uint32, _U32P]),
+    "gs_message_unwrap": (ctypes.c_int, [_U8P, ctypes.c_uint32, _U32P, _U32P, _U32P]),
+    "gs_set_rumor_key": (ctypes.c_int, [_P, ctypes.c_uint32, _U8P, ctypes.c_uint32]),
+    "gs_rumor_key": (ctypes.c_int, [_P, ctypes.c_uint32, _U8P, ctypes.c_uint32, _U32P]),
+    "gs_push_batch": (ctypes.c_int, [_P, ctypes.c_uint32, _U8P, ctypes.c_uint32, _U32P, _U32P]),
+    "gs_handle_received": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_uint32, _U8P, ctypes.c_uint32,
+                                          _U8P, ctypes.c_uint32, _U32P, _U32P]),
     "gs_dump_state": (ctypes.c_int, [_P, _U16P]),
     "gs_dump_records": (ctypes.c_int, [_P, _U16P, _U32P]),
     "gs_clear": (ctypes.c_int, [_P, ctypes.c_uint32]),
@@ -264,6 +276,64 @@ def coin_of(seed: int, epoch: int, rnd: int, node: int) -> int:
     return load_library().gs_coin(seed, epoch, rnd, node)
 
 
+# ------------------------------------------------------------ wire format
+def _buf(data: bytes):
+    return (ctypes.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+
+
+def rpc_encode(pull: bool, msg: bytes, counter: int) -> bytes:
+    """``Message::serialise`` (cfg(test), src/messages.rs:48-50) of
+    ``GossipRpc::{Push,Pull} { msg, counter }``: bincode."""
+    lib = load_library()
+    n = ctypes.c_uint32()
+    lib.gs_rpc_encode(1 if pull else 0, _buf(msg), len(msg), counter, None, 0, ctypes.byref(n))
+    out = (ctypes.c_uint8 * n.value)()
+    _check(lib.gs_rpc_encode(1 if pull else 0, _buf(msg), len(msg), counter, out, n.value, ctypes.byref(n)))
+    return bytes(out)
+
+
+def rpc_decode(data: bytes):
+    """``Message::deserialise`` (cfg(test), src/messages.rs:52-54) ->
+    ``(pull, msg, counter)``; raises ``GossipError`` (Serialisation) on bad bytes."""
+    lib = load_library()
+    pull, off, ln, ctr = ctypes.c_int(), ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint8()
+    _check(lib.gs_rpc_decode(_buf(data), len(data), ctypes.byref(pull), ctypes.byref(off), ctypes.byref(ln),
+                             ctypes.byref(ctr)))
+    return bool(pull.value), bytes(data[off.value:off.value + ln.value]), ctr.value
+
+
+def message_wrap(payload: bytes, signature: bytes) -> bytes:
+    """bincode of ``Message(payload, signature)`` (src/messages.rs:26-34); the
+    signature is not computed here (ed25519/SHA3-512 is out of scope)."""
+    assert len(signature) == 64
+    lib = load_library()
+    n = ctypes.c_uint32()
+    sig = _buf(signature)
+    lib.gs_message_wrap(_buf(payload), len(payload), sig, None, 0, ctypes.byref(n))
+    out = (ctypes.c_uint8 * n.value)()
+    _check(lib.gs_message_wrap(_buf(payload), len(payload), sig, out, n.value, ctypes.byref(n)))
+    return bytes(out)
+
+
+def message_unwrap(data: bytes):
+    """-> ``(payload, signature)`` of a bincode ``Message`` (not verified)."""
+    lib = load_library()
+    po, pl, so = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+    _check(lib.gs_message_unwrap(_buf(data), len(data), ctypes.byref(po), ctypes.byref(pl), ctypes.byref(so)))
+    return bytes(data[po.value:po.value + pl.value]), bytes(data[so.value:so.value + 64])
+
+
+def split_frames(data: bytes) -> List[bytes]:
+    """The RPCs of a u32-length-prefixed frame sequence (gs_push_batch,
+    gs_handle_received)."""
+    out, i = [], 0
+    while i < len(data):
+        m = int.from_bytes(data[i:i + 4], "little")
+        out.append(bytes(data[i + 4:i + 4 + m]))
+        i += 4 + m
+    return out
+
+
 # ---------------------------------------------------------------- network
 class Network:
     """A simulated full-mesh network of ``n_nodes`` Gossipers on one MI355X.
@@ -389,6 +459,40 @@ class Network:
         _check(self._lib.gs_known_counts_min(self._h, mk, ctypes.byref(t), ctypes.byref(c)))
         return int(t.value), int(c.value)
 
+    # wire format (include/safe_gossip.h, src/messages.rs)
+    def set_rumor_key(self, rumor: int, key: bytes) -> None:
+        _check(self._lib.gs_set_rumor_key(self._h, rumor, _buf(key), len(key)))
+
+    def rumor_key(self, rumor: int) -> bytes:
+        n = ctypes.c_uint32()
+        self._lib.gs_rumor_key(self._h, rumor, None, 0, ctypes.byref(n))
+        out = (ctypes.c_uint8 * max(1, n.value))()
+        _check(self._lib.gs_rumor_key(self._h, rumor, out, n.value, ctypes.byref(n)))
+        return bytes(out)[:n.value]
+
+    def push_batch(self, node: int) -> List[bytes]:
+        """``Gossiper::next_round``'s Push RPCs of ``node`` this round (bytes)."""
+        n, c = ctypes.c_uint32(), ctypes.c_uint32()
+        self._lib.gs_push_batch(self._h, node, None, 0, ctypes.byref(n), ctypes.byref(c))
+        out = (ctypes.c_uint8 * max(1, n.value))()
+        _check(self._lib.gs_push_batch(self._h, node, out, n.value, ctypes.byref(n), ctypes.byref(c)))
+        return split_frames(bytes(out)[:n.value])
+
+    def handle_received(self, node: int, peer: int, message: bytes) -> List[bytes]:
+        """``Gossiper::handle_received_message(peer, message)`` on ``node`` for a
+        peer outside the simulated network (``peer >= n``): the Pull RPCs."""
+        cap = 4096
+        while True:
+            out = (ctypes.c_uint8 * cap)()
+            n, c = ctypes.c_uint32(), ctypes.c_uint32()
+            st = self._lib.gs_handle_received(self._h, node, peer, _buf(message), len(message), out, cap,
+                                              ctypes.byref(n), ctypes.byref(c))
+            if st == 5 and n.value > cap:  # responses larger than the buffer: nothing was applied
+                cap = n.value
+                continue
+            _check(st)
+            return split_frames(bytes(out)[:n.value])
+
     def known_popcounts(self) -> np.ndarray:
         """``Gossiper::messages().len()`` of every node (device popcount)."""
         out = np.zeros(self.n, dtype=np.uint32)
@@ -454,6 +558,15 @@ class Gossiper:
 
     def statistics(self) -> Statistics:
         return self._net.statistics(self._node)
+
+    def push_batch(self) -> List[bytes]:
+        """What ``Gossiper::next_round`` returned this round (its Push RPCs)."""
+        return self._net.push_batch(self._node)
+
+    def handle_received_message(self, peer: int, message: bytes) -> List[bytes]:
+        """``Gossiper::handle_received_message`` (src/gossiper.rs:82-99) from a
+        peer outside the simulated network; returns the Pull responses."""
+        return self._net.handle_received(self._node, peer, message)
 
 
 def send_messages(net: Network, num_of_msgs: int):

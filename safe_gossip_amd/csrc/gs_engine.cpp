@@ -10,6 +10,9 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <set>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -80,6 +83,19 @@ struct gs_engine {
     u64 *inj_host = nullptr;  // pinned staging [2*cap]
     uint32_t inj_cap = 0;
     std::vector<std::pair<uint32_t, uint32_t>> pending;
+    // Wire format (gs_wire.cpp): the message bytes (BTreeMap key) of every
+    // rumor slot, and the external RPCs of the pending round (gs_handle_received)
+    std::vector<std::string> keys;
+    std::map<std::string, uint32_t> key_rumor;
+    std::vector<uint32_t> key_order;        // rumor slots in key (byte) order
+    struct Ext {
+        uint32_t node, seq, info, peer;
+    };
+    std::vector<Ext> ext;                   // in call order
+    std::set<std::pair<uint32_t, uint32_t>> ext_peers;  // (node, peer) heard from this round
+    u64 *ext_dev = nullptr;
+    uint32_t ext_cap = 0, ext_uploaded = 0;
+    uint16_t *node_state = nullptr;         // one node's observed codes [R]
     uint32_t round = 0;
     bool deliver_pending = false;
     // observation buffers (lazy)
@@ -153,7 +169,8 @@ void release(gs_engine *e) {
     if (e->ev_main) (void)hipEventDestroy(e->ev_main);
     if (e->cstream) (void)hipStreamDestroy(e->cstream);
     void *bufs[] = {e->pc, e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
-                    e->partials, e->obs_state, e->obs_rec, e->obs_psize, e->obs_pend};
+                    e->partials, e->obs_state, e->obs_rec, e->obs_psize, e->obs_pend, e->ext_dev,
+                    e->node_state};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (e->inj_host) (void)hipHostFree(e->inj_host);
@@ -183,6 +200,34 @@ gs_status reset_state(gs_engine *e) {
     e->pending.clear();
     e->obs_valid = false;
     e->started = false;
+    e->ext.clear();
+    e->ext_peers.clear();
+    e->ext_uploaded = 0;
+    return GS_OK;
+}
+
+// The pending round's external RPCs, sorted by (node, call order), on the device.
+gs_status upload_ext(gs_engine *e) {
+    const uint32_t m = (uint32_t)e->ext.size();
+    if (m == e->ext_uploaded) return GS_OK;
+    if (m > e->ext_cap) {
+        GS_HIP(hipStreamSynchronize(e->stream));
+        if (e->ext_dev) (void)hipFree(e->ext_dev);
+        e->ext_dev = nullptr;
+        e->ext_cap = 0;
+        const uint32_t cap = std::max<uint32_t>(1024, 2 * m);
+        GS_HIP(dalloc(&e->ext_dev, cap));
+        e->ext_cap = cap;
+    }
+    std::vector<gs_engine::Ext> v(e->ext);
+    std::stable_sort(v.begin(), v.end(), [](const gs_engine::Ext &a, const gs_engine::Ext &b) {
+        return a.node != b.node ? a.node < b.node : a.seq < b.seq;
+    });
+    std::vector<u64> keys(m);
+    for (uint32_t i = 0; i < m; ++i) keys[i] = ((u64)v[i].node << 32) | v[i].info;
+    GS_HIP(hipStreamSynchronize(e->stream));  // the previous upload may still be read
+    GS_HIP(hipMemcpy(e->ext_dev, keys.data(), m * sizeof(u64), hipMemcpyHostToDevice));
+    e->ext_uploaded = m;
     return GS_OK;
 }
 
@@ -237,6 +282,11 @@ gs::RoundArgs base_args(gs_engine *e) {
     }
     a.obs_rounds = e->round;
     a.flags = e->flags;
+    if (e->deliver_pending && !e->ext.empty()) {  // uploaded by the caller (upload_ext)
+        a.ext = e->ext_dev;
+        a.n_ext = e->ext_uploaded;
+    }
+    a.obs_only = 0xFFFFFFFFu;
     a.g = e->g;
     a.seed = e->seed;
     a.epoch = e->epoch;
@@ -351,6 +401,7 @@ gs_status seq_prepare(gs_engine *e) {
 gs_status observe(gs_engine *e, bool dumps) {
     if (e->obs_valid && !dumps) return GS_OK;
     gs_status st = ensure_obs(e, dumps);
+    if (st == GS_OK && e->deliver_pending) st = upload_ext(e);
     if (st != GS_OK) return st;
     gs::RoundArgs a = base_args(e);
     a.obs_known = e->obs_known;
@@ -526,6 +577,17 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
         e->dlv = !off && !e->seq && !e->shard && g.small && g.rpad <= 16 && gs::dlv_plan(n).binned;
     }
     e->plan = e->dlv ? gs::dlv_plan(n) : gs::csr_plan(n);
+    // Default message bytes of rumor slot r: bincode of a 4-byte Vec<u8>
+    // holding r big-endian (u64 length 4, then the bytes), so key order is
+    // slot order.  gs_set_rumor_key replaces them.
+    e->keys.resize(R);
+    e->key_order.resize(R);
+    for (uint32_t r = 0; r < R; ++r) {
+        const char k[12] = {4, 0, 0, 0, 0, 0, 0, 0, (char)(r >> 24), (char)(r >> 16), (char)(r >> 8), (char)r};
+        e->keys[r] = std::string(k, 12);
+        e->key_rumor[e->keys[r]] = r;
+        e->key_order[r] = r;
+    }
     {
         const char *v = std::getenv("SAFE_GOSSIP_AMD_CONCURRENT_INLISTS");
         e->concurrent_inlists = v && *v && *v != '0';
@@ -749,6 +811,7 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
     }
     uint32_t n_inj = 0;
     st = upload_injections(e, &n_inj);
+    if (st == GS_OK && e->deliver_pending) st = upload_ext(e);
     if (st != GS_OK) return st;
     gs::RoundArgs a = base_args(e);
     a.inj_key = e->inj_key;
@@ -780,6 +843,9 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
     e->round += 1;
     e->cur ^= 1;
     e->deliver_pending = true;
+    e->ext.clear();  // delivered by this round kernel (upload_ext syncs before reuse)
+    e->ext_peers.clear();
+    e->ext_uploaded = 0;
     e->obs_valid = false;
     if (++e->since_fold >= e->fold_every) {
         GS_HIP(gs::launch_stats_fold(e->st32, e->st64, e->g.n, e->stream));
@@ -1039,6 +1105,184 @@ float gs_last_round_kernel_ms(gs_engine *e) {
     float ms = -1.0f;
     if (hipEventElapsedTime(&ms, e->ev0, e->ev1) != hipSuccess) return -1.0f;
     return ms;
+}
+
+// ------------------------------------------------------------ wire format
+gs_status gs_set_rumor_key(gs_engine *e, uint32_t rumor, const uint8_t *key, uint32_t len) {
+    if (!e || (len && !key) || rumor >= e->g.R) return GS_ERR_INVALID_ARGUMENT;
+    const std::string k(reinterpret_cast<const char *>(key), len);
+    auto it = e->key_rumor.find(k);
+    if (it != e->key_rumor.end()) return it->second == rumor ? GS_OK : GS_ERR_INVALID_ARGUMENT;
+    e->key_rumor.erase(e->keys[rumor]);
+    e->keys[rumor] = k;
+    e->key_rumor[k] = rumor;
+    std::sort(e->key_order.begin(), e->key_order.end(),
+              [e](uint32_t x, uint32_t y) { return e->keys[x] < e->keys[y]; });  // BTreeMap<Vec<u8>> order
+    return GS_OK;
+}
+
+gs_status gs_rumor_key(const gs_engine *e, uint32_t rumor, uint8_t *out, uint32_t cap, uint32_t *len) {
+    if (!e || !len || rumor >= e->g.R) return GS_ERR_INVALID_ARGUMENT;
+    const std::string &k = e->keys[rumor];
+    *len = (uint32_t)k.size();
+    if (!out || cap < k.size()) return GS_ERR_SERIALISATION;
+    std::memcpy(out, k.data(), k.size());
+    return GS_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Appends one length-prefixed frame (u32 LE size, then the bincode GossipRpc).
+gs_status append_frame(int pull, const std::string &msg, uint8_t counter, uint8_t *out, uint32_t cap,
+                       uint32_t *len) {
+    uint32_t need = 0;
+    gs_rpc_encode(pull, nullptr, 0, 0, nullptr, 0, &need);
+    need += (uint32_t)msg.size();
+    const uint32_t at = *len;
+    *len += 4 + need;
+    if (!out || *len > cap) return GS_ERR_SERIALISATION;  // keep counting the size needed
+    for (int i = 0; i < 4; ++i) out[at + i] = (uint8_t)(need >> (8 * i));
+    uint32_t w = 0;
+    return gs_rpc_encode(pull, reinterpret_cast<const uint8_t *>(msg.data()), (uint32_t)msg.size(), counter,
+                         out + at + 4, need, &w);
+}
+
+// Post-delivery state codes of one node (gs_dump_state's codes), external
+// RPCs queued so far included: the observation kernel over the node's block.
+gs_status observe_node(gs_engine *e, uint32_t node, std::vector<uint16_t> &codes) {
+    gs_status st = upload_ext(e);
+    if (st != GS_OK) return st;
+    if (!e->node_state) GS_HIP(dalloc(&e->node_state, e->g.R));
+    gs::RoundArgs a = base_args(e);
+    a.obs_state = e->node_state;
+    a.obs_only = node;
+    const u64 seg0 = e->g.small ? (u64)node : (u64)node * e->g.W;
+    a.blk_off = (uint32_t)(seg0 / 256);
+    a.blk_count = 1;
+    if (e->deliver_pending) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
+    GS_HIP(gs::launch_round(a, e->deliver_pending ? 2 : 3, e->stream));
+    codes.resize(e->g.R);
+    GS_HIP(hipMemcpyAsync(codes.data(), e->node_state, e->g.R * sizeof(uint16_t), hipMemcpyDeviceToHost,
+                          e->stream));
+    GS_HIP(hipStreamSynchronize(e->stream));
+    return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+gs_status gs_push_batch(gs_engine *e, uint32_t node, uint8_t *out, uint32_t cap, uint32_t *len,
+                        uint32_t *count) {
+    if (!e || !len || !count || node >= e->g.n) return GS_ERR_INVALID_ARGUMENT;
+    if (e->shard) return GS_ERR_UNSUPPORTED;
+    *len = 0;
+    *count = 0;
+    if (e->round == 0) return GS_OK;  // no round run yet: no next_round call, no push batch
+    gs_status st = set_device(e);
+    if (st != GS_OK) return st;
+    if (e->faults.churn && gs::offline_of(e->seed, e->epoch, e->round, node, e->faults.churn))
+        return GS_OK;  // the harness skipped this node's next_round
+    // the planes of round t after phase 0 = Gossip::next_round's push list
+    const gs::Geometry &g = e->g;
+    std::vector<u64> w((size_t)gs::kPlanes * g.W);
+    uint32_t sh = 0;
+    if (g.small) {
+        GS_HIP(hipMemcpy(w.data(), e->S[e->cur] + (u64)(node >> g.lognpu) * gs::kPlanes,
+                         gs::kPlanes * sizeof(u64), hipMemcpyDeviceToHost));
+        sh = (node & ((1u << g.lognpu) - 1u)) << g.logr;
+    } else {
+        GS_HIP(hipMemcpy(w.data(), e->S[e->cur] + (u64)node * gs::kPlanes * g.W, w.size() * sizeof(u64),
+                         hipMemcpyDeviceToHost));
+    }
+    auto bit = [&](int p, uint32_t r) -> uint32_t {
+        return g.small ? (uint32_t)((w[p] >> (sh + r)) & 1u) : (uint32_t)((w[(size_t)p * g.W + (r >> 6)] >> (r & 63)) & 1u);
+    };
+    gs_status res = GS_OK;
+    for (uint32_t r : e->key_order) {  // src/gossip.rs:93-98, in map (key) order
+        const uint32_t c = bit(0, r), a0 = bit(1, r), a1 = bit(2, r);
+        if (!c && (a0 | a1)) {  // B: our_counter
+            if (append_frame(0, e->keys[r], (uint8_t)(a0 | (a1 << 1)), out, cap, len) != GS_OK) res = GS_ERR_SERIALISATION;
+            ++*count;
+        } else if (c && !(a0 & a1)) {  // C: 255
+            if (append_frame(0, e->keys[r], 255, out, cap, len) != GS_OK) res = GS_ERR_SERIALISATION;
+            ++*count;
+        }
+    }
+    if (*count == 0) {  // an empty Push: a fetch request (src/gossip.rs:104-111)
+        if (append_frame(0, std::string(), 0, out, cap, len) != GS_OK) res = GS_ERR_SERIALISATION;
+        *count = 1;
+    }
+    return res;
+}
+
+gs_status gs_handle_received(gs_engine *e, uint32_t node, uint32_t peer, const uint8_t *msg, uint32_t msg_len,
+                             uint8_t *out, uint32_t cap, uint32_t *out_len, uint32_t *out_count) {
+    if (!e || !msg || !out_len || !out_count || node >= e->g.n) return GS_ERR_INVALID_ARGUMENT;
+    *out_len = 0;
+    *out_count = 0;
+    if (e->shard || e->seq) return GS_ERR_UNSUPPORTED;
+    if (peer < e->g.n) return GS_ERR_INVALID_ARGUMENT;  // peers outside the simulated network
+    if (e->round == 0 || !e->deliver_pending) return GS_ERR_INVALID_ARGUMENT;  // after a next_round
+    int pull = 0;
+    uint32_t off = 0, mlen = 0;
+    uint8_t counter = 0;
+    // Message::deserialise failure: the reference logs it and returns no RPC
+    // (src/gossiper.rs:89-94)
+    gs_status st = gs_rpc_decode(msg, msg_len, &pull, &off, &mlen, &counter);
+    if (st != GS_OK) return st;
+    const bool empty = mlen == 0 && counter == 0;  // src/gossip.rs:153-154
+    uint32_t rumor = 0;
+    if (!empty) {
+        auto it = e->key_rumor.find(std::string(reinterpret_cast<const char *>(msg + off), mlen));
+        if (it == e->key_rumor.end()) return GS_ERR_INVALID_ARGUMENT;  // no rumor slot for this message
+        rumor = it->second;
+    }
+    // churn: a node the harness took offline this round receives nothing (its
+    // internal RPCs are dropped too); the RPC is dropped without effect
+    if (e->faults.churn && gs::offline_of(e->seed, e->epoch, e->round, node, e->faults.churn)) return GS_OK;
+    st = set_device(e);
+    if (st != GS_OK) return st;
+    const bool is_new = e->ext_peers.insert({node, peer}).second;  // src/gossip.rs:125
+    if (is_new && !pull) {
+        // Pull responses: the node's live entries now (src/gossip.rs:126-148)
+        std::vector<uint16_t> codes;
+        st = observe_node(e, node, codes);
+        if (st != GS_OK) return st;
+        gs_status res = GS_OK;
+        for (uint32_t r : e->key_order) {
+            const uint32_t tag = codes[r] >> 14;
+            if (tag == 1 || tag == 2) {
+                const uint8_t c = tag == 1 ? (uint8_t)((codes[r] >> 7) & 0x7Fu) : 255;
+                if (append_frame(1, e->keys[r], c, out, cap, out_len) != GS_OK) res = GS_ERR_SERIALISATION;
+                ++*out_count;
+            }
+        }
+        if (*out_count == 0) {
+            if (append_frame(1, std::string(), 0, out, cap, out_len) != GS_OK) res = GS_ERR_SERIALISATION;
+            *out_count = 1;
+        }
+        if (res != GS_OK) {  // out too small: nothing is queued; *out_len holds the size needed
+            e->ext_peers.erase({node, peer});
+            return res;
+        }
+    }
+    uint32_t info = (pull ? 0u : gs::kExtPush) | (is_new ? gs::kExtNew : 0u);
+    if (empty) {
+        info |= gs::kExtEmpty;
+    } else {
+        info |= rumor | ((uint32_t)counter << 12) | gs::kExtRec;
+        // only the last copy from a peer is kept in peer_counters (BTreeMap::insert)
+        for (auto &x : e->ext)
+            if (x.node == node && x.peer == peer && !(x.info & gs::kExtEmpty) && (x.info & 0xFFFu) == rumor)
+                x.info &= ~gs::kExtRec;
+    }
+    e->ext.push_back({node, (uint32_t)e->ext.size(), info, peer});
+    e->ext_uploaded = (uint32_t)-1;  // re-upload
+    e->obs_valid = false;
+    return GS_OK;
 }
 
 double gs_round_kernel_bytes(const gs_engine *e) {

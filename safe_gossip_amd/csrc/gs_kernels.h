@@ -49,12 +49,21 @@ struct RoundArgs {
     // code [n][2][W], and per node got << 7 | dep << 6 | level
     const u64 *Wb;
     const uint8_t *sinfo;
+    // External RPCs of round t (gs_handle_received), applied after every
+    // internal delivery: sorted keys node << 32 | info, info = rumor (12 bits)
+    // | counter << 12 | push << 20 | new peer << 21 | record << 22 | empty << 23
+    const u64 *ext;
+    uint32_t n_ext;
+    // launch only blocks [blk_off, blk_off + blk_count) (0: all), and with
+    // obs_only != ~0 observe only that node (its codes at obs_state[0..R))
+    uint32_t blk_off, blk_count, obs_only;
     Geometry g;
     uint64_t seed;
     uint32_t epoch;
     uint32_t round_new;       // t+1
     uint32_t cmax, maxc, maxr;
 };
+constexpr uint32_t kExtPush = 1u << 20, kExtNew = 1u << 21, kExtRec = 1u << 22, kExtEmpty = 1u << 23;
 
 // mode: 0 = transition only (first round), 1 = deliver round t + transition
 // to t+1, 2 = deliver round t and write observation outputs only,

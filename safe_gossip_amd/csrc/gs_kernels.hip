@@ -157,7 +157,8 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     constexpr bool DELIVER = (MODE == 1 || MODE == 2);
     constexpr bool TRANSITION = (MODE == 0 || MODE == 1);
     const Geometry &g = a.g;
-    const u64 seg = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t bid = blockIdx.x + a.blk_off;
+    const u64 seg = (u64)bid * blockDim.x + threadIdx.x;
     const bool valid = seg < g.nseg;
     Lane<SMALL> L;
     L.init(g, valid ? seg : 0);
@@ -170,7 +171,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     // eight strided 8-byte loads per lane.
     __shared__ __attribute__((aligned(16))) u64 stage[kBlockWords];
     const uint32_t npu_blk = SMALL ? (1u << g.lognpu) : 1u;
-    const u64 blk_base = (u64)blockIdx.x * (kBlockWords / npu_blk);
+    const u64 blk_base = (u64)bid * (kBlockWords / npu_blk);
     const uint32_t blk_v4 = (uint32_t)min((u64)(kBlockWords / npu_blk),
                                           g.units * kPlanes * (SMALL ? 1u : g.W) - blk_base) / 2u;
     static_assert(kStageIters == 4, "stage loads are unrolled by hand");
@@ -314,6 +315,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     Recv<!TRANSITION> rv;
     rv.init(A, B, B & a0 & ~a1);
     uint32_t psize = 0;
+    uint32_t ext_new = 0, ext_full = 0, ext_empty = 0, ext_recv = 0;  // external RPCs (node level)
     bool seq_gx = false, seq_skip = false;
     uint32_t seq_px = 0, seq_jz = kNone;
     if (DELIVER && valid) {
@@ -481,8 +483,43 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             rv.create(newc, pCl);
         }
         rv.recv += popc(pl);
+        if (!SHARD && !SEQ && a.n_ext) {
+            // External RPCs to x (gs_handle_received), after every internal
+            // delivery of the round, in call order (Gossip::receive,
+            // src/gossip.rs:118-163): a first RPC from a peer joins
+            // peers_in_this_round; a first Push is answered with x's live set
+            // at that point; a copy creates an absent entry (new_from_peer, not
+            // recorded) or is recorded on a B entry (the last copy per peer).
+            uint32_t lo = 0, hi = a.n_ext;
+            const u64 key = (u64)x << 32;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (a.ext[mid] < key) lo = mid + 1; else hi = mid;
+            }
+            for (uint32_t i = lo; i < a.n_ext && (uint32_t)(a.ext[i] >> 32) == x; ++i) {
+                const uint32_t info = (uint32_t)a.ext[i];
+                if (info & kExtNew) ++ext_new;
+                if ((info & kExtPush) && (info & kExtNew)) {
+                    uint32_t cnt = popc((B | C | rv.crB | rv.crC) & L.m);
+                    if (!SMALL) cnt = group_sum(cnt, g.W);
+                    if (cnt) ext_full += cnt; else ++ext_empty;
+                }
+                if (info & kExtEmpty) continue;
+                ++ext_recv;
+                const uint32_t r = info & 0xFFFu, c = (info >> 12) & 0xFFu;
+                if ((SMALL ? 0u : (r >> 6)) != L.j) continue;
+                const u64 bit = 1ull << (SMALL ? r : (r & 63u));
+                // a counter >= counter_max acts as C (anyC); 0 creates B and votes "less"
+                const u64 vC = c >= a.cmax ? bit : 0ull;
+                const u64 vB = (c >= 1u && c < a.cmax) ? bit : 0ull;
+                const u64 v2 = (c == 2u && c < a.cmax) ? bit : 0ull;
+                const u64 newc = rv.notyet & bit;
+                rv.record(rv.recB & bit & ((info & kExtRec) ? ~0ull : 0ull), vB, v2, vC);
+                rv.create(newc, vC);
+            }
+        }
         const bool gets = SEQ ? seq_gx : pulled;
-        psize = k + ((gets && !zin) ? 1u : 0u);  // |peers_in_this_round|
+        psize = k + ((gets && !zin) ? 1u : 0u) + ext_new;  // |peers_in_this_round|
     }
     const u64 crB = rv.crB, crC = rv.crC, anyC = rv.anyC;
 
@@ -517,11 +554,35 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         if (k > 0 && lc == 0) d_empty_pull = (first_create == kNone) ? k : first_create + 1u;
         d_recv = recv;
     }
+    d_full_sent += ext_full;
+    d_empty_pull += ext_empty;
+    d_recv += ext_recv;
     const bool leader = valid && (SMALL || L.j == 0);
 
     if (!TRANSITION) {
         // ---------------- observation (post phase 2 of round t) -------------
         if (!valid) return;
+        if (a.obs_only != 0xFFFFFFFFu) {  // one node's state codes only (obs_state[0..R))
+            if (x != a.obs_only) return;
+            const uint32_t nb = SMALL ? g.rpad : 64u;
+            for (uint32_t b = 0; b < nb; ++b) {
+                const uint32_t rr = SMALL ? b : L.j * 64u + b;
+                if (rr >= g.R) break;
+                const u64 bit = 1ull << b;
+                uint32_t bf = 0;
+#pragma unroll
+                for (int i = 0; i < 5; ++i) bf |= (uint32_t)((P[3 + i] >> b) & 1u) << i;
+                const uint32_t af = (uint32_t)((a0 >> b) & 1u) | ((uint32_t)((a1 >> b) & 1u) << 1);
+                uint16_t code = 0;
+                if (crB & bit) code = (uint16_t)((1u << 14) | (1u << 7));
+                else if (crC & bit) code = (uint16_t)(2u << 14);
+                else if (B & bit) code = (uint16_t)((1u << 14) | (af << 7) | bf);
+                else if (C & bit) code = (uint16_t)((2u << 14) | (af << 7) | bf);
+                else if (D & bit) code = (uint16_t)(3u << 14);
+                a.obs_state[rr] = code;
+            }
+            return;
+        }
         const uint32_t KW = (g.R + 63u) >> 6;
         const u64 known = (~A | crB | crC) & L.m;
         if (a.obs_known && (SMALL || L.j < KW)) a.obs_known[(u64)x * KW + L.j] = known;
@@ -713,7 +774,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     }
 
     // ---- push list + Statistics (src/gossip.rs:80,103-111)
-    if (blockIdx.x == 0 && threadIdx.x == 0)  // slot of round t, read by the host already
+    if (bid == 0 && threadIdx.x == 0)  // slot of round t, read by the host already
         __hip_atomic_store(&a.flags[(a.round_new + 1u) & 1u], 0u, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 0 && blk_live) {
@@ -740,7 +801,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
 template <bool SMALL, bool SHARD, bool SEQ, bool DLV = false>
 static hipError_t launch_mode(const RoundArgs &a, int mode, hipStream_t s) {
     const uint32_t block = 256;
-    const u64 grid = (a.g.nseg + block - 1) / block;
+    const u64 grid = a.blk_count ? a.blk_count : (a.g.nseg + block - 1) / block;
     if (grid == 0) return hipSuccess;
     switch (mode) {
     case 0: hipLaunchKernelGGL((round_kernel<SMALL, 0, SHARD, SEQ, DLV>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;

@@ -65,6 +65,11 @@ _SIGS = {
                                    ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                    ctypes.c_uint32]),
     "or_set_faults": (None, [_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
+    "or_push_list": (None, [_P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int32),
+                            ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_uint32)]),
+    "or_receive": (None, [_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int32,
+                          ctypes.c_uint8, ctypes.POINTER(ctypes.c_int32),
+                          ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_uint32)]),
     "or_derive_params": (None, [ctypes.c_uint32, _U8P]),
     # gs_dense.c: the dense bit-sliced OpenMP CPU line
     "dn_create": (_P, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32]),
@@ -216,6 +221,23 @@ class OracleNet:
 
     def known_total(self):
         return int(self._l.or_known_total(self.h))
+
+    def push_list(self, node):
+        """[(rumor or -1 for the empty Push, counter)] node pushes this round."""
+        r = (ctypes.c_int32 * (self.R + 1))()
+        c = (ctypes.c_uint8 * (self.R + 1))()
+        m = ctypes.c_uint32()
+        self._l.or_push_list(self.h, node, r, c, ctypes.byref(m))
+        return [(r[i], c[i]) for i in range(m.value)]
+
+    def receive(self, node, peer, push, rumor, counter):
+        """Gossip::receive of one RPC (rumor -1 = empty) from `peer` on
+        `node`; returns the Pull responses [(rumor or -1, counter)]."""
+        r = (ctypes.c_int32 * (self.R + 1))()
+        c = (ctypes.c_uint8 * (self.R + 1))()
+        m = ctypes.c_uint32()
+        self._l.or_receive(self.h, node, peer, 1 if push else 0, rumor, counter, r, c, ctypes.byref(m))
+        return [(r[i], c[i]) for i in range(m.value)]
 
     def send_messages(self, num_msgs, schedule=SCHED_SEQ):
         m = OrMetrics()

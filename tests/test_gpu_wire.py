@@ -1,0 +1,153 @@
+"""Byte-level boundary on the GPU engine, against the CPU oracle:
+
+* gs_push_batch = the bincode Push RPCs ``Gossiper::next_round`` returns
+  (src/gossiper.rs:70-79, src/gossip.rs:79-113), in message-key order;
+* gs_handle_received = ``Gossiper::handle_received_message`` (src/gossiper.rs:
+  82-99 -> src/gossip.rs:118-166) from peers outside the simulated network,
+  applied after the round's internal deliveries: the Pull responses must be
+  the oracle's, and the state, records, |P|, Statistics and known sets after
+  them -- and every later round -- must stay bit-exact.
+"""
+import numpy as np
+import pytest
+
+from oracle_lib import SCHED_2P, OracleNet
+from test_gpu_parity import SEED
+
+pytestmark = pytest.mark.gpu
+
+
+def _decode_batch(engine, net, frames, pull):
+    key_rumor = {net.rumor_key(r): r for r in range(net.R)}
+    out = []
+    for f in frames:
+        p, msg, ctr = engine.rpc_decode(f)
+        assert p == pull
+        out.append((-1 if (msg == b"" and ctr == 0) else key_rumor[msg], ctr))
+    return out
+
+
+def _key_sorted(net, lst):
+    # the oracle's maps are in rumor-index order; the reference's in key order
+    return sorted(lst, key=lambda rc: net.rumor_key(rc[0]) if rc[0] >= 0 else b"")
+
+
+def _compare(net, orc, off=None):
+    """Records and |P| of nodes offline this round are the oracle's stale
+    ones (see test_gpu_parity.run_parity); their state is compared."""
+    np.testing.assert_array_equal(net.dump_state(), orc.dump_state())
+    grec, gps = net.dump_records()
+    orec, ops = orc.dump_records()
+    if off is not None:
+        grec[off] = orec[off] = 0
+        gps[off] = ops[off] = 0
+    np.testing.assert_array_equal(gps, ops)
+    np.testing.assert_array_equal(grec, orec)
+    np.testing.assert_array_equal(net.statistics_all(), orc.statistics())
+    np.testing.assert_array_equal(net.known_all(), orc.known_all())
+
+
+@pytest.mark.parametrize("n,R,faults,custom_keys", [
+    (300, 16, None, False),          # delivery-record path
+    (200, 64, None, True),           # gather path, keys whose byte order is not slot order
+    (150, 130, (0.1, 0.05, 0.05), False),
+    (400, 8, (0.05, 0.05, 0.1), True),
+])
+def test_push_batches_match_oracle(engine, n, R, faults, custom_keys):
+    fk = dict(churn=faults[0], drop_push=faults[1], drop_pull=faults[2]) if faults else {}
+    from oracle_lib import fault_threshold
+    net = engine.Network(n, R, seed=SEED, **fk)
+    orc = OracleNet(n, R, seed=SEED, faults=[fault_threshold(p) for p in faults] if faults else None)
+    rng = np.random.default_rng(n + R)
+    if custom_keys:
+        for r in range(R):
+            net.set_rumor_key(r, bytes(rng.integers(0, 256, size=int(rng.integers(1, 30)), dtype=np.uint8)))
+    try:
+        for r in range(R):
+            x = engine.origin_of(SEED, 0, r, n)
+            net.send_new(x, r)
+            orc.send_new(x, r)
+        for rnd in range(8):
+            net.next_round()
+            orc.next_round(SCHED_2P)
+            for x in list(range(0, n, max(1, n // 40))) + [n - 1]:
+                got = _decode_batch(engine, net, net.push_batch(x), pull=False)
+                exp = _key_sorted(net, orc.push_list(x))
+                assert got == exp, f"round {rnd + 1} node {x}: {got} vs {exp}"
+    finally:
+        net.close()
+        orc.close()
+
+
+@pytest.mark.parametrize("n,R,faults", [
+    (300, 16, None),                  # delivery-record path
+    (250, 64, None),                  # gather path, one word
+    (120, 200, (0.05, 0.05, 0.05)),   # several words, faults
+    (500, 4, (0.1, 0.1, 0.1)),
+])
+def test_handle_received_matches_oracle(engine, n, R, faults):
+    from oracle_lib import fault_threshold
+    fk = dict(churn=faults[0], drop_push=faults[1], drop_pull=faults[2]) if faults else {}
+    net = engine.Network(n, R, seed=SEED, **fk)
+    orc = OracleNet(n, R, seed=SEED, faults=[fault_threshold(p) for p in faults] if faults else None)
+    rng = np.random.default_rng(7 * n + R)
+    params = net.params
+    try:
+        for r in range(0, R, 2):  # half the rumors start inside the network
+            x = engine.origin_of(SEED, 0, r, n)
+            net.send_new(x, r)
+            orc.send_new(x, r)
+        for rnd in range(1, 10):
+            net.next_round()
+            orc.next_round(SCHED_2P)
+            off = orc.offline(rnd) if faults else np.zeros(n, dtype=bool)
+            if rnd in (2, 3, 5):
+                # external peers n+1.. push / pull single rumors (some twice,
+                # some empty) into a few nodes, after the round's deliveries
+                for _ in range(25):
+                    y = int(rng.integers(n))
+                    peer = n + 1 + int(rng.integers(6))
+                    push = bool(rng.random() < 0.6)
+                    if rng.random() < 0.15:
+                        rumor, ctr = -1, 0
+                    else:
+                        rumor = int(rng.integers(R))
+                        ctr = int(rng.choice([0, 1, 2, 3, 7, 255, params[0] - 1 if params[0] > 1 else 1]))
+                    msg = b"" if rumor < 0 else net.rumor_key(rumor)
+                    got = _decode_batch(engine, net, net.handle_received(y, peer, engine.rpc_encode(not push, msg, ctr)),
+                                        pull=True)
+                    # a node offline this round (churn) drops it, like every RPC to it
+                    exp = [] if off[y] else orc.receive(y, peer, push, rumor, ctr)
+                    assert got == _key_sorted(net, exp), f"round {rnd} node {y} peer {peer}"
+            if rnd in (2, 3, 5) or rnd % 2 == 0:
+                _compare(net, orc, off)
+    finally:
+        net.close()
+        orc.close()
+
+
+def test_handle_received_errors(engine):
+    net = engine.Network(50, 8, seed=SEED)
+    try:
+        msg = engine.rpc_encode(False, net.rumor_key(3), 1)
+        with pytest.raises(engine.DeviceError, match="status -1"):
+            net.handle_received(0, 55, msg)        # before the first round
+        net.next_round()
+        with pytest.raises(engine.DeviceError, match="status -1"):
+            net.handle_received(0, 10, msg)        # peer inside the simulated network
+        with pytest.raises(engine.DeviceError, match="status -1"):
+            net.handle_received(0, 55, engine.rpc_encode(False, b"no such rumor", 1))
+        with pytest.raises(engine.GossipError, match="status 5"):
+            net.handle_received(0, 55, b"\x07\x00")  # undecodable
+        # a first Push from a new peer is answered: node 0 knows nothing yet
+        assert net.handle_received(0, 55, msg) == [engine.rpc_encode(True, b"", 0)]
+        # its copy created rumor 3 at node 0, visible at once
+        assert 3 in net.gossiper(0).messages()
+        # a second Push from the same peer this round gets no responses
+        assert net.handle_received(0, 55, engine.rpc_encode(False, net.rumor_key(5), 1)) == []
+        # a Pull never gets responses
+        assert net.handle_received(1, 56, engine.rpc_encode(True, net.rumor_key(5), 255)) == []
+        with pytest.raises(engine.DeviceError, match="status -1"):
+            net.set_rumor_key(2, net.rumor_key(3))  # keys are distinct
+    finally:
+        net.close()
