@@ -254,7 +254,12 @@ def main():
     # to deliver); that is the dominant kernel the roofline describes.
     kt = ktimes[1:] if len(ktimes) > 1 else ktimes
     kernel_ms = float(np.mean(kt)) if len(kt) else float("nan")
-    bytes_per = net.round_kernel_bytes()
+    bytes_dense = net.round_kernel_bytes()
+    # algorithmic bytes the timed launches had to move: with sparse records
+    # (wide 2P engine) words known to be zero are neither read nor rewritten
+    # and empty pushes are not gathered, so this is counted by the kernels
+    bytes_per, launches = (net.round_traffic() if hasattr(net, "round_traffic")
+                           else (bytes_dense, 0))
     achieved = bytes_per / (kernel_ms * 1e-3) / 1e9
 
     spread = None if args.no_spread else spread_run(net, epoch)
@@ -309,6 +314,10 @@ def main():
                 "kernel": "round_kernel<%s,1> (deliver round t + transition to t+1)"
                           % ("true" if R < 64 else "false"),
                 "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": bytes_per,
+                "bytes_counted_by": ("kernels (sparse records), %d launches" % launches) if launches
+                                    else "static model",
+                "dense_model_bytes_per_launch": bytes_dense,
+                "kernel_ms_per_round": [round(float(v), 4) for v in kt],
             },
             "cpu_baseline": cpu,
             "cpu_best": best,

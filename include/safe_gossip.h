@@ -162,6 +162,12 @@ void        gs_set_timing(gs_engine *e, int enable);
 int32_t     gs_round_kernel_times(gs_engine *e, float *out_ms, uint32_t max);
 /* Algorithmic HBM bytes of one round kernel (DESIGN.md, section Roofline). */
 double      gs_round_kernel_bytes(const gs_engine *e);
+/* Algorithmic HBM bytes per deliver+transition round kernel launched since
+ * gs_set_timing(e, 1), as counted by the kernels: with sparse records (the
+ * wide 2P engine) words known to be zero are neither read nor rewritten and
+ * pushers with nothing live are not gathered, so the bytes depend on the
+ * state; otherwise gs_round_kernel_bytes (and *launches = 0).  Synchronises. */
+gs_status   gs_round_traffic(gs_engine *e, double *bytes_per_launch, uint32_t *launches);
 
 /* ---- Sharded network (multi-GPU): one engine per rank owns the node range
  * [lo, lo+m).  Per round t the caller moves two sets of rows between ranks

@@ -121,6 +121,7 @@ SYMBOLS = {
     "gs_set_timing": (None, [_P, ctypes.c_int]),
     "gs_round_kernel_times": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_float), ctypes.c_uint32]),
     "gs_round_kernel_bytes": (ctypes.c_double, [_P]),
+    "gs_round_traffic": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), _U32P]),
     "gs_peer": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.c_uint32, ctypes.c_uint32]),
     "gs_origin": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
@@ -537,6 +538,14 @@ class Network:
 
     def round_kernel_bytes(self) -> float:
         return float(self._lib.gs_round_kernel_bytes(self._h))
+
+    def round_traffic(self):
+        """(algorithmic bytes per deliver+transition launch since set_timing(True),
+        launches counted): the bytes sparse records let the kernels skip are
+        not counted; launches = 0 means the static model (round_kernel_bytes)."""
+        b, m = ctypes.c_double(), ctypes.c_uint32()
+        _check(self._lib.gs_round_traffic(self._h, ctypes.byref(b), ctypes.byref(m)))
+        return float(b.value), int(m.value)
 
 
 class Gossiper:

@@ -18,35 +18,32 @@ GS_DEV void add5(u64 (&c)[5], u64 in) {
     }
 }
 
-// Bit-sliced "x >= K" for an nb-bit number per rumor, K a per-lane constant.
+// Bit-sliced "x >= K" for an NB-bit number per rumor, K a per-lane constant:
+// the borrow of x - K, LSB first (borrow' = k ? ~x | b : ~x & b, one 3-input
+// op per 32-bit half and bit), x >= K iff no final borrow.
 template <int NB>
 GS_DEV u64 ge_k(const u64 (&x)[NB], uint32_t K) {
-    if (K >= (1u << NB)) return 0ull;
-    u64 gt = 0ull, eq = ~0ull;
+    u64 b = 0ull;
 #pragma unroll
-    for (int i = NB - 1; i >= 0; --i) {
-        u64 ki = ((K >> i) & 1u) ? ~0ull : 0ull;
-        gt |= eq & x[i] & ~ki;
-        eq &= ~(x[i] ^ ki);
+    for (int i = 0; i < NB; ++i) {
+        const uint32_t m = 0u - ((K >> i) & 1u);
+        const u64 k = ((u64)m << 32) | m;
+        b = (~x[i] & b) | (k & (~x[i] | b));
     }
-    return gt | eq;
+    return K >= (1u << NB) ? 0ull : ~b;
 }
 
-// Same with K wave-uniform (max_rounds, max_c_rounds): scalar branches on the
-// bits of K, 2 ops per bit.
+// Same with K wave-uniform (max_rounds, max_c_rounds): the masks are scalar.
 template <int NB>
 GS_DEV u64 ge_u(const u64 (&x)[NB], uint32_t K) {
     if (K >= (1u << NB)) return 0ull;
-    u64 gt = 0ull, eq = ~0ull;
+    u64 b = 0ull;
 #pragma unroll
-    for (int i = NB - 1; i >= 0; --i) {
-        if ((K >> i) & 1u) {
-            eq &= x[i];
-        } else {
-            gt |= eq & x[i];
-        }
+    for (int i = 0; i < NB; ++i) {
+        const u64 k = ((K >> i) & 1u) ? ~0ull : 0ull;
+        b = (~x[i] & b) | (k & (~x[i] | b));
     }
-    return gt | eq;
+    return ~b;
 }
 
 struct Cls {
@@ -73,14 +70,18 @@ struct Lane {
             sh = (x & ((1u << lognpu) - 1u)) << logr;
             m = (1ull << g.rpad) - 1ull;  // rpad < 64 here
         } else {
-            x = (uint32_t)(seg / W);
-            j = (uint32_t)(seg % W);
-            base = (u64)x * kPlanes * W + j;
+            // W = 2^(logr - 6): shifts, not a 64-bit division by a runtime W
+            const uint32_t lw = logr - 6u;
+            x = (uint32_t)(seg >> lw);
+            j = (uint32_t)seg & (W - 1u);
+            base = ((u64)x << (lw + 3u)) + j;
             sh = 0;
             m = ~0ull;
         }
     }
-    GS_DEV u64 plane_index(uint32_t p) const { return SMALL ? base + p : base + (u64)p * W; }
+    GS_DEV u64 plane_index(uint32_t p) const {
+        return SMALL ? base + p : base + ((u64)p << (logr - 6u));
+    }
     // Exchange rows (SHARD): row e holds `np` planes of W words, [e][np][W]; a
     // node with R < 64 keeps its segment in the low bits of one word per plane.
     GS_DEV u64 row_index(uint32_t e, uint32_t np, uint32_t p) const {
@@ -104,7 +105,8 @@ struct Lane {
             r.a0 = (S[b + 1] >> ss) & m;
             r.a1 = (S[b + 2] >> ss) & m;
         } else {
-            u64 b = (u64)s * kPlanes * W + j;
+            const uint32_t lw = logr - 6u;
+            u64 b = ((u64)s << (lw + 3u)) + j;
             r.c = S[b];
 #if defined(GS_EXP_G1)
             r.a0 = r.c >> 1;

@@ -50,6 +50,25 @@ struct gs_engine {
         uint32_t serial = 0;
     } csr[2];
     bool dlv = false;  // delivery-record path (2P, R_pad <= 16, binned in-lists)
+    // Sparse records (wide 2P engine, W <= 8; gs_kernels.h RoundArgs): maps of
+    // plane buffer i, the accounting words and MODE-1 launches counted in them
+    // The sparse variant runs while the input planes are at least a quarter
+    // zero words (spr_active); zero words only decrease within a dissemination
+    // (A never returns), so once the dense variant takes over the maps are not
+    // kept again until the next reset.  The decision for round t+2 reads the
+    // density of round t's planes (copied to pinned memory, one round behind,
+    // so the host never waits on the running kernel).
+    bool spr = false;         // maps allocated (eligible engine, not disabled)
+    bool spr_always = false;  // SAFE_GOSSIP_AMD_SPARSE=on: never switch to dense
+    bool spr_active = false;
+    u64 *zb[2] = {nullptr, nullptr};
+    uint8_t *lb[2] = {nullptr, nullptr}, *ab[2] = {nullptr, nullptr};
+    u64 *acct = nullptr;
+    uint32_t acct_launches = 0, dense_launches = 0;  // mode-1 launches since set_timing(1)
+    u64 *dens = nullptr;       // [2][kDensSlots], by parity of the round written
+    u64 *dens_host = nullptr;  // pinned copy [2][kDensSlots]
+    hipEvent_t ev_dens[2] = {nullptr, nullptr};
+    uint32_t dens_round[2] = {0, 0};  // round whose density each slot holds (0: none)
     uint32_t *pc = nullptr;  // DLV: push codes of the current round [n]
     hipStream_t cstream = nullptr;
     hipEvent_t ev_built[2] = {nullptr, nullptr};  // set i complete
@@ -168,7 +187,10 @@ void release(gs_engine *e) {
     }
     if (e->ev_main) (void)hipEventDestroy(e->ev_main);
     if (e->cstream) (void)hipStreamDestroy(e->cstream);
-    void *bufs[] = {e->pc, e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
+    for (int i = 0; i < 2; ++i)
+        if (e->ev_dens[i]) (void)hipEventDestroy(e->ev_dens[i]);
+    if (e->dens_host) (void)hipHostFree(e->dens_host);
+    void *bufs[] = {e->zb[0], e->zb[1], e->lb[0], e->lb[1], e->ab[0], e->ab[1], e->acct, e->dens, e->pc, e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
                     e->partials, e->obs_state, e->obs_rec, e->obs_psize, e->obs_pend, e->ext_dev,
                     e->node_state};
     for (void *b : bufs)
@@ -192,6 +214,15 @@ gs_status reset_state(gs_engine *e) {
     if (e->offc) GS_HIP(hipMemsetAsync(e->offc, 0, (size_t)g.n * sizeof(uint32_t), e->stream));
     e->since_fold = 0;
     GS_HIP(hipMemsetAsync(e->flags, 0, 4 * sizeof(uint32_t), e->stream));
+    if (e->spr) {  // both plane buffers are zero: every word zero, no node live
+        for (int i = 0; i < 2; ++i) {
+            GS_HIP(hipMemsetAsync(e->zb[i], 0xFF, gs::spr_zb_words(g) * sizeof(u64), e->stream));
+            GS_HIP(hipMemsetAsync(e->lb[i], 0, gs::spr_node_bytes(g), e->stream));
+            GS_HIP(hipMemsetAsync(e->ab[i], 0xFF, gs::spr_node_bytes(g), e->stream));
+        }
+        e->spr_active = true;
+        e->dens_round[0] = e->dens_round[1] = 0;
+    }
     e->cur = 0;
     e->round = 0;
     e->seq_round = ~0u;
@@ -577,6 +608,17 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
         e->dlv = !off && !e->seq && !e->shard && g.small && g.rpad <= 16 && gs::dlv_plan(n).binned;
     }
     e->plan = e->dlv ? gs::dlv_plan(n) : gs::csr_plan(n);
+    {
+        // Sparse records on the wide 2P path (W <= 8, so a wave's node bits
+        // are whole bytes).  SAFE_GOSSIP_AMD_SPARSE = off (default) | dense
+        // (same) | auto (the sparse variant while a quarter of the words are
+        // unknown) | on (the sparse variant every round).  Opt-in: measured
+        // slower than the dense variant at config 4.
+        const char *v = std::getenv("SAFE_GOSSIP_AMD_SPARSE");
+        const std::string m = v ? v : "off";
+        e->spr = m != "off" && m != "dense" && !e->seq && !e->shard && !e->dlv && !g.small && g.W <= 8;
+        e->spr_always = m == "on";
+    }
     // Default message bytes of rumor slot r: bincode of a 4-byte Vec<u8>
     // holding r big-endian (u64 length 4, then the bytes), so key order is
     // slot order.  gs_set_rumor_key replaces them.
@@ -629,6 +671,17 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
          dalloc(&e->flags, 4) == hipSuccess && dalloc(&e->st32, (size_t)4 * n) == hipSuccess &&
          dalloc(&e->st64, (size_t)4 * n) == hipSuccess;
     if (ok && e->dlv) ok = dalloc(&e->pc, n) == hipSuccess;
+    for (int i = 0; i < 2 && ok && e->spr; ++i)
+        ok = dalloc(&e->zb[i], gs::spr_zb_words(g)) == hipSuccess &&
+             dalloc(&e->lb[i], gs::spr_node_bytes(g)) == hipSuccess &&
+             dalloc(&e->ab[i], gs::spr_node_bytes(g)) == hipSuccess;
+    if (ok && e->spr)
+        ok = dalloc(&e->dens, 2 * gs::kDensSlots) == hipSuccess &&
+             hipHostMalloc((void **)&e->dens_host, 2 * gs::kDensSlots * sizeof(u64), 0) == hipSuccess &&
+             hipEventCreateWithFlags(&e->ev_dens[0], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&e->ev_dens[1], hipEventDisableTiming) == hipSuccess &&
+             dalloc(&e->acct, gs::kAcctSlots) == hipSuccess &&
+             hipMemset(e->acct, 0, gs::kAcctSlots * sizeof(u64)) == hipSuccess;
     if (ok && e->seq)
         ok = dalloc(&e->Wb, (size_t)n * 2 * g.W) == hipSuccess && dalloc(&e->sinfo, n) == hipSuccess &&
              dalloc(&e->seqw, (size_t)gs::seq_blocks(n) * gs::kSeqLists + gs::kSeqLists + n) == hipSuccess;
@@ -817,13 +870,41 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
     a.inj_key = e->inj_key;
     a.inj_mask = e->inj_mask;
     a.n_inj = n_inj;
+    const uint32_t R0 = e->round;
+    if (e->spr_active && !e->spr_always && R0 >= 2) {
+        // density of round R0-1's planes (written by the launch of two calls
+        // ago): switch to the dense variant once under a quarter are zero words
+        const uint32_t par = (R0 - 1) & 1u;
+        if (e->dens_round[par] == R0 - 1) {
+            GS_HIP(hipEventSynchronize(e->ev_dens[par]));
+            u64 zw = 0;
+            for (uint32_t i = 0; i < gs::kDensSlots; ++i) zw += e->dens_host[par * gs::kDensSlots + i];
+            if (4 * zw < e->g.nseg) e->spr_active = false;
+        }
+    }
+    const bool sparse = e->spr_active;
+    if (sparse) {
+        a.zb_cur = e->zb[e->cur];
+        a.zb_nxt = e->zb[e->cur ^ 1];
+        a.lb_cur = e->lb[e->cur];
+        a.lb_nxt = e->lb[e->cur ^ 1];
+        a.ab_cur = e->ab[e->cur];
+        a.ab_nxt = e->ab[e->cur ^ 1];
+        a.dens = e->dens + ((R0 + 1) & 1u) * gs::kDensSlots;
+        GS_HIP(hipMemsetAsync(a.dens, 0, gs::kDensSlots * sizeof(u64), e->stream));
+        if (e->deliver_pending) {
+            a.acct = e->acct;
+            e->acct_launches++;
+        }
+    } else if (e->deliver_pending) {
+        e->dense_launches++;
+    }
     hipEvent_t t0 = e->ev0, t1 = e->ev1;
     if (e->timing && e->tcount < kTimingSlots) {
         t0 = e->tev[2 * e->tcount];
         t1 = e->tev[2 * e->tcount + 1];
         e->tcount++;
     }
-    const uint32_t R0 = e->round;
     const uint32_t rs = R0 & 1u;  // set holding round t = e->round
     if (e->shard) {
         GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[(R0 + 1) % 3], 0));
@@ -836,6 +917,13 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
     if (e->timing) GS_HIP(hipEventRecord(t0, e->stream));
     GS_HIP(gs::launch_round(a, e->deliver_pending ? 1 : 0, e->stream));
     if (e->timing) GS_HIP(hipEventRecord(t1, e->stream));
+    if (sparse) {  // this round's density, for the call after next
+        const uint32_t par = (R0 + 1) & 1u;
+        GS_HIP(hipMemcpyAsync(e->dens_host + par * gs::kDensSlots, a.dens, gs::kDensSlots * sizeof(u64),
+                              hipMemcpyDeviceToHost, e->stream));
+        GS_HIP(hipEventRecord(e->ev_dens[par], e->stream));
+        e->dens_round[par] = R0 + 1;
+    }
     if (!e->shard) GS_HIP(hipEventRecord(e->ev_read[rs], e->stream));
     e->ev0 = t0;
     e->ev1 = t1;
@@ -1084,6 +1172,13 @@ void gs_set_timing(gs_engine *e, int enable) {
             }
     }
     e->tcount = 0;
+    if (e->timing && e->spr) {  // restart the traffic accounting with the ring
+        (void)hipSetDevice(e->device);
+        if (hipMemsetAsync(e->acct, 0, gs::kAcctSlots * sizeof(u64), e->stream) == hipSuccess) {
+            e->acct_launches = 0;
+            e->dense_launches = 0;
+        }
+    }
 }
 
 int32_t gs_round_kernel_times(gs_engine *e, float *out_ms, uint32_t max) {
@@ -1297,6 +1392,41 @@ double gs_round_kernel_bytes(const gs_engine *e) {
     // 16 w + the next round's push code 4.
     if (e->dlv) return n * (2.0 * rp + 60.0);
     return n * (2.75 * rp + 68.0);
+}
+
+gs_status gs_round_traffic(gs_engine *e, double *bytes_per_launch, uint32_t *launches) {
+    if (!e || !bytes_per_launch || !launches) return GS_ERR_INVALID_ARGUMENT;
+    const double dense = gs_round_kernel_bytes(e);
+    if (!e->spr) {
+        *bytes_per_launch = dense;
+        *launches = 0;
+        return GS_OK;
+    }
+    gs_status st = set_device(e);
+    if (st != GS_OK) return st;
+    std::vector<u64> v(gs::kAcctSlots);
+    GS_HIP(hipStreamSynchronize(e->stream));
+    GS_HIP(hipMemcpy(v.data(), e->acct, v.size() * sizeof(u64), hipMemcpyDeviceToHost));
+    double segs = 0, rows = 0;
+    for (u64 w : v) {
+        segs += (double)(w & 0xFFFFFFFFull);
+        rows += (double)(w >> 32);
+    }
+    const uint32_t Ls = e->acct_launches, Ld = e->dense_launches;
+    *launches = Ls + Ld;
+    if (Ls + Ld == 0) {
+        *bytes_per_launch = dense;
+        return GS_OK;
+    }
+    // sparse launches: per node the 68 B of gs_round_kernel_bytes plus the maps
+    // (zero-word bits of both buffers read, one written; live / all-A bits
+    // written); per plane segment moved 64 B (8 planes x 8 B); per class row
+    // gathered 24 B (3 planes x 8 B, per 64-rumor word).  Dense launches: the
+    // static model.
+    const double n = e->g.n, W = e->g.W;
+    const double sparse_total = Ls * n * (68.0 + (3.0 * W + 2.0) / 8.0) + 64.0 * segs + 24.0 * rows;
+    *bytes_per_launch = (sparse_total + Ld * dense) / (Ls + Ld);
+    return GS_OK;
 }
 
 }  // extern "C"

@@ -57,6 +57,22 @@ struct RoundArgs {
     // launch only blocks [blk_off, blk_off + blk_count) (0: all), and with
     // obs_only != ~0 observe only that node (its codes at obs_state[0..R))
     uint32_t blk_off, blk_count, obs_only;
+    // Sparse records (wide 2P engine, W <= 8; null otherwise), exact for the
+    // plane buffer they describe: zb = a bit per segment "all 8 planes zero"
+    // (a word of unknown rumors), lb = a bit per node "some B or C entry"
+    // (its push is not empty), ab = a bit per node "no known entry".  A zero
+    // word is neither loaded nor rewritten over a zero word, and a pusher with
+    // nothing live is not gathered ("Sparse records").
+    // Written by the sparse-variant transition launches (modes 0 and 1), which
+    // the engine uses while a dissemination is young; null = dense variant.
+    const u64 *zb_cur;
+    u64 *zb_nxt;
+    const uint8_t *lb_cur, *ab_cur;
+    uint8_t *lb_nxt, *ab_nxt;
+    u64 *acct;                // mode 1: [kAcctSlots] packed (plane segments read +
+                              // written) | lane gathers << 32, one atomic per block
+    u64 *dens;                // [kDensSlots] zero words of the round-(t+1) planes
+                              // (spread atomics, cleared by the engine per launch)
     Geometry g;
     uint64_t seed;
     uint32_t epoch;
@@ -64,6 +80,11 @@ struct RoundArgs {
     uint32_t cmax, maxc, maxr;
 };
 constexpr uint32_t kExtPush = 1u << 20, kExtNew = 1u << 21, kExtRec = 1u << 22, kExtEmpty = 1u << 23;
+constexpr uint32_t kAcctSlots = 4096;  // accounting atomics spread over this many words
+constexpr uint32_t kDensSlots = 16;    // density counts spread over this many words
+// Sparse-record map sizes: zb words per buffer, lb / ab bytes per buffer.
+inline u64 spr_zb_words(const Geometry &g) { return (g.nseg + 255u) / 256u * 4u + 4u; }
+inline u64 spr_node_bytes(const Geometry &g) { return ((u64)g.n + 63u) / 64u * 8u + 64u; }
 
 // mode: 0 = transition only (first round), 1 = deliver round t + transition
 // to t+1, 2 = deliver round t and write observation outputs only,

@@ -152,7 +152,71 @@ GS_DEV Cls decode16(uint32_t code) {
 // DLV: delivery records (gs_common.h DlvRec) replace every class-plane
 // gather: a lane's pushers' push codes are in its own record and its pull
 // batch in PULL[x], both read coalesced.
-template <bool SMALL, int MODE, bool SHARD, bool SEQ, bool DLV>
+// Sparse records: the 256 bits of a block's segments, word i = wave i.
+struct Bits256 {
+    u64 w0, w1, w2, w3;
+    GS_DEV void load(const u64 *p) {
+        w0 = p[0];
+        w1 = p[1];
+        w2 = p[2];
+        w3 = p[3];
+    }
+    // word i for a wave-uniform i (scalar selects, no indexed access)
+    GS_DEV u64 word(uint32_t i) const {
+        return (w0 & (0ull - (u64)(i == 0u))) | (w1 & (0ull - (u64)(i == 1u))) | (w2 & (0ull - (u64)(i == 2u))) |
+               (w3 & (0ull - (u64)(i == 3u)));
+    }
+    GS_DEV uint32_t count() const { return popc(w0) + popc(w1) + popc(w2) + popc(w3); }
+};
+GS_DEV bool map_bit(const uint8_t *__restrict__ m, uint32_t i) { return ((m[i >> 3] >> (i & 7u)) & 1u) != 0; }
+// Staging chunk c = t + 256*i of a block (16 B = words 2c, 2c+1 of its
+// records [node][plane][W]) covers plane words of segments s0 and s0+1
+// (W >= 2) or s0 (W = 1), with s0 = chunk_seg(t) + 64*i: bit chunk_seg(t) of
+// word i.  True when they are all known zero.
+GS_DEV uint32_t chunk_seg(uint32_t t, uint32_t logw) {
+    const uint32_t w0 = 2u * t;
+    return (((w0 >> (logw + 3u)) << logw) | (w0 & ((1u << logw) - 1u))) & 63u;
+}
+GS_DEV bool chunk_zero(u64 word, uint32_t bit, uint32_t logw) {
+    const u64 m = logw ? 3ull : 1ull;
+    return ((word >> bit) & m) == m;
+}
+// Keep the bits of m at multiples of W = 2^logw (W <= 8), packed to the bottom.
+GS_DEV u64 compress_stride(u64 m, uint32_t logw) {
+    if (logw == 1u) {
+        m &= 0x5555555555555555ull;
+        m = (m | (m >> 1)) & 0x3333333333333333ull;
+        m = (m | (m >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+        m = (m | (m >> 4)) & 0x00FF00FF00FF00FFull;
+        m = (m | (m >> 8)) & 0x0000FFFF0000FFFFull;
+        m = (m | (m >> 16)) & 0x00000000FFFFFFFFull;
+    } else if (logw == 2u) {
+        m &= 0x1111111111111111ull;
+        m = (m | (m >> 3)) & 0x0303030303030303ull;
+        m = (m | (m >> 6)) & 0x000F000F000F000Full;
+        m = (m | (m >> 12)) & 0x000000FF000000FFull;
+        m = (m | (m >> 24)) & 0x000000000000FFFFull;
+    } else if (logw == 3u) {
+        m &= 0x0101010101010101ull;
+        m = (m | (m >> 7)) & 0x0003000300030003ull;
+        m = (m | (m >> 14)) & 0x0000000F0000000Full;
+        m = (m | (m >> 28)) & 0x00000000000000FFull;
+    }
+    return m;
+}
+// OR / AND of each aligned group of W bits, into the group's lowest bit.
+GS_DEV u64 group_or_bits(u64 m, uint32_t logw) {
+    for (uint32_t o = 1; o < (1u << logw); o <<= 1) m |= m >> o;
+    return m;
+}
+GS_DEV u64 group_and_bits(u64 m, uint32_t logw) {
+    for (uint32_t o = 1; o < (1u << logw); o <<= 1) m &= m >> o;
+    return m;
+}
+
+// SPRK: the sparse-records variant (wide 2P engine, transition modes), launched
+// while a dissemination is young (gs_engine.cpp picks it per round).
+template <bool SMALL, int MODE, bool SHARD, bool SEQ, bool DLV, bool SPRK = false>
 __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     constexpr bool DELIVER = (MODE == 1 || MODE == 2);
     constexpr bool TRANSITION = (MODE == 0 || MODE == 1);
@@ -165,10 +229,34 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     const uint32_t x = L.x;
     const u64 *__restrict__ S = a.Scur;
 
+    // ---- sparse records (wide 2P engine): the zero-word bits of the block's
+    // 256 segments in the round-t planes (zc) and in the planes the
+    // round-(t+1) output overwrites (zn)
+    constexpr bool spr = SPRK && !SMALL && !SHARD && !SEQ && !DLV && TRANSITION;
+    Bits256 zc = {}, zn = {};
+    bool skip_planes = false, gchk = false;
+    __shared__ u64 acc_blk;
+    __shared__ uint32_t zero_blk;  // zero words of the block in the round-(t+1) planes
+    __shared__ uint32_t blk_any;  // some node pushes a live rumor in round t+1
+    if (threadIdx.x == 0) blk_any = 0;
+    if (spr) {
+        zc.load(a.zb_cur + (u64)bid * 4u);
+        zn.load(a.zb_nxt + (u64)bid * 4u);
+        skip_planes = true;
+        // gathers check the live / all-A maps first (L2 hits): most pushes are
+        // empty while a dissemination is young
+        gchk = DELIVER;
+        if (threadIdx.x == 0) {
+            acc_blk = 0;
+            zero_blk = 0;
+        }
+    }
+
     // ---- own round-t planes: the block's records are one contiguous range
     // (W <= 256), loaded first with 16-byte coalesced loads (clamped, so every
     // load is unconditional) and transposed through LDS below, instead of
-    // eight strided 8-byte loads per lane.
+    // eight strided 8-byte loads per lane.  Sparse records: a chunk whose two
+    // words are known zero is not loaded.
     __shared__ __attribute__((aligned(16))) u64 stage[kBlockWords];
     const uint32_t npu_blk = SMALL ? (1u << g.lognpu) : 1u;
     const u64 blk_base = (u64)bid * (kBlockWords / npu_blk);
@@ -176,10 +264,21 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                                           g.units * kPlanes * (SMALL ? 1u : g.W) - blk_base) / 2u;
     static_assert(kStageIters == 4, "stage loads are unrolled by hand");
     const uint4 *src4 = reinterpret_cast<const uint4 *>(S + blk_base);
-    const uint4 st0 = src4[min(threadIdx.x, blk_v4 - 1u)];
-    const uint4 st1 = src4[min(threadIdx.x + 256u, blk_v4 - 1u)];
-    const uint4 st2 = src4[min(threadIdx.x + 512u, blk_v4 - 1u)];
-    const uint4 st3 = src4[min(threadIdx.x + 768u, blk_v4 - 1u)];
+    const uint32_t logw = SMALL ? 0u : g.logr - 6u;
+    const uint32_t cbit = chunk_seg(threadIdx.x, logw);
+    uint4 st0 = {0u, 0u, 0u, 0u}, st1 = {0u, 0u, 0u, 0u}, st2 = {0u, 0u, 0u, 0u}, st3 = {0u, 0u, 0u, 0u};
+    if (skip_planes) {
+        const uint32_t t = threadIdx.x;
+        if (t < blk_v4 && !chunk_zero(zc.w0, cbit, logw)) st0 = src4[t];
+        if (t + 256u < blk_v4 && !chunk_zero(zc.w1, cbit, logw)) st1 = src4[t + 256u];
+        if (t + 512u < blk_v4 && !chunk_zero(zc.w2, cbit, logw)) st2 = src4[t + 512u];
+        if (t + 768u < blk_v4 && !chunk_zero(zc.w3, cbit, logw)) st3 = src4[t + 768u];
+    } else {
+        st0 = src4[min(threadIdx.x, blk_v4 - 1u)];
+        st1 = src4[min(threadIdx.x + 256u, blk_v4 - 1u)];
+        st2 = src4[min(threadIdx.x + 512u, blk_v4 - 1u)];
+        st3 = src4[min(threadIdx.x + 768u, blk_v4 - 1u)];
+    }
 
     // ---- coalesced per-node metadata (level 1)
     uint4 in = {0, 0, 0, 0};   // SHARD: {first, k|zi<<16, e0, e1}
@@ -238,6 +337,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     // of t(x) ahead of x.  Slots past k / r load x's own row (an L2 hit) so no
     // load is conditional.  Rarer deeper in-lists are walked afterwards.
     Cls q[kBatchK], e[kBatchE], qz = {0, 0, 0}, wz = {0, 0, 0};
+    uint32_t ngath = 0;  // class rows gathered (pushers, t(x)): accounting
 #pragma unroll
     for (uint32_t i = 0; i < kBatchK; ++i) q[i] = {0, 0, 0};
 #pragma unroll
@@ -260,9 +360,32 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                     qz.a1 = 0;
                 }
             }
+        } else if (gchk) {
+            // sparse: look the pushers and t(x)'s earlier pushers up in the
+            // live map and t(x) in the all-A map (2 MB at config 4: L2 hits),
+            // then gather only rows that carry something.  A row with nothing
+            // live pushes nothing, exactly as the zero row does; t(x)'s row
+            // also decides what t(x) lacks, so only an all-A t(x) is skipped.
+            bool gq[kBatchK], ge[kBatchE];
+#pragma unroll
+            for (uint32_t i = 0; i < kBatchK; ++i) gq[i] = i < k && map_bit(a.lb_cur, in8.s[i]);
+#pragma unroll
+            for (uint32_t i = 0; i < kBatchE; ++i) ge[i] = i < r && map_bit(a.lb_cur, sb8.e[i]);
+            const bool gz = valid && !map_bit(a.ab_cur, z);
+#pragma unroll
+            for (uint32_t i = 0; i < kBatchK; ++i) {
+                if (gq[i]) q[i] = L.load_cls(S, in8.s[i]);
+                ngath += gq[i] ? 1u : 0u;
+            }
+            if (gz) qz = L.load_cls(S, z);
+            ngath += gz ? 1u : 0u;
+#pragma unroll
+            for (uint32_t i = 0; i < kBatchE; ++i)
+                if (ge[i]) e[i] = L.load_cls(S, sb8.e[i]);
         } else {
 #pragma unroll
             for (uint32_t i = 0; i < kBatchK; ++i) q[i] = L.load_cls(S, i < k ? in8.s[i] : x);
+            ngath += min(k, kBatchK) + (valid ? 1u : 0u);
             if (SEQ && !seq_inl) {  // W(x), coalesced (qz holds its code planes)
                 if (valid && (sinf & kSeqGot)) {
                     const u64 wi = ((u64)x * 2u) * g.W + L.j;
@@ -298,6 +421,28 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         P[p] = SMALL ? ((v >> L.sh) & L.m) : v;
     }
 
+    // Sparse variant: a wave all of whose segments are unknown words that
+    // receive nothing live (no live pusher, an all-A t(x), no live pusher of
+    // t(x) ahead of x) and get no injection or external RPC stays all-A, and
+    // its nodes only count empty pushes and empty pulls: it skips phases 1-2
+    // and the transition (a wave-uniform branch: no vector work issued).
+    bool wtriv = false;
+    if (spr && a.n_inj == 0 && a.n_ext == 0 && a.f.churn == 0) {
+        u64 any = 0;
+#pragma unroll
+        for (int p = 0; p < kPlanes; ++p) any |= P[p];
+        bool busy = any != 0;
+        if (DELIVER) {
+#pragma unroll
+            for (uint32_t i = 0; i < kBatchK; ++i) busy |= (q[i].c | q[i].a0 | q[i].a1) != 0;
+#pragma unroll
+            for (uint32_t i = 0; i < kBatchE; ++i) busy |= (e[i].c | e[i].a0 | e[i].a1) != 0;
+            busy |= (qz.c | qz.a0 | qz.a1) != 0;
+            busy |= k > kBatchK || r > kBatchE;
+        }
+        wtriv = __ballot(valid && busy) == 0ull;
+    }
+
     const u64 isC = P[0], a0 = P[1], a1 = P[2];
     const u64 A = ~isC & ~a0 & ~a1 & L.m;
     const u64 B = ~isC & (a0 | a1);
@@ -318,8 +463,8 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     uint32_t ext_new = 0, ext_full = 0, ext_empty = 0, ext_recv = 0;  // external RPCs (node level)
     bool seq_gx = false, seq_skip = false;
     uint32_t seq_px = 0, seq_jz = kNone;
-    if (DELIVER && valid) {
-        if (k > 30u) atomicOr(&a.flags[2], 1u);
+    if (DELIVER && valid && k > 30u) atomicOr(&a.flags[2], 1u);
+    if (DELIVER && valid && !wtriv) {
         bool zin = false;
         u64 pv2, pvB, pCl;
         if (DLV) {
@@ -449,7 +594,9 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             for (uint32_t i = kBatchK; i < k; ++i) {  // in-degree > kBatchK (1.9% of nodes)
                 const uint32_t s = i < kInline ? pick_inline(in8.s, i) : a.src[in8.first() + (i - kInline)];
                 zin |= s == z;
-                rv.push(L.load_cls(S, s), i, k, !(pulled && s == z));
+                const bool gs_ = !gchk || map_bit(a.lb_cur, s);
+                ngath += gs_ ? 1u : 0u;
+                rv.push(gs_ ? L.load_cls(S, s) : Cls{0, 0, 0}, i, k, !(pulled && s == z));
             }
             // Pull batch from z: z's live set plus what z created from pushers
             // ahead of x.
@@ -460,14 +607,17 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             for (uint32_t i = 0; i < kBatchE; ++i)
                 if (i < r) sibling(e[i], pnot, pB, pC);
             if (r > kBatchE && pnot && pulled) {  // rank > kBatchE (rare)
+                auto sib_row = [&](uint32_t s) -> Cls {
+                    return (!gchk || map_bit(a.lb_cur, s)) ? L.load_cls(S, s) : Cls{0, 0, 0};
+                };
                 for (uint32_t i = kBatchE; i < min(r, kSibInline); ++i)
-                    sibling(L.load_cls(S, pick_sib(sb8.e, i)), pnot, pB, pC);
+                    sibling(sib_row(pick_sib(sb8.e, i)), pnot, pB, pC);
                 if (r > kSibInline && pnot) {  // rank > 3: 0.2% of nodes
                     const InRec zin8 = a.IN8[z];
                     for (uint32_t i = kSibInline; i < r && pnot; ++i) {
                         const uint32_t s = i < kInline ? pick_inline(zin8.s, i)
                                                        : a.src[zin8.first() + (i - kInline)];
-                        sibling(L.load_cls(S, s), pnot, pB, pC);
+                        sibling(sib_row(s), pnot, pB, pC);
                     }
                 }
             }
@@ -526,7 +676,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     // ---- node-level statistics of the deliveries
     uint32_t lc = popc(liveX);
     uint32_t part_cw = rv.part_cw, recv = rv.recv, first_create = rv.first_create;
-    if (DELIVER && !SMALL) {
+    if (DELIVER && !SMALL && !wtriv) {
         lc = group_sum(lc, g.W);
         part_cw = group_sum(part_cw, g.W);
         recv = group_sum(recv, g.W);
@@ -635,101 +785,105 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     }
 
     // ---------------- phase 0 of round t+1 at x ----------------------------
-    // Gossip::new_message (insert = replace with MessageState::new, records
-    // dropped) for the rumors injected at x this round.
-    u64 inj = 0;
-    if (a.n_inj && valid) {
-        const u64 key = SMALL ? (u64)x : seg;
-        uint32_t lo = 0, hi = a.n_inj;
-        while (lo < hi) {
-            uint32_t mid = (lo + hi) >> 1;
-            if (a.inj_key[mid] < key) lo = mid + 1; else hi = mid;
+    u64 N[kPlanes] = {0, 0, 0, 0, 0, 0, 0, 0};  // a trivial wave stays all-A
+    u64 Bn = 0, Cn = 0;
+    bool on_next = true;
+    if (!wtriv) {
+            // Gossip::new_message (insert = replace with MessageState::new, records
+        // dropped) for the rumors injected at x this round.
+        u64 inj = 0;
+        if (a.n_inj && valid) {
+            const u64 key = SMALL ? (u64)x : seg;
+            uint32_t lo = 0, hi = a.n_inj;
+            while (lo < hi) {
+                uint32_t mid = (lo + hi) >> 1;
+                if (a.inj_key[mid] < key) lo = mid + 1; else hi = mid;
+            }
+            if (lo < a.n_inj && a.inj_key[lo] == key) inj = a.inj_mask[lo] & L.m;
         }
-        if (lo < a.n_inj && a.inj_key[lo] == key) inj = a.inj_mask[lo] & L.m;
-    }
-    const u64 ninj = ~inj;
-    const u64 Bold = B & ninj, Cold = C & ninj, Dold = D & ninj;
-    const u64 cB = crB & ninj, cC = crC & ninj;
-    const u64 Bf = Bold | cB | inj;  // entries in state B entering next_round
-    const u64 Cf = Cold | cC;        // entries in state C entering next_round
+        const u64 ninj = ~inj;
+        const u64 Bold = B & ninj, Cold = C & ninj, Dold = D & ninj;
+        const u64 cB = crB & ninj, cC = crC & ninj;
+        const u64 Bf = Bold | cB | inj;  // entries in state B entering next_round
+        const u64 Cf = Cold | cC;        // entries in state C entering next_round
 
-    // B (src/message_state.rs:94-147).  0-filled peers vote "less", so with
-    // no C copy the median rule is: bump iff 2*ge > |P| iff ge >= |P|/2+1.
-    const u64 oc1 = (Bold & a0 & ~a1) | cB | inj;
-    const u64 oc2 = Bold & a1 & ~a0;
-    const uint32_t thr = psize / 2u + 1u;
-    // Churn: a node offline in round t+1 skips next_round; it keeps its
-    // pre-transition state (created entries folded in as B{0,1} / C{0,0}) and
-    // the two per-rumor votes next_round will use (bump, anyC) in `pend`.  A
-    // node returning from offline (off_t) takes its votes from there.
-    const bool on_next = !(a.f.churn && valid && offline_of(a.seed, a.epoch, a.round_new, a.node_lo + x, a.f.churn));
-    u64 bump, anyCe;
-    if (off_t && valid) {
-        const u64 pidx = ((u64)x * 2u) * g.W + L.j;
-        bump = a.pend[pidx] & Bold;
-        anyCe = a.pend[pidx + g.W] & ninj;
-    } else {
-        bump = ge_k<5>(rv.cv, thr) & (Bold | cB);  // cv counts only B entries' votes
-        anyCe = anyC & ninj;
-    }
-    u64 nr[6];  // round + 1
-    {
-        u64 carry = ~0ull;
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            const u64 rb = P[3 + i] & Bold;
-            nr[i] = rb ^ carry;
-            carry &= rb;
+        // B (src/message_state.rs:94-147).  0-filled peers vote "less", so with
+        // no C copy the median rule is: bump iff 2*ge > |P| iff ge >= |P|/2+1.
+        const u64 oc1 = (Bold & a0 & ~a1) | cB | inj;
+        const u64 oc2 = Bold & a1 & ~a0;
+        const uint32_t thr = psize / 2u + 1u;
+        // Churn: a node offline in round t+1 skips next_round; it keeps its
+        // pre-transition state (created entries folded in as B{0,1} / C{0,0}) and
+        // the two per-rumor votes next_round will use (bump, anyC) in `pend`.  A
+        // node returning from offline (off_t) takes its votes from there.
+        on_next = !(a.f.churn && valid && offline_of(a.seed, a.epoch, a.round_new, a.node_lo + x, a.f.churn));
+        u64 bump, anyCe;
+        if (off_t && valid) {
+            const u64 pidx = ((u64)x * 2u) * g.W + L.j;
+            bump = a.pend[pidx] & Bold;
+            anyCe = a.pend[pidx + g.W] & ninj;
+        } else {
+            bump = ge_k<5>(rv.cv, thr) & (Bold | cB);  // cv counts only B entries' votes
+            anyCe = anyC & ninj;
         }
-        nr[5] = carry;
-    }
-    const u64 toD = ge_u<6>(nr, a.maxr);
-    const u64 oc1n = oc1 & ~bump;
-    const u64 oc2n = (oc1 & bump) | (oc2 & ~bump);
-    const u64 oc3n = oc2 & bump;
-    const u64 ocge = a.cmax <= 1u ? ~0ull : (a.cmax == 2u ? (oc2n | oc3n) : oc3n);
-    const u64 toC = anyCe | ocge;
-    const u64 BD = Bf & toD, BC = Bf & ~toD & toC, BB = Bf & ~toD & ~toC;
-
-    // C (src/message_state.rs:148-168): round+1; D if round+rib >= max_rounds
-    // or round >= max_c_rounds.
-    const u64 cr0 = a0 & Cold, cr1 = a1 & Cold;
-    const u64 d[3] = {~cr0, cr1 ^ cr0, cr1 & cr0};
-    u64 rib[5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) rib[i] = P[3 + i] & Cold;
-    u64 sum[6];
-    {
-        u64 c = 0;
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            const u64 di = i < 3 ? d[i] : 0ull;
-            sum[i] = rib[i] ^ di ^ c;
-            c = (rib[i] & di) | (c & (rib[i] ^ di));
+        u64 nr[6];  // round + 1
+        {
+            u64 carry = ~0ull;
+    #pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                const u64 rb = P[3 + i] & Bold;
+                nr[i] = rb ^ carry;
+                carry &= rb;
+            }
+            nr[5] = carry;
         }
-        sum[5] = c;
-    }
-    const u64 CtoD = ge_u<6>(sum, a.maxr) | ge_u<3>(d, a.maxc);
-    const u64 CD = Cf & CtoD, CC = Cf & ~CtoD;
+        const u64 toD = ge_u<6>(nr, a.maxr);
+        const u64 oc1n = oc1 & ~bump;
+        const u64 oc2n = (oc1 & bump) | (oc2 & ~bump);
+        const u64 oc3n = oc2 & bump;
+        const u64 ocge = a.cmax <= 1u ? ~0ull : (a.cmax == 2u ? (oc2n | oc3n) : oc3n);
+        const u64 toC = anyCe | ocge;
+        const u64 BD = Bf & toD, BC = Bf & ~toD & toC, BB = Bf & ~toD & ~toC;
 
-    const u64 Dn = BD | CD | Dold;
-    const u64 Cn = BC | CC;
-    const u64 Bn = BB;
-    u64 N[kPlanes];
-    N[0] = Cn | Dn;
-    N[1] = (Bn & oc1n) | (CC & d[0]) | Dn;
-    N[2] = (Bn & oc2n) | (CC & d[1]) | Dn;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) N[3 + i] = ((Bn | BC) & nr[i]) | (CC & rib[i]);
-    if (!on_next) {  // frozen: pre-transition planes + votes (the lane is valid)
-        N[0] = (isC & ninj) | cC;
-        N[1] = (a0 & ninj) | cB | inj;
-        N[2] = a1 & ninj;
-#pragma unroll
-        for (int i = 0; i < 5; ++i) N[3 + i] = P[3 + i] & ninj;
-        const u64 pidx = ((u64)x * 2u) * g.W + L.j;
-        a.pend[pidx] = bump;
-        a.pend[pidx + g.W] = anyCe & (Bold | cB);
+        // C (src/message_state.rs:148-168): round+1; D if round+rib >= max_rounds
+        // or round >= max_c_rounds.
+        const u64 cr0 = a0 & Cold, cr1 = a1 & Cold;
+        const u64 d[3] = {~cr0, cr1 ^ cr0, cr1 & cr0};
+        u64 rib[5];
+    #pragma unroll
+        for (int i = 0; i < 5; ++i) rib[i] = P[3 + i] & Cold;
+        u64 sum[6];
+        {
+            u64 c = 0;
+    #pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                const u64 di = i < 3 ? d[i] : 0ull;
+                sum[i] = rib[i] ^ di ^ c;
+                c = (rib[i] & di) | (c & (rib[i] ^ di));
+            }
+            sum[5] = c;
+        }
+        const u64 CtoD = ge_u<6>(sum, a.maxr) | ge_u<3>(d, a.maxc);
+        const u64 CD = Cf & CtoD, CC = Cf & ~CtoD;
+
+        const u64 Dn = BD | CD | Dold;
+        Cn = BC | CC;
+        Bn = BB;
+        N[0] = Cn | Dn;
+        N[1] = (Bn & oc1n) | (CC & d[0]) | Dn;
+        N[2] = (Bn & oc2n) | (CC & d[1]) | Dn;
+    #pragma unroll
+        for (int i = 0; i < 5; ++i) N[3 + i] = ((Bn | BC) & nr[i]) | (CC & rib[i]);
+        if (!on_next) {  // frozen: pre-transition planes + votes (the lane is valid)
+            N[0] = (isC & ninj) | cC;
+            N[1] = (a0 & ninj) | cB | inj;
+            N[2] = a1 & ninj;
+    #pragma unroll
+            for (int i = 0; i < 5; ++i) N[3 + i] = P[3 + i] & ninj;
+            const u64 pidx = ((u64)x * 2u) * g.W + L.j;
+            a.pend[pidx] = bump;
+            a.pend[pidx + g.W] = anyCe & (Bold | cB);
+        }
     }
 
     // DLV: the push code of round t+1 (b0 | b1 << 16), which the in-list
@@ -740,10 +894,61 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         a.pc_out[x] = (uint32_t)b0 | ((uint32_t)b1 << 16);
     }
 
+    // ---- sparse records of the round-(t+1) planes: zero-word bits (one u64
+    // per wave), node live / all-A bits (64/W per wave, W <= 8: whole bytes);
+    // the group and packing work is on wave-uniform ballots (scalar ALU)
+    if (spr) {
+        const u64 any = N[0] | N[1] | N[2] | N[3] | N[4] | N[5] | N[6] | N[7];
+        const bool wz = valid && any == 0;
+        const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const u64 seg0 = seg - lane;
+        const u64 vC = N[0] & ~(N[1] & N[2]), vB = ~N[0] & (N[1] | N[2]);
+        const u64 bz = __ballot(wz), blive = __ballot(valid && (vB | vC) != 0);
+        const u64 cl = compress_stride(group_or_bits(blive, logw), logw);
+        const u64 ca = compress_stride(group_and_bits(bz, logw), logw);
+        if (lane == 0 && seg0 < g.nseg) {
+            a.zb_nxt[seg0 >> 6] = bz;
+            atomicAdd(&zero_blk, popc(bz));
+            const uint32_t per = 64u >> logw;  // nodes per wave
+            const u64 byte0 = (seg0 >> logw) >> 3;  // first node of the wave / 8
+            if (per == 64u) {
+                *reinterpret_cast<u64 *>(a.lb_nxt + byte0) = cl;
+                *reinterpret_cast<u64 *>(a.ab_nxt + byte0) = ca;
+            } else if (per == 32u) {
+                *reinterpret_cast<uint32_t *>(a.lb_nxt + byte0) = (uint32_t)cl;
+                *reinterpret_cast<uint32_t *>(a.ab_nxt + byte0) = (uint32_t)ca;
+            } else if (per == 16u) {
+                *reinterpret_cast<uint16_t *>(a.lb_nxt + byte0) = (uint16_t)cl;
+                *reinterpret_cast<uint16_t *>(a.ab_nxt + byte0) = (uint16_t)ca;
+            } else {
+                a.lb_nxt[byte0] = (uint8_t)cl;
+                a.ab_nxt[byte0] = (uint8_t)ca;
+            }
+        }
+        if (MODE == 1 && a.acct) {
+            // algorithmic plane segments moved: read unless known zero, written
+            // unless zero over zero; class rows gathered 
+            const bool zcl = ((zc.word(wv) >> lane) & 1ull) != 0, znl = ((zn.word(wv) >> lane) & 1ull) != 0;
+            const bool rd = valid && !(skip_planes && zcl);
+            const bool wr = valid && !(skip_planes && wz && znl);
+            uint32_t ng = 0;  // ngath <= 3 + 1 + (kMaxIn - 3) < 32: five bit ballots
+#pragma unroll
+            for (uint32_t b = 0; b < 5u; ++b) ng += popc(__ballot((ngath >> b) & 1u)) << b;
+            const u64 v = (u64)(popc(__ballot(rd)) + popc(__ballot(wr))) | ((u64)ng << 32);
+            if (lane == 0) atomicAdd(&acc_blk, v);
+        }
+    }
+
     // ---- write round-(t+1) planes (through LDS, 16-byte coalesced stores)
     uint32_t live_new = (valid && on_next) ? popc(Bn | Cn) : 0u;
     if (!SMALL) live_new = group_sum(live_new, g.W);
-    const int blk_live = __syncthreads_or(live_new != 0u);  // also: every lane is done reading stage
+    if (__ballot(live_new != 0u) != 0ull && (threadIdx.x & 63u) == 0u) blk_any = 1u;
+    __syncthreads();  // also: every lane is done reading stage
+    const bool blk_live = blk_any != 0u;
+    if (spr && threadIdx.x == 0) {
+        if (MODE == 1 && a.acct) atomicAdd(&a.acct[bid & (kAcctSlots - 1u)], acc_blk);
+        if (a.dens) atomicAdd(&a.dens[bid & (kDensSlots - 1u)], (u64)zero_blk);
+    }
     if (SMALL) {
         const uint32_t npu = 1u << g.lognpu;
 #pragma unroll
@@ -761,8 +966,20 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         const uint4 *src4 = reinterpret_cast<const uint4 *>(stage);
         uint4 *dst4 = reinterpret_cast<uint4 *>(a.Snext + blk_base);
         // streaming (nontemporal) stores: 3.11 -> 3.01 ms per round kernel at
-        // config 4 (nontemporal plane loads measured slower: 3.27 ms)
-        for (uint32_t i = threadIdx.x; i < blk_v4; i += blockDim.x) nt_store4(src4[i], &dst4[i]);
+        // config 4 (nontemporal plane loads measured slower: 3.27 ms).
+        // Sparse records: zero over known zero is not rewritten.
+        if (skip_planes) {
+#pragma unroll
+            for (uint32_t it = 0; it < 4u; ++it) {
+                const uint32_t i = threadIdx.x + 256u * it;
+                if (i >= blk_v4) break;
+                const uint4 v = src4[i];
+                if ((v.x | v.y | v.z | v.w) == 0u && chunk_zero(zn.word(it), cbit, logw)) continue;
+                nt_store4(v, &dst4[i]);
+            }
+        } else {
+            for (uint32_t i = threadIdx.x; i < blk_v4; i += blockDim.x) nt_store4(src4[i], &dst4[i]);
+        }
     }
     if (SHARD && valid && a.spos_next[x] != 0xFFFFFFFFu) {
         // push row of round t+1: the push batch's class code, to owner(t_{t+1}(x))
@@ -803,6 +1020,17 @@ static hipError_t launch_mode(const RoundArgs &a, int mode, hipStream_t s) {
     const uint32_t block = 256;
     const u64 grid = a.blk_count ? a.blk_count : (a.g.nseg + block - 1) / block;
     if (grid == 0) return hipSuccess;
+    if constexpr (!SMALL && !SHARD && !SEQ && !DLV) {
+        if (a.zb_nxt && (mode == 0 || mode == 1)) {  // sparse records
+            if (mode == 0)
+                hipLaunchKernelGGL((round_kernel<false, 0, false, false, false, true>), dim3((uint32_t)grid),
+                                   dim3(block), 0, s, a);
+            else
+                hipLaunchKernelGGL((round_kernel<false, 1, false, false, false, true>), dim3((uint32_t)grid),
+                                   dim3(block), 0, s, a);
+            return hipGetLastError();
+        }
+    }
     switch (mode) {
     case 0: hipLaunchKernelGGL((round_kernel<SMALL, 0, SHARD, SEQ, DLV>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
     case 1: hipLaunchKernelGGL((round_kernel<SMALL, 1, SHARD, SEQ, DLV>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
