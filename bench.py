@@ -68,6 +68,12 @@ def parse():
                    help="budget of the CPU-oracle sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-spread", action="store_true", help="skip the rounds-to-full-spread run")
+    p.add_argument("--parts", type=int, default=None,
+                   help="pipeline parts per rank (N>1; default 4 with RCCL: the exchanges of one "
+                        "part overlap the round kernel of another)")
+    p.add_argument("--sharded", action="store_true",
+                   help="run the sharded engine even at N=1 (one RCCL rank: exchanges are "
+                        "self-copies; measures the sharded path's overhead and overlap)")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (RCCL, one GPU per rank) or gloo (host-staged rows; rehearsal of "
                         "the N>1 path with several ranks on one GPU)")
@@ -193,7 +199,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
-    if world > 1:
+    if world > 1 or args.sharded:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29517")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         import torch.distributed as dist
         if args.dist_backend == "gloo":
             local = local % torch.cuda.device_count()
@@ -213,10 +224,10 @@ def main():
     fk = dict(churn=args.faults[0], drop_push=args.faults[1], drop_pull=args.faults[2])
     if args.schedule != "2P":
         fk["schedule"] = args.schedule
-    if world > 1:
+    if dist is not None:
         from safe_gossip_amd.sharded import ShardedNetwork
         net = ShardedNetwork(n, R, world, seed=args.seed, epoch=0, device=local,
-                             transport="dist", **fk)
+                             transport="dist", parts=args.parts, **fk)
     else:
         net = sg.Network(n, R, seed=args.seed, epoch=0, device=local, **fk)
 
@@ -306,7 +317,8 @@ def main():
                 "params": list(net.params),
                 "parallelism": (f"node-range shards x{dist.get_world_size()}, "
                                 + ("RCCL" if args.dist_backend == "nccl" else args.dist_backend)
-                                + " all-to-all push/pull rows") if world > 1 else "single-gpu",
+                                + f" all-to-all push/pull rows, {net.parts} pipeline part(s) per rank")
+                               if dist is not None else "single-gpu",
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -170,29 +170,42 @@ double      gs_round_kernel_bytes(const gs_engine *e);
 gs_status   gs_round_traffic(gs_engine *e, double *bytes_per_launch, uint32_t *launches);
 
 /* ---- Sharded network (multi-GPU): one engine per rank owns the node range
- * [lo, lo+m).  Per round t the caller moves two sets of rows between ranks
- *  with FIXED-SIZE all-to-all exchanges (equal splits:
- * no row count ever reaches the host, a round needs no host synchronisation):
- *   A(t): exchange-A buffer set t % 2, block d of sendA -> block g of rank d's
- *         recvA (block = info[8] u64 words: push rows of round t and the
- *         source ids of round t+1 for the in-lists, built one round ahead);
- *   B(t): block d of sendB -> block g of rank d's recvB (info[9] words).
- * Sequence per round t >= 1, after gs_next_round has produced round t:
- *   [t == 1: A(0) on set 0] -> A(t) on set t % 2 -> gs_shard_pull -> B(t)
- *   -> gs_next_round (round t+1).
- * Exchanges must be ordered on the engine stream (gs_stream).  gs_send_new
- * takes global node ids owned by this rank; observers report the owned nodes
- * only.  A capacity overflow (probability < 1e-50 per round) is reported as
- * GS_ERR_DEVICE_LIMIT by gs_sync / gs_clear / the observers. */
+ * [lo, lo+m), cut into P pipeline parts of mP nodes.  Per round t the caller
+ * moves two sets of rows between ranks with FIXED-SIZE
+ * all-to-all exchanges (equal splits: no row count ever reaches the host, a
+ * round needs no host synchronisation).  Both buffers are part-major: part h's
+ * region starts at row h*world*capP and holds one sub-block per rank, so the
+ * exchange of one part is ONE equal-split all-to-all over a contiguous region:
+ *   A_h(t): exchange-A buffer set t % 2, part h: world sub-blocks of capP rows
+ *           (the last part: capP + idrows rows, the idrows carrying the source
+ *           ids of round t+1 for the in-lists, built one round ahead) -- push
+ *           rows of round t of the sources in part h;
+ *   B_h(t): part h of sendB -> part h of recvB, world sub-blocks of capP rows.
+ * A row is `row words` u64.  Sequence per round t >= 1, after round t exists:
+ *   [t == 1: A_{P-1}(0) on set 0] -> all A_h(t) -> gs_shard_pull -> B_h(t) ->
+ *   for h < P-1: gs_shard_round_part(h) (needs B_h(t); its rows are A_h(t+1))
+ *   -> gs_next_round (the remaining parts: round t+1 exists) -> A_{P-1}(t+1).
+ * So A_h(t+1) and B_{h+1}(t) run while the round kernel of another part does.
+ * Exchanges must be ordered against the engine stream (gs_stream).
+ * gs_send_new takes global node ids owned by this rank; observers report the
+ * owned nodes only.  A capacity overflow (probability < 1e-50 per round) is
+ * reported as GS_ERR_DEVICE_LIMIT by gs_sync / gs_clear / the observers. */
 gs_status   gs_shard_create(const gs_config *cfg, uint32_t rank, uint32_t world, gs_engine **out);
-/* info = {lo, m, cap (row slots per block of B), capA (row slots per block
- *         of A), row words, world, rank, nodes per rank, u64 words per block
- *         of A, u64 words per block of B, 0, 0} */
+/* The same with `parts` (1..4) pipeline parts (gs_shard_create: 1). */
+gs_status   gs_shard_create_parts(const gs_config *cfg, uint32_t rank, uint32_t world, uint32_t parts,
+                                  gs_engine **out);
+/* info = {lo, m, capP (row slots per rank sub-block of a part), idrows (id
+ *         rows per sub-block of A's last part), row words, world, rank, nodes
+ *         per rank, parts P, nodes per part mP, rows of an A buffer (world *
+ *         (P*capP + idrows)), rows of a B buffer (world * P * capP)} */
 gs_status   gs_shard_info(const gs_engine *e, uint32_t info[12]);
-/* Device buffers of world blocks each: sendA[2], recvA[2] (info[8] words per
- * block), sendB, recvB (info[9] words per block). */
+/* Device buffers: sendA[2], recvA[2] (info[10] rows each), sendB, recvB
+ * (info[11] rows each). */
 gs_status   gs_shard_bind(gs_engine *e, void *sendA0, void *sendA1, void *recvA0, void *recvA1,
                           void *sendB, void *recvB);
+/* Round kernel of pipeline part `part` of the pending round (parts in order,
+ * part < P-1; gs_next_round launches the rest and completes the round). */
+gs_status   gs_shard_round_part(gs_engine *e, uint32_t part);
 /* After exchange A of the current round: the pull rows (into sendB), and the
  * next round's in-lists on the side stream. */
 gs_status   gs_shard_pull(gs_engine *e);

@@ -136,6 +136,9 @@ SYMBOLS = {
     # sharded engines (safe_gossip_amd.sharded)
     "gs_shard_create": (ctypes.c_int, [ctypes.POINTER(_Config), ctypes.c_uint32, ctypes.c_uint32,
                                        ctypes.POINTER(_P)]),
+    "gs_shard_create_parts": (ctypes.c_int, [ctypes.POINTER(_Config), ctypes.c_uint32, ctypes.c_uint32,
+                                             ctypes.c_uint32, ctypes.POINTER(_P)]),
+    "gs_shard_round_part": (ctypes.c_int, [_P, ctypes.c_uint32]),
     "gs_shard_info": (ctypes.c_int, [_P, _U32P]),
     "gs_shard_bind": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P]),
     "gs_shard_pull": (ctypes.c_int, [_P]),

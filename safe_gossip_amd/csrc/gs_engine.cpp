@@ -95,6 +95,12 @@ struct gs_engine {
     u64 *sendA[2] = {nullptr, nullptr}, *recvA[2] = {nullptr, nullptr};
     u64 *sendB = nullptr, *recvB = nullptr;
     uint32_t pulled_round = 0;  // round whose gs_shard_pull ran (its plan of t+2 is launched)
+    // Pipeline parts of the round in progress (gs_shard_round_part): parts
+    // [0, parts_done) are launched with the arguments `ra` (mode ra_mode).
+    uint32_t parts_done = 0;
+    gs::RoundArgs ra{};
+    int ra_mode = 0;
+    bool ra_sparse = false;
     uint32_t *st32 = nullptr;  // [n][4] u32 deltas
     u64 *st64 = nullptr;       // [n][4] folded totals
     uint32_t fold_every = 1, since_fold = 0;
@@ -125,11 +131,14 @@ struct gs_engine {
     uint32_t obs_pend_cap = 0;
     bool obs_valid = false;
     bool started = false;          // some send_new since the last clear (Error::AlreadyStarted)
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t lt0 = nullptr, lt1 = nullptr;  // the last round's first / last timing event
     bool timing = false, timed = false;
-    // per-round kernel timing ring (gs_round_kernel_times)
-    std::vector<hipEvent_t> tev;  // pairs
+    // per-round kernel timing ring (gs_round_kernel_times): kMaxParts event
+    // pairs per round (one per pipeline part; the round's time is their sum)
+    std::vector<hipEvent_t> tev;
+    std::vector<uint8_t> tparts;  // parts timed per slot
     uint32_t tcount = 0;
+    uint32_t tslot = ~0u;  // timing slot of the round in progress
 };
 
 namespace {
@@ -197,8 +206,6 @@ void release(gs_engine *e) {
         if (b) (void)hipFree(b);
     if (e->inj_host) (void)hipHostFree(e->inj_host);
     for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
-    if (e->ev0) (void)hipEventDestroy(e->ev0);
-    if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
@@ -227,6 +234,7 @@ gs_status reset_state(gs_engine *e) {
     e->round = 0;
     e->seq_round = ~0u;
     e->pulled_round = 0;
+    e->parts_done = 0;
     e->deliver_pending = false;
     e->pending.clear();
     e->obs_valid = false;
@@ -536,7 +544,7 @@ namespace {
 
 // Common constructor: a whole network (world == 0) or the node range of rank
 // `rank` of a network sharded over `world` ranks.
-gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_engine **out) {
+gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uint32_t parts, gs_engine **out) {
     if (!cfg || !out) return GS_ERR_INVALID_ARGUMENT;
     *out = nullptr;
     const uint32_t nglob = cfg->n_nodes, R = cfg->n_rumors;
@@ -546,7 +554,8 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
     // (gs_common.h kTgMask), whatever the parameters.
     if (nglob > gs::kTgMask + 1u) return GS_ERR_UNSUPPORTED;
     gs::ShardPlan sp{};
-    if (world) sp = gs::shard_plan(nglob, world, rank, R >= 64 ? (next_pow2(R) / 64) : 1u);
+    if (world && (parts == 0 || parts > gs::kMaxParts)) return GS_ERR_INVALID_ARGUMENT;
+    if (world) sp = gs::shard_plan(nglob, world, rank, R >= 64 ? (next_pow2(R) / 64) : 1u, parts);
     const uint32_t n = world ? sp.m : nglob;  // nodes owned by this engine
     uint8_t p[3];
     gs_derive_params(nglob, p);
@@ -637,9 +646,21 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, gs_
     // Per round a node's u32 Statistics deltas grow by at most 32*R_pad + 32
     // (in-degree <= 30 is enforced); fold them into u64 well before a wrap.
     e->fold_every = (uint32_t)std::max<uint64_t>(1, 0xFFFFFFFFull / (32ull * g.rpad + 32) / 2);
-    bool ok = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&e->cstream, hipStreamNonBlocking) == hipSuccess &&
-              hipEventCreate(&e->ev0) == hipSuccess && hipEventCreate(&e->ev1) == hipSuccess;
+    bool ok;
+    if (e->shard) {
+        // Shard engines share the device with the process group's collective
+        // stream (normal priority): the engine stream takes a high-priority
+        // and the plan / in-list side stream a low-priority hardware queue, so
+        // neither is serialised behind an exchange on a shared queue (HIP
+        // round-robins streams of one priority over GPU_MAX_HW_QUEUES queues).
+        int least = 0, greatest = 0;
+        ok = hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
+             hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, greatest) == hipSuccess &&
+             hipStreamCreateWithPriority(&e->cstream, hipStreamNonBlocking, least) == hipSuccess;
+    } else {
+        ok = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess &&
+             hipStreamCreateWithFlags(&e->cstream, hipStreamNonBlocking) == hipSuccess;
+    }
     for (int i = 0; i < 3 && ok && e->shard; ++i) {
         const size_t words = gs::shard_plan_words(e->sp, &e->spl);
         ok = hipEventCreateWithFlags(&e->ev_plan[i], hipEventDisableTiming) == hipSuccess &&
@@ -723,11 +744,17 @@ gs_status launch_edges(gs_engine *e, uint32_t r) {
 
 extern "C" {
 
-gs_status gs_create(const gs_config *cfg, gs_engine **out) { return create_engine(cfg, 0, 0, out); }
+gs_status gs_create(const gs_config *cfg, gs_engine **out) { return create_engine(cfg, 0, 0, 0, out); }
 
 gs_status gs_shard_create(const gs_config *cfg, uint32_t rank, uint32_t world, gs_engine **out) {
     if (world == 0) return GS_ERR_INVALID_ARGUMENT;
-    return create_engine(cfg, rank, world, out);
+    return create_engine(cfg, rank, world, 1, out);
+}
+
+gs_status gs_shard_create_parts(const gs_config *cfg, uint32_t rank, uint32_t world, uint32_t parts,
+                                gs_engine **out) {
+    if (world == 0) return GS_ERR_INVALID_ARGUMENT;
+    return create_engine(cfg, rank, world, parts, out);
 }
 
 gs_status gs_shard_info(const gs_engine *e, uint32_t info[12]) {
@@ -735,15 +762,16 @@ gs_status gs_shard_info(const gs_engine *e, uint32_t info[12]) {
     const uint32_t wa = 2 * e->g.W;  // u64 words per row (2-plane class code)
     info[0] = e->sp.lo;
     info[1] = e->sp.m;
-    info[2] = e->sp.cap;
-    info[3] = e->sp.capA;
+    info[2] = e->sp.capP;
+    info[3] = e->sp.idrows;
     info[4] = wa;
     info[5] = e->sp.G;
     info[6] = e->sp.g;
     info[7] = e->sp.chunk;
-    info[8] = e->sp.capA * wa;  // u64 words per exchange-A block
-    info[9] = e->sp.cap * wa;   // u64 words per exchange-B block
-    info[10] = info[11] = 0;
+    info[8] = e->sp.P;
+    info[9] = e->sp.mP;
+    info[10] = gs::shard_slotsA(e->sp);  // rows of an exchange-A buffer
+    info[11] = e->sp.G * e->sp.P * e->sp.capP;  // rows of an exchange-B buffer
     return GS_OK;
 }
 
@@ -792,8 +820,7 @@ gs_status gs_shard_pull(gs_engine *e) {
     a.EP = ed + e->sel.EP;
     a.recvA = e->recvA[t % 2];
     a.sendB = e->sendB;
-    a.cap = e->sp.cap;
-    a.capA = e->sp.capA;
+    a.P = e->sp;
     a.g = e->g;
     GS_HIP(gs::launch_pull(a, e->stream));
     return GS_OK;
@@ -845,14 +872,17 @@ gs_status gs_set_params(gs_engine *e, const uint8_t params[3]) {
     return GS_OK;
 }
 
-gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
-    if (!e) return GS_ERR_INVALID_ARGUMENT;
-    if ((e->shard ? e->n_global : e->g.n) < 2) return GS_ERR_NO_PEERS;  // src/gossiper.rs:71-74
-    if (e->shard && !e->sendB) return GS_ERR_INVALID_ARGUMENT;  // gs_shard_bind first
-    // a shard delivers round t only after its exchanges (gs_shard_pull)
-    if (e->shard && e->round > 0 && e->pulled_round != e->round) return GS_ERR_INVALID_ARGUMENT;
-    gs_status st = set_device(e);
-    if (st != GS_OK) return st;
+}  // extern "C"
+
+namespace {
+
+// ------------------------------------------------------------ round
+// A round is launched as one or more pipeline parts (shard engines: the
+// node-range parts of gs_shard_create_parts; otherwise one part = the whole
+// grid): round_begin sequences the round and fixes its arguments, launch_part
+// launches one part's blocks, round_end does the bookkeeping after the last.
+gs_status round_begin(gs_engine *e) {
+    gs_status st = GS_OK;
     if (e->shard) {
         // cstream work launched below may reuse buffers read before this point
         GS_HIP(hipEventRecord(e->ev_main, e->stream));
@@ -899,12 +929,6 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
     } else if (e->deliver_pending) {
         e->dense_launches++;
     }
-    hipEvent_t t0 = e->ev0, t1 = e->ev1;
-    if (e->timing && e->tcount < kTimingSlots) {
-        t0 = e->tev[2 * e->tcount];
-        t1 = e->tev[2 * e->tcount + 1];
-        e->tcount++;
-    }
     const uint32_t rs = R0 & 1u;  // set holding round t = e->round
     if (e->shard) {
         GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[(R0 + 1) % 3], 0));
@@ -914,9 +938,47 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
         st = seq_prepare(e);  // SEQ: pull batches of round t (no-op for 2P)
         if (st != GS_OK) return st;
     }
-    if (e->timing) GS_HIP(hipEventRecord(t0, e->stream));
-    GS_HIP(gs::launch_round(a, e->deliver_pending ? 1 : 0, e->stream));
-    if (e->timing) GS_HIP(hipEventRecord(t1, e->stream));
+    e->ra = a;
+    e->ra_mode = e->deliver_pending ? 1 : 0;
+    e->ra_sparse = sparse;
+    e->tslot = ~0u;
+    if (e->timing && e->tcount < kTimingSlots) {
+        e->tslot = e->tcount++;
+        e->tparts[e->tslot] = 0;
+    }
+    return GS_OK;
+}
+
+gs_status launch_part(gs_engine *e, uint32_t h) {
+    gs::RoundArgs a = e->ra;
+    if (e->shard && e->sp.P > 1) {  // blocks of part h (blk_count 0 would mean the whole grid)
+        const u64 nblk = (e->g.nseg + 255) / 256;
+        const u64 per = e->g.small ? (u64)e->sp.bP : (u64)e->sp.mP * e->g.W / 256;
+        const u64 b0 = std::min<u64>((u64)h * per, nblk), b1 = std::min<u64>(b0 + per, nblk);
+        if (b1 == b0) return GS_OK;
+        a.blk_off = (uint32_t)b0;
+        a.blk_count = (uint32_t)(b1 - b0);
+    }
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    if (e->timing && e->tslot != ~0u) {
+        t0 = e->tev[2 * ((size_t)e->tslot * gs::kMaxParts + h)];
+        t1 = e->tev[2 * ((size_t)e->tslot * gs::kMaxParts + h) + 1];
+        if (!e->tparts[e->tslot]) e->lt0 = t0;  // first timed part
+        e->tparts[e->tslot] |= (uint8_t)(1u << h);
+        e->lt1 = t1;
+    }
+    if (t0) GS_HIP(hipEventRecord(t0, e->stream));
+    GS_HIP(gs::launch_round(a, e->ra_mode, e->stream));
+    if (t1) GS_HIP(hipEventRecord(t1, e->stream));
+    return GS_OK;
+}
+
+gs_status round_end(gs_engine *e, gs_round_report *report) {
+    gs_status st = GS_OK;
+    const uint32_t R0 = e->round;
+    const bool sparse = e->ra_sparse;
+    const uint32_t rs = R0 & 1u;  // set holding round t = e->round
+    const gs::RoundArgs &a = e->ra;
     if (sparse) {  // this round's density, for the call after next
         const uint32_t par = (R0 + 1) & 1u;
         GS_HIP(hipMemcpyAsync(e->dens_host + par * gs::kDensSlots, a.dens, gs::kDensSlots * sizeof(u64),
@@ -925,8 +987,6 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
         e->dens_round[par] = R0 + 1;
     }
     if (!e->shard) GS_HIP(hipEventRecord(e->ev_read[rs], e->stream));
-    e->ev0 = t0;
-    e->ev1 = t1;
     e->timed = e->timing;
     e->round += 1;
     e->cur ^= 1;
@@ -1002,6 +1062,42 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
         if (fl[2]) return GS_ERR_DEVICE_LIMIT;
     }
     return GS_OK;
+}
+
+gs_status round_checks(gs_engine *e) {
+    if ((e->shard ? e->n_global : e->g.n) < 2) return GS_ERR_NO_PEERS;  // src/gossiper.rs:71-74
+    if (e->shard && !e->sendB) return GS_ERR_INVALID_ARGUMENT;  // gs_shard_bind first
+    // a shard delivers round t only after its exchanges (gs_shard_pull)
+    if (e->shard && e->round > 0 && e->pulled_round != e->round) return GS_ERR_INVALID_ARGUMENT;
+    return set_device(e);
+}
+
+}  // namespace
+
+extern "C" {
+
+gs_status gs_shard_round_part(gs_engine *e, uint32_t part) {
+    if (!e || !e->shard || part != e->parts_done || part >= e->sp.P) return GS_ERR_INVALID_ARGUMENT;
+    gs_status st = round_checks(e);
+    if (st == GS_OK && part == 0) st = round_begin(e);
+    if (st == GS_OK) st = launch_part(e, part);
+    if (st != GS_OK) {
+        e->parts_done = 0;
+        return st;
+    }
+    e->parts_done = part + 1;
+    return GS_OK;
+}
+
+gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
+    if (!e) return GS_ERR_INVALID_ARGUMENT;
+    gs_status st = round_checks(e);
+    if (st == GS_OK && e->parts_done == 0) st = round_begin(e);
+    const uint32_t parts = e->shard ? e->sp.P : 1u;
+    for (uint32_t h = e->parts_done; st == GS_OK && h < parts; ++h) st = launch_part(e, h);
+    e->parts_done = 0;
+    if (st != GS_OK) return st;
+    return round_end(e, report);
 }
 
 gs_status gs_statistics_all(gs_engine *e, uint64_t *out) {
@@ -1164,7 +1260,8 @@ void gs_set_timing(gs_engine *e, int enable) {
     e->timing = enable != 0;
     if (e->timing && e->tev.empty()) {
         (void)hipSetDevice(e->device);
-        e->tev.resize(2 * (size_t)kTimingSlots, nullptr);
+        e->tev.resize(2 * (size_t)kTimingSlots * gs::kMaxParts, nullptr);
+        e->tparts.assign(kTimingSlots, 0);
         for (auto &ev : e->tev)
             if (hipEventCreate(&ev) != hipSuccess) {
                 e->timing = false;
@@ -1186,19 +1283,25 @@ int32_t gs_round_kernel_times(gs_engine *e, float *out_ms, uint32_t max) {
     if (hipStreamSynchronize(e->stream) != hipSuccess) return -1;
     const uint32_t m = std::min(max, e->tcount);
     for (uint32_t i = 0; i < m; ++i) {
-        float ms = -1.0f;
-        if (hipEventElapsedTime(&ms, e->tev[2 * i], e->tev[2 * i + 1]) != hipSuccess) return -1;
-        out_ms[i] = ms;
+        float sum = 0.0f;
+        for (uint32_t h = 0; h < gs::kMaxParts; ++h) {
+            if (!(e->tparts[i] & (1u << h))) continue;
+            const size_t k = 2 * ((size_t)i * gs::kMaxParts + h);
+            float ms = -1.0f;
+            if (hipEventElapsedTime(&ms, e->tev[k], e->tev[k + 1]) != hipSuccess) return -1;
+            sum += ms;
+        }
+        out_ms[i] = sum;
     }
     e->tcount = 0;
     return (int32_t)m;
 }
 
 float gs_last_round_kernel_ms(gs_engine *e) {
-    if (!e || !e->timed) return -1.0f;
-    if (hipEventSynchronize(e->ev1) != hipSuccess) return -1.0f;
+    if (!e || !e->timed || !e->lt0 || !e->lt1) return -1.0f;
+    if (hipEventSynchronize(e->lt1) != hipSuccess) return -1.0f;
     float ms = -1.0f;
-    if (hipEventElapsedTime(&ms, e->ev0, e->ev1) != hipSuccess) return -1.0f;
+    if (hipEventElapsedTime(&ms, e->lt0, e->lt1) != hipSuccess) return -1.0f;
     return ms;
 }
 

@@ -174,6 +174,7 @@ hipError_t launch_seq_pull_pass(const SeqArgs &a, uint32_t level, uint32_t start
 // ---------------------------------------------------------------- shards
 // One rank's slice of a network sharded over G ranks (gs_shard.hip).
 constexpr uint32_t kMaxShards = 64;
+constexpr uint32_t kMaxParts = 4;  // pipeline parts of a rank's node range
 struct ShardPlan {
     uint32_t n;         // global nodes
     uint32_t G, g;      // ranks, this rank
@@ -181,10 +182,51 @@ struct ShardPlan {
     uint32_t lo, m;     // owned range [lo, lo+m)
     uint32_t nblk_own;  // 256-source plan blocks over the owned range
     uint32_t W;         // words per plane of a row (rows are 2W words)
-    uint32_t cap;       // row slots per (source rank, destination rank) block
-    uint32_t capA;      // row slots per exchange-A block: cap rows + cap u32 ids
-    CsrPlan edges;      // counting sort of the G*capA receive slots over the m targets
+    // Pipeline parts: the owned range is cut into P parts of mP nodes (a
+    // multiple of 256, the same on every rank); the round kernel of part h
+    // runs while the exchanges of the other parts are in flight.  Each
+    // exchange is stored part-major: part h's region holds one sub-block of
+    // capP row slots per rank (exchange A: the last part's sub-blocks also
+    // carry idrows rows of next-round source ids), so the exchange of one part
+    // is ONE equal-split all-to-all over a contiguous region.
+    uint32_t P, mP, bP; // parts, nodes per part, plan blocks per part
+    uint32_t capP;      // row slots per (source rank, destination rank, part)
+    uint32_t idrows;    // rows of u32 ids per block of the last part of A (P*capP ids)
+    CsrPlan edges;      // counting sort of the A receive slots over the m targets
 };
+// Row slot of (rank block s, part h, index i) in an exchange-A / -B buffer.
+__host__ __device__ inline uint32_t shard_blockA(const ShardPlan &P, uint32_t h) {
+    return P.capP + (h + 1u == P.P ? P.idrows : 0u);
+}
+__host__ __device__ inline uint32_t shard_a_slot(const ShardPlan &P, uint32_t s, uint32_t h, uint32_t i) {
+    return h * P.G * P.capP + s * shard_blockA(P, h) + i;
+}
+__host__ __device__ inline uint32_t shard_b_slot(const ShardPlan &P, uint32_t s, uint32_t h, uint32_t i) {
+    return (h * P.G + s) * P.capP + i;
+}
+__host__ __device__ inline uint32_t shard_slotsA(const ShardPlan &P) {
+    return P.G * (P.P * P.capP + P.idrows);
+}
+struct SlotPos {
+    uint32_t s, h, i;  // i >= capP: an id row
+};
+__host__ __device__ inline SlotPos shard_a_decode(const ShardPlan &P, uint32_t e) {
+    const uint32_t reg = P.G * P.capP;
+    uint32_t h = e / reg;
+    if (h > P.P - 1u) h = P.P - 1u;
+    const uint32_t r = e - h * reg, ba = shard_blockA(P, h);
+    const uint32_t s = r / ba;
+    return SlotPos{s, h, r - s * ba};
+}
+// Pushers are listed in ascending source order = ascending (s, h, i).
+__host__ __device__ inline uint32_t shard_slot_key(const ShardPlan &P, const SlotPos &q) {
+    return (q.s * P.P + q.h) * P.capP + q.i;
+}
+__host__ __device__ inline uint32_t shard_key_slot(const ShardPlan &P, uint32_t key) {
+    const uint32_t per = P.P * P.capP;
+    const uint32_t s = key / per, r = key - s * per, h = r / P.capP;
+    return shard_a_slot(P, s, h, r - h * P.capP);
+}
 // u32-word offsets inside one plan set (round r: targets and send slots of
 // the owned sources) and one in-list set (round r: receive-slot in-lists).
 struct ShardPlanLayout {
@@ -193,7 +235,7 @@ struct ShardPlanLayout {
 struct ShardEdgeLayout {
     size_t E_id, E_key, M, tot, base, EP, IN, IN2, pairs;
 };
-ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W);
+ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t parts);
 size_t shard_plan_words(const ShardPlan &P, ShardPlanLayout *L);
 size_t shard_edge_words(const ShardPlan &P, ShardEdgeLayout *L);
 // Plan of `round`: owned targets, send slots, and the ids of every block of
@@ -212,8 +254,8 @@ struct PullArgs {
     const uint32_t *IN2;   // their third pushers
     const uint32_t *EP;
     const u64 *recvA;      // round-t push rows received (slots of 2W words)
-    u64 *sendB;            // pull rows out (exchange-B slots)
-    uint32_t cap, capA;    // slot e of A (block e / capA) is slot e - (e / capA)(capA - cap) of B
+    u64 *sendB;            // pull rows out (exchange-B slots: A slot (s, h, i) -> B slot (s, h, i))
+    ShardPlan P;
     Geometry g;            // local geometry (n = m)
 };
 hipError_t launch_pull(const PullArgs &a, hipStream_t s);

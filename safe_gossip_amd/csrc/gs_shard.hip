@@ -1,27 +1,32 @@
 // gs_shard.hip -- kernels of a SHARD engine: one rank's node range of a
 // network sharded over G ranks.
 //
-// Per round t, rank g owns nodes [lo, lo+m).  Data moves between ranks in two
-// exchanges of FIXED-SIZE blocks (RCCL all-to-all with equal splits over xGMI,
-// or device copies when the shards share a GPU), so no row count ever has to
-// reach the host and a round is enqueued without a host synchronisation:
-//   A (push rows):  block d of rank g's send buffer = cap row slots of 2W
-//                   words (g's sources targeting rank d, ascending, as the
-//                   2-plane class code of their round-t push batch: 01
-//                   counter 1, 10 counter 2, 11 counter 255) followed by cap
-//                   u32 source ids of round t+1's sources targeting d
-//                   (ascending; 0xFFFFFFFF = empty slot).  Rank g's receive
-//                   buffer then holds, block by block in rank order, the rows
-//                   of ALL sources targeting g in ascending source order, and
-//                   the ids of next round's, from which it builds next round's
-//                   in-lists while this round is still being delivered.
+// Per round t, rank g owns nodes [lo, lo+m), cut into P pipeline parts of mP
+// nodes.  Data moves between ranks in two exchanges of FIXED-SIZE blocks (RCCL
+// all-to-all with equal splits over xGMI, or device copies when the shards
+// share a GPU), so no row count ever has to reach the host and a round is
+// enqueued without a host synchronisation.  Both buffers are part-major:
+// part h's region holds one sub-block of capP row slots per rank, and each
+// part moves in an all-to-all of its own, so the exchanges of one part overlap
+// the round kernel of another (gs_shard_round_part):
+//   A (push rows):  sub-block (d, h) of rank g's send buffer = g's part-h
+//                   sources targeting rank d, ascending, as the 2-plane class
+//                   code of their round-t push batch (01 counter 1, 10 counter
+//                   2, 11 counter 255); the last part's sub-blocks carry after
+//                   their rows the P*capP u32 source ids of round t+1's sources
+//                   targeting d (id of (part h, index i) at h*capP + i;
+//                   0xFFFFFFFF = empty slot).  Rank g then holds the rows of ALL
+//                   sources targeting g; listed in (rank, part, index) order
+//                   they are in ascending source order, and the ids of next
+//                   round's let it build next round's in-lists while this round
+//                   is still being delivered.
 //   B (pull rows):  the owner of z returns, for each pusher x of z, the pull
 //                   batch Gossip::receive built for x (src/gossip.rs:124-151):
 //                   z's live set plus the entries z created from pushers ahead
-//                   of x, as a 2-plane class code; block layout of A without
-//                   the id slots.
-// Capacity: cap = mean + 16 sd + 64 rows per (source rank, destination rank)
-// pair (binomial counts); an overflow raises the device-limit flag.
+//                   of x, as a 2-plane class code; sub-block layout of A
+//                   without the id rows.
+// Capacity: capP = mean + 16 sd + 64 rows per (source rank, destination rank,
+// part) sub-block (binomial counts); an overflow raises the device-limit flag.
 // Per-rank work is O(m): a plan computes the Philox targets of the OWNED
 // sources only; a receiver recomputes the targets of the ids it receives.
 //   plan_count / plan_scan / plan_emit / plan_idle : targets, send slots
@@ -48,9 +53,14 @@ GS_DEV uint32_t dest_rank(const ShardPlan &P, uint32_t t) {
     return (t & kTgDead) ? P.G : (t & kTgMask) / P.chunk;
 }
 
-// Id slots of block d inside an exchange-A buffer.
+// Id slots of block d inside an exchange-A buffer: the idrows rows after the
+// capP row slots of d's sub-block of the last part (P*capP ids; the id of
+// next round's source (part h, index i) at h*capP + i).
 GS_DEV uint32_t *id_slots(const ShardPlan &P, u64 *bufA, uint32_t d) {
-    return reinterpret_cast<uint32_t *>(bufA + ((u64)d * P.capA + P.cap) * (2u * P.W));
+    return reinterpret_cast<uint32_t *>(bufA + (u64)shard_a_slot(P, d, P.P - 1u, P.capP) * (2u * P.W));
+}
+GS_DEV const uint32_t *id_slots(const ShardPlan &P, const u64 *bufA, uint32_t d) {
+    return reinterpret_cast<const uint32_t *>(bufA + (u64)shard_a_slot(P, d, P.P - 1u, P.capP) * (2u * P.W));
 }
 
 __global__ __launch_bounds__(kPlanBlock) void plan_count(ShardPlan P, uint64_t seed, uint32_t epoch,
@@ -109,21 +119,23 @@ GS_DEV uint32_t chunked_scan(uint32_t *v, uint32_t count, uint32_t stride, uint3
     return tot;
 }
 
-// One block per destination d: bc_d[.][d] over the owned blocks -> offsets
-// within block d of the exchange, cnt[d] = rows sent to d.
+// One block per (destination d, part h): bc_d[.][d] over the part's plan
+// blocks -> offsets within sub-block (d, h) of the exchange, cnt[d * P + h] =
+// rows part h sends to d.
 __global__ __launch_bounds__(kPlanScanThreads) void plan_scan(ShardPlan P, uint32_t *bc_d, uint32_t *cnt,
                                                               uint32_t *flags) {
     __shared__ uint32_t lds[kPlanScanThreads / 64];
-    const uint32_t d = blockIdx.x;
-    const uint32_t c = chunked_scan(bc_d + d, P.nblk_own, P.G, lds);
+    const uint32_t d = blockIdx.x / P.P, h = blockIdx.x - d * P.P;
+    const uint32_t b0 = min(h * P.bP, P.nblk_own), b1 = min(b0 + P.bP, P.nblk_own);
+    const uint32_t c = chunked_scan(bc_d + (u64)b0 * P.G + d, b1 - b0, P.G, lds);
     if (threadIdx.x == 0) {
-        cnt[d] = c;
-        if (c > P.cap) atomicOr(&flags[2], 1u);  // more rows than the block holds
+        cnt[blockIdx.x] = c;
+        if (c > P.capP) atomicOr(&flags[2], 1u);  // more rows than the sub-block holds
     }
 }
 
-// Send slots of every owned source (stable: ascending x within each block d)
-// and the ids of block d.
+// Send slots of every owned source (stable: ascending x within each
+// sub-block (d, h)) and the ids of block d.
 __global__ __launch_bounds__(kPlanBlock) void plan_emit(ShardPlan P, const uint32_t *__restrict__ tg,
                                                         const uint32_t *__restrict__ off_d, uint32_t *SPOSA,
                                                         uint32_t *SPOSB, u64 *bufA) {
@@ -146,37 +158,37 @@ __global__ __launch_bounds__(kPlanBlock) void plan_emit(ShardPlan P, const uint3
         uint32_t before = 0;
         for (uint32_t w = 0; w < wid; ++w) before += wcnt[d][w];
         const uint32_t i = off_d[(u64)blockIdx.x * P.G + d] + before + myrank;
-        if (i < P.cap) {  // an overflow is flagged by plan_scan
-            sa = d * P.capA + i;
-            sb = d * P.cap + i;
-            id_slots(P, bufA, d)[i] = P.lo + xl;
+        const uint32_t h = blockIdx.x / P.bP;  // the part of this plan block
+        if (i < P.capP) {  // an overflow is flagged by plan_scan
+            sa = shard_a_slot(P, d, h, i);
+            sb = shard_b_slot(P, d, h, i);
+            id_slots(P, bufA, d)[h * P.capP + i] = P.lo + xl;
         }
     }
     SPOSA[xl] = sa;
     SPOSB[xl] = sb;
 }
 
-// Empty id slots of every block (past cnt[d]).
+// Empty id slots of every sub-block (d, h) (past cnt[d * P + h]).
 __global__ __launch_bounds__(256) void plan_idle(ShardPlan P, const uint32_t *__restrict__ cnt, u64 *bufA) {
-    const uint32_t d = blockIdx.y;
+    const uint32_t d = blockIdx.y / P.P, h = blockIdx.y - d * P.P;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < P.cap && i >= cnt[d]) id_slots(P, bufA, d)[i] = kNoId;
+    if (i < P.capP && i >= cnt[blockIdx.y]) id_slots(P, bufA, d)[h * P.capP + i] = kNoId;
 }
 
 // ------------------------------------------------ in-lists of receive slots
-// Receive slot e = s * capA + i (block s = source rank): its id, and the
-// local target of that source (recomputed from the Philox stream), or
-// kNoId for an empty slot (and for the id slots themselves).
+// Receive slot e = (source rank s, part h, index i) of exchange A: its id, and
+// the local target of that source (recomputed from the Philox stream), or
+// kNoId for an empty slot (and for the id rows themselves).
 __global__ __launch_bounds__(256) void edge_keys(ShardPlan P, const u64 *__restrict__ recvA, uint64_t seed,
                                                  uint32_t epoch, uint32_t round, Faults f, uint32_t *E_id,
                                                  uint32_t *E_key, uint32_t *flags) {
-    const uint32_t s = blockIdx.y;
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.capA) return;
-    const u64 e = (u64)s * P.capA + i;
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= shard_slotsA(P)) return;
+    const SlotPos q = shard_a_decode(P, e);
     uint32_t id = kNoId, key = kNoId;
-    if (i < P.cap) {
-        id = reinterpret_cast<const uint32_t *>(recvA + ((u64)s * P.capA + P.cap) * (2u * P.W))[i];
+    if (q.i < P.capP) {
+        id = id_slots(P, recvA, q.s)[q.h * P.capP + q.i];
         if (id != kNoId) {
             const uint32_t tw = target_word(seed, epoch, round, id, P.n, f);
             const uint32_t t = tw & kTgMask;
@@ -232,7 +244,8 @@ __global__ __launch_bounds__(kScanBlock) void edge_scan_small(const uint32_t *in
     }
 }
 
-__global__ __launch_bounds__(256) void edge_bin_scatter(CsrPlan p, const uint32_t *__restrict__ E_key,
+// pairs = (target within the bin, source-order key of the slot)
+__global__ __launch_bounds__(256) void edge_bin_scatter(CsrPlan p, ShardPlan P, const uint32_t *__restrict__ E_key,
                                                         const uint32_t *__restrict__ M,
                                                         const uint32_t *__restrict__ base, u64 *pairs) {
     extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
@@ -246,13 +259,14 @@ __global__ __launch_bounds__(256) void edge_bin_scatter(CsrPlan p, const uint32_
         const uint32_t t = E_key[e];
         if (t == kNoId) continue;
         const uint32_t pos = atomicAdd(&cur[t >> p.logbin], 1u);
-        pairs[pos] = ((u64)(t & lm) << 32) | (uint32_t)e;
+        pairs[pos] = ((u64)(t & lm) << 32) | shard_slot_key(P, shard_a_decode(P, (uint32_t)e));
     }
 }
 
 // One block per bin of local targets: counting sort by target, then each
-// node's receive slots in ascending order (= its pushers in ascending order).
-__global__ __launch_bounds__(256) void edge_bin_sort(const u64 *__restrict__ pairs, CsrPlan p,
+// node's pushers in ascending source order (by slot key), stored as receive
+// slots.
+__global__ __launch_bounds__(256) void edge_bin_sort(const u64 *__restrict__ pairs, CsrPlan p, ShardPlan P,
                                                      uint32_t nodes_total,
                                                      const uint32_t *__restrict__ base,
                                                      const uint32_t *__restrict__ tot, uint32_t *EP,
@@ -289,7 +303,7 @@ __global__ __launch_bounds__(256) void edge_bin_sort(const u64 *__restrict__ pai
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nodes; i += blockDim.x) {
         const uint32_t a = start + (i ? h[i - 1] : 0u), e = start + h[i];
-        for (uint32_t q = a + 1; q < e; ++q) {  // receive slots ascending = pushers ascending
+        for (uint32_t q = a + 1; q < e; ++q) {  // slot keys ascending = pushers ascending
             const uint32_t v = EP[q];
             uint32_t r = q;
             while (r > a && EP[r - 1] > v) {
@@ -298,6 +312,7 @@ __global__ __launch_bounds__(256) void edge_bin_sort(const u64 *__restrict__ pai
             }
             EP[r] = v;
         }
+        for (uint32_t q = a; q < e; ++q) EP[q] = shard_key_slot(P, EP[q]);
         const uint32_t k = e - a;
         const uint32_t tz = tg[nb0 + i] & kTgMask;  // t(z): did it push to z?
         uint32_t zi = 0xFFFFu;
@@ -308,7 +323,7 @@ __global__ __launch_bounds__(256) void edge_bin_sort(const u64 *__restrict__ pai
     }
 }
 
-ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W) {
+ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t parts) {
     ShardPlan P{};
     P.n = n;
     P.G = G;
@@ -322,16 +337,20 @@ ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W) {
     P.lo = (uint32_t)lo;
     P.m = (uint32_t)(hi - lo);
     P.nblk_own = (uint32_t)(((u64)P.m + kPlanBlock - 1) / kPlanBlock);
-    // rows from one rank's sources to one rank: ~Binomial(chunk, chunk/(n-1));
+    P.P = std::max<uint32_t>(1, std::min(parts, kMaxParts));
+    const u64 mp = ((chunk + P.P - 1) / P.P + kPlanBlock - 1) / kPlanBlock * kPlanBlock;
+    P.mP = (uint32_t)mp;
+    P.bP = (uint32_t)(mp / kPlanBlock);
+    // rows from one part of one rank to one rank: ~Binomial(mP, chunk/(n-1));
     // 16 standard deviations (the same on every rank: equal exchange splits)
-    const double mean = (double)chunk * (double)chunk / std::max(1.0, (double)n - 1.0);
-    double capd = std::min<double>((double)chunk, mean + 16.0 * std::sqrt(mean + 1.0) + 64.0);
-    const u64 q = std::max<u64>(64, 4ull * W);  // cap u32 ids fill whole rows of 2W words
-    P.cap = (uint32_t)(((u64)std::ceil(capd) + q - 1) / q * q);
-    P.capA = P.cap + P.cap / (4u * W);
-    // counting sort of the G * capA receive slots over the m local targets
+    const double mean = (double)mp * (double)chunk / std::max(1.0, (double)n - 1.0);
+    double capd = std::min<double>((double)mp, mean + 16.0 * std::sqrt(mean + 1.0) + 64.0);
+    const u64 q = std::max<u64>(64, 4ull * W);  // P*capP u32 ids fill whole rows of 2W words
+    P.capP = (uint32_t)(((u64)std::ceil(capd) + q - 1) / q * q);
+    P.idrows = P.P * P.capP / (4u * W);
+    // counting sort of the receive slots of A over the m local targets
     CsrPlan &c = P.edges;
-    c.n = std::max<uint32_t>(G * P.capA, 1);
+    c.n = std::max<uint32_t>(shard_slotsA(P), 1);
     uint32_t bin = 4096;
     while ((u64)bin * 16384u < P.m) bin <<= 1;
     c.bin = bin;
@@ -355,7 +374,7 @@ size_t shard_plan_words(const ShardPlan &P, ShardPlanLayout *L) {
     L->SPOSA = take(P.m);
     L->SPOSB = take(P.m);
     L->bc_d = take((size_t)P.nblk_own * P.G);
-    L->cnt = take(P.G);
+    L->cnt = take((size_t)P.G * P.P);
     return off;
 }
 
@@ -366,7 +385,7 @@ size_t shard_edge_words(const ShardPlan &P, ShardEdgeLayout *L) {
         off += (words + 3) / 4 * 4;
         return o;
     };
-    const size_t slots = (size_t)P.G * P.capA;
+    const size_t slots = shard_slotsA(P);
     L->E_id = take(slots);
     L->E_key = take(slots);
     L->M = take((size_t)P.edges.ba * P.edges.nb);
@@ -386,14 +405,14 @@ hipError_t launch_shard_plan(const ShardPlan &P, const ShardPlanLayout &L, uint3
     if (P.nblk_own) {
         hipLaunchKernelGGL(plan_count, dim3(P.nblk_own), dim3(kPlanBlock), 0, s, P, seed, epoch, round, f, tg,
                            bc_d);
-        hipLaunchKernelGGL(plan_scan, dim3(P.G), dim3(kPlanScanThreads), 0, s, P, bc_d, cnt, flags);
+        hipLaunchKernelGGL(plan_scan, dim3(P.G * P.P), dim3(kPlanScanThreads), 0, s, P, bc_d, cnt, flags);
         hipLaunchKernelGGL(plan_emit, dim3(P.nblk_own), dim3(kPlanBlock), 0, s, P, tg, bc_d, w + L.SPOSA,
                            w + L.SPOSB, bufA);
     } else {
-        hipError_t e = hipMemsetAsync(cnt, 0, P.G * sizeof(uint32_t), s);
+        hipError_t e = hipMemsetAsync(cnt, 0, (size_t)P.G * P.P * sizeof(uint32_t), s);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(plan_idle, dim3((P.cap + 255) / 256, P.G), dim3(256), 0, s, P, cnt, bufA);
+    hipLaunchKernelGGL(plan_idle, dim3((P.capP + 255) / 256, P.G * P.P), dim3(256), 0, s, P, cnt, bufA);
     return hipGetLastError();
 }
 
@@ -406,21 +425,21 @@ hipError_t launch_shard_edges(const ShardPlan &P, const ShardEdgeLayout &L, uint
     uint4 *IN = reinterpret_cast<uint4 *>(w + L.IN);
     u64 *pairs = reinterpret_cast<u64 *>(w + L.pairs);
     const CsrPlan &c = P.edges;
-    hipLaunchKernelGGL(edge_keys, dim3((P.capA + 255) / 256, P.G), dim3(256), 0, s, P, recvA, seed, epoch, round,
-                       f, E_id, E_key, flags);
+    hipLaunchKernelGGL(edge_keys, dim3((shard_slotsA(P) + 255) / 256), dim3(256), 0, s, P, recvA, seed, epoch,
+                       round, f, E_id, E_key, flags);
     const size_t lds_nb = (size_t)c.nb * sizeof(uint32_t);
     hipLaunchKernelGGL(edge_bin_count, dim3(c.ba), dim3(256), lds_nb, s, c, E_key, M);
     static_assert(kScanBlock == 256, "edge_col_scan: one thread per chunk (ba <= 256)");
     hipLaunchKernelGGL(edge_col_scan, dim3(c.nb), dim3(256), 0, s, M, c, tot);
     hipLaunchKernelGGL(edge_scan_small, dim3(1), dim3(kScanBlock), 0, s, tot, base, c.nb);
-    hipLaunchKernelGGL(edge_bin_scatter, dim3(c.ba), dim3(256), lds_nb, s, c, E_key, M, base, pairs);
+    hipLaunchKernelGGL(edge_bin_scatter, dim3(c.ba), dim3(256), lds_nb, s, c, P, E_key, M, base, pairs);
     const size_t lds_sort = ((size_t)c.bin + 16) * sizeof(uint32_t);
     if (lds_sort > 65536) {
         hipError_t e = hipFuncSetAttribute((const void *)edge_bin_sort,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sort);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(edge_bin_sort, dim3(c.nb), dim3(256), lds_sort, s, pairs, c, P.m, base, tot, EP, IN,
+    hipLaunchKernelGGL(edge_bin_sort, dim3(c.nb), dim3(256), lds_sort, s, pairs, c, P, P.m, base, tot, EP, IN,
                        IN2, E_id, tg);
     return hipGetLastError();
 }
@@ -450,8 +469,8 @@ __global__ __launch_bounds__(256) void pull_kernel(PullArgs a) {
     const uint32_t k = in.y & 0xFFFFu;
     for (uint32_t i = 0; i < k; ++i) {
         const uint32_t e = i == 0 ? in.z : (i == 1 ? in.w : (i == 2 ? e2 : a.EP[in.x + i]));
-        const uint32_t s = e / a.capA;             // source rank: slot e of exchange A
-        const uint32_t eb = e - s * (a.capA - a.cap);  // the same slot of exchange B
+        const SlotPos q = shard_a_decode(a.P, e);            // slot e of exchange A
+        const uint32_t eb = shard_b_slot(a.P, q.s, q.h, q.i);  // the same slot of exchange B
         const u64 pcl = zC | pC;
         a.sendB[L.row_index(eb, 2, 0)] = zB1 | pB | pcl;  // code bit 0: counter 1 or 255
         a.sendB[L.row_index(eb, 2, 1)] = zB2 | pcl;       // code bit 1: counter 2 or 255

@@ -11,6 +11,15 @@ no count is read back and a round runs without a host synchronisation):
 * B -- pull rows: the owner of each target returns, per pusher, the pull batch
   ``Gossip::receive`` built (``src/gossip.rs:124-151``), in the reverse layout.
 
+Pipeline parts: a rank's node range is cut into ``parts`` parts and both
+exchanges are stored part-major, so the rows of one part move in one
+all-to-all of their own.  The round kernel runs part by part: part h starts
+as soon as its pull rows (B_h) are in, and its push rows of the next round
+(A_h) leave while the following part is updated -- with RCCL the collectives
+run on the process group's stream, overlapped with the round kernel on the
+engine's stream (``async_op`` works waited on the engine stream, never on the
+host).
+
 Transports:
 
 * ``"dist"``  -- one shard per process, ``torch.distributed.all_to_all_single``
@@ -45,27 +54,32 @@ def _lib():
 class _Shard:
     """One rank's engine plus its exchange buffers (torch device tensors)."""
 
-    def __init__(self, lib, cfg, rank, world, torch, device):
+    def __init__(self, lib, cfg, rank, world, parts, torch, device):
         self.lib = lib
         h = _P()
-        _check(lib.gs_shard_create(ctypes.byref(cfg), rank, world, ctypes.byref(h)))
+        _check(lib.gs_shard_create_parts(ctypes.byref(cfg), rank, world, parts, ctypes.byref(h)))
         self.h = h
         info = (ctypes.c_uint32 * 12)()
         _check(lib.gs_shard_info(h, info))
-        (self.lo, self.m, self.cap, self.capA, self.wa, self.world, self.rank, self.chunk,
-         self.blockA, self.blockB) = list(info)[:10]
+        (self.lo, self.m, self.capP, self.idrows, self.wa, self.world, self.rank, self.chunk,
+         self.parts, self.mP, self.rowsA, self.rowsB) = list(info)
         dev = torch.device("cuda", device)
         i64 = torch.int64
-        G = self.world
         # exchange A: two buffer sets (round parity); B: one
-        self.sendA = [torch.zeros(G * self.blockA, dtype=i64, device=dev) for _ in range(2)]
-        self.recvA = [torch.zeros(G * self.blockA, dtype=i64, device=dev) for _ in range(2)]
-        self.sendB = torch.zeros(G * self.blockB, dtype=i64, device=dev)
-        self.recvB = torch.zeros(G * self.blockB, dtype=i64, device=dev)
+        self.sendA = [torch.zeros(self.rowsA * self.wa, dtype=i64, device=dev) for _ in range(2)]
+        self.recvA = [torch.zeros(self.rowsA * self.wa, dtype=i64, device=dev) for _ in range(2)]
+        self.sendB = torch.zeros(self.rowsB * self.wa, dtype=i64, device=dev)
+        self.recvB = torch.zeros(self.rowsB * self.wa, dtype=i64, device=dev)
         _check(lib.gs_shard_bind(h, self.sendA[0].data_ptr(), self.sendA[1].data_ptr(),
                                  self.recvA[0].data_ptr(), self.recvA[1].data_ptr(),
                                  self.sendB.data_ptr(), self.recvB.data_ptr()))
         self.stream = torch.cuda.ExternalStream(lib.gs_stream(h), device=dev)
+
+    def region(self, which: str, h: int):
+        """Part h of an exchange buffer: (first u64 word, u64 words per rank
+        sub-block); the part's world sub-blocks are contiguous."""
+        rows = self.capP + (self.idrows if which == "A" and h == self.parts - 1 else 0)
+        return h * self.world * self.capP * self.wa, rows * self.wa
 
     def close(self):
         if self.h:
@@ -86,7 +100,8 @@ class ShardedNetwork:
 
     def __init__(self, n_nodes: int, n_rumors: int, world: int, seed: int = 0x5AFE6055,
                  epoch: int = 0, params=None, device: int = 0, transport: str = "local",
-                 group=None, churn: float = 0.0, drop_push: float = 0.0, drop_pull: float = 0.0):
+                 group=None, churn: float = 0.0, drop_push: float = 0.0, drop_pull: float = 0.0,
+                 parts: Optional[int] = None):
         import torch
         self.torch = torch
         self.lib = _lib()
@@ -107,22 +122,32 @@ class ShardedNetwork:
         self.faults = (fault_threshold(churn), fault_threshold(drop_push), fault_threshold(drop_pull))
         cfg.churn, cfg.drop_push, cfg.drop_pull = self.faults
         self._cfg = cfg
+        self.host_staged = False
         if transport == "local":
-            self.shards = [_Shard(self.lib, cfg, r, world, torch, device) for r in range(world)]
+            self.parts = 1 if parts is None else parts
+            self.shards = [_Shard(self.lib, cfg, r, world, self.parts, torch, device) for r in range(world)]
         elif transport == "dist":
             import torch.distributed as dist
             self.dist = dist
             self.rank = dist.get_rank(group)
             assert dist.get_world_size(group) == world
-            self.shards = [_Shard(self.lib, cfg, self.rank, world, torch, device)]
             self.host_staged = dist.get_backend(group) == "gloo"
+            # four parts overlap the RCCL exchanges with the round kernel
+            # (and keep each collective small: a 1.1 GB self-exchange of one
+            # part was seen to stall RCCL on a single rank)
+            self.parts = (1 if self.host_staged else 4) if parts is None else parts
+            self.shards = [_Shard(self.lib, cfg, self.rank, world, self.parts, torch, device)]
         else:
             raise ValueError(transport)
         self.round = 0
         self._delivered = True
+        self._pendA = []   # async works of exchange A of the current round
+        self._pendB = {}   # part -> async work of exchange B of the current round
 
     # ------------------------------------------------------------ lifecycle
     def close(self):
+        if getattr(self, "shards", []):
+            self._wait_all()
         for s in getattr(self, "shards", []):
             s.close()
         self.shards = []
@@ -156,61 +181,85 @@ class ShardedNetwork:
         for s in self.shards:
             _check(self.lib.gs_sync(s.h))
 
+    # ------------------------------------------------------------ exchanges
+    def _exchange(self, which, h, k=0):
+        """Part h of exchange A (buffer set k) or B: sub-block d of every
+        rank's send region -> sub-block (its rank) of rank d's receive region.
+        Returns an async work (RCCL) or None (done)."""
+        if self.transport == "local":
+            self._sync_all()
+            for d, dst in enumerate(self.shards):
+                for r, src in enumerate(self.shards):
+                    off, w = src.region(which, h)
+                    if which == "A":
+                        sb, rb = src.sendA[k], dst.recvA[k]
+                    else:
+                        sb, rb = src.sendB, dst.recvB
+                    rb[off + r * w:off + (r + 1) * w].copy_(sb[off + d * w:off + (d + 1) * w])
+            self.torch.cuda.synchronize(self.device)
+            return None
+        s = self.shards[0]
+        off, w = s.region(which, h)
+        span = slice(off, off + self.world * w)
+        send, recv = (s.sendA[k], s.recvA[k]) if which == "A" else (s.sendB, s.recvB)
+        torch, dist = self.torch, self.dist
+        if self.host_staged:  # gloo: rows through host memory, synchronously
+            _check(self.lib.gs_sync(s.h))
+            hout = torch.empty(self.world * w, dtype=torch.int64)
+            dist.all_to_all_single(hout, send[span].cpu(), group=self.group)
+            recv[span].copy_(hout.to(recv.device))
+            torch.cuda.synchronize(self.device)
+            return None
+        # RCCL: the collective waits for the engine stream's work so far and
+        # runs on the process group's stream; the engine stream waits for it
+        # only when its rows are needed (_wait)
+        with torch.cuda.stream(s.stream):
+            return dist.all_to_all_single(recv[span], send[span], group=self.group, async_op=True)
+
+    def _wait(self, work):
+        if work is not None:
+            with self.torch.cuda.stream(self.shards[0].stream):
+                work.wait()
+
+    def _wait_all(self):
+        for w in self._pendA:
+            self._wait(w)
+        self._pendA = []
+        for w in self._pendB.values():
+            self._wait(w)
+        self._pendB = {}
+
     def _deliver(self):
-        """Exchange A (and A(0)'s ids in round 1), pull rows, exchange B of the
-        current round, all ordered on the engine stream(s)."""
+        """Exchange A of the current round complete (and, in round 1, the ids
+        of round 1: part P-1 of buffer set 0), the pull rows, and every part
+        of exchange B issued.  The parts of B are waited for by next_round part
+        by part (observers wait for all)."""
         if self._delivered or self.round == 0:
             return
         t = self.round
-        sets = [0, 1] if t == 1 else [t % 2]
-        if self.transport == "local":
-            self._sync_all()
-            for k in sets:
-                self._local_exchange("A", k)
-            for s in self.shards:
-                _check(self.lib.gs_shard_pull(s.h))
-            self._sync_all()
-            self._local_exchange("B")
-        else:
-            s = self.shards[0]
-            for k in sets:
-                self._dist_exchange(s, s.sendA[k], s.recvA[k])
+        if t == 1:
+            self._pendA.append(self._exchange("A", self.parts - 1, 0))
+        for w in self._pendA:
+            self._wait(w)
+        self._pendA = []
+        for s in self.shards:
             _check(self.lib.gs_shard_pull(s.h))
-            self._dist_exchange(s, s.sendB, s.recvB)
+        self._pendB = {h: self._exchange("B", h) for h in range(self.parts)}
         self._delivered = True
 
-    def _local_exchange(self, which, k=0):
-        """Block d of every shard's send buffer -> block (its rank) of shard d's
-        receive buffer (device copies; the shards share this GPU)."""
-        G = self.world
-        for d in range(G):
-            dst = self.shards[d]
-            for r in range(G):
-                src = self.shards[r]
-                if which == "A":
-                    w = src.blockA
-                    dst.recvA[k][r * w:(r + 1) * w].copy_(src.sendA[k][d * w:(d + 1) * w])
-                else:
-                    w = src.blockB
-                    dst.recvB[r * w:(r + 1) * w].copy_(src.sendB[d * w:(d + 1) * w])
-        self.torch.cuda.synchronize(self.device)
-
-    def _dist_exchange(self, s, send, recv):
-        """One equal-split all_to_all on the engine stream (RCCL), or staged
-        through host memory (gloo)."""
-        torch, dist = self.torch, self.dist
-        if self.host_staged:
-            _check(self.lib.gs_sync(s.h))
-            hout = torch.empty(recv.numel(), dtype=torch.int64)
-            dist.all_to_all_single(hout, send.cpu(), group=self.group)
-            recv.copy_(hout.to(recv.device))
-            torch.cuda.synchronize(self.device)
-        else:
-            with torch.cuda.stream(s.stream):
-                dist.all_to_all_single(recv, send, group=self.group)
-
     def next_round(self, report: bool = True) -> Optional[RoundReport]:
+        """Deliver round t (pull rows, exchange B) and produce round t+1, part
+        by part: part h's round kernel waits for B_h only, and A_h(t+1) leaves
+        as soon as it is written."""
         self._deliver()
+        t = self.round
+        k = (t + 1) % 2
+        for h in range(self.parts - 1):
+            self._wait(self._pendB.pop(h, None))
+            for s in self.shards:
+                _check(self.lib.gs_shard_round_part(s.h, h))
+            self._pendA.append(self._exchange("A", h, k))
+        self._wait(self._pendB.pop(self.parts - 1, None))
         live = False
         for s in self.shards:
             if report:
@@ -219,6 +268,7 @@ class ShardedNetwork:
                 live |= bool(r.any_live)
             else:
                 _check(self.lib.gs_next_round(s.h, None))
+        self._pendA.append(self._exchange("A", self.parts - 1, k))
         self.round += 1
         self._delivered = False
         if not report:
@@ -232,12 +282,14 @@ class ShardedNetwork:
 
     def clear(self, epoch: Optional[int] = None) -> None:
         self.epoch = self.epoch + 1 if epoch is None else epoch
+        self._wait_all()  # no exchange of the old epoch may still write the buffers
         for s in self.shards:
             _check(self.lib.gs_clear(s.h, self.epoch))
         self.round = 0
         self._delivered = True
 
     def sync(self) -> None:
+        self._wait_all()
         self._sync_all()
 
     # measurement hooks (this process's first shard)
@@ -259,6 +311,9 @@ class ShardedNetwork:
     # ------------------------------------------------------------ observers
     def _per_shard(self, fn):
         self._deliver()
+        for w in self._pendB.values():
+            self._wait(w)
+        self._pendB = {}
         return [fn(s) for s in self.shards]
 
     def _gather_rows(self, parts):

@@ -18,6 +18,12 @@ is exchanged or derived from other ranks' schedules:
      entries z created from earlier pushers, as a 2-plane class code); a
      receiver whose pull batch is dropped ignores it.
 
+Pipeline parts (gs_shard_create_parts): the owned range is cut into `parts`
+parts of mP nodes and each part's rows move in an all-to-all of their own
+(sub-blocks of capP rows); the receiver lists its pushers in (source rank,
+part, index) order, which is ascending source order, and B answers part by
+part in the same sub-blocks.
+
 Delivery and transition then use Model's bit-sliced algebra on the received
 rows only, so a rank never reads another rank's state directly.  Faults follow
 Model (flags of every edge derived locally from the Philox stream, like the
@@ -34,23 +40,32 @@ def shard_range(n, G, g):
     return lo, min(lo + chunk, n) - lo, chunk
 
 
-def shard_cap(n, G, W=1):
-    """Row slots per (source rank, destination rank) block (shard_plan)."""
+def part_nodes(n, G, parts):
+    """Nodes per pipeline part (shard_plan: whole 256-node plan blocks)."""
+    chunk = shard_range(n, G, 0)[2]
+    return -(-(-(-chunk // parts)) // 256) * 256
+
+
+def shard_cap(n, G, W=1, parts=1):
+    """Row slots per (source rank, destination rank, part) sub-block (shard_plan)."""
     import math
     chunk = shard_range(n, G, 0)[2]
-    mean = chunk * chunk / max(1.0, n - 1.0)
-    cap = min(float(chunk), mean + 16.0 * math.sqrt(mean + 1.0) + 64.0)
+    mp = part_nodes(n, G, parts)
+    mean = mp * chunk / max(1.0, n - 1.0)
+    cap = min(float(mp), mean + 16.0 * math.sqrt(mean + 1.0) + 64.0)
     q = max(64, 4 * W)
     return -(-math.ceil(cap) // q) * q
 
 
 class ShardModel(Model):
-    def __init__(self, n, R, seed, epoch, params, peer_fn, rank, world, a2a, fault_fn=None):
+    def __init__(self, n, R, seed, epoch, params, peer_fn, rank, world, a2a, fault_fn=None, parts=1):
         super().__init__(n, R, seed, epoch, params, peer_fn, fault_fn)
         assert R <= 62
         self.rank, self.world, self.a2a = rank, world, a2a
         self.lo, self.m, self.chunk = shard_range(n, world, rank)
-        self.cap = shard_cap(n, world)
+        self.parts = parts
+        self.mP = part_nodes(n, world, parts)
+        self.cap = shard_cap(n, world, parts=parts)
         self.tg, self.fl = {}, {}
         self.P = {x: [0] * 8 for x in self.owned()}
         self.stats = {x: [0] * 5 for x in self.owned()}
@@ -59,6 +74,10 @@ class ShardModel(Model):
     def owned(self):
         return range(self.lo, self.lo + self.m)
 
+    def part(self, h):
+        a = min(self.lo + h * self.mP, self.lo + self.m)
+        return range(a, min(a + self.mP, self.lo + self.m))
+
     def owner(self, x):
         return x // self.chunk
 
@@ -66,16 +85,20 @@ class ShardModel(Model):
         """Exchanges A and B of the current round (needs self.tg of round t)."""
         if self.exchanged or not self.deliver_pending:
             return
-        G, cap = self.world, self.cap
-        sendA = [[] for _ in range(G)]
-        for x in self.owned():
-            if not self.fl[x] & DEAD:
-                sendA[self.owner(self.tg[x])].append([x] + list(self.cls(x)))
-        for part in sendA:
-            assert len(part) <= cap, "block capacity exceeded (the engine flags a device limit)"
-            part.extend([[-1, 0, 0, 0]] * (cap - len(part)))
-        recvA = self.a2a(sendA, 4)
-        rows = [r for part in recvA for r in part if r[0] >= 0]
+        G, cap, P = self.world, self.cap, self.parts
+        sendA, recvA = [], []  # [part][rank] sub-blocks
+        for h in range(P):
+            sa = [[] for _ in range(G)]
+            for x in self.part(h):
+                if not self.fl[x] & DEAD:
+                    sa[self.owner(self.tg[x])].append([x] + list(self.cls(x)))
+            for blk in sa:
+                assert len(blk) <= cap, "block capacity exceeded (the engine flags a device limit)"
+                blk.extend([[-1, 0, 0, 0]] * (cap - len(blk)))
+            sendA.append(sa)
+            recvA.append(self.a2a(sa, 4))
+        # pushers in (source rank, part, index) order = ascending source order
+        rows = [r for s in range(G) for h in range(P) for r in recvA[h][s] if r[0] >= 0]
         srcs = [r[0] for r in rows]
         assert srcs == sorted(srcs), "receive rows must be in ascending source order"
         # the receiver's own view of each source's target (Philox, edge_keys)
@@ -85,17 +108,16 @@ class ShardModel(Model):
         for s, qc, q0, q1 in rows:
             assert self.lo <= tgt[s] < self.lo + self.m, "row sent to a rank that does not own its target"
             ins[tgt[s]].append((s, (qc, q0, q1)))
-        sendB = []
-        for part in recvA:
-            sendB.append([[r[0]] + list(self.pull_row(tgt[r[0]], r[0], ins[tgt[r[0]]]))
-                          if r[0] >= 0 else [-1, 0, 0] for r in part])
-        recvB = self.a2a(sendB, 3)
         pull = {}
-        for d in range(G):
-            assert [r[0] for r in recvB[d]] == [r[0] for r in sendA[d]], "B order = A order"
-            for x, b0, b1 in recvB[d]:
-                if x >= 0:
-                    pull[x] = (b0, b1)
+        for h in range(P):  # B_h answers A_h's rows in the same sub-blocks
+            sendB = [[[r[0]] + list(self.pull_row(tgt[r[0]], r[0], ins[tgt[r[0]]]))
+                      if r[0] >= 0 else [-1, 0, 0] for r in blk] for blk in recvA[h]]
+            recvB = self.a2a(sendB, 3)
+            for d in range(G):
+                assert [r[0] for r in recvB[d]] == [r[0] for r in sendA[h][d]], "B order = A order"
+                for x, b0, b1 in recvB[d]:
+                    if x >= 0:
+                        pull[x] = (b0, b1)
         self.ins, self.pull = ins, pull
         self.exchanged = True
 

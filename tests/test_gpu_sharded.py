@@ -15,16 +15,18 @@ from test_gpu_parity import SEED, run_parity
 pytestmark = pytest.mark.gpu
 
 
-def _maker(world):
+def _maker(world, parts=1):
     from safe_gossip_amd.sharded import ShardedNetwork
 
     def make(n, R, seed, epoch, params, **faults):
         return ShardedNetwork(n, R, world, seed=seed, epoch=epoch, params=params,
-                              transport="local", **faults)
+                              transport="local", parts=parts, **faults)
     return make
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+# (world, pipeline parts): parts cut each rank's node range; the exchanges
+# are part-major and the round kernel runs part by part
+@pytest.mark.parametrize("world,parts", [(2, 1), (3, 1), (4, 1), (2, 2), (3, 3), (4, 4)])
 @pytest.mark.parametrize("n,R,kind,params", [
     (8, 3, "example", None),
     (5, 3, "trickle", None),
@@ -43,11 +45,11 @@ def _maker(world):
     (900, 7, "origins", (2, 3, 5)),
     (1100, 1, "trickle", (1, 1, 3)),
 ])
-def test_sharded_parity(engine, world, n, R, kind, params):
-    run_parity(engine, n, R, kind, params, make_net=_maker(world))
+def test_sharded_parity(engine, world, parts, n, R, kind, params):
+    run_parity(engine, n, R, kind, params, make_net=_maker(world, parts))
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world,parts", [(2, 1), (3, 1), (2, 2), (3, 4)])
 @pytest.mark.parametrize("n,R,kind,faults", [
     (8, 3, "example", (0.2, 0.1, 0.1)),
     (700, 3, "trickle", (0.1, 0.1, 0.1)),
@@ -55,24 +57,33 @@ def test_sharded_parity(engine, world, n, R, kind, params):
     (520, 100, "reinject", (0.3, 0.2, 0.2)),
     (1000, 256, "origins", (0.1, 0.0, 0.3)),
 ])
-def test_sharded_parity_faults(engine, world, n, R, kind, faults):
-    run_parity(engine, n, R, kind, make_net=_maker(world), faults=faults)
+def test_sharded_parity_faults(engine, world, parts, n, R, kind, faults):
+    run_parity(engine, n, R, kind, make_net=_maker(world, parts), faults=faults)
 
 
-def test_sharded_larger(engine):
+@pytest.mark.parametrize("parts", [1, 2])
+def test_sharded_larger(engine, parts):
     # 3 shards whose chunk boundaries fall inside 256-node blocks' neighbours.
-    run_parity(engine, 20000, 64, "origins", check_every=4, make_net=_maker(3))
+    run_parity(engine, 20000, 64, "origins", check_every=4, make_net=_maker(3, parts))
 
 
-def test_sharded_more_ranks_than_chunks(engine):
-    # world 8 over 600 nodes: chunk rounding leaves trailing ranks empty.
-    run_parity(engine, 600, 48, "origins", make_net=_maker(8))
+@pytest.mark.parametrize("parts", [1, 3])
+def test_sharded_more_ranks_than_chunks(engine, parts):
+    # world 8 over 600 nodes: chunk rounding leaves trailing ranks (and parts) empty.
+    run_parity(engine, 600, 48, "origins", make_net=_maker(8, parts))
+
+
+@pytest.mark.parametrize("R", [16, 256])
+def test_sharded_parts_full_rank_parts(engine, R):
+    # 2 ranks x 2 parts of 4096 nodes each: every part holds whole plan blocks
+    # and receives rows from every (rank, part) sub-block.
+    run_parity(engine, 16384, R, "origins", check_every=3, make_net=_maker(2, 2))
 
 
 def test_sharded_clear(engine):
     from safe_gossip_amd.sharded import ShardedNetwork
     n, R = 500, 32
-    net = ShardedNetwork(n, R, 2, transport="local")
+    net = ShardedNetwork(n, R, 2, transport="local", parts=2)
     orc = OracleNet(n, R)
     for epoch in (0, 5):
         for r in range(R):

@@ -22,7 +22,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, cases, q, backend="gloo"):
+def _worker(rank, world, port, cases, q, backend="gloo", parts=None):
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -38,7 +38,7 @@ def _worker(rank, world, port, cases, q, backend="gloo"):
 
         def make(n, R, seed, epoch, params):
             return ShardedNetwork(n, R, world, seed=seed, epoch=epoch, params=params, device=0,
-                                  transport="dist")
+                                  transport="dist", parts=parts)
         for n, R, kind in cases:
             run_parity(sg, n, R, kind, make_net=make)
         q.put(("ok", rank))
@@ -49,14 +49,16 @@ def _worker(rank, world, port, cases, q, backend="gloo"):
         dist.destroy_process_group()
 
 
-def test_sharded_dist_gloo_two_ranks(engine):
+@pytest.mark.parametrize("parts", [1, 2])
+def test_sharded_dist_gloo_two_ranks(engine, parts):
     import torch.multiprocessing as mp
     world = 2
     cases = [(600, 48, "origins"), (1000, 3, "trickle"), (700, 256, "reinject")]
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q, "gloo", parts))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -70,14 +72,17 @@ def test_sharded_dist_gloo_two_ranks(engine):
     assert len(msgs) == world and all(m[0] == "ok" for m in msgs), msgs
 
 
-def test_sharded_dist_rccl_single_rank(engine):
-    # the RCCL transport end to end: equal-split all_to_all_single of the
-    # exchange buffers on the engine's stream, no host synchronisation per round
+@pytest.mark.parametrize("parts", [1, 2])
+def test_sharded_dist_rccl_single_rank(engine, parts):
+    # the RCCL transport end to end: equal-split all_to_all_single of each
+    # part's exchange region as async works waited on the engine's stream
+    # (parts 2: the exchanges of one part overlap the other part's round
+    # kernel), no host synchronisation per round
     import torch.multiprocessing as mp
     cases = [(600, 48, "origins"), (700, 256, "reinject"), (1000, 3, "trickle")]
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    p = ctx.Process(target=_worker, args=(0, 1, _free_port(), cases, q, "nccl"))
+    p = ctx.Process(target=_worker, args=(0, 1, _free_port(), cases, q, "nccl", parts))
     p.start()
     p.join(timeout=200)
     if p.is_alive():

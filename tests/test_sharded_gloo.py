@@ -41,7 +41,7 @@ def _a2a(send, width):
             for s in range(G)]
 
 
-def _worker(rank, world, port, n, R, params, kind, q, faults=None):
+def _worker(rank, world, port, n, R, params, kind, q, faults=None, parts=1):
     sys.path.insert(0, HERE)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -54,7 +54,7 @@ def _worker(rank, world, port, n, R, params, kind, q, faults=None):
         orc = OracleNet(n, R, seed=SEED, params=params, faults=thr) if rank == 0 else None
         prm = params or oracle_lib.derive_params(n)
         fault_fn = (lambda rnd, x: L.or_fault(SEED, 0, rnd, x, *thr)) if faults else None
-        sm = ShardModel(n, R, SEED, 0, prm, L.or_peer, rank, world, _a2a, fault_fn)
+        sm = ShardModel(n, R, SEED, 0, prm, L.or_peer, rank, world, _a2a, fault_fn, parts)
         rng = np.random.default_rng(n)
         for rnd in range(1, 50):
             inj = []
@@ -102,18 +102,20 @@ def _worker(rank, world, port, n, R, params, kind, q, faults=None):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n,R,params,kind,faults", [
-    (2, 600, 16, None, "origins", None),      # ranks own 512 / 88 nodes
-    (2, 700, 8, (3, 2, 9), "reinject", None),
-    (3, 600, 12, None, "origins", None),      # 256 / 256 / 88
-    (2, 600, 16, None, "origins", (0.1, 0.1, 0.1)),    # config 5 faults
-    (3, 600, 8, None, "reinject", (0.3, 0.2, 0.2)),
+@pytest.mark.parametrize("world,n,R,params,kind,faults,parts", [
+    (2, 600, 16, None, "origins", None, 1),      # ranks own 512 / 88 nodes
+    (2, 700, 8, (3, 2, 9), "reinject", None, 1),
+    (3, 600, 12, None, "origins", None, 1),      # 256 / 256 / 88
+    (2, 600, 16, None, "origins", (0.1, 0.1, 0.1), 1),    # config 5 faults
+    (3, 600, 8, None, "reinject", (0.3, 0.2, 0.2), 1),
+    (2, 1100, 16, None, "origins", None, 2),     # pipeline parts of 256 nodes
+    (3, 1600, 8, None, "reinject", (0.1, 0.1, 0.1), 3),
 ])
-def test_sharded_protocol_gloo(oracle, world, n, R, params, kind, faults):
+def test_sharded_protocol_gloo(oracle, world, n, R, params, kind, faults, parts):
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, R, params, kind, q, faults))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, R, params, kind, q, faults, parts))
              for r in range(world)]
     for p in procs:
         p.start()
