@@ -1,0 +1,408 @@
+// gs_dlv4.hip -- the delivery-record (DLV) round kernel with FOUR nodes per
+// lane (2P schedule, R_pad <= 16, transition modes 0 and 1).
+//
+// On the DLV path (gs_common.h DlvRec) every input of a node's round is read
+// coalesced: its record (pushers' push codes), its pull batch, its target
+// word, its planes.  With one node per lane the bit-sliced algebra of
+// gs_kernels.hip ran on R_pad of the 64 bits of every u64 operation (16 of 64
+// at config 5) and the kernel was VALU-bound (982 VALU instructions per wave,
+// profiles/r2_dlv4).  Here a lane owns four consecutive nodes whose R_pad-bit
+// segments sit side by side in one 4*R_pad-bit field of the plane word, so
+// MessageState::next_round (src/message_state.rs:86-171) and the absorption of
+// push and pull batches (src/gossip.rs:118-163) run once per four nodes; only
+// what is per node stays per node: in-degree, the first-creation index,
+// |peers_in_this_round|, the median threshold (a per-segment comparator),
+// churn, and the five Statistics counters (src/gossip.rs:103-111,139-163).
+// The algebra is the per-node kernel's (gs_kernels.hip, round_kernel DLV
+// path), term by term; observation launches and rounds with external RPCs
+// still run that kernel.
+#include "gs_device.h"
+#include "gs_kernels.h"
+
+namespace gs {
+
+constexpr uint32_t kNpl = 4;           // nodes per lane
+constexpr uint32_t kDlv4Threads = 256;
+
+// Bit-sliced "x >= K" with K given per segment: km[i] holds bit i of every
+// segment's K spread over that segment (the borrow chain of ge_k).
+template <int NB>
+GS_DEV u64 ge_seg(const u64 (&x)[NB], const u64 (&km)[NB]) {
+    u64 b = 0ull;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) b = (~x[i] & b) | (km[i] & (~x[i] | b));
+    return ~b;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kDlv4Threads) void round_kernel_dlv4(RoundArgs a) {
+    constexpr bool DELIVER = MODE == 1;
+    const Geometry &g = a.g;
+    const uint32_t n_nodes = g.n;
+    const uint32_t rp = g.rpad, lr = g.logr, lognpu = g.lognpu;  // rp <= 16: npu >= 4
+    const uint32_t lane = blockIdx.x * kDlv4Threads + threadIdx.x;
+    const uint32_t x0 = lane * kNpl;
+    const uint32_t nv = x0 < n_nodes ? min(kNpl, n_nodes - x0) : 0u;  // valid nodes of the lane
+    const u64 m1 = (1ull << rp) - 1ull;
+    u64 M[kNpl];  // segment of node x0 + q within the lane's field
+    u64 mV = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kNpl; ++q) {
+        M[q] = q < nv ? m1 << (q * rp) : 0ull;
+        mV |= M[q];
+    }
+    // the lane's field: bits [shL, shL + 4*rp) of plane word `unit`
+    const uint32_t lpw_log = lognpu - 2u;  // lanes per word = npu / 4
+    const uint32_t shL = (x0 & ((1u << lognpu) - 1u)) << lr;
+
+    // ---- own round-t planes, staged through LDS (16-byte coalesced loads)
+    __shared__ __attribute__((aligned(16))) u64 stage[kDlv4Threads * kNpl * kPlanes / 4];  // >= 8 words per unit
+    const uint32_t units_blk = (kDlv4Threads * kNpl) >> lognpu;
+    const u64 unit0 = (u64)blockIdx.x * units_blk;
+    const uint32_t blk_units = (uint32_t)min((u64)units_blk, g.units - min(g.units, unit0));
+    const uint32_t blk_v4 = blk_units * (kPlanes / 2u);
+    {
+        const uint4 *src4 = reinterpret_cast<const uint4 *>(a.Scur + unit0 * kPlanes);
+        uint4 *dst4 = reinterpret_cast<uint4 *>(stage);
+        uint4 v[4];
+#pragma unroll
+        for (uint32_t it = 0; it < 4; ++it) {
+            const uint32_t i = threadIdx.x + kDlv4Threads * it;
+            v[it] = src4[min(i, blk_v4 - 1u)];  // blk_v4 >= 4: every block owns a unit
+        }
+#pragma unroll
+        for (uint32_t it = 0; it < 4; ++it) {
+            const uint32_t i = threadIdx.x + kDlv4Threads * it;
+            if (i < blk_v4) dst4[i] = v[it];
+        }
+    }
+
+    // ---- per-node metadata (coalesced: 16-B records, 4-B words, 4 nodes per lane)
+    uint32_t kk[kNpl], dzi[kNpl], dfirst[kNpl], c0[kNpl], c1[kNpl], tgw[kNpl], dp[kNpl];
+#pragma unroll
+    for (uint32_t q = 0; q < kNpl; ++q) kk[q] = dzi[q] = dfirst[q] = c0[q] = c1[q] = tgw[q] = dp[q] = 0u;
+    if (DELIVER) {
+        if (nv == kNpl) {
+            const uint4 t4 = *reinterpret_cast<const uint4 *>(a.tg + x0);
+            const uint4 p4 = *reinterpret_cast<const uint4 *>(a.pull + x0);
+            tgw[0] = t4.x; tgw[1] = t4.y; tgw[2] = t4.z; tgw[3] = t4.w;
+            dp[0] = p4.x; dp[1] = p4.y; dp[2] = p4.z; dp[3] = p4.w;
+        } else {
+#pragma unroll
+            for (uint32_t q = 0; q < kNpl; ++q)
+                if (q < nv) {
+                    tgw[q] = a.tg[x0 + q];
+                    dp[q] = a.pull[x0 + q];
+                }
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kNpl; ++q) {
+            const DlvRec r = a.DR[q < nv ? x0 + q : 0u];  // node 0: a harmless valid address
+            kk[q] = q < nv ? (r.meta & 31u) : 0u;
+            dzi[q] = (r.meta >> 5) & 31u;
+            dfirst[q] = r.first;
+            c0[q] = r.c[0];
+            c1[q] = r.c[1];
+        }
+    }
+    __syncthreads();
+    u64 P[kPlanes];
+    {
+        const uint32_t ul = (lane >> lpw_log) - blockIdx.x * units_blk;  // the lane's word within the block
+#pragma unroll
+        for (int p = 0; p < kPlanes; ++p) P[p] = nv ? (stage[ul * kPlanes + p] >> shL) & mV : 0ull;
+    }
+
+    const u64 isC = P[0], a0 = P[1], a1 = P[2];
+    const u64 A = ~isC & ~a0 & ~a1 & mV;
+    const u64 B = ~isC & (a0 | a1);
+    const u64 C = isC & ~(a0 & a1);
+    const u64 D = isC & a0 & a1;
+    const u64 liveX = B | C;
+
+    // ---- phases 1 and 2 of round t (Gossip::receive), four nodes at once
+    u64 notyet = A, recB = B, oc1r = B & a0 & ~a1, crB = 0, crC = 0, anyC = 0;
+    u64 cv[5] = {0, 0, 0, 0, 0};
+    uint32_t part_cw[kNpl], fc[kNpl], recv[kNpl], psize[kNpl];
+    u64 pulledM = 0, offM = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kNpl; ++q) {
+        part_cw[q] = recv[q] = psize[q] = 0u;
+        fc[q] = kNone;
+        if (DELIVER && !(tgw[q] & kTgNoPull)) pulledM |= M[q];
+        if (DELIVER && (tgw[q] & kTgOff)) offM |= M[q];
+    }
+    if (DELIVER) {
+        uint32_t kmax = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kNpl; ++q) {
+            kmax = max(kmax, kk[q]);
+            if (kk[q] > 30u) atomicOr(&a.flags[2], 1u);
+        }
+        for (uint32_t i = 0; i < kmax; ++i) {
+            // push batch of pusher i of every node that has one (2-plane code:
+            // 01 counter 1, 10 counter 2, 11 counter 255); t(x)'s push copy is
+            // superseded by its pull copy (message_state.rs:79), so not recorded
+            u64 b0 = 0, b1 = 0, recm = ~0ull;
+#pragma unroll
+            for (uint32_t q = 0; q < kNpl; ++q) {
+                if (i < kk[q]) {
+                    const uint32_t code = i == 0 ? c0[q] : (i == 1 ? c1[q] : a.dtail[dfirst[q] + i - kDlvInline]);
+                    b0 |= ((u64)code & m1) << (q * rp);
+                    b1 |= ((u64)(code >> 16) & m1) << (q * rp);
+                    if ((pulledM & M[q]) && i == dzi[q]) recm &= ~M[q];
+                }
+            }
+            const u64 vC = b0 & b1, vB = b0 ^ b1, v2 = b1 & ~b0, sl = b0 | b1;
+            const u64 newc = notyet & sl;           // new_from_peer: not recorded
+            const u64 rec = recB & sl & recm;       // MessageState::receive on B
+            anyC |= rec & vC;
+            add5(cv, rec & vB & (v2 | oc1r));
+            crB |= newc & ~vC;
+            crC |= newc & vC;
+            recB |= newc & ~vC;
+            oc1r |= newc & ~vC;
+            notyet &= ~newc;
+#pragma unroll
+            for (uint32_t q = 0; q < kNpl; ++q) {
+                const uint32_t pc = popc(newc & M[q]);
+                part_cw[q] += (kk[q] - 1u - i) * pc;  // later pushers' pull rows include it
+                if (pc && fc[q] == kNone) fc[q] = i;
+                recv[q] += popc(sl & M[q]);
+            }
+        }
+        // the pull batch t(x) returned (built by the in-list build; the slot
+        // of a node whose pull is not delivered holds garbage: masked out
+        // before it is shifted into place)
+        u64 pb0 = 0, pb1 = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kNpl; ++q) {
+            pb0 |= ((u64)dp[q] & m1) << (q * rp);
+            pb1 |= ((u64)(dp[q] >> 16) & m1) << (q * rp);
+        }
+        pb0 &= pulledM;
+        pb1 &= pulledM;
+        const u64 pv2 = pb1 & ~pb0, pvB = pb0 ^ pb1, pCl = pb0 & pb1, pl = pb0 | pb1;
+        {
+            const u64 newc = notyet & pl;
+            const u64 rec = recB & pl;
+            anyC |= rec & pCl;
+            add5(cv, rec & pvB & (pv2 | oc1r));
+            crB |= newc & ~pCl;
+            crC |= newc & pCl;
+            recB |= newc & ~pCl;
+            oc1r |= newc & ~pCl;
+            notyet &= ~newc;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kNpl; ++q) {
+            recv[q] += popc(pl & M[q]);
+            const bool pulled = (pulledM & M[q]) != 0;
+            psize[q] = kk[q] + ((pulled && dzi[q] == kDlvNoZ) ? 1u : 0u);  // |peers_in_this_round|
+        }
+    }
+
+    // ---- phase 0 of round t+1: injections, MessageState::next_round
+    u64 inj = 0;
+    if (a.n_inj && nv) {
+        uint32_t lo = 0, hi = a.n_inj;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (a.inj_key[mid] < x0) lo = mid + 1; else hi = mid;
+        }
+        for (uint32_t i = lo; i < a.n_inj && a.inj_key[i] < (u64)x0 + nv; ++i)
+            inj |= (a.inj_mask[i] & m1) << ((uint32_t)(a.inj_key[i] - x0) * rp);
+    }
+    const u64 ninj = ~inj;
+    const u64 Bold = B & ninj, Cold = C & ninj, Dold = D & ninj;
+    const u64 cB = crB & ninj, cC = crC & ninj;
+    const u64 Bf = Bold | cB | inj;
+    const u64 Cf = Cold | cC;
+    const u64 oc1 = (Bold & a0 & ~a1) | cB | inj;
+    const u64 oc2 = Bold & a1 & ~a0;
+    // median rule with 0-filled peers: bump iff ge >= |P|/2 + 1, per node
+    u64 km[5] = {0, 0, 0, 0, 0}, kbig = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kNpl; ++q) {
+        const uint32_t thr = psize[q] / 2u + 1u;
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+            if ((thr >> i) & 1u) km[i] |= M[q];
+        if (thr >= 32u) kbig |= M[q];
+    }
+    u64 bump = ge_seg<5>(cv, km) & ~kbig & (Bold | cB);
+    u64 anyCe = anyC & ninj;
+    if (DELIVER && offM) {  // back from offline: the votes its skipped next_round kept
+#pragma unroll
+        for (uint32_t q = 0; q < kNpl; ++q)
+            if (offM & M[q]) {
+                const u64 *pe = a.pend + (u64)(x0 + q) * 2u;
+                bump = (bump & ~M[q]) | (((pe[0] & m1) << (q * rp)) & Bold);
+                anyCe = (anyCe & ~M[q]) | (((pe[1] & m1) << (q * rp)) & ninj);
+            }
+    }
+    u64 nr[6];  // round + 1
+    {
+        u64 carry = ~0ull;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const u64 rb = P[3 + i] & Bold;
+            nr[i] = rb ^ carry;
+            carry &= rb;
+        }
+        nr[5] = carry;
+    }
+    const u64 toD = ge_u<6>(nr, a.maxr);
+    const u64 oc1n = oc1 & ~bump;
+    const u64 oc2n = (oc1 & bump) | (oc2 & ~bump);
+    const u64 oc3n = oc2 & bump;
+    const u64 ocge = a.cmax <= 1u ? ~0ull : (a.cmax == 2u ? (oc2n | oc3n) : oc3n);
+    const u64 toC = anyCe | ocge;
+    const u64 BD = Bf & toD, BC = Bf & ~toD & toC, BB = Bf & ~toD & ~toC;
+    const u64 cr0 = a0 & Cold, cr1 = a1 & Cold;
+    const u64 d[3] = {~cr0, cr1 ^ cr0, cr1 & cr0};
+    u64 rib[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) rib[i] = P[3 + i] & Cold;
+    u64 sum[6];
+    {
+        u64 c = 0;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const u64 di = i < 3 ? d[i] : 0ull;
+            sum[i] = rib[i] ^ di ^ c;
+            c = (rib[i] & di) | (c & (rib[i] ^ di));
+        }
+        sum[5] = c;
+    }
+    const u64 CtoD = ge_u<6>(sum, a.maxr) | ge_u<3>(d, a.maxc);
+    const u64 CD = Cf & CtoD, CC = Cf & ~CtoD;
+    const u64 Dn = BD | CD | Dold;
+    const u64 Cn = BC | CC;
+    const u64 Bn = BB;
+    u64 N[kPlanes];
+    N[0] = Cn | Dn;
+    N[1] = (Bn & oc1n) | (CC & d[0]) | Dn;
+    N[2] = (Bn & oc2n) | (CC & d[1]) | Dn;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) N[3 + i] = ((Bn | BC) & nr[i]) | (CC & rib[i]);
+
+    // churn: a node offline in round t+1 skips next_round and keeps its
+    // pre-transition state and the two votes in `pend`
+    u64 onM = mV;
+    if (a.f.churn) {
+#pragma unroll
+        for (uint32_t q = 0; q < kNpl; ++q)
+            if (q < nv && offline_of(a.seed, a.epoch, a.round_new, a.node_lo + x0 + q, a.f.churn)) onM &= ~M[q];
+    }
+    if (onM != mV) {
+        const u64 fz = mV & ~onM;
+        const u64 F[3] = {(isC & ninj) | cC, (a0 & ninj) | cB | inj, a1 & ninj};
+#pragma unroll
+        for (int p = 0; p < kPlanes; ++p) {
+            const u64 f = p < 3 ? F[p] : (P[p] & ninj);
+            N[p] = (N[p] & onM) | (f & fz);
+        }
+        const u64 av = anyCe & (Bold | cB);
+#pragma unroll
+        for (uint32_t q = 0; q < kNpl; ++q)
+            if (fz & M[q]) {
+                u64 *pe = a.pend + (u64)(x0 + q) * 2u;
+                pe[0] = (bump >> (q * rp)) & m1;
+                pe[1] = (av >> (q * rp)) & m1;
+            }
+    }
+
+    // ---- push codes of round t+1 for the in-list build (4 B per node)
+    {
+        const u64 vC = N[0] & ~(N[1] & N[2]), vB = ~N[0] & (N[1] | N[2]);
+        const u64 b0 = (vB & N[1] & ~N[2]) | vC, b1 = (vB & N[2] & ~N[1]) | vC;
+        uint32_t pc[kNpl];
+#pragma unroll
+        for (uint32_t q = 0; q < kNpl; ++q)
+            pc[q] = (uint32_t)((b0 >> (q * rp)) & m1) | ((uint32_t)((b1 >> (q * rp)) & m1) << 16);
+        if (nv == kNpl) {
+            *reinterpret_cast<uint4 *>(a.pc_out + x0) = make_uint4(pc[0], pc[1], pc[2], pc[3]);
+        } else {
+#pragma unroll
+            for (uint32_t q = 0; q < kNpl; ++q)
+                if (q < nv) a.pc_out[x0 + q] = pc[q];
+        }
+    }
+
+    // ---- write round-(t+1) planes (lanes of one word OR their fields; LDS
+    // stage, 16-byte coalesced nontemporal stores)
+    __shared__ uint32_t blk_any;
+    if (threadIdx.x == 0) blk_any = 0;
+    uint32_t live[kNpl];
+    bool any_live = false;
+#pragma unroll
+    for (uint32_t q = 0; q < kNpl; ++q) {
+        live[q] = (onM & M[q]) ? popc((Bn | Cn) & M[q]) : 0u;
+        any_live |= live[q] != 0u;
+    }
+    __syncthreads();  // every lane is done reading stage; blk_any is cleared
+    {
+        const uint32_t ul = (lane >> lpw_log) - blockIdx.x * units_blk;
+        const uint32_t lpw = 1u << lpw_log;
+#pragma unroll
+        for (int p = 0; p < kPlanes; ++p) {
+            u64 v = (N[p] & mV) << shL;
+            for (uint32_t o = 1; o < lpw; o <<= 1) v |= __shfl_xor(v, (int)o, 64);
+            if ((lane & (lpw - 1u)) == 0u && nv) stage[ul * kPlanes + p] = v;
+        }
+    }
+    if (__ballot(any_live) != 0ull && (threadIdx.x & 63u) == 0u) blk_any = 1u;
+    __syncthreads();
+    {
+        const uint4 *src4 = reinterpret_cast<const uint4 *>(stage);
+        uint4 *dst4 = reinterpret_cast<uint4 *>(a.Snext + unit0 * kPlanes);
+#pragma unroll
+        for (uint32_t it = 0; it < 4; ++it) {
+            const uint32_t i = threadIdx.x + kDlv4Threads * it;
+            if (i < blk_v4) nt_store4(src4[i], &dst4[i]);
+        }
+    }
+
+    // ---- any-live flag of round t+1, Statistics (src/gossip.rs:80,103-111)
+    if (blockIdx.x == 0 && threadIdx.x == 0)  // slot of round t, read by the host already
+        __hip_atomic_store(&a.flags[(a.round_new + 1u) & 1u], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0 && blk_any) {
+        uint32_t *f = &a.flags[a.round_new & 1u];
+        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) atomicOr(f, 1u);
+    }
+#ifndef GS_EXP_NO_STATS
+    uint4 *st = reinterpret_cast<uint4 *>(a.st32) + x0;
+#pragma unroll
+    for (uint32_t q = 0; q < kNpl; ++q) {
+        if (q >= nv) break;
+        uint32_t d_full = 0, d_empty_pull = 0;
+        if (DELIVER) {
+            const uint32_t lc = popc(liveX & M[q]);
+            d_full = kk[q] * lc + part_cw[q];  // pull rows sent by x
+            if (kk[q] > 0 && lc == 0) d_empty_pull = (fc[q] == kNone) ? kk[q] : fc[q] + 1u;
+        }
+        const bool on = (onM & M[q]) != 0;
+        uint4 v = st[q];
+        v.x += d_empty_pull;                          // empty_pull_sent
+        v.y += (on && live[q] == 0u) ? 1u : 0u;       // empty_push_sent
+        v.z += live[q] + d_full;                      // full_message_sent
+        v.w += recv[q];                               // full_message_received
+        st[q] = v;
+        if (!on) a.offc[x0 + q] += 1u;
+    }
+#endif
+}
+
+hipError_t launch_round_dlv4(const RoundArgs &a, int mode, hipStream_t s) {
+    const u64 lanes = ((u64)a.g.n + kNpl - 1) / kNpl;
+    const u64 grid = (lanes + kDlv4Threads - 1) / kDlv4Threads;
+    if (grid == 0) return hipSuccess;
+    if (mode == 0)
+        hipLaunchKernelGGL(round_kernel_dlv4<0>, dim3((uint32_t)grid), dim3(kDlv4Threads), 0, s, a);
+    else
+        hipLaunchKernelGGL(round_kernel_dlv4<1>, dim3((uint32_t)grid), dim3(kDlv4Threads), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace gs

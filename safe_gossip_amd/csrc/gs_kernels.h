@@ -73,6 +73,7 @@ struct RoundArgs {
                               // written) | lane gathers << 32, one atomic per block
     u64 *dens;                // [kDensSlots] zero words of the round-(t+1) planes
                               // (spread atomics, cleared by the engine per launch)
+    uint32_t dlv_pack;        // DLV transition launches: four nodes per lane (gs_dlv4.hip)
     Geometry g;
     uint64_t seed;
     uint32_t epoch;
@@ -90,6 +91,9 @@ inline u64 spr_node_bytes(const Geometry &g) { return ((u64)g.n + 63u) / 64u * 8
 // to t+1, 2 = deliver round t and write observation outputs only,
 // 3 = observe without pending deliveries.
 hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s);
+// DLV transition launches (modes 0 and 1, no external RPCs) with four nodes
+// per lane (gs_dlv4.hip).
+hipError_t launch_round_dlv4(const RoundArgs &a, int mode, hipStream_t s);
 
 // Plan of the in-list build (gs_inlist.hip).
 struct CsrPlan {

@@ -303,6 +303,32 @@ def test_parity_small_gather_path(engine, monkeypatch, n, R, kind, faults):
     run_parity(engine, n, R, kind, faults=faults)
 
 
+@pytest.mark.parametrize("n,R,kind,faults", [
+    (5, 16, "origins", None),                  # one lane, one partial field
+    (1030, 1, "trickle", (0.05, 0.05, 0.05)),  # 16 lanes per word, ragged last word
+    (1023, 2, "origins", None),                # 8 lanes per word
+    (777, 4, "reinject", (0.1, 0.1, 0.1)),     # 4 lanes per word
+    (999, 7, "origins", (0.02, 0.0, 0.1)),     # R_pad 8: 2 lanes per word
+    (1026, 16, "reinject", (0.2, 0.1, 0.1)),   # one word per lane, ragged last lane
+])
+def test_parity_delivery_records_packed(engine, n, R, kind, faults):
+    # the DLV transition kernel with four nodes per lane (gs_dlv4.hip): every
+    # R_pad <= 16 field width, partial lanes and words, churn (pend votes)
+    run_parity(engine, n, R, kind, faults=faults)
+
+
+@pytest.mark.parametrize("n,R,kind,faults", [
+    (300, 16, "origins", None),
+    (2000, 1, "trickle", (0.1, 0.05, 0.05)),
+    (500, 8, "reinject", (0.05, 0.1, 0.1)),
+])
+def test_parity_delivery_records_node_per_lane(engine, monkeypatch, n, R, kind, faults):
+    # the one-node-per-lane DLV transition (SAFE_GOSSIP_AMD_DLV_PACK=0), the
+    # kernel observation launches use, stays bit-exact as a transition too
+    monkeypatch.setenv("SAFE_GOSSIP_AMD_DLV_PACK", "0")
+    run_parity(engine, n, R, kind, faults=faults)
+
+
 def test_parity_delivery_records_larger(engine):
     # delivery records at 20k nodes: many in-list tails (in-degree > 2) and
     # pull scans through t(x)'s tail, with faults, every 3rd round checked
