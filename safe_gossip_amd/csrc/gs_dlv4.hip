@@ -23,6 +23,11 @@ namespace gs {
 
 constexpr uint32_t kNpl = 4;           // nodes per lane
 constexpr uint32_t kDlv4Threads = 256;
+// 4 waves per SIMD (128 VGPRs): 2.63 -> 2.36 ms at config 5 against the
+// unconstrained 134-VGPR build (3 waves)
+#ifndef GS_DLV4_MINW
+#define GS_DLV4_MINW 4
+#endif
 
 // Bit-sliced "x >= K" with K given per segment: km[i] holds bit i of every
 // segment's K spread over that segment (the borrow chain of ge_k).
@@ -35,7 +40,7 @@ GS_DEV u64 ge_seg(const u64 (&x)[NB], const u64 (&km)[NB]) {
 }
 
 template <int MODE>
-__global__ __launch_bounds__(kDlv4Threads) void round_kernel_dlv4(RoundArgs a) {
+__global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(RoundArgs a) {
     constexpr bool DELIVER = MODE == 1;
     const Geometry &g = a.g;
     const uint32_t n_nodes = g.n;
@@ -106,12 +111,12 @@ __global__ __launch_bounds__(kDlv4Threads) void round_kernel_dlv4(RoundArgs a) {
         }
     }
     __syncthreads();
+    // class planes now; the five b planes only for the transition (still in
+    // LDS then: fewer registers live across the deliveries)
+    const uint32_t ul = (lane >> lpw_log) - blockIdx.x * units_blk;  // the lane's word within the block
     u64 P[kPlanes];
-    {
-        const uint32_t ul = (lane >> lpw_log) - blockIdx.x * units_blk;  // the lane's word within the block
 #pragma unroll
-        for (int p = 0; p < kPlanes; ++p) P[p] = nv ? (stage[ul * kPlanes + p] >> shL) & mV : 0ull;
-    }
+    for (int p = 0; p < 3; ++p) P[p] = nv ? (stage[ul * kPlanes + p] >> shL) & mV : 0ull;
 
     const u64 isC = P[0], a0 = P[1], a1 = P[2];
     const u64 A = ~isC & ~a0 & ~a1 & mV;
@@ -202,6 +207,18 @@ __global__ __launch_bounds__(kDlv4Threads) void round_kernel_dlv4(RoundArgs a) {
         }
     }
 
+    // Statistics deltas of the deliveries
+    uint32_t d_empty_pull[kNpl], d_full[kNpl];
+#pragma unroll
+    for (uint32_t q = 0; q < kNpl; ++q) {
+        d_empty_pull[q] = d_full[q] = 0u;
+        if (DELIVER) {
+            const uint32_t lc = popc(liveX & M[q]);
+            d_full[q] = kk[q] * lc + part_cw[q];  // pull rows sent by x
+            if (kk[q] > 0 && lc == 0) d_empty_pull[q] = (fc[q] == kNone) ? kk[q] : fc[q] + 1u;
+        }
+    }
+
     // ---- phase 0 of round t+1: injections, MessageState::next_round
     u64 inj = 0;
     if (a.n_inj && nv) {
@@ -241,6 +258,8 @@ __global__ __launch_bounds__(kDlv4Threads) void round_kernel_dlv4(RoundArgs a) {
                 anyCe = (anyCe & ~M[q]) | (((pe[1] & m1) << (q * rp)) & ninj);
             }
     }
+#pragma unroll
+    for (int p = 3; p < kPlanes; ++p) P[p] = nv ? (stage[ul * kPlanes + p] >> shL) & mV : 0ull;
     u64 nr[6];  // round + 1
     {
         u64 carry = ~0ull;
@@ -313,6 +332,13 @@ __global__ __launch_bounds__(kDlv4Threads) void round_kernel_dlv4(RoundArgs a) {
             }
     }
 
+    // the Statistics counters this round updates (read now: the stores below
+    // cover the load's latency)
+    uint4 *st = reinterpret_cast<uint4 *>(a.st32) + x0;
+    uint4 stv[kNpl];
+#pragma unroll
+    for (uint32_t q = 0; q < kNpl; ++q) stv[q] = q < nv ? st[q] : make_uint4(0u, 0u, 0u, 0u);
+
     // ---- push codes of round t+1 for the in-list build (4 B per node)
     {
         const u64 vC = N[0] & ~(N[1] & N[2]), vB = ~N[0] & (N[1] | N[2]);
@@ -343,7 +369,6 @@ __global__ __launch_bounds__(kDlv4Threads) void round_kernel_dlv4(RoundArgs a) {
     }
     __syncthreads();  // every lane is done reading stage; blk_any is cleared
     {
-        const uint32_t ul = (lane >> lpw_log) - blockIdx.x * units_blk;
         const uint32_t lpw = 1u << lpw_log;
 #pragma unroll
         for (int p = 0; p < kPlanes; ++p) {
@@ -371,27 +396,18 @@ __global__ __launch_bounds__(kDlv4Threads) void round_kernel_dlv4(RoundArgs a) {
         uint32_t *f = &a.flags[a.round_new & 1u];
         if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) atomicOr(f, 1u);
     }
-#ifndef GS_EXP_NO_STATS
-    uint4 *st = reinterpret_cast<uint4 *>(a.st32) + x0;
 #pragma unroll
     for (uint32_t q = 0; q < kNpl; ++q) {
         if (q >= nv) break;
-        uint32_t d_full = 0, d_empty_pull = 0;
-        if (DELIVER) {
-            const uint32_t lc = popc(liveX & M[q]);
-            d_full = kk[q] * lc + part_cw[q];  // pull rows sent by x
-            if (kk[q] > 0 && lc == 0) d_empty_pull = (fc[q] == kNone) ? kk[q] : fc[q] + 1u;
-        }
         const bool on = (onM & M[q]) != 0;
-        uint4 v = st[q];
-        v.x += d_empty_pull;                          // empty_pull_sent
+        uint4 v = stv[q];
+        v.x += d_empty_pull[q];                       // empty_pull_sent
         v.y += (on && live[q] == 0u) ? 1u : 0u;       // empty_push_sent
-        v.z += live[q] + d_full;                      // full_message_sent
+        v.z += live[q] + d_full[q];                   // full_message_sent
         v.w += recv[q];                               // full_message_received
         st[q] = v;
         if (!on) a.offc[x0 + q] += 1u;
     }
-#endif
 }
 
 hipError_t launch_round_dlv4(const RoundArgs &a, int mode, hipStream_t s) {
