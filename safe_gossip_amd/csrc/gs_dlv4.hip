@@ -21,7 +21,6 @@
 
 namespace gs {
 
-constexpr uint32_t kNpl = 4;           // nodes per lane
 constexpr uint32_t kDlv4Threads = 256;
 // 4 waves per SIMD (128 VGPRs): 2.63 -> 2.36 ms at config 5 against the
 // unconstrained 134-VGPR build (3 waves)
@@ -29,17 +28,46 @@ constexpr uint32_t kDlv4Threads = 256;
 #define GS_DLV4_MINW 4
 #endif
 
-// Bit-sliced "x >= K" with K given per segment: km[i] holds bit i of every
-// segment's K spread over that segment (the borrow chain of ge_k).
-template <int NB>
-GS_DEV u64 ge_seg(const u64 (&x)[NB], const u64 (&km)[NB]) {
-    u64 b = 0ull;
+// The lane word T holds the lane's nodes side by side (u32: two 16-bit or
+// four <= 8-bit segments; u64: four 16-bit segments); the bit-sliced helpers
+// of gs_device.h for either width.
+template <typename T>
+GS_DEV uint32_t popcT(T v) {
+    if constexpr (sizeof(T) == 8) return (uint32_t)__popcll(v);
+    else return (uint32_t)__popc(v);
+}
+template <typename T>
+GS_DEV void add5T(T (&c)[5], T in) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const T t = c[i] & in;
+        c[i] ^= in;
+        in = t;
+    }
+}
+// "x >= K" for a wave-uniform K (the borrow chain of x - K)
+template <int NB, typename T>
+GS_DEV T ge_uT(const T (&x)[NB], uint32_t K) {
+    if (K >= (1u << NB)) return (T)0;
+    T b = 0;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const T k = ((K >> i) & 1u) ? (T)~(T)0 : (T)0;
+        b = (~x[i] & b) | (k & (~x[i] | b));
+    }
+    return ~b;
+}
+// "x >= K" with K given per segment: km[i] holds bit i of every segment's K
+// spread over that segment.
+template <int NB, typename T>
+GS_DEV T ge_seg(const T (&x)[NB], const T (&km)[NB]) {
+    T b = 0;
 #pragma unroll
     for (int i = 0; i < NB; ++i) b = (~x[i] & b) | (km[i] & (~x[i] | b));
     return ~b;
 }
 
-template <int MODE>
+template <int MODE, typename T, uint32_t kNpl>
 __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(RoundArgs a) {
     constexpr bool DELIVER = MODE == 1;
     const Geometry &g = a.g;
@@ -48,16 +76,17 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
     const uint32_t lane = blockIdx.x * kDlv4Threads + threadIdx.x;
     const uint32_t x0 = lane * kNpl;
     const uint32_t nv = x0 < n_nodes ? min(kNpl, n_nodes - x0) : 0u;  // valid nodes of the lane
-    const u64 m1 = (1ull << rp) - 1ull;
-    u64 M[kNpl];  // segment of node x0 + q within the lane's field
-    u64 mV = 0;
+    const T m1 = (1ull << rp) - 1ull;
+    T M[kNpl];  // segment of node x0 + q within the lane's field
+    T mV = 0;
 #pragma unroll
     for (uint32_t q = 0; q < kNpl; ++q) {
-        M[q] = q < nv ? m1 << (q * rp) : 0ull;
+        M[q] = q < nv ? m1 << (q * rp) : (T)0;
         mV |= M[q];
     }
     // the lane's field: bits [shL, shL + 4*rp) of plane word `unit`
-    const uint32_t lpw_log = lognpu - 2u;  // lanes per word = npu / 4
+    constexpr uint32_t kLogNpl = kNpl == 4 ? 2u : (kNpl == 2 ? 1u : 0u);
+    const uint32_t lpw_log = lognpu - kLogNpl;  // lanes per word = npu / kNpl
     const uint32_t shL = (x0 & ((1u << lognpu) - 1u)) << lr;
 
     // ---- own round-t planes, staged through LDS (16-byte coalesced loads)
@@ -69,14 +98,14 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
     {
         const uint4 *src4 = reinterpret_cast<const uint4 *>(a.Scur + unit0 * kPlanes);
         uint4 *dst4 = reinterpret_cast<uint4 *>(stage);
-        uint4 v[4];
+        uint4 v[kNpl];  // at most kNpl uint4 per thread (R_pad 16: 8 words per kNpl nodes)
 #pragma unroll
-        for (uint32_t it = 0; it < 4; ++it) {
+        for (uint32_t it = 0; it < kNpl; ++it) {
             const uint32_t i = threadIdx.x + kDlv4Threads * it;
             v[it] = src4[min(i, blk_v4 - 1u)];  // blk_v4 >= 4: every block owns a unit
         }
 #pragma unroll
-        for (uint32_t it = 0; it < 4; ++it) {
+        for (uint32_t it = 0; it < kNpl; ++it) {
             const uint32_t i = threadIdx.x + kDlv4Threads * it;
             if (i < blk_v4) dst4[i] = v[it];
         }
@@ -87,11 +116,16 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
 #pragma unroll
     for (uint32_t q = 0; q < kNpl; ++q) kk[q] = dzi[q] = dfirst[q] = c0[q] = c1[q] = tgw[q] = dp[q] = 0u;
     if (DELIVER) {
-        if (nv == kNpl) {
+        if (kNpl == 4 && nv == kNpl) {
             const uint4 t4 = *reinterpret_cast<const uint4 *>(a.tg + x0);
             const uint4 p4 = *reinterpret_cast<const uint4 *>(a.pull + x0);
-            tgw[0] = t4.x; tgw[1] = t4.y; tgw[2] = t4.z; tgw[3] = t4.w;
-            dp[0] = p4.x; dp[1] = p4.y; dp[2] = p4.z; dp[3] = p4.w;
+            tgw[0] = t4.x; tgw[1] = t4.y; tgw[kNpl > 2 ? 2 : 0] = t4.z; tgw[kNpl > 3 ? 3 : 0] = t4.w;
+            dp[0] = p4.x; dp[1] = p4.y; dp[kNpl > 2 ? 2 : 0] = p4.z; dp[kNpl > 3 ? 3 : 0] = p4.w;
+        } else if (kNpl == 2 && nv == kNpl) {
+            const uint2 t2 = *reinterpret_cast<const uint2 *>(a.tg + x0);
+            const uint2 p2 = *reinterpret_cast<const uint2 *>(a.pull + x0);
+            tgw[0] = t2.x; tgw[1] = t2.y;
+            dp[0] = p2.x; dp[1] = p2.y;
         } else {
 #pragma unroll
             for (uint32_t q = 0; q < kNpl; ++q)
@@ -114,22 +148,22 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
     // class planes now; the five b planes only for the transition (still in
     // LDS then: fewer registers live across the deliveries)
     const uint32_t ul = (lane >> lpw_log) - blockIdx.x * units_blk;  // the lane's word within the block
-    u64 P[kPlanes];
+    T P[kPlanes];
 #pragma unroll
-    for (int p = 0; p < 3; ++p) P[p] = nv ? (stage[ul * kPlanes + p] >> shL) & mV : 0ull;
+    for (int p = 0; p < 3; ++p) P[p] = nv ? (T)(stage[ul * kPlanes + p] >> shL) & mV : (T)0;
 
-    const u64 isC = P[0], a0 = P[1], a1 = P[2];
-    const u64 A = ~isC & ~a0 & ~a1 & mV;
-    const u64 B = ~isC & (a0 | a1);
-    const u64 C = isC & ~(a0 & a1);
-    const u64 D = isC & a0 & a1;
-    const u64 liveX = B | C;
+    const T isC = P[0], a0 = P[1], a1 = P[2];
+    const T A = ~isC & ~a0 & ~a1 & mV;
+    const T B = ~isC & (a0 | a1);
+    const T C = isC & ~(a0 & a1);
+    const T D = isC & a0 & a1;
+    const T liveX = B | C;
 
     // ---- phases 1 and 2 of round t (Gossip::receive), four nodes at once
-    u64 notyet = A, recB = B, oc1r = B & a0 & ~a1, crB = 0, crC = 0, anyC = 0;
-    u64 cv[5] = {0, 0, 0, 0, 0};
+    T notyet = A, recB = B, oc1r = B & a0 & ~a1, crB = 0, crC = 0, anyC = 0;
+    T cv[5] = {0, 0, 0, 0, 0};
     uint32_t part_cw[kNpl], fc[kNpl], recv[kNpl], psize[kNpl];
-    u64 pulledM = 0, offM = 0;
+    T pulledM = 0, offM = 0;
 #pragma unroll
     for (uint32_t q = 0; q < kNpl; ++q) {
         part_cw[q] = recv[q] = psize[q] = 0u;
@@ -148,21 +182,21 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
             // push batch of pusher i of every node that has one (2-plane code:
             // 01 counter 1, 10 counter 2, 11 counter 255); t(x)'s push copy is
             // superseded by its pull copy (message_state.rs:79), so not recorded
-            u64 b0 = 0, b1 = 0, recm = ~0ull;
+            T b0 = 0, b1 = 0, recm = (T)~(T)0;
 #pragma unroll
             for (uint32_t q = 0; q < kNpl; ++q) {
                 if (i < kk[q]) {
                     const uint32_t code = i == 0 ? c0[q] : (i == 1 ? c1[q] : a.dtail[dfirst[q] + i - kDlvInline]);
-                    b0 |= ((u64)code & m1) << (q * rp);
-                    b1 |= ((u64)(code >> 16) & m1) << (q * rp);
+                    b0 |= ((T)code & m1) << (q * rp);
+                    b1 |= ((T)(code >> 16) & m1) << (q * rp);
                     if ((pulledM & M[q]) && i == dzi[q]) recm &= ~M[q];
                 }
             }
-            const u64 vC = b0 & b1, vB = b0 ^ b1, v2 = b1 & ~b0, sl = b0 | b1;
-            const u64 newc = notyet & sl;           // new_from_peer: not recorded
-            const u64 rec = recB & sl & recm;       // MessageState::receive on B
+            const T vC = b0 & b1, vB = b0 ^ b1, v2 = b1 & ~b0, sl = b0 | b1;
+            const T newc = notyet & sl;           // new_from_peer: not recorded
+            const T rec = recB & sl & recm;       // MessageState::receive on B
             anyC |= rec & vC;
-            add5(cv, rec & vB & (v2 | oc1r));
+            add5T(cv, rec & vB & (v2 | oc1r));
             crB |= newc & ~vC;
             crC |= newc & vC;
             recB |= newc & ~vC;
@@ -170,29 +204,29 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
             notyet &= ~newc;
 #pragma unroll
             for (uint32_t q = 0; q < kNpl; ++q) {
-                const uint32_t pc = popc(newc & M[q]);
+                const uint32_t pc = popcT(newc & M[q]);
                 part_cw[q] += (kk[q] - 1u - i) * pc;  // later pushers' pull rows include it
                 if (pc && fc[q] == kNone) fc[q] = i;
-                recv[q] += popc(sl & M[q]);
+                recv[q] += popcT(sl & M[q]);
             }
         }
         // the pull batch t(x) returned (built by the in-list build; the slot
         // of a node whose pull is not delivered holds garbage: masked out
         // before it is shifted into place)
-        u64 pb0 = 0, pb1 = 0;
+        T pb0 = 0, pb1 = 0;
 #pragma unroll
         for (uint32_t q = 0; q < kNpl; ++q) {
-            pb0 |= ((u64)dp[q] & m1) << (q * rp);
-            pb1 |= ((u64)(dp[q] >> 16) & m1) << (q * rp);
+            pb0 |= ((T)dp[q] & m1) << (q * rp);
+            pb1 |= ((T)(dp[q] >> 16) & m1) << (q * rp);
         }
         pb0 &= pulledM;
         pb1 &= pulledM;
-        const u64 pv2 = pb1 & ~pb0, pvB = pb0 ^ pb1, pCl = pb0 & pb1, pl = pb0 | pb1;
+        const T pv2 = pb1 & ~pb0, pvB = pb0 ^ pb1, pCl = pb0 & pb1, pl = pb0 | pb1;
         {
-            const u64 newc = notyet & pl;
-            const u64 rec = recB & pl;
+            const T newc = notyet & pl;
+            const T rec = recB & pl;
             anyC |= rec & pCl;
-            add5(cv, rec & pvB & (pv2 | oc1r));
+            add5T(cv, rec & pvB & (pv2 | oc1r));
             crB |= newc & ~pCl;
             crC |= newc & pCl;
             recB |= newc & ~pCl;
@@ -201,7 +235,7 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
         }
 #pragma unroll
         for (uint32_t q = 0; q < kNpl; ++q) {
-            recv[q] += popc(pl & M[q]);
+            recv[q] += popcT(pl & M[q]);
             const bool pulled = (pulledM & M[q]) != 0;
             psize[q] = kk[q] + ((pulled && dzi[q] == kDlvNoZ) ? 1u : 0u);  // |peers_in_this_round|
         }
@@ -213,14 +247,14 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
     for (uint32_t q = 0; q < kNpl; ++q) {
         d_empty_pull[q] = d_full[q] = 0u;
         if (DELIVER) {
-            const uint32_t lc = popc(liveX & M[q]);
+            const uint32_t lc = popcT(liveX & M[q]);
             d_full[q] = kk[q] * lc + part_cw[q];  // pull rows sent by x
             if (kk[q] > 0 && lc == 0) d_empty_pull[q] = (fc[q] == kNone) ? kk[q] : fc[q] + 1u;
         }
     }
 
     // ---- phase 0 of round t+1: injections, MessageState::next_round
-    u64 inj = 0;
+    T inj = 0;
     if (a.n_inj && nv) {
         uint32_t lo = 0, hi = a.n_inj;
         while (lo < hi) {
@@ -228,17 +262,17 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
             if (a.inj_key[mid] < x0) lo = mid + 1; else hi = mid;
         }
         for (uint32_t i = lo; i < a.n_inj && a.inj_key[i] < (u64)x0 + nv; ++i)
-            inj |= (a.inj_mask[i] & m1) << ((uint32_t)(a.inj_key[i] - x0) * rp);
+            inj |= ((T)a.inj_mask[i] & m1) << ((uint32_t)(a.inj_key[i] - x0) * rp);
     }
-    const u64 ninj = ~inj;
-    const u64 Bold = B & ninj, Cold = C & ninj, Dold = D & ninj;
-    const u64 cB = crB & ninj, cC = crC & ninj;
-    const u64 Bf = Bold | cB | inj;
-    const u64 Cf = Cold | cC;
-    const u64 oc1 = (Bold & a0 & ~a1) | cB | inj;
-    const u64 oc2 = Bold & a1 & ~a0;
+    const T ninj = ~inj;
+    const T Bold = B & ninj, Cold = C & ninj, Dold = D & ninj;
+    const T cB = crB & ninj, cC = crC & ninj;
+    const T Bf = Bold | cB | inj;
+    const T Cf = Cold | cC;
+    const T oc1 = (Bold & a0 & ~a1) | cB | inj;
+    const T oc2 = Bold & a1 & ~a0;
     // median rule with 0-filled peers: bump iff ge >= |P|/2 + 1, per node
-    u64 km[5] = {0, 0, 0, 0, 0}, kbig = 0;
+    T km[5] = {0, 0, 0, 0, 0}, kbig = 0;
 #pragma unroll
     for (uint32_t q = 0; q < kNpl; ++q) {
         const uint32_t thr = psize[q] / 2u + 1u;
@@ -247,59 +281,59 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
             if ((thr >> i) & 1u) km[i] |= M[q];
         if (thr >= 32u) kbig |= M[q];
     }
-    u64 bump = ge_seg<5>(cv, km) & ~kbig & (Bold | cB);
-    u64 anyCe = anyC & ninj;
+    T bump = ge_seg<5>(cv, km) & ~kbig & (Bold | cB);
+    T anyCe = anyC & ninj;
     if (DELIVER && offM) {  // back from offline: the votes its skipped next_round kept
 #pragma unroll
         for (uint32_t q = 0; q < kNpl; ++q)
             if (offM & M[q]) {
                 const u64 *pe = a.pend + (u64)(x0 + q) * 2u;
-                bump = (bump & ~M[q]) | (((pe[0] & m1) << (q * rp)) & Bold);
-                anyCe = (anyCe & ~M[q]) | (((pe[1] & m1) << (q * rp)) & ninj);
+                bump = (bump & ~M[q]) | (((T)pe[0] & m1) << (q * rp) & Bold);
+                anyCe = (anyCe & ~M[q]) | (((T)pe[1] & m1) << (q * rp) & ninj);
             }
     }
 #pragma unroll
-    for (int p = 3; p < kPlanes; ++p) P[p] = nv ? (stage[ul * kPlanes + p] >> shL) & mV : 0ull;
-    u64 nr[6];  // round + 1
+    for (int p = 3; p < kPlanes; ++p) P[p] = nv ? (T)(stage[ul * kPlanes + p] >> shL) & mV : (T)0;
+    T nr[6];  // round + 1
     {
-        u64 carry = ~0ull;
+        T carry = (T)~(T)0;
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
-            const u64 rb = P[3 + i] & Bold;
+            const T rb = P[3 + i] & Bold;
             nr[i] = rb ^ carry;
             carry &= rb;
         }
         nr[5] = carry;
     }
-    const u64 toD = ge_u<6>(nr, a.maxr);
-    const u64 oc1n = oc1 & ~bump;
-    const u64 oc2n = (oc1 & bump) | (oc2 & ~bump);
-    const u64 oc3n = oc2 & bump;
-    const u64 ocge = a.cmax <= 1u ? ~0ull : (a.cmax == 2u ? (oc2n | oc3n) : oc3n);
-    const u64 toC = anyCe | ocge;
-    const u64 BD = Bf & toD, BC = Bf & ~toD & toC, BB = Bf & ~toD & ~toC;
-    const u64 cr0 = a0 & Cold, cr1 = a1 & Cold;
-    const u64 d[3] = {~cr0, cr1 ^ cr0, cr1 & cr0};
-    u64 rib[5];
+    const T toD = ge_uT<6>(nr, a.maxr);
+    const T oc1n = oc1 & ~bump;
+    const T oc2n = (oc1 & bump) | (oc2 & ~bump);
+    const T oc3n = oc2 & bump;
+    const T ocge = a.cmax <= 1u ? (T)~(T)0 : (a.cmax == 2u ? (oc2n | oc3n) : oc3n);
+    const T toC = anyCe | ocge;
+    const T BD = Bf & toD, BC = Bf & ~toD & toC, BB = Bf & ~toD & ~toC;
+    const T cr0 = a0 & Cold, cr1 = a1 & Cold;
+    const T d[3] = {~cr0, cr1 ^ cr0, cr1 & cr0};
+    T rib[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) rib[i] = P[3 + i] & Cold;
-    u64 sum[6];
+    T sum[6];
     {
-        u64 c = 0;
+        T c = 0;
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
-            const u64 di = i < 3 ? d[i] : 0ull;
+            const T di = i < 3 ? d[i] : (T)0;
             sum[i] = rib[i] ^ di ^ c;
             c = (rib[i] & di) | (c & (rib[i] ^ di));
         }
         sum[5] = c;
     }
-    const u64 CtoD = ge_u<6>(sum, a.maxr) | ge_u<3>(d, a.maxc);
-    const u64 CD = Cf & CtoD, CC = Cf & ~CtoD;
-    const u64 Dn = BD | CD | Dold;
-    const u64 Cn = BC | CC;
-    const u64 Bn = BB;
-    u64 N[kPlanes];
+    const T CtoD = ge_uT<6>(sum, a.maxr) | ge_uT<3>(d, a.maxc);
+    const T CD = Cf & CtoD, CC = Cf & ~CtoD;
+    const T Dn = BD | CD | Dold;
+    const T Cn = BC | CC;
+    const T Bn = BB;
+    T N[kPlanes];
     N[0] = Cn | Dn;
     N[1] = (Bn & oc1n) | (CC & d[0]) | Dn;
     N[2] = (Bn & oc2n) | (CC & d[1]) | Dn;
@@ -308,27 +342,27 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
 
     // churn: a node offline in round t+1 skips next_round and keeps its
     // pre-transition state and the two votes in `pend`
-    u64 onM = mV;
+    T onM = mV;
     if (a.f.churn) {
 #pragma unroll
         for (uint32_t q = 0; q < kNpl; ++q)
             if (q < nv && offline_of(a.seed, a.epoch, a.round_new, a.node_lo + x0 + q, a.f.churn)) onM &= ~M[q];
     }
     if (onM != mV) {
-        const u64 fz = mV & ~onM;
-        const u64 F[3] = {(isC & ninj) | cC, (a0 & ninj) | cB | inj, a1 & ninj};
+        const T fz = mV & ~onM;
+        const T F[3] = {(isC & ninj) | cC, (a0 & ninj) | cB | inj, a1 & ninj};
 #pragma unroll
         for (int p = 0; p < kPlanes; ++p) {
-            const u64 f = p < 3 ? F[p] : (P[p] & ninj);
+            const T f = p < 3 ? F[p] : (P[p] & ninj);
             N[p] = (N[p] & onM) | (f & fz);
         }
-        const u64 av = anyCe & (Bold | cB);
+        const T av = anyCe & (Bold | cB);
 #pragma unroll
         for (uint32_t q = 0; q < kNpl; ++q)
             if (fz & M[q]) {
                 u64 *pe = a.pend + (u64)(x0 + q) * 2u;
-                pe[0] = (bump >> (q * rp)) & m1;
-                pe[1] = (av >> (q * rp)) & m1;
+                pe[0] = (u64)((bump >> (q * rp)) & m1);
+                pe[1] = (u64)((av >> (q * rp)) & m1);
             }
     }
 
@@ -341,14 +375,17 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
 
     // ---- push codes of round t+1 for the in-list build (4 B per node)
     {
-        const u64 vC = N[0] & ~(N[1] & N[2]), vB = ~N[0] & (N[1] | N[2]);
-        const u64 b0 = (vB & N[1] & ~N[2]) | vC, b1 = (vB & N[2] & ~N[1]) | vC;
+        const T vC = N[0] & ~(N[1] & N[2]), vB = ~N[0] & (N[1] | N[2]);
+        const T b0 = (vB & N[1] & ~N[2]) | vC, b1 = (vB & N[2] & ~N[1]) | vC;
         uint32_t pc[kNpl];
 #pragma unroll
         for (uint32_t q = 0; q < kNpl; ++q)
             pc[q] = (uint32_t)((b0 >> (q * rp)) & m1) | ((uint32_t)((b1 >> (q * rp)) & m1) << 16);
-        if (nv == kNpl) {
-            *reinterpret_cast<uint4 *>(a.pc_out + x0) = make_uint4(pc[0], pc[1], pc[2], pc[3]);
+        if (kNpl == 4 && nv == kNpl) {
+            *reinterpret_cast<uint4 *>(a.pc_out + x0) =
+                make_uint4(pc[0], pc[1], pc[kNpl > 2 ? 2 : 0], pc[kNpl > 3 ? 3 : 0]);
+        } else if (kNpl == 2 && nv == kNpl) {
+            *reinterpret_cast<uint2 *>(a.pc_out + x0) = make_uint2(pc[0], pc[1]);
         } else {
 #pragma unroll
             for (uint32_t q = 0; q < kNpl; ++q)
@@ -364,7 +401,7 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
     bool any_live = false;
 #pragma unroll
     for (uint32_t q = 0; q < kNpl; ++q) {
-        live[q] = (onM & M[q]) ? popc((Bn | Cn) & M[q]) : 0u;
+        live[q] = (onM & M[q]) ? popcT((Bn | Cn) & M[q]) : 0u;
         any_live |= live[q] != 0u;
     }
     __syncthreads();  // every lane is done reading stage; blk_any is cleared
@@ -372,7 +409,7 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
         const uint32_t lpw = 1u << lpw_log;
 #pragma unroll
         for (int p = 0; p < kPlanes; ++p) {
-            u64 v = (N[p] & mV) << shL;
+            u64 v = (u64)(N[p] & mV) << shL;
             for (uint32_t o = 1; o < lpw; o <<= 1) v |= __shfl_xor(v, (int)o, 64);
             if ((lane & (lpw - 1u)) == 0u && nv) stage[ul * kPlanes + p] = v;
         }
@@ -383,7 +420,7 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
         const uint4 *src4 = reinterpret_cast<const uint4 *>(stage);
         uint4 *dst4 = reinterpret_cast<uint4 *>(a.Snext + unit0 * kPlanes);
 #pragma unroll
-        for (uint32_t it = 0; it < 4; ++it) {
+        for (uint32_t it = 0; it < kNpl; ++it) {
             const uint32_t i = threadIdx.x + kDlv4Threads * it;
             if (i < blk_v4) nt_store4(src4[i], &dst4[i]);
         }
@@ -410,15 +447,24 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
     }
 }
 
-hipError_t launch_round_dlv4(const RoundArgs &a, int mode, hipStream_t s) {
-    const u64 lanes = ((u64)a.g.n + kNpl - 1) / kNpl;
+template <typename T, uint32_t NPL>
+static hipError_t launch_dlv4_t(const RoundArgs &a, int mode, hipStream_t s) {
+    const u64 lanes = ((u64)a.g.n + NPL - 1) / NPL;
     const u64 grid = (lanes + kDlv4Threads - 1) / kDlv4Threads;
     if (grid == 0) return hipSuccess;
     if (mode == 0)
-        hipLaunchKernelGGL(round_kernel_dlv4<0>, dim3((uint32_t)grid), dim3(kDlv4Threads), 0, s, a);
+        hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL>), dim3((uint32_t)grid), dim3(kDlv4Threads), 0, s, a);
     else
-        hipLaunchKernelGGL(round_kernel_dlv4<1>, dim3((uint32_t)grid), dim3(kDlv4Threads), 0, s, a);
+        hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL>), dim3((uint32_t)grid), dim3(kDlv4Threads), 0, s, a);
     return hipGetLastError();
+}
+
+// Lane word per R_pad: u32 holding two 16-bit or four <= 8-bit segments
+// (default); dlv_pack == 2 selects u64 words of four 16-bit segments.
+hipError_t launch_round_dlv4(const RoundArgs &a, int mode, hipStream_t s) {
+    if (a.g.rpad > 16) return hipErrorInvalidValue;
+    if (a.g.rpad == 16) return a.dlv_pack == 2 ? launch_dlv4_t<u64, 4>(a, mode, s) : launch_dlv4_t<uint32_t, 2>(a, mode, s);
+    return launch_dlv4_t<uint32_t, 4>(a, mode, s);
 }
 
 }  // namespace gs

@@ -50,7 +50,10 @@ struct gs_engine {
         uint32_t serial = 0;
     } csr[2];
     bool dlv = false;  // delivery-record path (2P, R_pad <= 16, binned in-lists)
-    bool dlv_pack = true;  // its transition launches with four nodes per lane (SAFE_GOSSIP_AMD_DLV_PACK=0: one)
+    // its transition launches with several nodes per lane (gs_dlv4.hip):
+    // SAFE_GOSSIP_AMD_DLV_PACK = 0 one node per lane, u64 four 16-bit nodes
+    // per 64-bit lane word, otherwise (default) a 32-bit lane word
+    uint32_t dlv_pack = 1;
     // Sparse records (wide 2P engine, W <= 8; gs_kernels.h RoundArgs): maps of
     // plane buffer i, the accounting words and MODE-1 launches counted in them
     // The sparse variant runs while the input planes are at least a quarter
@@ -327,7 +330,7 @@ gs::RoundArgs base_args(gs_engine *e) {
         a.n_ext = e->ext_uploaded;
     }
     a.obs_only = 0xFFFFFFFFu;
-    a.dlv_pack = e->dlv_pack ? 1u : 0u;
+    a.dlv_pack = e->dlv_pack;
     a.g = e->g;
     a.seed = e->seed;
     a.epoch = e->epoch;
@@ -620,7 +623,8 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
     }
     {
         const char *v = std::getenv("SAFE_GOSSIP_AMD_DLV_PACK");
-        e->dlv_pack = !(v && *v == '0');
+        const std::string m = v ? v : "";
+        e->dlv_pack = m == "0" ? 0u : (m == "u64" ? 2u : 1u);
     }
     e->plan = e->dlv ? gs::dlv_plan(n) : gs::csr_plan(n);
     {

@@ -73,7 +73,8 @@ struct RoundArgs {
                               // written) | lane gathers << 32, one atomic per block
     u64 *dens;                // [kDensSlots] zero words of the round-(t+1) planes
                               // (spread atomics, cleared by the engine per launch)
-    uint32_t dlv_pack;        // DLV transition launches: four nodes per lane (gs_dlv4.hip)
+    uint32_t dlv_pack;        // DLV transition launches: 0 one node per lane, 1 a 32-bit lane
+                              // word of several nodes, 2 a 64-bit one (gs_dlv4.hip)
     Geometry g;
     uint64_t seed;
     uint32_t epoch;

@@ -312,8 +312,20 @@ def test_parity_small_gather_path(engine, monkeypatch, n, R, kind, faults):
     (1026, 16, "reinject", (0.2, 0.1, 0.1)),   # one word per lane, ragged last lane
 ])
 def test_parity_delivery_records_packed(engine, n, R, kind, faults):
-    # the DLV transition kernel with four nodes per lane (gs_dlv4.hip): every
-    # R_pad <= 16 field width, partial lanes and words, churn (pend votes)
+    # the DLV transition kernel with several nodes per 32-bit lane word
+    # (gs_dlv4.hip: two at R_pad 16, four below): every R_pad <= 16 field
+    # width, partial lanes and words, churn (pend votes)
+    run_parity(engine, n, R, kind, faults=faults)
+
+
+@pytest.mark.parametrize("n,R,kind,faults", [
+    (5, 16, "origins", None),
+    (1026, 16, "reinject", (0.2, 0.1, 0.1)),
+    (2050, 13, "origins", (0.02, 0.05, 0.05)),
+])
+def test_parity_delivery_records_packed_u64(engine, monkeypatch, n, R, kind, faults):
+    # R_pad 16 with four nodes per 64-bit lane word (SAFE_GOSSIP_AMD_DLV_PACK=u64)
+    monkeypatch.setenv("SAFE_GOSSIP_AMD_DLV_PACK", "u64")
     run_parity(engine, n, R, kind, faults=faults)
 
 
