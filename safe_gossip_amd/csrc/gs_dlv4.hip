@@ -463,7 +463,11 @@ static hipError_t launch_dlv4_t(const RoundArgs &a, int mode, hipStream_t s) {
 // (default); dlv_pack == 2 selects u64 words of four 16-bit segments.
 hipError_t launch_round_dlv4(const RoundArgs &a, int mode, hipStream_t s) {
     if (a.g.rpad > 16) return hipErrorInvalidValue;
-    if (a.g.rpad == 16) return a.dlv_pack == 2 ? launch_dlv4_t<u64, 4>(a, mode, s) : launch_dlv4_t<uint32_t, 2>(a, mode, s);
+    if (a.g.rpad == 16) {
+        if (a.dlv_pack == 2) return launch_dlv4_t<u64, 4>(a, mode, s);
+        if (a.dlv_pack == 3) return launch_dlv4_t<uint32_t, 1>(a, mode, s);
+        return launch_dlv4_t<uint32_t, 2>(a, mode, s);
+    }
     return launch_dlv4_t<uint32_t, 4>(a, mode, s);
 }
 

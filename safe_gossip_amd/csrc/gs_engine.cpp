@@ -624,7 +624,7 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
     {
         const char *v = std::getenv("SAFE_GOSSIP_AMD_DLV_PACK");
         const std::string m = v ? v : "";
-        e->dlv_pack = m == "0" ? 0u : (m == "u64" ? 2u : 1u);
+        e->dlv_pack = m == "0" ? 0u : (m == "u64" ? 2u : (m == "u32x1" ? 3u : 1u));
     }
     e->plan = e->dlv ? gs::dlv_plan(n) : gs::csr_plan(n);
     {
