@@ -471,9 +471,13 @@ __global__ __launch_bounds__(kInlThreads) void dl_fine(InListArgs a) {
 // created from the pushers ahead), partitioned by the pusher's coarse source
 // bucket for the pull pass-back (pb_fine, pb_place).  Halving the bin keeps
 // ids and codes in LDS.
-constexpr uint32_t kHalfLog = kBinLog - 1;
+#ifndef GS_DLV_SPLIT_LOG
+#define GS_DLV_SPLIT_LOG 1
+#endif
+constexpr uint32_t kSplitLog = GS_DLV_SPLIT_LOG;   // sort blocks per bin = 2^kSplitLog
+constexpr uint32_t kHalfLog = kBinLog - kSplitLog;
 constexpr uint32_t kHalf = 1u << kHalfLog;
-constexpr uint32_t kHalfCap = kBinCap / 2;
+constexpr uint32_t kHalfCap = kBinCap >> kSplitLog;
 constexpr uint32_t kHalfPer = kHalf / kInlThreads;  // targets per thread
 
 __global__ __launch_bounds__(kInlThreads) void inl_sort_dlv(InListArgs a) {
@@ -949,7 +953,7 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
             hipLaunchKernelGGL(dl_coarse, dim3(p.ba), dim3(kInlThreads), lds_c, s, ab);
             hipLaunchKernelGGL(dl_fine, dim3((kCoarseCap + kPartChunk - 1) / kPartChunk, nc), dim3(kInlThreads),
                                lds_f, s, ab);
-            hipLaunchKernelGGL(inl_sort_dlv, dim3(p.nb, 2), dim3(kInlThreads), lds_dlv, s, ab);
+            hipLaunchKernelGGL(inl_sort_dlv, dim3(p.nb, 1u << kSplitLog), dim3(kInlThreads), lds_dlv, s, ab);
             const size_t lds_pb = ((size_t)kPartChunk + kPartChunk / 2 + kPartChunk / 4) * sizeof(uint32_t);
             e = hipFuncSetAttribute((const void *)pb_fine, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_pb);
             if (e != hipSuccess) return e;
