@@ -275,15 +275,18 @@ def main():
 
     spread = None if args.no_spread else spread_run(net, epoch)
 
+    # PMC traffic of the same kernel from the committed rocprofv3 run of this
+    # workload (profiles/summarize.py writes one file per (nodes, rumors))
     traffic = None
-    pmc_path = os.path.join(REPO, "profiles", "pmc_latest.json")
-    if os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-            if pmc.get("nodes") == n and pmc.get("rumors") == R:
-                traffic = pmc.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    for name in (f"pmc_n{n}_r{R}.json", "pmc_latest.json"):
+        pmc_path = os.path.join(REPO, "profiles", name)
+        if traffic is None and os.path.exists(pmc_path) and world == 1:
+            try:
+                pmc = json.load(open(pmc_path))
+                if pmc.get("nodes") == n and pmc.get("rumors") == R:
+                    traffic = pmc.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
 
     cpu = best = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -323,8 +326,7 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "round_kernel<%s,1> (deliver round t + transition to t+1)"
-                          % ("true" if R < 64 else "false"),
+                "kernel": net.round_kernel_name() + " (deliver round t + transition to t+1)",
                 "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": bytes_per,
                 "bytes_counted_by": ("kernels (sparse records), %d launches" % launches) if launches
                                     else "static model",

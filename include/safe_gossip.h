@@ -162,6 +162,9 @@ void        gs_set_timing(gs_engine *e, int enable);
 int32_t     gs_round_kernel_times(gs_engine *e, float *out_ms, uint32_t max);
 /* Algorithmic HBM bytes of one round kernel (DESIGN.md, section Roofline). */
 double      gs_round_kernel_bytes(const gs_engine *e);
+/* Name of the deliver+transition kernel this engine launches (the one
+ * gs_round_kernel_bytes describes), e.g. "round_kernel_dlv4<1,u32,2>". */
+const char *gs_round_kernel_name(const gs_engine *e);
 /* Algorithmic HBM bytes per deliver+transition round kernel launched since
  * gs_set_timing(e, 1), as counted by the kernels: with sparse records (the
  * wide 2P engine) words known to be zero are neither read nor rewritten and

@@ -63,6 +63,7 @@ def main():
                            "read request; each request moves a 128-B line, calibrated in "
                            "profiles/r2/pmc_calib_and_cfg5.json)")
         summary["dominant"] = latest
+        json.dump(latest, open(os.path.join(HERE, f"pmc_n{a.nodes}_r{a.rumors}.json"), "w"), indent=1)
         if not a.no_latest:
             json.dump(latest, open(os.path.join(HERE, "pmc_latest.json"), "w"), indent=1)
     json.dump(summary, open(os.path.join(out, "summary.json"), "w"), indent=1)

@@ -121,6 +121,7 @@ SYMBOLS = {
     "gs_set_timing": (None, [_P, ctypes.c_int]),
     "gs_round_kernel_times": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_float), ctypes.c_uint32]),
     "gs_round_kernel_bytes": (ctypes.c_double, [_P]),
+    "gs_round_kernel_name": (ctypes.c_char_p, [_P]),
     "gs_round_traffic": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), _U32P]),
     "gs_peer": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.c_uint32, ctypes.c_uint32]),
@@ -541,6 +542,9 @@ class Network:
 
     def round_kernel_bytes(self) -> float:
         return float(self._lib.gs_round_kernel_bytes(self._h))
+
+    def round_kernel_name(self) -> str:
+        return self._lib.gs_round_kernel_name(self._h).decode()
 
     def round_traffic(self):
         """(algorithmic bytes per deliver+transition launch since set_timing(True),

@@ -1507,6 +1507,20 @@ double gs_round_kernel_bytes(const gs_engine *e) {
     return n * (2.75 * rp + 68.0);
 }
 
+const char *gs_round_kernel_name(const gs_engine *e) {
+    if (!e) return "";
+    if (e->shard) return e->g.small ? "round_kernel<true,1,SHARD>" : "round_kernel<false,1,SHARD>";
+    if (e->seq) return e->g.small ? "round_kernel<true,1,SEQ>" : "round_kernel<false,1,SEQ>";
+    if (e->dlv) {
+        if (e->dlv_pack == 0) return "round_kernel<true,1,DLV> (one node per lane)";
+        if (e->g.rpad < 16) return "round_kernel_dlv4<1,u32,4>";
+        return e->dlv_pack == 2 ? "round_kernel_dlv4<1,u64,4>"
+                                : (e->dlv_pack == 3 ? "round_kernel_dlv4<1,u32,1>" : "round_kernel_dlv4<1,u32,2>");
+    }
+    if (e->spr) return "round_kernel<false,1,SPARSE>";
+    return e->g.small ? "round_kernel<true,1>" : "round_kernel<false,1>";
+}
+
 gs_status gs_round_traffic(gs_engine *e, double *bytes_per_launch, uint32_t *launches) {
     if (!e || !bytes_per_launch || !launches) return GS_ERR_INVALID_ARGUMENT;
     const double dense = gs_round_kernel_bytes(e);

@@ -308,6 +308,9 @@ class ShardedNetwork:
     def round_kernel_bytes(self) -> float:
         return float(self.lib.gs_round_kernel_bytes(self.shards[0].h))
 
+    def round_kernel_name(self) -> str:
+        return self.lib.gs_round_kernel_name(self.shards[0].h).decode()
+
     # ------------------------------------------------------------ observers
     def _per_shard(self, fn):
         self._deliver()
