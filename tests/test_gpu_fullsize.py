@@ -1,0 +1,73 @@
+"""BASELINE configs 3 and 4 at their full sizes, and the packed delivery-record
+kernel against the one-node-per-lane one at a config-5-shaped size.
+
+Configs 3 and 4 (2^20 x 64, 2^24 x 256: the bench workload) are too large for
+the oracle; they are checked by the accounting laws of the reference that a
+lost, duplicated or misrouted copy breaks (src/gossip.rs:80,103,139,155):
+Statistics.rounds = rounds x n, every full copy sent is received, known sets
+only grow, the processed flag (src/gossiper.rs:209-212) agrees with the
+empty-push count, and no device limit is hit.
+
+The packed DLV kernel (gs_dlv4.hip) is checked bit-exactly against the per-node
+kernel of gs_kernels.hip -- itself bit-exact against the oracle at oracle sizes
+(test_gpu_parity.py) -- on 2^24 + 12345 nodes x 16 rumors with config 5's
+faults: every state code, Statistics row and known set, every round.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5AFE6055
+
+
+@pytest.mark.parametrize("n,R,rounds", [(1 << 20, 64, 8), (1 << 24, 256, 5)])
+def test_full_size_accounting(engine, n, R, rounds):
+    net = engine.Network(n, R, seed=SEED)
+    try:
+        for r in range(R):
+            net.send_new(engine.origin_of(SEED, 0, r, n), r)
+        prev_known = net.known_all()
+        prev = net.statistics_reduce("sum")
+        for rnd in range(1, rounds + 1):
+            rep = net.next_round()
+            assert rep.round == rnd
+            st = net.statistics_reduce("sum")
+            assert st.rounds == rnd * n, f"round {rnd}: Statistics.rounds"
+            assert st.full_message_received == st.full_message_sent, f"round {rnd}: copies lost"
+            d_empty_push = st.empty_push_sent - prev.empty_push_sent
+            assert rep.any_live == (d_empty_push < n), f"round {rnd}: processed flag"
+            known = net.known_all()
+            assert not np.any(prev_known & ~known), f"round {rnd}: a known rumor was lost"
+            prev_known, prev = known, st
+        t, _ = net.known_counts()
+        assert t > R * 3 ** (rounds - 2)
+        net.sync()  # no device limit hit
+    finally:
+        net.close()
+
+
+def test_packed_dlv_matches_node_per_lane(engine, monkeypatch):
+    n, R = (1 << 24) + 12345, 16
+    faults = dict(churn=0.01, drop_push=0.01, drop_pull=0.01)
+    monkeypatch.setenv("SAFE_GOSSIP_AMD_DLV_PACK", "1")
+    a = engine.Network(n, R, seed=SEED, **faults)
+    monkeypatch.setenv("SAFE_GOSSIP_AMD_DLV_PACK", "0")
+    b = engine.Network(n, R, seed=SEED, **faults)
+    try:
+        for r in range(R):
+            x = engine.origin_of(SEED, 0, r, n)
+            a.send_new(x, r)
+            b.send_new(x, r)
+        for rnd in range(1, 7):
+            ra, rb = a.next_round(), b.next_round()
+            assert ra.any_live == rb.any_live
+            np.testing.assert_array_equal(a.dump_state(), b.dump_state(), err_msg=f"state round {rnd}")
+            np.testing.assert_array_equal(a.statistics_all(), b.statistics_all(),
+                                          err_msg=f"statistics round {rnd}")
+            np.testing.assert_array_equal(a.known_all(), b.known_all(), err_msg=f"known round {rnd}")
+        a.sync()
+        b.sync()
+    finally:
+        a.close()
+        b.close()
