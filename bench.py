@@ -328,8 +328,8 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                 "kernel": net.round_kernel_name() + " (deliver round t + transition to t+1)",
                 "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": bytes_per,
-                "bytes_counted_by": ("kernels (sparse records), %d launches" % launches) if launches
-                                    else "static model",
+                "bytes_counted_by": ("kernels (rows actually gathered + planes moved), %d launches"
+                                     % launches) if launches else "static model",
                 "dense_model_bytes_per_launch": bytes_dense,
                 "kernel_ms_per_round": [round(float(v), 4) for v in kt],
             },

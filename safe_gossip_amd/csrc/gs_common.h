@@ -164,6 +164,26 @@ struct alignas(16) InRec {
 struct alignas(16) SibRec {
     uint32_t tag, e[kSibInline];
 };
+// Live-filtered gathers (2P gather path, binned in-lists): the build of round
+// t's lists reads two node maps of round t's planes, "live" (some B or C
+// entry: its push row is not empty) and "complete" (no A entry: it creates
+// nothing), and marks the class rows the round kernel may skip because they
+// cannot change a result, in bits the records do not otherwise use:
+//   InRec.kf bits 28-30  pusher i = 0..2 pushes nothing (binned tails:
+//                        first < 2^23)
+//   SibRec.tag bits 5-6  sibling i = 0, 1 is not live or t(x) is complete
+//                        (no creation to pass on); rank < 32
+//   SibRec.e[2] bit 31   the same for sibling 2 (node ids are < 2^29)
+//   SibRec.tag bit 7     some earlier sibling is live and t(x) incomplete
+//                        (t(x)'s A-set is needed)
+// and a per-source bit map zl = t(x) is live.
+constexpr uint32_t kInSkipShift = 28;
+constexpr uint32_t kInFlagMask = (1u << kInSkipShift) - 1u;
+constexpr uint32_t kSibSkipShift = 5;
+constexpr uint32_t kSkipBit = 1u << 31;
+constexpr uint32_t kIdMask = kSkipBit - 1u;
+constexpr uint32_t kSibZNeed = 1u << 7;
+constexpr uint32_t kSibRankMask = 0x1Fu;
 
 // Delivery records (R_pad <= 16, 2P, binned in-lists; gs_inlist.hip): the
 // in-list build carries every pusher's push code to its receiver and returns

@@ -47,8 +47,16 @@ struct gs_engine {
         gs::SibRec *SIB8 = nullptr;
         gs::DlvRec *DR = nullptr;  // DLV path: delivery records (src holds the tails' codes)
         uint32_t *pull = nullptr;  // DLV path: PULL[x]
+        u64 *zl = nullptr;         // live-filtered gathers: per source "t(x) is live"
         uint32_t serial = 0;
     } csr[2];
+    // Live-filtered gathers (gs_common.h kSkipBit): node maps "live" and
+    // "complete" of the planes the last transition launch wrote, read by the
+    // in-list build that follows it on the same stream.  On for the 2P gather
+    // path with binned in-lists (W <= 8); SAFE_GOSSIP_AMD_FILTER=0 disables.
+    bool filt = false;
+    u64 *lvm = nullptr, *cpm = nullptr;
+    uint32_t filt_launches = 0;  // MODE-1 launches counted in acct since set_timing(1)
     bool dlv = false;  // delivery-record path (2P, R_pad <= 16, binned in-lists)
     // its transition launches with several nodes per lane (gs_dlv4.hip):
     // SAFE_GOSSIP_AMD_DLV_PACK = 0 one node per lane, u64 four 16-bit nodes
@@ -182,7 +190,7 @@ void release(gs_engine *e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->cstream) (void)hipStreamSynchronize(e->cstream);
     for (auto &c : e->csr) {
-        void *cb[] = {c.src, c.tg, c.scratch, c.region, c.IN8, c.SIB8, c.DR, c.pull};
+        void *cb[] = {c.src, c.tg, c.scratch, c.region, c.IN8, c.SIB8, c.DR, c.pull, c.zl};
         for (void *b : cb)
             if (b) (void)hipFree(b);
     }
@@ -203,7 +211,7 @@ void release(gs_engine *e) {
     for (int i = 0; i < 2; ++i)
         if (e->ev_dens[i]) (void)hipEventDestroy(e->ev_dens[i]);
     if (e->dens_host) (void)hipHostFree(e->dens_host);
-    void *bufs[] = {e->zb[0], e->zb[1], e->lb[0], e->lb[1], e->ab[0], e->ab[1], e->acct, e->dens, e->pc, e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
+    void *bufs[] = {e->lvm, e->cpm, e->zb[0], e->zb[1], e->lb[0], e->lb[1], e->ab[0], e->ab[1], e->acct, e->dens, e->pc, e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
                     e->partials, e->obs_state, e->obs_rec, e->obs_psize, e->obs_pend, e->ext_dev,
                     e->node_state};
     for (void *b : bufs)
@@ -313,6 +321,11 @@ gs::RoundArgs base_args(gs_engine *e) {
         a.src = cs.src;
         a.tg = cs.tg;
         a.serial = cs.serial;
+        if (e->filt) {
+            a.zlm = cs.zl;
+            a.lvm = e->lvm;
+            a.cpm = e->cpm;
+        }
     }
     a.st32 = e->st32;
     a.st64 = e->st64;
@@ -653,6 +666,12 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         const char *v = std::getenv("SAFE_GOSSIP_AMD_CONCURRENT_INLISTS");
         e->concurrent_inlists = v && *v && *v != '0';
     }
+    {
+        const char *v = std::getenv("SAFE_GOSSIP_AMD_FILTER");
+        const bool off = v && *v == '0';
+        e->filt = !off && !e->shard && !e->seq && !e->dlv && !e->spr && !e->concurrent_inlists &&
+                  e->plan.binned && (g.small || g.W <= 8);
+    }
     // Per round a node's u32 Statistics deltas grow by at most 32*R_pad + 32
     // (in-degree <= 30 is enforced); fold them into u64 well before a wrap.
     e->fold_every = (uint32_t)std::max<uint64_t>(1, 0xFFFFFFFFull / (32ull * g.rpad + 32) / 2);
@@ -696,12 +715,18 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         } else if (ok) {
             ok = dalloc(&c.IN8, n) == hipSuccess && dalloc(&c.SIB8, n) == hipSuccess &&
                  hipMemset(c.SIB8, 0, std::max<size_t>(n, 1) * sizeof(gs::SibRec)) == hipSuccess;
+            if (ok && e->filt) ok = dalloc(&c.zl, gs::node_map_words(n)) == hipSuccess;
         }
     }
     ok = ok && dalloc(&e->S[0], sw) == hipSuccess && dalloc(&e->S[1], sw) == hipSuccess &&
          dalloc(&e->flags, 4) == hipSuccess && dalloc(&e->st32, (size_t)4 * n) == hipSuccess &&
          dalloc(&e->st64, (size_t)4 * n) == hipSuccess;
     if (ok && e->dlv) ok = dalloc(&e->pc, n) == hipSuccess;
+    if (ok && e->filt)
+        ok = dalloc(&e->lvm, gs::node_map_words(n)) == hipSuccess &&
+             dalloc(&e->cpm, gs::node_map_words(n)) == hipSuccess &&
+             dalloc(&e->acct, gs::kAcctSlots) == hipSuccess &&
+             hipMemset(e->acct, 0, gs::kAcctSlots * sizeof(u64)) == hipSuccess;
     for (int i = 0; i < 2 && ok && e->spr; ++i)
         ok = dalloc(&e->zb[i], gs::spr_zb_words(g)) == hipSuccess &&
              dalloc(&e->lb[i], gs::spr_node_bytes(g)) == hipSuccess &&
@@ -939,6 +964,10 @@ gs_status round_begin(gs_engine *e) {
     } else if (e->deliver_pending) {
         e->dense_launches++;
     }
+    if (e->filt && e->deliver_pending && e->timing) {  // rows gathered, for gs_round_traffic
+        a.acct = e->acct;
+        e->filt_launches++;
+    }
     const uint32_t rs = R0 & 1u;  // set holding round t = e->round
     if (e->shard) {
         GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[(R0 + 1) % 3], 0));
@@ -1051,6 +1080,11 @@ gs_status round_end(gs_engine *e, gs_round_report *report) {
         la.epoch = e->epoch;
         la.round = e->round;
         la.f = e->faults;
+        if (e->filt) {  // skip flags from the maps the round kernel just wrote
+            la.lvm = e->lvm;
+            la.cpm = e->cpm;
+            la.zl = c.zl;
+        }
         if (e->dlv) {  // records carry the push codes of the new round's planes
             la.dlv = 1;
             la.S = e->S[e->cur];
@@ -1279,11 +1313,12 @@ void gs_set_timing(gs_engine *e, int enable) {
             }
     }
     e->tcount = 0;
-    if (e->timing && e->spr) {  // restart the traffic accounting with the ring
+    if (e->timing && (e->spr || e->filt)) {  // restart the traffic accounting with the ring
         (void)hipSetDevice(e->device);
         if (hipMemsetAsync(e->acct, 0, gs::kAcctSlots * sizeof(u64), e->stream) == hipSuccess) {
             e->acct_launches = 0;
             e->dense_launches = 0;
+            e->filt_launches = 0;
         }
     }
 }
@@ -1518,12 +1553,40 @@ const char *gs_round_kernel_name(const gs_engine *e) {
                                 : (e->dlv_pack == 3 ? "round_kernel_dlv4<1,u32,1>" : "round_kernel_dlv4<1,u32,2>");
     }
     if (e->spr) return "round_kernel<false,1,SPARSE>";
+    if (e->filt) return e->g.small ? "round_kernel<true,1> (live-filtered gathers)"
+                                   : "round_kernel<false,1> (live-filtered gathers)";
     return e->g.small ? "round_kernel<true,1>" : "round_kernel<false,1>";
 }
 
 gs_status gs_round_traffic(gs_engine *e, double *bytes_per_launch, uint32_t *launches) {
     if (!e || !bytes_per_launch || !launches) return GS_ERR_INVALID_ARGUMENT;
     const double dense = gs_round_kernel_bytes(e);
+    if (e->filt) {
+        // Live-filtered launches: per node the 68 B of gs_round_kernel_bytes
+        // plus its zl bit and the two map bits written; per plane segment moved
+        // 8 planes of it (64 B per 64-rumor word, R_pad B for a small
+        // segment); per class row gathered 3 planes of it (24 B / 3 R_pad/8 B).
+        gs_status st = set_device(e);
+        if (st != GS_OK) return st;
+        *launches = e->filt_launches;
+        if (e->filt_launches == 0) {
+            *bytes_per_launch = dense;
+            return GS_OK;
+        }
+        std::vector<u64> v(gs::kAcctSlots);
+        GS_HIP(hipStreamSynchronize(e->stream));
+        GS_HIP(hipMemcpy(v.data(), e->acct, v.size() * sizeof(u64), hipMemcpyDeviceToHost));
+        double segs = 0, rows = 0;
+        for (u64 w : v) {
+            segs += (double)(w & 0xFFFFFFFFull);
+            rows += (double)(w >> 32);
+        }
+        const double n = e->g.n, rp = e->g.rpad;
+        const double seg_b = e->g.small ? rp : 64.0, row_b = e->g.small ? 3.0 * rp / 8.0 : 24.0;
+        *bytes_per_launch = (e->filt_launches * n * (68.0 + 3.0 / 8.0) + seg_b * segs + row_b * rows) /
+                            e->filt_launches;
+        return GS_OK;
+    }
     if (!e->spr) {
         *bytes_per_launch = dense;
         *launches = 0;

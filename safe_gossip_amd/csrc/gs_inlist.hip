@@ -41,8 +41,13 @@ namespace {
 constexpr uint32_t kBinLog = GS_INL_BINLOG;
 constexpr uint32_t kBin = 1u << kBinLog;          // targets per bin
 constexpr uint32_t kBinCap = kBin + kBin / 4;     // region capacity per bin
-constexpr uint32_t kChunk = 16384;                // sources per inl_bin block
+#ifndef GS_INL_CHUNK
+#define GS_INL_CHUNK 16384
+#endif
+constexpr uint32_t kChunk = GS_INL_CHUNK;         // sources per inl_bin block
 constexpr uint32_t kInlThreads = 1024;
+constexpr uint32_t kBinPer = kChunk / kInlThreads;  // sources per inl_bin thread
+static_assert(kChunk % kInlThreads == 0, "inl_bin: whole sources per thread");
 constexpr uint32_t kBinnedMaxBins = 8192;         // n <= 2^27 (per-bin LDS state is 6 B)
 constexpr uint32_t kFlagLimit = 2u;               // flags[2] bit: a device limit was hit
 
@@ -54,24 +59,52 @@ GS_DEV uint32_t target_of(const InListArgs &a, uint32_t x) {
 
 // Per-target record emission, shared by both paths.  `lst` holds y's k
 // sources ascending (LDS or global); `first` is where lst[kInline..k) are
-// (already) stored in a.src.
+// (already) stored in a.src.  Live-filtered gathers (a.lvm, binned path
+// only): bit 31 of each lst entry is the source's live bit (kLiveTag, set by
+// inl_sort), `yc` = y is complete.
+constexpr uint32_t kLiveTag = 1u << 31;
 GS_DEV void emit_target(const InListArgs &a, uint32_t y, const uint32_t *lst, uint32_t k,
-                        uint32_t first) {
+                        uint32_t first, bool yc = false) {
     InRec r;
     if (k > kMaxIn) {
         atomicOr(&a.flags[2], kFlagLimit);
         k = kMaxIn;
     }
     r.kf = (first << kFirstShift) | k;
+    // Live-filtered gathers (gs_common.h kSkipBit): the live bits of y's
+    // first pushers; y complete (yc) creates nothing to pass on
+    const bool filt = a.lvm != nullptr;
+    uint32_t lv = 0;  // live bits of the first kInline pushers
+    if (filt) {
 #pragma unroll
-    for (uint32_t i = 0; i < kInline; ++i) r.s[i] = i < k ? lst[i] : 0u;
+        for (uint32_t i = 0; i < kInline; ++i)
+            if (i < k && (lst[i] & kLiveTag)) lv |= 1u << i;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kInline; ++i) r.s[i] = i < k ? (lst[i] & kIdMask) : 0u;
+    if (filt) r.kf |= (~lv & 7u) << kInSkipShift;  // skip flags of pushers 0..2
     a.IN8[y] = r;
+#ifdef GS_EXP_NO_SIB
+    k = 0;  // timing only: no SibRec writes
+#endif
+    bool any_live = false;  // some pusher ahead of lst[j] is live
     for (uint32_t j = 1; j < k; ++j) {
+        const uint32_t prev = j - 1u;
+        any_live |= filt && (lst[prev] & kLiveTag) != 0;
+        // filtered and nothing ahead of lst[j] to pass on (no live sibling, or y
+        // complete): the round kernel would gather nothing from the record, so
+        // it is not written (a stale serial reads as rank 0, the same result)
+        const bool zneed = any_live && !yc;
+        if (filt && !zneed) continue;
         SibRec sr;
-        sr.tag = ((a.serial & kSerialMask) << 8) | j;
+        // (filtered and written: y is incomplete, so sibling i is skipped iff
+        // it is not live)
+        sr.tag = ((a.serial & kSerialMask) << 8) | j | (zneed ? kSibZNeed : 0u) |
+                 (filt ? ((~lv & 3u) << kSibSkipShift) : 0u);
 #pragma unroll
-        for (uint32_t i = 0; i < kSibInline; ++i) sr.e[i] = i < j ? lst[i] : 0u;
-        a.SIB8[lst[j]] = sr;
+        for (uint32_t i = 0; i < kSibInline; ++i) sr.e[i] = i < j ? (lst[i] & kIdMask) : 0u;
+        if (filt && !((lv >> 2) & 1u)) sr.e[2] |= kSkipBit;
+        a.SIB8[lst[j] & kIdMask] = sr;
     }
 }
 
@@ -104,7 +137,7 @@ GS_DEV uint32_t emit_tail(const InListArgs &a, const uint32_t *lst, uint32_t k, 
     const uint32_t m = tail_len<>(k);
     if (m == 0 || cur == kNone) return 0u;
     const uint32_t first = cur;
-    for (uint32_t j = 0; j < m; ++j) a.src[first + j] = lst[kInline + j];
+    for (uint32_t j = 0; j < m; ++j) a.src[first + j] = lst[kInline + j] & kIdMask;
     cur += m;
     return first;
 }
@@ -132,12 +165,33 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
     __syncthreads();
     const uint32_t lo = blockIdx.x * kChunk;
     const uint32_t hi = min(p.n, lo + kChunk);
-    for (uint32_t x = lo + threadIdx.x; x < hi; x += kInlThreads) {
-        const uint32_t t = target_of(a, x);
-        a.tg[x] = t;
-        if (!(t & kTgDead)) {
-            const uint32_t b = (t & kTgMask) >> kBinLog;
-            atomicAdd(&cnt[b >> 1], 1u << ((b & 1u) << 4));
+    // the thread's kBinPer sources lo + threadIdx.x + q * kInlThreads: targets
+    // kept in registers (kTgDead past hi) for the stage pass below
+    uint32_t tq[kBinPer];
+#pragma unroll
+    for (uint32_t q = 0; q < kBinPer; ++q) {
+        const uint32_t x = lo + threadIdx.x + q * kInlThreads;
+        tq[q] = kTgDead;
+        if (x < hi) {
+            tq[q] = target_of(a, x);
+            a.tg[x] = tq[q];
+            if (!(tq[q] & kTgDead)) {
+                const uint32_t b = (tq[q] & kTgMask) >> kBinLog;
+                atomicAdd(&cnt[b >> 1], 1u << ((b & 1u) << 4));
+            }
+        }
+    }
+    if (a.zl) {
+        // live-filtered gathers: "t(x) is live", a word per 64 sources (the
+        // map lookups, L2 hits, issued together)
+        bool lq[kBinPer];
+#pragma unroll
+        for (uint32_t q = 0; q < kBinPer; ++q) lq[q] = !(tq[q] & kTgDead) && map_test(a.lvm, tq[q] & kTgMask);
+#pragma unroll
+        for (uint32_t q = 0; q < kBinPer; ++q) {
+            const uint32_t x0 = lo + (threadIdx.x & ~63u) + q * kInlThreads;  // the wave's first source
+            const u64 b = __ballot(lq[q]);
+            if ((threadIdx.x & 63u) == 0u && x0 < hi) a.zl[x0 >> 6] = b;
         }
     }
     __syncthreads();
@@ -167,12 +221,13 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
         run += c;
     }
     __syncthreads();
-    for (uint32_t x = lo + threadIdx.x; x < hi; x += kInlThreads) {
-        const uint32_t t = a.tg[x];  // written above by this thread
-        if (t & kTgDead) continue;
+#pragma unroll
+    for (uint32_t q = 0; q < kBinPer; ++q) {
+        const uint32_t t = tq[q];
+        if (t & kTgDead) continue;  // (also every slot past hi)
         const uint32_t b = (t & kTgMask) >> kBinLog, sh16 = (b & 1u) << 4;
         const uint32_t pos = (atomicAdd(&cnt[b >> 1], 1u << sh16) >> sh16) & 0xFFFFu;
-        stage[pos] = x;
+        stage[pos] = lo + threadIdx.x + q * kInlThreads;
         stage_lt[pos] = (uint16_t)(t & (kBin - 1u));
     }
     __syncthreads();
@@ -220,6 +275,19 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
         el[q] = ok ? (uint32_t)a.region_lt[(u64)b * kBinCap + i] : kNone;
     }
     for (uint32_t i = threadIdx.x; i < kBin / 2; i += kInlThreads) h[i] = 0u;
+    // live-filtered gathers: the bin's "complete" bits (coalesced) and the
+    // live bit of every entry (L2-resident map lookups, issued together),
+    // carried as bit 31 of the sorted ids (kLiveTag)
+    __shared__ uint32_t cpl[kBin / 32];
+    const bool filt = a.lvm != nullptr;
+    uint32_t lt_tag[kSortPer];
+    if (filt) {
+        for (uint32_t i = threadIdx.x; i < kBin / 32; i += kInlThreads)
+            cpl[i] = t0 + 32u * i < p.n ? reinterpret_cast<const uint32_t *>(a.cpm)[(t0 >> 5) + i] : 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < kSortPer; ++q)
+            lt_tag[q] = (el[q] != kNone && map_test(a.lvm, ex[q])) ? kLiveTag : 0u;
+    }
     __syncthreads();
     if (threadIdx.x == 0) a.scratch[b] = 0u;  // ready for the next build of this set
 #pragma unroll
@@ -248,7 +316,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
             const uint32_t old = atomicAdd(&h[el[q] >> 1], 1u << shf);
             // DLV: the entry's index in the region (its id and code are
             // re-read from there, an L2-resident window)
-            sorted[(old >> shf) & 0xFFFFu] = ex[q];
+            sorted[(old >> shf) & 0xFFFFu] = ex[q] | (filt ? lt_tag[q] : 0u);
         }
     }
     __syncthreads();
@@ -263,16 +331,17 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
         const uint32_t s = lt ? half_of(h, lt - 1) : 0u;
         uint32_t *lst = sorted + s;
         const uint32_t k = e - s;
-        for (uint32_t q = 1; q < k; ++q) {  // Poisson(1)-sized: insertion sort
+        for (uint32_t q = 1; q < k; ++q) {  // Poisson(1)-sized: insertion sort (by id)
             const uint32_t v = lst[q];
             uint32_t r = q;
-            while (r > 0 && lst[r - 1] > v) {
+            while (r > 0 && (lst[r - 1] & kIdMask) > (v & kIdMask)) {
                 lst[r] = lst[r - 1];
                 --r;
             }
             lst[r] = v;
         }
-        emit_target(a, t0 + lt, lst, k, emit_tail(a, lst, k, cur));
+        const bool yc = filt && ((cpl[lt >> 5] >> (lt & 31u)) & 1u) != 0;
+        emit_target(a, t0 + lt, lst, k, emit_tail(a, lst, k, cur), yc);
     }
 }
 
@@ -614,7 +683,8 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort_dlv(InListArgs a) {
             pB |= nw & ~vC;
             pC |= nw & vC;
             pnot &= ~sl;
-            atomicAdd(&pcnt[sid[j] >> kCoarseLog], 1u);
+            // an empty pull batch is not passed back: PULL[] reads 0 for it
+            if (scd[j]) atomicAdd(&pcnt[sid[j] >> kCoarseLog], 1u);
         }
     }
     __syncthreads();
@@ -627,6 +697,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort_dlv(InListArgs a) {
     __syncthreads();
     const uint32_t placed = min(total, kHalfCap);
     for (uint32_t j = threadIdx.x; j < placed; j += kInlThreads) {
+        if (!scd[j]) continue;  // empty pull (pb_place zero-fills)
         const uint32_t x = sid[j], cb = x >> kCoarseLog;
         const uint32_t slot = pres[cb] + atomicAdd(&pcnt[cb], 1u);  // < 2^kCoarseLog: one per source
         const u64 o = ((u64)cb << kCoarseLog) + slot;
@@ -697,8 +768,10 @@ __global__ __launch_bounds__(kInlThreads) void pb_fine(InListArgs a) {
 }
 
 // Pull pass-back, level 3: per source bin, the pulls into an LDS image of
-// PULL[bin], written out coalesced.  A slot nobody wrote belongs to a node
-// whose pull is not delivered this round; the round kernel ignores it.
+// PULL[bin], written out coalesced.  Only non-empty pull batches are passed
+// back (while a dissemination is young most pulls are empty): a slot nobody
+// wrote is an empty pull, or one not delivered this round, which the round
+// kernel ignores.
 __global__ __launch_bounds__(kInlThreads) void pb_place(InListArgs a) {
     __shared__ uint32_t img[kBin];
     const CsrPlan &p = a.p;
@@ -706,6 +779,8 @@ __global__ __launch_bounds__(kInlThreads) void pb_place(InListArgs a) {
     const uint32_t b = blockIdx.x;
     const uint32_t cnt = min(a.scratch[p.nb + 1 + 2 * nc + b], kBin);
     const PullArrays pa = pull_arrays(a.region, p.nb);
+    for (uint32_t i = threadIdx.x; i < kBin; i += kInlThreads) img[i] = 0u;
+    __syncthreads();
     for (uint32_t i = threadIdx.x; i < cnt; i += kInlThreads) {
         const u64 o = (u64)b * kBin + i;
         img[pa.fx[o]] = pa.fv[o];
@@ -933,6 +1008,8 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
         if (e == hipSuccess)
             e = hipFuncSetAttribute(ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(p.dlv ? lds_dlv : lds_sort));
         if (e != hipSuccess) return e;
+        if (p.dlv && (a.lvm || a.zl)) return hipErrorInvalidValue;  // DLV records gather nothing
+        if ((a.lvm == nullptr) != (a.zl == nullptr) || (a.lvm && !a.cpm)) return hipErrorInvalidValue;
         InListArgs ab = a;
         ab.region_lt = reinterpret_cast<uint16_t *>(a.region + (size_t)p.nb * kBinCap);
         ab.region_code = a.region + (size_t)p.nb * kBinCap * 3 / 2;
@@ -965,6 +1042,8 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
         }
         return hipGetLastError();
     }
+    // the generic path writes no skip flags (live-filtered gathers are binned only)
+    if (a.lvm || a.zl) return hipErrorInvalidValue;
     const size_t lds_nb = (size_t)p.nb * sizeof(uint32_t);
     hipLaunchKernelGGL(csr_bin_count, dim3(p.ba), dim3(256), lds_nb, s, a);
     hipLaunchKernelGGL(csr_col_scan, dim3((p.nb + 255) / 256), dim3(256), 0, s, a);

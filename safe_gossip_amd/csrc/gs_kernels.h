@@ -73,6 +73,12 @@ struct RoundArgs {
                               // written) | lane gathers << 32, one atomic per block
     u64 *dens;                // [kDensSlots] zero words of the round-(t+1) planes
                               // (spread atomics, cleared by the engine per launch)
+    // Live-filtered gathers (gs_common.h kSkipBit; null: every row gathered):
+    // zlm = a bit per source "t(x) is live" of round t (in-list build), and
+    // the node maps of the round-(t+1) planes this launch writes (transition
+    // modes), read by the next build: lvm "live", cpm "complete".
+    const u64 *zlm;
+    u64 *lvm, *cpm;
     uint32_t dlv_pack;        // DLV transition launches: 0 one node per lane, 1 a 32-bit lane
                               // word of several nodes, 2 a 64-bit one (gs_dlv4.hip)
     Geometry g;
@@ -87,6 +93,9 @@ constexpr uint32_t kDensSlots = 16;    // density counts spread over this many w
 // Sparse-record map sizes: zb words per buffer, lb / ab bytes per buffer.
 inline u64 spr_zb_words(const Geometry &g) { return (g.nseg + 255u) / 256u * 4u + 4u; }
 inline u64 spr_node_bytes(const Geometry &g) { return ((u64)g.n + 63u) / 64u * 8u + 64u; }
+// Node bit maps of the live-filtered gathers: u64 words (+ one spare word).
+inline u64 node_map_words(uint32_t n) { return ((u64)n + 63u) / 64u + 1u; }
+__host__ __device__ inline bool map_test(const u64 *m, uint32_t i) { return ((m[i >> 6] >> (i & 63u)) & 1ull) != 0; }
 
 // mode: 0 = transition only (first round), 1 = deliver round t + transition
 // to t+1, 2 = deliver round t and write observation outputs only,
@@ -141,6 +150,11 @@ struct InListArgs {
     uint64_t seed;
     uint32_t epoch, round;
     Faults f;           // edges that are not delivered are left out of the lists
+    // Live-filtered gathers (binned path; null: no skip flags): node maps of
+    // the round's planes ("live", "complete", written by the round kernel
+    // before) and the per-source map zl = "t(x) is live" written here.
+    const u64 *lvm, *cpm;
+    u64 *zl;
 };
 // Peer choices of `round` (into tg) and their in-lists (IN8, SIB8 tagged with
 // `serial`).  Depends on nothing but the Philox stream, so it runs on its own

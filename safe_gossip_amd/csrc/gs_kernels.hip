@@ -281,6 +281,13 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     }
 
     // ---- coalesced per-node metadata (level 1)
+    // Statistics deltas of x, loaded with the other level-1 reads so the
+    // read-modify-write at the end adds no dependent memory round trip
+    // (GS_STATS_LATE: loaded after the transition, as before).
+#ifndef GS_STATS_LATE
+    uint4 stv = {0u, 0u, 0u, 0u};
+    if (TRANSITION && valid && (SMALL || L.j == 0)) stv = reinterpret_cast<const uint4 *>(a.st32)[x];
+#endif
     uint4 in = {0, 0, 0, 0};   // SHARD: {first, k|zi<<16, e0, e1}
     InRec in8 = {};            // {first << 5 | k, s0..s2}
     SibRec sb8 = {};           // {serial<<8 | rank of x in in(z), e0..e2}; stale unless rank >= 1
@@ -291,6 +298,17 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     bool seq_dep = false;  // SEQ: W(x) includes W(t(x)) (kSeqDep)
     DlvRec dr = {};     // DLV: x's record
     uint32_t dpull = 0;  // DLV: x's pull batch
+    // live-filtered gathers (2P gather path; gs_common.h kSkipBit)
+    const bool filt = !SHARD && !SEQ && !DLV && !spr && a.zlm != nullptr;
+    u64 zlw = 0;            // the zl word of x: bit x & 63 = t(x) is live
+    uint32_t qskip = 0;     // inline pushers that push nothing
+    uint32_t eskip = 0;     // inline siblings that cannot pass anything on
+    bool zneed = false;     // a live sibling ahead of x and t(x) incomplete
+    bool gq[kBatchK], ge[kBatchE], gz = true;  // filtered: rows wanted
+#pragma unroll
+    for (uint32_t i = 0; i < kBatchK; ++i) gq[i] = true;
+#pragma unroll
+    for (uint32_t i = 0; i < kBatchE; ++i) ge[i] = true;
     if (DELIVER) {
         if (DLV) {
             dr = a.DR[x];  // x = 0 on invalid lanes: a harmless valid address
@@ -312,7 +330,17 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             k = valid ? in8.k() : 0u;
             if (SEQ) sinf = a.sinfo[x];
             sb8 = a.SIB8[x];
-            r = (valid && (sb8.tag >> 8) == (a.serial & kSerialMask)) ? (sb8.tag & 0xFFu) : 0u;
+            if (filt) zlw = a.zlm[x >> 6];
+            const bool sib_ok = valid && (sb8.tag >> 8) == (a.serial & kSerialMask);
+            r = sib_ok ? (sb8.tag & kSibRankMask) : 0u;
+            if (filt) {
+                // live-filtered gathers: the skip flags (gs_common.h)
+                qskip = in8.kf >> kInSkipShift;
+                in8.kf &= kInFlagMask;
+                eskip = ((sb8.tag >> kSibSkipShift) & 3u) | ((sb8.e[2] >> 31) << 2);
+                sb8.e[2] &= kIdMask;
+                zneed = sib_ok && (sb8.tag & kSibZNeed) != 0;
+            }
             if (SEQ) {
                 seq_inl = valid && (sinf & kSeqGot) && (sinf & kSeqLevelMask) == kSeqInline;
                 seq_dep = seq_inl && (sinf & kSeqDep);
@@ -382,6 +410,28 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
 #pragma unroll
             for (uint32_t i = 0; i < kBatchE; ++i)
                 if (ge[i]) e[i] = L.load_cls(S, sb8.e[i]);
+        } else if (filt) {
+            // live-filtered: a row that cannot change any result (a pusher with
+            // nothing live, a t(x) with nothing live and no live sibling ahead
+            // of x to create from, a sibling that is not live or whose target
+            // is complete) is not gathered; its place holds the empty row
+            // (a skipped load is branched around, not redirected to an L2 hit:
+            // with most rows skipped that measured 0.1-0.2 ms faster per launch)
+#pragma unroll
+            for (uint32_t i = 0; i < kBatchK; ++i) {
+                gq[i] = i < k && !((qskip >> i) & 1u);
+                if (gq[i]) q[i] = L.load_cls(S, in8.s[i]);
+                ngath += gq[i] ? 1u : 0u;
+            }
+            gz = valid && !(tgw & kTgNoPull) && (((zlw >> (x & 63u)) & 1ull) != 0 || zneed);
+            if (gz) qz = L.load_cls(S, z);
+            ngath += gz ? 1u : 0u;
+#pragma unroll
+            for (uint32_t i = 0; i < kBatchE; ++i) {
+                ge[i] = i < r && !((eskip >> i) & 1u);
+                if (ge[i]) e[i] = L.load_cls(S, sb8.e[i]);
+                ngath += ge[i] ? 1u : 0u;
+            }
         } else {
 #pragma unroll
             for (uint32_t i = 0; i < kBatchK; ++i) q[i] = L.load_cls(S, i < k ? in8.s[i] : x);
@@ -442,6 +492,10 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         }
         wtriv = __ballot(valid && busy) == 0ull;
     }
+
+    // filtered: a skipped t(x) row stays the empty row it was initialised to;
+    // skipped pushers and siblings are not absorbed at all (an empty row
+    // changes nothing but |P|, which k counts)
 
     const u64 isC = P[0], a0 = P[1], a1 = P[2];
     const u64 A = ~isC & ~a0 & ~a1 & L.m;
@@ -588,7 +642,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             for (uint32_t i = 0; i < kBatchK; ++i) {
                 if (i < k) {
                     zin |= in8.s[i] == z;
-                    rv.push(q[i], i, k, !(pulled && in8.s[i] == z));
+                    if (!filt || gq[i]) rv.push(q[i], i, k, !(pulled && in8.s[i] == z));
                 }
             }
             for (uint32_t i = kBatchK; i < k; ++i) {  // in-degree > kBatchK (1.9% of nodes)
@@ -605,19 +659,24 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             u64 pnot = ~qz.c & ~qz.a0 & ~qz.a1 & L.m, pB = 0, pC = 0;
 #pragma unroll
             for (uint32_t i = 0; i < kBatchE; ++i)
-                if (i < r) sibling(e[i], pnot, pB, pC);
-            if (r > kBatchE && pnot && pulled) {  // rank > kBatchE (rare)
-                auto sib_row = [&](uint32_t s) -> Cls {
-                    return (!gchk || map_bit(a.lb_cur, s)) ? L.load_cls(S, s) : Cls{0, 0, 0};
+                if (i < r && (!filt || ge[i])) sibling(e[i], pnot, pB, pC);
+            // (filtered: no live sibling ahead of x, or t(x) complete -- nothing
+            // deeper can be passed on either)
+            if (r > kBatchE && pnot && pulled && (!filt || zneed)) {  // rank > kBatchE (rare)
+                auto sib_row = [&](uint32_t s, bool skip) -> Cls {
+                    if (skip || (gchk && !map_bit(a.lb_cur, s))) return Cls{0, 0, 0};
+                    ++ngath;
+                    return L.load_cls(S, s);
                 };
                 for (uint32_t i = kBatchE; i < min(r, kSibInline); ++i)
-                    sibling(sib_row(pick_sib(sb8.e, i)), pnot, pB, pC);
+                    sibling(sib_row(pick_sib(sb8.e, i), ((eskip >> i) & 1u) != 0), pnot, pB, pC);
                 if (r > kSibInline && pnot) {  // rank > 3: 0.2% of nodes
-                    const InRec zin8 = a.IN8[z];
+                    InRec zin8 = a.IN8[z];
+                    if (filt) zin8.kf &= kInFlagMask;  // (skip flags above the tail start)
                     for (uint32_t i = kSibInline; i < r && pnot; ++i) {
                         const uint32_t s = i < kInline ? pick_inline(zin8.s, i)
                                                        : a.src[zin8.first() + (i - kInline)];
-                        sibling(sib_row(s), pnot, pB, pC);
+                        sibling(sib_row(s, false), pnot, pB, pC);
                     }
                 }
             }
@@ -894,6 +953,61 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         a.pc_out[x] = (uint32_t)b0 | ((uint32_t)b1 << 16);
     }
 
+    // ---- live-filtered gathers: node maps of the round-(t+1) planes, "live"
+    // (its push row is not empty) and "complete" (no A entry), for the next
+    // in-list build; one ballot per wave (W <= 8: a wave's nodes are whole bytes)
+    if (TRANSITION && a.lvm) {
+        // live = B | C entries, A = no entry; from the transition's Bn / Cn
+        // (N[0] = C | D), or from the stored planes of a frozen offline node
+        u64 lvw, aw;
+        if (a.f.churn == 0u) {
+            lvw = Bn | Cn;
+            aw = ~(N[0] | Bn) & L.m;
+        } else {
+            lvw = ((N[0] & ~(N[1] & N[2])) | (~N[0] & (N[1] | N[2]))) & L.m;
+            aw = ~N[0] & ~N[1] & ~N[2] & L.m;
+        }
+        const u64 bl = __ballot(valid && lvw != 0);
+        const u64 bc = __ballot(valid && aw == 0);
+        const uint32_t lane = threadIdx.x & 63u;
+        const u64 seg0 = seg - lane;
+        if (lane == 0 && seg0 < g.nseg) {
+            if (SMALL) {  // a lane per node: the wave's 64 nodes are one map word
+                a.lvm[seg0 >> 6] = bl;
+                a.cpm[seg0 >> 6] = bc;
+            } else {
+                const uint32_t lw = g.logr - 6u;
+                const u64 cl = compress_stride(group_or_bits(bl, lw), lw);
+                const u64 cc = compress_stride(group_and_bits(bc, lw), lw);
+                uint8_t *ml = reinterpret_cast<uint8_t *>(a.lvm), *mc = reinterpret_cast<uint8_t *>(a.cpm);
+                const u64 byte0 = (seg0 >> lw) >> 3;  // first node of the wave / 8
+                if (lw == 0u) {
+                    *reinterpret_cast<u64 *>(ml + byte0) = cl;
+                    *reinterpret_cast<u64 *>(mc + byte0) = cc;
+                } else if (lw == 1u) {
+                    *reinterpret_cast<uint32_t *>(ml + byte0) = (uint32_t)cl;
+                    *reinterpret_cast<uint32_t *>(mc + byte0) = (uint32_t)cc;
+                } else if (lw == 2u) {
+                    *reinterpret_cast<uint16_t *>(ml + byte0) = (uint16_t)cl;
+                    *reinterpret_cast<uint16_t *>(mc + byte0) = (uint16_t)cc;
+                } else {
+                    ml[byte0] = (uint8_t)cl;
+                    mc[byte0] = (uint8_t)cc;
+                }
+            }
+        }
+#ifndef GS_EXP_NO_ACCT
+        if (MODE == 1 && a.acct && filt) {
+            // traffic accounting: plane segments read + written, lane gathers
+            uint32_t ng = 0;  // ngath < 64: six bit ballots
+#pragma unroll
+            for (uint32_t b = 0; b < 6u; ++b) ng += popc(__ballot(valid && ((ngath >> b) & 1u))) << b;
+            const u64 v = (u64)(2u * popc(__ballot(valid))) | ((u64)ng << 32);
+            if (lane == 0) atomicAdd(&a.acct[(bid * 4u + (threadIdx.x >> 6)) & (kAcctSlots - 1u)], v);
+        }
+#endif
+    }
+
     // ---- sparse records of the round-(t+1) planes: zero-word bits (one u64
     // per wave), node live / all-A bits (64/W per wave, W <= 8: whole bytes);
     // the group and packing work is on wave-uniform ballots (scalar ALU)
@@ -1004,7 +1118,11 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         // rounds is the engine's round count (every node runs every round);
         // the other four are u32 deltas folded into u64 before they can wrap.
         uint4 *st = reinterpret_cast<uint4 *>(a.st32) + x;
+#ifdef GS_STATS_LATE
         uint4 v = *st;
+#else
+        uint4 v = stv;
+#endif
         v.x += d_empty_pull;                       // empty_pull_sent
         v.y += (on_next && live_new == 0u) ? 1u : 0u;  // empty_push_sent
         v.z += live_new + d_full_sent;             // full_message_sent

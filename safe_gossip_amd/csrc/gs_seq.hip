@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256) void seq_pull_pass(SeqArgs a, uint32_t level, 
     if ((si & kSeqLevelMask) != level) return;  // the last list holds every level >= 15
     const uint32_t z = a.tg[y] & kTgMask;
     const SibRec sb = a.SIB8[y];
-    const uint32_t r = ((sb.tag >> 8) == (a.serial & kSerialMask)) ? (sb.tag & 0xFFu) : 0u;
+    const uint32_t r = ((sb.tag >> 8) == (a.serial & kSerialMask)) ? (sb.tag & kSibRankMask) : 0u;
     const bool dep = (si & kSeqDep) != 0;
     const Cls qz = L.load_cls(a.S, z);
     Cls wz = {0, 0, 0};

@@ -393,13 +393,15 @@ def test_parity_sparse_records_after_clear(engine, monkeypatch):
 
 def test_sparse_records_full_dissemination(engine, monkeypatch):
     # 2^20 nodes x 256 rumors, all injected in round 1 (the config-4 workload
-    # at 1/16 size) through 24 rounds: the sparse path (auto, then every block
-    # checking) ends bit-identical to the dense one, and the traffic counted by
-    # the kernels stays below the dense model and above the streamed floor
+    # at 1/16 size) through 24 rounds: the live-filtered gathers (the default)
+    # and the sparse path (auto, then every block checking) end bit-identical
+    # to the unfiltered dense kernel, and the traffic counted by the kernels
+    # stays below the dense model and above the streamed floor
     n, R = 1 << 20, 256
     out = {}
-    for mode in ("dense", "auto", "on"):
+    for mode, filt in (("dense", "0"), ("dense", "1"), ("auto", "1"), ("on", "1")):
         monkeypatch.setenv("SAFE_GOSSIP_AMD_SPARSE", mode)
+        monkeypatch.setenv("SAFE_GOSSIP_AMD_FILTER", filt)
         net = engine.Network(n, R, seed=SEED)
         for r in range(R):
             net.send_new(engine.origin_of(SEED, 0, r, n), r)
@@ -409,15 +411,43 @@ def test_sparse_records_full_dissemination(engine, monkeypatch):
         net.sync()
         b, launches = net.round_traffic()
         dense = net.round_kernel_bytes()
-        if mode == "dense":  # no maps: the static model
+        name = net.round_kernel_name()
+        if mode == "dense" and filt == "0":  # no maps: the static model
             assert launches == 0 and b == dense
-        else:                # sparse launches counted, dense ones at the model
+            assert "filtered" not in name
+        else:                # every deliver launch counted by the kernels
             assert launches == 23
-            assert n * 68 < b < 0.9 * dense, (b, dense)
-        out[mode] = (net.known_all(), net.statistics_all(),
-                     [net.push_batch(x) for x in range(0, n, 4099)])
+            # (the filtered count includes t(x)'s earlier pushers' rows, which
+            # the static model leaves out)
+            assert n * 68 < b < (0.9 if mode != "dense" else 1.0) * dense, (b, dense)
+            assert mode != "dense" or "live-filtered" in name
+        out[(mode, filt)] = (net.known_all(), net.statistics_all(),
+                             [net.push_batch(x) for x in range(0, n, 4099)])
         net.close()
-    for mode in ("auto", "on"):
-        np.testing.assert_array_equal(out[mode][0], out["dense"][0])
-        np.testing.assert_array_equal(out[mode][1], out["dense"][1])
-        assert out[mode][2] == out["dense"][2]
+    ref = out[("dense", "0")]
+    for key, got in out.items():
+        np.testing.assert_array_equal(got[0], ref[0])
+        np.testing.assert_array_equal(got[1], ref[1])
+        assert got[2] == ref[2], key
+
+
+@pytest.mark.parametrize("n,R,kind,faults", [
+    (101, 32, "reinject", None),                # small segments (R_pad 32)
+    (300, 64, "trickle", None),
+    (130, 256, "reinject", (0.1, 0.1, 0.2)),
+    (33, 512, "origins", None),
+    (500, 16, "origins", (0.05, 0.05, 0.05)),   # small gather path (no DLV)
+])
+def test_parity_unfiltered(engine, monkeypatch, n, R, kind, faults):
+    # every other 2P gather-path test runs the live-filtered gathers (the
+    # default); the unfiltered kernel (SAFE_GOSSIP_AMD_FILTER=0) stays exact
+    monkeypatch.setenv("SAFE_GOSSIP_AMD_FILTER", "0")
+    monkeypatch.setenv("SAFE_GOSSIP_AMD_NO_DLV", "1")
+    run_parity(engine, n, R, kind, faults=faults)
+
+
+def test_parity_filtered_larger(engine):
+    # 20k nodes x 256 rumors through a whole dissemination: live and complete
+    # maps change every round, in-list tails and deep sibling walks (rank > 3)
+    # under the skip flags, faults on; every 3rd round checked
+    run_parity(engine, 20000, 256, "origins", check_every=3, faults=(0.02, 0.05, 0.05))
