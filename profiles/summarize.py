@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--rumors", type=int, default=256)
     ap.add_argument("--dominant", default=DOMINANT, help="substring of the dominant kernel's name")
     ap.add_argument("--no-latest", action="store_true", help="do not update profiles/pmc_latest.json")
+    ap.add_argument("--skip-first", type=int, default=2,
+                    help="dominant-kernel launches before the timed window (the bench's warmup "
+                         "rounds that deliver: warmup 3 -> 2), left out of the PMC means")
     a = ap.parse_args()
     out = os.path.join(HERE, a.tag)
     os.makedirs(out, exist_ok=True)
@@ -45,9 +48,11 @@ def main():
         if not os.path.exists(path):
             continue
         vals = collections.defaultdict(list)
-        for x in csv.DictReader(open(path)):
+        for x in sorted(csv.DictReader(open(path)), key=lambda r: int(r["Dispatch_Id"])):
             vals[x["Kernel_Name"]].append(float(x["Counter_Value"]))
         for k, v in vals.items():
+            if a.dominant in k and len(v) > a.skip_first:
+                v = v[a.skip_first:]  # the timed window's launches, as bench.py averages them
             pmc[k][counter + "_KiB_mean"] = sum(v) / len(v)
     dom = next((k for k in pmc if a.dominant in k), None)
     summary = dict(kernels=kernels, pmc=pmc)

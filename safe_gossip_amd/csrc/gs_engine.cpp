@@ -56,6 +56,7 @@ struct gs_engine {
     // path with binned in-lists (W <= 8); SAFE_GOSSIP_AMD_FILTER=0 disables.
     bool filt = false;
     u64 *lvm = nullptr, *cpm = nullptr;
+    u64 *rows_dev = nullptr;     // [2] per in-list set: node class rows its flags leave to gather
     uint32_t filt_launches = 0;  // MODE-1 launches counted in acct since set_timing(1)
     bool dlv = false;  // delivery-record path (2P, R_pad <= 16, binned in-lists)
     // its transition launches with several nodes per lane (gs_dlv4.hip):
@@ -211,7 +212,7 @@ void release(gs_engine *e) {
     for (int i = 0; i < 2; ++i)
         if (e->ev_dens[i]) (void)hipEventDestroy(e->ev_dens[i]);
     if (e->dens_host) (void)hipHostFree(e->dens_host);
-    void *bufs[] = {e->lvm, e->cpm, e->zb[0], e->zb[1], e->lb[0], e->lb[1], e->ab[0], e->ab[1], e->acct, e->dens, e->pc, e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
+    void *bufs[] = {e->lvm, e->cpm, e->rows_dev, e->zb[0], e->zb[1], e->lb[0], e->lb[1], e->ab[0], e->ab[1], e->acct, e->dens, e->pc, e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
                     e->partials, e->obs_state, e->obs_rec, e->obs_psize, e->obs_pend, e->ext_dev,
                     e->node_state};
     for (void *b : bufs)
@@ -725,6 +726,7 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
     if (ok && e->filt)
         ok = dalloc(&e->lvm, gs::node_map_words(n)) == hipSuccess &&
              dalloc(&e->cpm, gs::node_map_words(n)) == hipSuccess &&
+             dalloc(&e->rows_dev, 2) == hipSuccess &&
              dalloc(&e->acct, gs::kAcctSlots) == hipSuccess &&
              hipMemset(e->acct, 0, gs::kAcctSlots * sizeof(u64)) == hipSuccess;
     for (int i = 0; i < 2 && ok && e->spr; ++i)
@@ -966,6 +968,7 @@ gs_status round_begin(gs_engine *e) {
     }
     if (e->filt && e->deliver_pending && e->timing) {  // rows gathered, for gs_round_traffic
         a.acct = e->acct;
+        a.rows_cnt = e->rows_dev + (R0 & 1u);  // counted by the build of round t's lists
         e->filt_launches++;
     }
     const uint32_t rs = R0 & 1u;  // set holding round t = e->round
@@ -1084,6 +1087,8 @@ gs_status round_end(gs_engine *e, gs_round_report *report) {
             la.lvm = e->lvm;
             la.cpm = e->cpm;
             la.zl = c.zl;
+            la.rows = e->rows_dev + ns;
+            GS_HIP(hipMemsetAsync(la.rows, 0, sizeof(u64), bs));
         }
         if (e->dlv) {  // records carry the push codes of the new round's planes
             la.dlv = 1;
@@ -1563,9 +1568,9 @@ gs_status gs_round_traffic(gs_engine *e, double *bytes_per_launch, uint32_t *lau
     const double dense = gs_round_kernel_bytes(e);
     if (e->filt) {
         // Live-filtered launches: per node the 68 B of gs_round_kernel_bytes
-        // plus its zl bit and the two map bits written; per plane segment moved
-        // 8 planes of it (64 B per 64-rumor word, R_pad B for a small
-        // segment); per class row gathered 3 planes of it (24 B / 3 R_pad/8 B).
+        // plus its zl bit and the two map bits written, and its planes read
+        // and written (2 R_pad B); per node class row the build left to gather
+        // (pushers, t(x), t(x)'s earlier pushers) 3 planes of R_pad bits.
         gs_status st = set_device(e);
         if (st != GS_OK) return st;
         *launches = e->filt_launches;
@@ -1576,15 +1581,8 @@ gs_status gs_round_traffic(gs_engine *e, double *bytes_per_launch, uint32_t *lau
         std::vector<u64> v(gs::kAcctSlots);
         GS_HIP(hipStreamSynchronize(e->stream));
         GS_HIP(hipMemcpy(v.data(), e->acct, v.size() * sizeof(u64), hipMemcpyDeviceToHost));
-        double segs = 0, rows = 0;
-        for (u64 w : v) {
-            segs += (double)(w & 0xFFFFFFFFull);
-            rows += (double)(w >> 32);
-        }
-        const double n = e->g.n, rp = e->g.rpad;
-        const double seg_b = e->g.small ? rp : 64.0, row_b = e->g.small ? 3.0 * rp / 8.0 : 24.0;
-        *bytes_per_launch = (e->filt_launches * n * (68.0 + 3.0 / 8.0) + seg_b * segs + row_b * rows) /
-                            e->filt_launches;
+        const double rows = (double)v[0], n = e->g.n, rp = e->g.rpad;
+        *bytes_per_launch = n * (68.0 + 3.0 / 8.0 + 2.0 * rp) + 3.0 * rp / 8.0 * rows / e->filt_launches;
         return GS_OK;
     }
     if (!e->spr) {

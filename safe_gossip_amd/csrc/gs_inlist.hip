@@ -61,10 +61,13 @@ GS_DEV uint32_t target_of(const InListArgs &a, uint32_t x) {
 // sources ascending (LDS or global); `first` is where lst[kInline..k) are
 // (already) stored in a.src.  Live-filtered gathers (a.lvm, binned path
 // only): bit 31 of each lst entry is the source's live bit (kLiveTag, set by
-// inl_sort), `yc` = y is complete.
+// inl_sort), `yc` = y is complete, `yl` = y is live.  Returns the node class
+// rows the records leave the round kernel to gather for y's pushers and their
+// pull rows (pushers' rows, siblings' rows, t(x) rows the siblings force;
+// traffic accounting, 0 unfiltered).
 constexpr uint32_t kLiveTag = 1u << 31;
-GS_DEV void emit_target(const InListArgs &a, uint32_t y, const uint32_t *lst, uint32_t k,
-                        uint32_t first, bool yc = false) {
+GS_DEV uint32_t emit_target(const InListArgs &a, uint32_t y, const uint32_t *lst, uint32_t k,
+                            uint32_t first, bool yc = false, bool yl = true) {
     InRec r;
     if (k > kMaxIn) {
         atomicOr(&a.flags[2], kFlagLimit);
@@ -84,6 +87,7 @@ GS_DEV void emit_target(const InListArgs &a, uint32_t y, const uint32_t *lst, ui
     for (uint32_t i = 0; i < kInline; ++i) r.s[i] = i < k ? (lst[i] & kIdMask) : 0u;
     if (filt) r.kf |= (~lv & 7u) << kInSkipShift;  // skip flags of pushers 0..2
     a.IN8[y] = r;
+    uint32_t rows = filt ? (uint32_t)__popc(lv) + (k > kInline ? k - kInline : 0u) : 0u;
 #ifdef GS_EXP_NO_SIB
     k = 0;  // timing only: no SibRec writes
 #endif
@@ -96,6 +100,9 @@ GS_DEV void emit_target(const InListArgs &a, uint32_t y, const uint32_t *lst, ui
         // it is not written (a stale serial reads as rank 0, the same result)
         const bool zneed = any_live && !yc;
         if (filt && !zneed) continue;
+        if (filt)  // live siblings among the first kSibInline, the deeper ones, t(x) if forced
+            rows += (uint32_t)__popc(lv & ((1u << min(j, kSibInline)) - 1u)) +
+                    (j > kSibInline ? j - kSibInline : 0u) + (yl ? 0u : 1u);
         SibRec sr;
         // (filtered and written: y is incomplete, so sibling i is skipped iff
         // it is not live)
@@ -106,6 +113,7 @@ GS_DEV void emit_target(const InListArgs &a, uint32_t y, const uint32_t *lst, ui
         if (filt && !((lv >> 2) & 1u)) sr.e[2] |= kSkipBit;
         a.SIB8[lst[j] & kIdMask] = sr;
     }
+    return rows;
 }
 
 // Pushers i >= kInline of a target go to the shared tail array.  A block
@@ -160,7 +168,9 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
     uint16_t *off = reinterpret_cast<uint16_t *>(cnt + (p.nb + 1) / 2);  // [nb] chunk-local bin starts
     uint16_t *res = off + p.nb;                // [nb] reserved start in the bin's region
     __shared__ uint32_t lds_scan[kInlThreads / 64];
+    __shared__ uint32_t zrows;  // filtered: t(x) rows the zl bits leave to gather
     if (blockIdx.x == 0 && threadIdx.x == 0) a.scratch[p.nb] = 0u;  // tail count; inl_sort runs after
+    if (threadIdx.x == 0) zrows = 0u;
     for (uint32_t i = threadIdx.x; i < (p.nb + 1) / 2; i += kInlThreads) cnt[i] = 0u;
     __syncthreads();
     const uint32_t lo = blockIdx.x * kChunk;
@@ -187,14 +197,18 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
         bool lq[kBinPer];
 #pragma unroll
         for (uint32_t q = 0; q < kBinPer; ++q) lq[q] = !(tq[q] & kTgDead) && map_test(a.lvm, tq[q] & kTgMask);
+        uint32_t zr = 0;  // (wave-uniform)
 #pragma unroll
         for (uint32_t q = 0; q < kBinPer; ++q) {
             const uint32_t x0 = lo + (threadIdx.x & ~63u) + q * kInlThreads;  // the wave's first source
             const u64 b = __ballot(lq[q]);
             if ((threadIdx.x & 63u) == 0u && x0 < hi) a.zl[x0 >> 6] = b;
+            if (a.rows) zr += (uint32_t)__popcll(__ballot(lq[q] && !(tq[q] & kTgNoPull)));
         }
+        if (a.rows && (threadIdx.x & 63u) == 0u && zr) atomicAdd(&zrows, zr);
     }
     __syncthreads();
+    if (a.rows && threadIdx.x == 0 && zrows) atomicAdd(a.rows, (u64)zrows);
     // exclusive scan of the bin counts: thread i owns bins [i*per, i*per + per)
     const uint32_t per = (p.nb + kInlThreads - 1) / kInlThreads;
     const uint32_t b0 = threadIdx.x * per;
@@ -278,12 +292,15 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
     // live-filtered gathers: the bin's "complete" bits (coalesced) and the
     // live bit of every entry (L2-resident map lookups, issued together),
     // carried as bit 31 of the sorted ids (kLiveTag)
-    __shared__ uint32_t cpl[kBin / 32];
+    __shared__ uint32_t cpl[kBin / 32], lvl[kBin / 32];
     const bool filt = a.lvm != nullptr;
     uint32_t lt_tag[kSortPer];
     if (filt) {
-        for (uint32_t i = threadIdx.x; i < kBin / 32; i += kInlThreads)
-            cpl[i] = t0 + 32u * i < p.n ? reinterpret_cast<const uint32_t *>(a.cpm)[(t0 >> 5) + i] : 0u;
+        for (uint32_t i = threadIdx.x; i < kBin / 32; i += kInlThreads) {
+            const bool in = t0 + 32u * i < p.n;
+            cpl[i] = in ? reinterpret_cast<const uint32_t *>(a.cpm)[(t0 >> 5) + i] : 0u;
+            lvl[i] = in ? reinterpret_cast<const uint32_t *>(a.lvm)[(t0 >> 5) + i] : 0u;
+        }
 #pragma unroll
         for (uint32_t q = 0; q < kSortPer; ++q)
             lt_tag[q] = (el[q] != kNone && map_test(a.lvm, ex[q])) ? kLiveTag : 0u;
@@ -326,6 +343,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
     for (uint32_t lt = threadIdx.x; lt < nodes; lt += kInlThreads)
         mine += tail_len<>(half_of(h, lt) - (lt ? half_of(h, lt - 1) : 0u));
     uint32_t cur = reserve_tails<kInlThreads>(a, mine, &a.scratch[p.nb], lds_scan);
+    uint32_t rows = 0;  // filtered: class rows left to gather (traffic accounting)
     for (uint32_t lt = threadIdx.x; lt < nodes; lt += kInlThreads) {
         const uint32_t e = half_of(h, lt);
         const uint32_t s = lt ? half_of(h, lt - 1) : 0u;
@@ -341,7 +359,13 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
             lst[r] = v;
         }
         const bool yc = filt && ((cpl[lt >> 5] >> (lt & 31u)) & 1u) != 0;
-        emit_target(a, t0 + lt, lst, k, emit_tail(a, lst, k, cur), yc);
+        const bool yl = filt && ((lvl[lt >> 5] >> (lt & 31u)) & 1u) != 0;
+        rows += emit_target(a, t0 + lt, lst, k, emit_tail(a, lst, k, cur), yc, yl);
+    }
+    if (a.rows) {
+        uint32_t total;
+        (void)block_exclusive_scan_t<kInlThreads>(rows, lds_scan, total);
+        if (threadIdx.x == 0 && total) atomicAdd(a.rows, (u64)total);
     }
 }
 

@@ -79,6 +79,8 @@ struct RoundArgs {
     // modes), read by the next build: lvm "live", cpm "complete".
     const u64 *zlm;
     u64 *lvm, *cpm;
+    const u64 *rows_cnt;      // filtered, timed launches: node class rows the round's
+                              // build flagged for gathering (added to acct[0] once)
     uint32_t dlv_pack;        // DLV transition launches: 0 one node per lane, 1 a 32-bit lane
                               // word of several nodes, 2 a 64-bit one (gs_dlv4.hip)
     Geometry g;
@@ -155,6 +157,7 @@ struct InListArgs {
     // before) and the per-source map zl = "t(x) is live" written here.
     const u64 *lvm, *cpm;
     u64 *zl;
+    u64 *rows;          // + node class rows the flags leave to gather (zeroed by the caller)
 };
 // Peer choices of `round` (into tg) and their in-lists (IN8, SIB8 tagged with
 // `serial`).  Depends on nothing but the Philox stream, so it runs on its own

@@ -492,7 +492,6 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         }
         wtriv = __ballot(valid && busy) == 0ull;
     }
-
     // filtered: a skipped t(x) row stays the empty row it was initialised to;
     // skipped pushers and siblings are not absorbed at all (an empty row
     // changes nothing but |P|, which k counts)
@@ -996,16 +995,9 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                 }
             }
         }
-#ifndef GS_EXP_NO_ACCT
-        if (MODE == 1 && a.acct && filt) {
-            // traffic accounting: plane segments read + written, lane gathers
-            uint32_t ng = 0;  // ngath < 64: six bit ballots
-#pragma unroll
-            for (uint32_t b = 0; b < 6u; ++b) ng += popc(__ballot(valid && ((ngath >> b) & 1u))) << b;
-            const u64 v = (u64)(2u * popc(__ballot(valid))) | ((u64)ng << 32);
-            if (lane == 0) atomicAdd(&a.acct[(bid * 4u + (threadIdx.x >> 6)) & (kAcctSlots - 1u)], v);
-        }
-#endif
+        // traffic accounting of timed launches: the class rows this round's
+        // build left to gather (counted there, off the kernel's path)
+        if (MODE == 1 && a.acct && a.rows_cnt && bid == 0 && threadIdx.x == 0) atomicAdd(a.acct, *a.rows_cnt);
     }
 
     // ---- sparse records of the round-(t+1) planes: zero-word bits (one u64
