@@ -22,11 +22,15 @@ cfg4, the configuration the metric is quoted on that fits one GPU.
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N, or plain
 `python bench.py --gpus N`, which starts that launcher itself): ONE network
-of the same n x R sharded by node range over the N ranks (safe_gossip_amd.sharded,
-DESIGN.md section 7): every round exchanges push rows and pull rows with RCCL
-all_to_all_single over xGMI on the engine's stream.  Total work is fixed, so
-"scaling" is "strong".  Barrier + synchronize around the timed region, time =
-max over ranks.  The roofline line describes rank 0's round kernel.
+of the same n x R over the N ranks.  Default --mode slices: every rank holds
+all n nodes and R/N of the rumors (safe_gossip_amd.sliced, DESIGN.md section
+7b); rumors evolve independently, so a round's only exchange is one RCCL
+all_reduce(MIN) of 2 bytes per node (the empty-RPC Statistics), overlapped
+with the next round.  --mode nodes: the node range sharded over the ranks
+(safe_gossip_amd.sharded), push and pull rows exchanged
+with RCCL all_to_all_single every round.  Total work is fixed, so "scaling"
+is "strong".  Barrier + synchronize around the timed region, time = max over
+ranks.  The roofline line describes rank 0's round kernel.
 """
 import argparse
 import json
@@ -71,6 +75,8 @@ def parse():
     p.add_argument("--parts", type=int, default=None,
                    help="pipeline parts per rank (N>1; default 4 with RCCL: the exchanges of one "
                         "part overlap the round kernel of another)")
+    p.add_argument("--mode", default="slices", choices=["slices", "nodes"],
+                   help="N>1 (or --sharded): rumor slices per rank (default) or node-range shards")
     p.add_argument("--sharded", action="store_true",
                    help="run the sharded engine even at N=1 (one RCCL rank: exchanges are "
                         "self-copies; measures the sharded path's overhead and overlap)")
@@ -91,7 +97,7 @@ def inject_all(net, epoch):
     import safe_gossip_amd as sg
     for r in range(net.R):
         x = sg.origin_of(net.seed, epoch, r, net.n)
-        if getattr(net, "transport", None) == "dist":
+        if getattr(net, "transport", None) == "dist" and hasattr(net, "shards"):
             s = net.shards[0]
             if not s.lo <= x < s.lo + s.m:
                 continue
@@ -224,7 +230,10 @@ def main():
     fk = dict(churn=args.faults[0], drop_push=args.faults[1], drop_pull=args.faults[2])
     if args.schedule != "2P":
         fk["schedule"] = args.schedule
-    if dist is not None:
+    if dist is not None and args.mode == "slices":
+        from safe_gossip_amd.sliced import SlicedNetwork
+        net = SlicedNetwork(n, R, world, seed=args.seed, epoch=0, device=local, transport="dist", **fk)
+    elif dist is not None:
         from safe_gossip_amd.sharded import ShardedNetwork
         net = ShardedNetwork(n, R, world, seed=args.seed, epoch=0, device=local,
                              transport="dist", parts=args.parts, **fk)
@@ -318,9 +327,15 @@ def main():
                 "faults": {"churn": args.faults[0], "drop_push": args.faults[1],
                            "drop_pull": args.faults[2]},
                 "params": list(net.params),
-                "parallelism": (f"node-range shards x{dist.get_world_size()}, "
-                                + ("RCCL" if args.dist_backend == "nccl" else args.dist_backend)
-                                + f" all-to-all push/pull rows, {net.parts} pipeline part(s) per rank")
+                "parallelism": ((f"rumor slices x{dist.get_world_size()} (all {n} nodes, "
+                                 f"{R // world}-{-(-R // world)} rumors per rank), "
+                                 + ("RCCL" if args.dist_backend == "nccl" else args.dist_backend)
+                                 + " all_reduce(MIN) of 2 B/node empty-RPC counts per round, "
+                                   "overlapped with the next round")
+                                if args.mode == "slices" else
+                                (f"node-range shards x{dist.get_world_size()}, "
+                                 + ("RCCL" if args.dist_backend == "nccl" else args.dist_backend)
+                                 + f" all-to-all push/pull rows, {net.parts} pipeline part(s) per rank"))
                                if dist is not None else "single-gpu",
             },
             "roofline": {

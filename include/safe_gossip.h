@@ -82,7 +82,10 @@ typedef struct {
                                 every RPC to or from it dropped, state kept  */
     uint32_t drop_push;      /* push batch not delivered (so never answered) */
     uint32_t drop_pull;      /* pull batch not delivered                     */
-    uint32_t reserved1[4];
+    /* Nonzero: this engine holds one rumor slice of a rumor-sliced network
+     * (gs_slice_*; 2P only, no external RPCs).                               */
+    uint32_t rumor_slice;
+    uint32_t reserved1[3];
 } gs_config;
 
 /* src/gossip.rs:209-221, same field order. */
@@ -214,6 +217,35 @@ gs_status   gs_shard_round_part(gs_engine *e, uint32_t part);
 gs_status   gs_shard_pull(gs_engine *e);
 /* The engine's HIP stream (hipStream_t), to order collectives on it. */
 uint64_t    gs_stream(const gs_engine *e);
+
+/* ---- Rumor-sliced network (multi-GPU): rank g holds
+ * ALL n nodes and the rumors [lo_g, lo_g + R_g) as a plain engine of R_g
+ * rumor slots created with cfg.rumor_slice = 1 (same seed, epoch and
+ * parameters on every rank).  Rumors evolve independently: a MessageState
+ * sees only copies of its own rumor (src/message_state.rs:73-84), and
+ * peers_in_this_round counts RPCs (src/gossip.rs:125), which every node sends
+ * whether its batch is empty or not (src/gossip.rs:105-111) -- so the slices
+ * exchange no state.  Only the EMPTY-RPC Statistics depend on every slice: a
+ * push is empty iff it is empty in every slice, and x's empty pulls are its
+ * answered pushers up to its first creating one, a count that is monotone in
+ * the slice's first creation, so the network's count is the MIN over the
+ * slices of each slice's count.  The round kernel of round t writes them
+ * (empty pulls per node, then empty pushes per node: 2n bytes) into buffer
+ * t & 1 instead of its Statistics; the caller all-reduces the buffer with MIN
+ * over the slices and hands it back with gs_slice_apply, in round order,
+ * before the buffer is written again (round t+2) and before any observer.
+ * Observers report the slice's rumors, and Statistics with this slice's
+ * full_message_sent / full_message_received (the network's are the SUM over
+ * slices) and empty_pull_sent WITHOUT the pending round's empty pulls, which
+ * the observer call leaves in `obs` (n bytes; the caller adds their MIN
+ * over the slices). */
+/* Device buffers (caller-owned, bound before the first round / observer):
+ * buf0, buf1 for rounds t with t & 1 == 0 / 1 (2n bytes each), obs for the
+ * observers (n bytes). */
+gs_status   gs_slice_bind(gs_engine *e, void *buf0, void *buf1, void *obs);
+/* Add buffer `which` (0 / 1, already reduced with MIN over the slices) to the
+ * Statistics, on the engine stream (gs_stream). */
+gs_status   gs_slice_apply(gs_engine *e, uint32_t which);
 
 /* ---- Wire format (src/messages.rs) ----------------------------------------
  * GossipRpc as maidsafe_utilities::serialisation (bincode, fixed-width little

@@ -65,7 +65,7 @@ class _Config(ctypes.Structure):
         ("max_rounds", ctypes.c_uint8), ("schedule", ctypes.c_uint8),
         ("device", ctypes.c_int32), ("churn", ctypes.c_uint32),
         ("drop_push", ctypes.c_uint32), ("drop_pull", ctypes.c_uint32),
-        ("reserved1", ctypes.c_uint32 * 4),
+        ("rumor_slice", ctypes.c_uint32), ("reserved1", ctypes.c_uint32 * 3),
     ]
 
 
@@ -144,6 +144,9 @@ SYMBOLS = {
     "gs_shard_bind": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P]),
     "gs_shard_pull": (ctypes.c_int, [_P]),
     "gs_stream": (ctypes.c_uint64, [_P]),
+    # rumor-sliced engines (safe_gossip_amd.sliced)
+    "gs_slice_bind": (ctypes.c_int, [_P, _P, _P, _P]),
+    "gs_slice_apply": (ctypes.c_int, [_P, ctypes.c_uint32]),
 }
 
 _LIB = None
@@ -351,9 +354,10 @@ class Network:
 
     def __init__(self, n_nodes: int, n_rumors: int, seed: int = 0x5AFE6055, epoch: int = 0,
                  params=None, device: int = 0, churn: float = 0.0, drop_push: float = 0.0,
-                 drop_pull: float = 0.0, schedule: str = "2P"):
+                 drop_pull: float = 0.0, schedule: str = "2P", _rumor_slice: bool = False):
         self._lib = load_library()
         cfg = _Config()
+        cfg.rumor_slice = 1 if _rumor_slice else 0  # safe_gossip_amd.sliced
         if schedule not in SCHEDULES:
             raise ValueError(f"schedule {schedule!r} not in {sorted(SCHEDULES)}")
         cfg.schedule = SCHEDULES[schedule]

@@ -97,6 +97,12 @@ struct gs_engine {
     // set t % 2 (gs_shard.hip).
     bool shard = false;
     uint32_t n_global = 0;
+    // Rumor slice (cfg.rumor_slice): this engine holds a slice of the rumors
+    // of all n nodes; the round kernel writes this slice's empty-RPC counts to
+    // eb[0..1] (2n bytes, by round parity) and eb[2] (n bytes, observations),
+    // caller-owned (gs_slice_bind), reduced with MIN over the slices.
+    bool slice = false;
+    uint8_t *eb[3] = {nullptr, nullptr, nullptr};
     gs::ShardPlan sp{};
     gs::ShardPlanLayout spl{};
     gs::ShardEdgeLayout sel{};
@@ -458,6 +464,7 @@ gs_status seq_prepare(gs_engine *e) {
 // Fill the observation buffers with the state after the last delivery.
 gs_status observe(gs_engine *e, bool dumps) {
     if (e->obs_valid && !dumps) return GS_OK;
+    if (e->slice && !e->eb[2]) return GS_ERR_INVALID_ARGUMENT;  // gs_slice_bind first
     gs_status st = ensure_obs(e, dumps);
     if (st == GS_OK && e->deliver_pending) st = upload_ext(e);
     if (st != GS_OK) return st;
@@ -469,6 +476,7 @@ gs_status observe(gs_engine *e, bool dumps) {
         a.obs_state = e->obs_state;
         a.obs_rec = e->obs_rec;
     }
+    if (e->slice) a.emin = e->eb[2];  // pending empty pulls of this slice
     if (e->deliver_pending) {
         if (e->shard) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_edges[e->round % 2], 0));
         else GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
@@ -585,9 +593,13 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         return GS_ERR_UNSUPPORTED;
     if (cfg->schedule > GS_SCHED_SEQ) return GS_ERR_INVALID_ARGUMENT;
     if (world && cfg->schedule == GS_SCHED_SEQ) return GS_ERR_UNSUPPORTED;  // chains cross ranks
+    // rumor slices: the 2P single-engine path (SEQ's empty pulls are not a MIN
+    // over slices of a per-slice count, and node shards slice nodes instead)
+    if (cfg->rumor_slice && (world || cfg->schedule == GS_SCHED_SEQ)) return GS_ERR_UNSUPPORTED;
 
     gs_engine *e = new gs_engine();
     e->shard = world != 0;
+    e->slice = cfg->rumor_slice != 0;
     e->n_global = nglob;
     e->sp = sp;
     e->seed = cfg->seed;
@@ -633,7 +645,8 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         // build.  SAFE_GOSSIP_AMD_NO_DLV=1 forces gathers.
         const char *v = std::getenv("SAFE_GOSSIP_AMD_NO_DLV");
         const bool off = v && *v && *v != '0';
-        e->dlv = !off && !e->seq && !e->shard && g.small && g.rpad <= 16 && gs::dlv_plan(n).binned;
+        // (not in a rumor slice: its kernels count empty RPCs in place)
+        e->dlv = !off && !e->seq && !e->shard && !e->slice && g.small && g.rpad <= 16 && gs::dlv_plan(n).binned;
     }
     {
         const char *v = std::getenv("SAFE_GOSSIP_AMD_DLV_PACK");
@@ -938,6 +951,7 @@ gs_status round_begin(gs_engine *e) {
     a.inj_mask = e->inj_mask;
     a.n_inj = n_inj;
     const uint32_t R0 = e->round;
+    if (e->slice) a.emin = e->eb[(R0 + 1u) & 1u];  // round R0+1's buffer
     if (e->spr_active && !e->spr_always && R0 >= 2) {
         // density of round R0-1's planes (written by the launch of two calls
         // ago): switch to the dense variant once under a quarter are zero words
@@ -1116,6 +1130,7 @@ gs_status round_end(gs_engine *e, gs_round_report *report) {
 gs_status round_checks(gs_engine *e) {
     if ((e->shard ? e->n_global : e->g.n) < 2) return GS_ERR_NO_PEERS;  // src/gossiper.rs:71-74
     if (e->shard && !e->sendB) return GS_ERR_INVALID_ARGUMENT;  // gs_shard_bind first
+    if (e->slice && !e->eb[0]) return GS_ERR_INVALID_ARGUMENT;  // gs_slice_bind first
     // a shard delivers round t only after its exchanges (gs_shard_pull)
     if (e->shard && e->round > 0 && e->pulled_round != e->round) return GS_ERR_INVALID_ARGUMENT;
     return set_device(e);
@@ -1147,6 +1162,24 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
     e->parts_done = 0;
     if (st != GS_OK) return st;
     return round_end(e, report);
+}
+
+gs_status gs_slice_bind(gs_engine *e, void *buf0, void *buf1, void *obs) {
+    if (!e || !e->slice || !buf0 || !buf1 || !obs) return GS_ERR_INVALID_ARGUMENT;
+    e->eb[0] = static_cast<uint8_t *>(buf0);
+    e->eb[1] = static_cast<uint8_t *>(buf1);
+    e->eb[2] = static_cast<uint8_t *>(obs);
+    return GS_OK;
+}
+
+gs_status gs_slice_apply(gs_engine *e, uint32_t which) {
+    if (!e || !e->slice || which > 1) return GS_ERR_INVALID_ARGUMENT;
+    gs_status st = set_device(e);
+    if (st != GS_OK) return st;
+    if (!e->eb[which]) return GS_ERR_INVALID_ARGUMENT;
+    GS_HIP(gs::launch_slice_apply(e->st32, e->eb[which], e->g.n, e->stream));
+    e->obs_valid = false;
+    return GS_OK;
 }
 
 gs_status gs_statistics_all(gs_engine *e, uint64_t *out) {
@@ -1471,7 +1504,7 @@ gs_status gs_handle_received(gs_engine *e, uint32_t node, uint32_t peer, const u
     if (!e || !msg || !out_len || !out_count || node >= e->g.n) return GS_ERR_INVALID_ARGUMENT;
     *out_len = 0;
     *out_count = 0;
-    if (e->shard || e->seq) return GS_ERR_UNSUPPORTED;
+    if (e->shard || e->seq || e->slice) return GS_ERR_UNSUPPORTED;
     if (peer < e->g.n) return GS_ERR_INVALID_ARGUMENT;  // peers outside the simulated network
     if (e->round == 0 || !e->deliver_pending) return GS_ERR_INVALID_ARGUMENT;  // after a next_round
     int pull = 0;

@@ -81,6 +81,14 @@ struct RoundArgs {
     u64 *lvm, *cpm;
     const u64 *rows_cnt;      // filtered, timed launches: node class rows the round's
                               // build flagged for gathering (added to acct[0] once)
+    // Rumor-sliced network (gs_slice_*): this engine holds one slice of the
+    // rumors of every node, so a node's RPC is empty only when it is empty in
+    // every slice.  The kernels then leave empty_pull / empty_push out of st32
+    // and write this slice's per-node counts instead, emin[x] (empty pulls x
+    // sent) and emin[n + x] (1: x's push is empty); the caller reduces them
+    // with MIN over the slices and adds them back (launch_slice_apply).
+    // Observation launches write their pending empty pulls to emin[x].
+    uint8_t *emin;
     uint32_t dlv_pack;        // DLV transition launches: 0 one node per lane, 1 a 32-bit lane
                               // word of several nodes, 2 a 64-bit one (gs_dlv4.hip)
     Geometry g;
@@ -164,6 +172,8 @@ struct InListArgs {
 // stream concurrently with the round kernel of the round before.
 hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s);
 hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, hipStream_t s);
+// Rumor slices: st32 empty_pull / empty_push += emin[x] / emin[n + x].
+hipError_t launch_slice_apply(uint32_t *st32, const uint8_t *emin, uint32_t n, hipStream_t s);
 
 // ---------------------------------------------------------------- SEQ
 // The literal harness order (gs_seq.hip): per round, seq_levels classifies

@@ -800,7 +800,8 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                 const u64 *b64 = a.st64 + (u64)x * 4;
                 u64 *o = a.obs_stats + (u64)x * 5;
                 o[0] = a.obs_rounds - (a.offc ? a.offc[x] : 0u);  // next_round calls
-                o[1] = b64[0] + d32.x + d_empty_pull;
+                if (a.emin) a.emin[x] = (uint8_t)min(d_empty_pull, 255u);  // slice: reduced by the caller
+                o[1] = b64[0] + d32.x + (a.emin ? 0u : d_empty_pull);
                 o[2] = b64[1] + d32.y;
                 o[3] = b64[2] + d32.z + d_full_sent;
                 o[4] = b64[3] + d32.w + d_recv;
@@ -1115,8 +1116,14 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
 #else
         uint4 v = stv;
 #endif
-        v.x += d_empty_pull;                       // empty_pull_sent
-        v.y += (on_next && live_new == 0u) ? 1u : 0u;  // empty_push_sent
+        const uint32_t d_empty_push = (on_next && live_new == 0u) ? 1u : 0u;
+        if (a.emin) {  // rumor slice: empty only if empty in every slice (MIN, caller)
+            a.emin[x] = (uint8_t)min(d_empty_pull, 255u);
+            a.emin[(u64)g.n + x] = (uint8_t)d_empty_push;
+        } else {
+            v.x += d_empty_pull;                   // empty_pull_sent
+            v.y += d_empty_push;                   // empty_push_sent
+        }
         v.z += live_new + d_full_sent;             // full_message_sent
         v.w += d_recv;                             // full_message_received
         *st = v;
@@ -1161,6 +1168,24 @@ hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s) {
         return launch_mode<true, false, false, true>(a, mode, s);
     }
     return a.g.small ? launch_mode<true, false, false>(a, mode, s) : launch_mode<false, false, false>(a, mode, s);
+}
+
+// Rumor slices: add a round's empty-RPC counts, reduced with MIN over the
+// slices by the caller (gs_slice_apply), to the u32 Statistics deltas.
+__global__ __launch_bounds__(256) void slice_apply(uint32_t *st32, const uint8_t *__restrict__ emin, uint32_t n) {
+    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= n) return;
+    uint2 *p = reinterpret_cast<uint2 *>(st32 + 4u * (u64)x);
+    uint2 v = *p;
+    v.x += emin[x];                 // empty_pull_sent
+    v.y += emin[(u64)n + x];        // empty_push_sent
+    *p = v;
+}
+
+hipError_t launch_slice_apply(uint32_t *st32, const uint8_t *emin, uint32_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(slice_apply, dim3((n + 255u) / 256u), dim3(256), 0, s, st32, emin, n);
+    return hipGetLastError();
 }
 
 // Fold the u32 statistics deltas into the u64 totals (before they can wrap).
