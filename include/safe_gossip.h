@@ -231,21 +231,26 @@ uint64_t    gs_stream(const gs_engine *e);
  * the slice's first creation, so the network's count is the MIN over the
  * slices of each slice's count.  The round kernel of round t writes them
  * (empty pulls per node, then empty pushes per node: 2n bytes) into buffer
- * t & 1 instead of its Statistics; the caller all-reduces the buffer with MIN
- * over the slices and hands it back with gs_slice_apply, in round order,
- * before the buffer is written again (round t+2) and before any observer.
+ * t % 3 instead of its Statistics; the caller all-reduces the buffer with MIN
+ * over the slices and hands it back, before the buffer is written again
+ * (round t+3), with gs_slice_apply (added at once) or gs_slice_defer (added by
+ * the next round kernel, no extra pass; an observer adds it first).
  * Observers report the slice's rumors, and Statistics with this slice's
  * full_message_sent / full_message_received (the network's are the SUM over
  * slices) and empty_pull_sent WITHOUT the pending round's empty pulls, which
  * the observer call leaves in `obs` (n bytes; the caller adds their MIN
  * over the slices). */
 /* Device buffers (caller-owned, bound before the first round / observer):
- * buf0, buf1 for rounds t with t & 1 == 0 / 1 (2n bytes each), obs for the
+ * buf0..buf2 for rounds t with t % 3 == 0 / 1 / 2 (2n bytes each), obs for the
  * observers (n bytes). */
-gs_status   gs_slice_bind(gs_engine *e, void *buf0, void *buf1, void *obs);
-/* Add buffer `which` (0 / 1, already reduced with MIN over the slices) to the
- * Statistics, on the engine stream (gs_stream). */
+gs_status   gs_slice_bind(gs_engine *e, void *buf0, void *buf1, void *buf2, void *obs);
+/* Add round buffer `which` (0..2, already reduced with MIN over the slices)
+ * to the Statistics, on the engine stream (gs_stream). */
 gs_status   gs_slice_apply(gs_engine *e, uint32_t which);
+/* The same, folded into the next round kernel's Statistics update (one
+ * buffer at a time; a second call adds the first at once).  The buffer must
+ * stay unchanged until that kernel ran. */
+gs_status   gs_slice_defer(gs_engine *e, uint32_t which);
 
 /* ---- Wire format (src/messages.rs) ----------------------------------------
  * GossipRpc as maidsafe_utilities::serialisation (bincode, fixed-width little

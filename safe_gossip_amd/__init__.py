@@ -145,8 +145,9 @@ SYMBOLS = {
     "gs_shard_pull": (ctypes.c_int, [_P]),
     "gs_stream": (ctypes.c_uint64, [_P]),
     # rumor-sliced engines (safe_gossip_amd.sliced)
-    "gs_slice_bind": (ctypes.c_int, [_P, _P, _P, _P]),
+    "gs_slice_bind": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "gs_slice_apply": (ctypes.c_int, [_P, ctypes.c_uint32]),
+    "gs_slice_defer": (ctypes.c_int, [_P, ctypes.c_uint32]),
 }
 
 _LIB = None

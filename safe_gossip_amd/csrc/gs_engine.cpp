@@ -99,10 +99,12 @@ struct gs_engine {
     uint32_t n_global = 0;
     // Rumor slice (cfg.rumor_slice): this engine holds a slice of the rumors
     // of all n nodes; the round kernel writes this slice's empty-RPC counts to
-    // eb[0..1] (2n bytes, by round parity) and eb[2] (n bytes, observations),
-    // caller-owned (gs_slice_bind), reduced with MIN over the slices.
+    // eb[0..2] (2n bytes, round t writes eb[t % 3]) and eb[3] (n bytes,
+    // observations), caller-owned (gs_slice_bind), reduced with MIN over the
+    // slices; eb_defer = a reduced buffer the next transition launch adds.
     bool slice = false;
-    uint8_t *eb[3] = {nullptr, nullptr, nullptr};
+    uint8_t *eb[4] = {nullptr, nullptr, nullptr, nullptr};
+    int eb_defer = -1;
     gs::ShardPlan sp{};
     gs::ShardPlanLayout spl{};
     gs::ShardEdgeLayout sel{};
@@ -251,6 +253,7 @@ gs_status reset_state(gs_engine *e) {
     }
     e->cur = 0;
     e->round = 0;
+    e->eb_defer = -1;  // (Statistics restart from zero)
     e->seq_round = ~0u;
     e->pulled_round = 0;
     e->parts_done = 0;
@@ -464,7 +467,11 @@ gs_status seq_prepare(gs_engine *e) {
 // Fill the observation buffers with the state after the last delivery.
 gs_status observe(gs_engine *e, bool dumps) {
     if (e->obs_valid && !dumps) return GS_OK;
-    if (e->slice && !e->eb[2]) return GS_ERR_INVALID_ARGUMENT;  // gs_slice_bind first
+    if (e->slice && !e->eb[3]) return GS_ERR_INVALID_ARGUMENT;  // gs_slice_bind first
+    if (e->slice && e->eb_defer >= 0) {  // a deferred reduced buffer: add it now
+        GS_HIP(gs::launch_slice_apply(e->st32, e->eb[e->eb_defer], e->g.n, e->stream));
+        e->eb_defer = -1;
+    }
     gs_status st = ensure_obs(e, dumps);
     if (st == GS_OK && e->deliver_pending) st = upload_ext(e);
     if (st != GS_OK) return st;
@@ -476,7 +483,7 @@ gs_status observe(gs_engine *e, bool dumps) {
         a.obs_state = e->obs_state;
         a.obs_rec = e->obs_rec;
     }
-    if (e->slice) a.emin = e->eb[2];  // pending empty pulls of this slice
+    if (e->slice) a.emin = e->eb[3];  // pending empty pulls of this slice
     if (e->deliver_pending) {
         if (e->shard) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_edges[e->round % 2], 0));
         else GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
@@ -951,7 +958,11 @@ gs_status round_begin(gs_engine *e) {
     a.inj_mask = e->inj_mask;
     a.n_inj = n_inj;
     const uint32_t R0 = e->round;
-    if (e->slice) a.emin = e->eb[(R0 + 1u) & 1u];  // round R0+1's buffer
+    if (e->slice) {
+        a.emin = e->eb[(R0 + 1u) % 3u];  // round R0+1's buffer
+        if (e->eb_defer >= 0) a.eadd = e->eb[e->eb_defer];
+        e->eb_defer = -1;
+    }
     if (e->spr_active && !e->spr_always && R0 >= 2) {
         // density of round R0-1's planes (written by the launch of two calls
         // ago): switch to the dense variant once under a quarter are zero words
@@ -1164,16 +1175,28 @@ gs_status gs_next_round(gs_engine *e, gs_round_report *report) {
     return round_end(e, report);
 }
 
-gs_status gs_slice_bind(gs_engine *e, void *buf0, void *buf1, void *obs) {
-    if (!e || !e->slice || !buf0 || !buf1 || !obs) return GS_ERR_INVALID_ARGUMENT;
+gs_status gs_slice_bind(gs_engine *e, void *buf0, void *buf1, void *buf2, void *obs) {
+    if (!e || !e->slice || !buf0 || !buf1 || !buf2 || !obs) return GS_ERR_INVALID_ARGUMENT;
     e->eb[0] = static_cast<uint8_t *>(buf0);
     e->eb[1] = static_cast<uint8_t *>(buf1);
-    e->eb[2] = static_cast<uint8_t *>(obs);
+    e->eb[2] = static_cast<uint8_t *>(buf2);
+    e->eb[3] = static_cast<uint8_t *>(obs);
+    return GS_OK;
+}
+
+gs_status gs_slice_defer(gs_engine *e, uint32_t which) {
+    if (!e || !e->slice || which > 2 || !e->eb[which]) return GS_ERR_INVALID_ARGUMENT;
+    gs_status st = set_device(e);
+    if (st != GS_OK) return st;
+    if (e->eb_defer >= 0)  // one deferred buffer at a time: add the older one now
+        GS_HIP(gs::launch_slice_apply(e->st32, e->eb[e->eb_defer], e->g.n, e->stream));
+    e->eb_defer = (int)which;
+    e->obs_valid = false;
     return GS_OK;
 }
 
 gs_status gs_slice_apply(gs_engine *e, uint32_t which) {
-    if (!e || !e->slice || which > 1) return GS_ERR_INVALID_ARGUMENT;
+    if (!e || !e->slice || which > 2) return GS_ERR_INVALID_ARGUMENT;
     gs_status st = set_device(e);
     if (st != GS_OK) return st;
     if (!e->eb[which]) return GS_ERR_INVALID_ARGUMENT;

@@ -88,7 +88,10 @@ struct RoundArgs {
     // sent) and emin[n + x] (1: x's push is empty); the caller reduces them
     // with MIN over the slices and adds them back (launch_slice_apply).
     // Observation launches write their pending empty pulls to emin[x].
+    // eadd: a reduced buffer of an earlier round, added to st32 by this
+    // transition launch (gs_slice_defer: no separate apply pass).
     uint8_t *emin;
+    const uint8_t *eadd;
     uint32_t dlv_pack;        // DLV transition launches: 0 one node per lane, 1 a 32-bit lane
                               // word of several nodes, 2 a 64-bit one (gs_dlv4.hip)
     Geometry g;

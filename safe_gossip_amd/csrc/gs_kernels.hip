@@ -1120,6 +1120,10 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         if (a.emin) {  // rumor slice: empty only if empty in every slice (MIN, caller)
             a.emin[x] = (uint8_t)min(d_empty_pull, 255u);
             a.emin[(u64)g.n + x] = (uint8_t)d_empty_push;
+            if (a.eadd) {  // an earlier round's network counts (reduced by the caller)
+                v.x += a.eadd[x];
+                v.y += a.eadd[(u64)g.n + x];
+            }
         } else {
             v.x += d_empty_pull;                   // empty_pull_sent
             v.y += d_empty_push;                   // empty_push_sent

@@ -17,16 +17,16 @@ one that creates an entry, none if it has a live entry) is a nondecreasing
 function of that first creation, so the network's count is the MIN over the
 slices of each slice's count.  Per round each engine writes these two counts
 (2 bytes per node) instead of adding them to its Statistics; one
-``all_reduce(MIN)`` over the ranks and ``gs_slice_apply`` add the network's
-counts back.  ``full_message_sent`` / ``full_message_received`` count messages
+``all_reduce(MIN)`` over the ranks, and the next round kernel adds the
+network's counts back (``gs_slice_defer``).  ``full_message_sent`` / ``full_message_received`` count messages
 and are summed over the slices when observed.
 
 Transports:
 
 * ``"dist"``  -- one slice per process, ``torch.distributed`` (``nccl`` =
   RCCL over xGMI: the all-reduce of round t runs on the process group's stream
-  while the engine runs round t+1, and is applied before round t+2 reuses the
-  buffer; ``gloo``: host-staged, synchronous).
+  while the engine runs round t+1, and round t+2's kernel adds it to the
+  Statistics; ``gloo``: host-staged, synchronous).
 * ``"local"`` -- all slices in this process on one device (tests).
 
 PyTorch is plumbing here (device buffers, streams, collectives); all protocol
@@ -52,11 +52,10 @@ class _Slice:
                            _rumor_slice=True)
         self.lib, self.h = self.net._lib, self.net._h
         dev = torch.device("cuda", device)
-        self.buf = [torch.zeros(2 * n, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.buf = [torch.zeros(2 * n, dtype=torch.uint8, device=dev) for _ in range(3)]
         self.obs = torch.zeros(max(n, 1), dtype=torch.uint8, device=dev)
         torch.cuda.synchronize(dev)
-        _check(self.lib.gs_slice_bind(self.h, self.buf[0].data_ptr(), self.buf[1].data_ptr(),
-                                      self.obs.data_ptr()))
+        _check(self.lib.gs_slice_bind(self.h, *(b.data_ptr() for b in self.buf), self.obs.data_ptr()))
         self.stream = torch.cuda.ExternalStream(self.lib.gs_stream(self.h), device=dev)
 
     def close(self):
@@ -162,18 +161,19 @@ class SlicedNetwork:
         self.torch.cuda.synchronize(self.device)
 
     def _reduce_round(self, b: int):
-        """Round t's empty counts (buffer b = t & 1): MIN over the slices, then
-        added to every slice's Statistics.  RCCL: asynchronous, applied on the
-        engine stream one round later (_apply_pending)."""
+        """Round t's empty counts (buffer b = t % 3): MIN over the slices, then
+        added to every slice's Statistics.  RCCL: asynchronous; one round later
+        the engine stream waits for it and round t+2's kernel adds it
+        (gs_slice_defer, _apply_pending)."""
         if self.transport == "local":
             self._min_local([s.buf[b] for s in self.slices])
-            for s in self.slices:
-                _check(s.lib.gs_slice_apply(s.h, b))
+            for s in self.slices:  # added by the next round kernel (or an observer)
+                _check(s.lib.gs_slice_defer(s.h, b))
             return
         s = self.slices[0]
         if self.host_staged:
             self._min_dist_sync(s.buf[b])
-            _check(s.lib.gs_slice_apply(s.h, b))
+            _check(s.lib.gs_slice_defer(s.h, b))
             return
         with self.torch.cuda.stream(s.stream):
             w = self.dist.all_reduce(s.buf[b], op=self.dist.ReduceOp.MIN, group=self.group,
@@ -186,7 +186,10 @@ class SlicedNetwork:
             w, b = self._pend.pop(0)
             with self.torch.cuda.stream(s.stream):
                 w.wait()  # the engine stream waits, not the host
-            _check(s.lib.gs_slice_apply(s.h, b))
+            if keep:  # folded into the next round kernel (no extra pass)
+                _check(s.lib.gs_slice_defer(s.h, b))
+            else:
+                _check(s.lib.gs_slice_apply(s.h, b))
 
     def _flush(self):
         self._apply_pending(0)
@@ -200,7 +203,7 @@ class SlicedNetwork:
             if r is not None:
                 live |= r.any_live
         self.round += 1
-        self._reduce_round(self.round & 1)
+        self._reduce_round(self.round % 3)
         self._apply_pending(1)
         if not report:
             return None
