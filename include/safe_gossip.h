@@ -230,7 +230,7 @@ uint64_t    gs_stream(const gs_engine *e);
  * answered pushers up to its first creating one, a count that is monotone in
  * the slice's first creation, so the network's count is the MIN over the
  * slices of each slice's count.  The round kernel of round t writes them
- * (empty pulls per node, then empty pushes per node: 2n bytes) into buffer
+ * (per node x: byte 2x empty pulls, byte 2x+1 empty push; 2n bytes) into buffer
  * t % 3 instead of its Statistics; the caller all-reduces the buffer with MIN
  * over the slices and hands it back, before the buffer is written again
  * (round t+3), with gs_slice_apply (added at once) or gs_slice_defer (added by

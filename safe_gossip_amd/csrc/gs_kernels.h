@@ -84,9 +84,9 @@ struct RoundArgs {
     // Rumor-sliced network (gs_slice_*): this engine holds one slice of the
     // rumors of every node, so a node's RPC is empty only when it is empty in
     // every slice.  The kernels then leave empty_pull / empty_push out of st32
-    // and write this slice's per-node counts instead, emin[x] (empty pulls x
-    // sent) and emin[n + x] (1: x's push is empty); the caller reduces them
-    // with MIN over the slices and adds them back (launch_slice_apply).
+    // and write this slice's per-node counts instead, emin[2x] (empty pulls x
+    // sent) and emin[2x + 1] (1: x's push is empty); the caller reduces them
+    // with MIN over the slices, byte by byte, and adds them back.
     // Observation launches write their pending empty pulls to emin[x].
     // eadd: a reduced buffer of an earlier round, added to st32 by this
     // transition launch (gs_slice_defer: no separate apply pass).
@@ -175,7 +175,7 @@ struct InListArgs {
 // stream concurrently with the round kernel of the round before.
 hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s);
 hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, hipStream_t s);
-// Rumor slices: st32 empty_pull / empty_push += emin[x] / emin[n + x].
+// Rumor slices: st32 empty_pull / empty_push += emin[2x] / emin[2x + 1].
 hipError_t launch_slice_apply(uint32_t *st32, const uint8_t *emin, uint32_t n, hipStream_t s);
 
 // ---------------------------------------------------------------- SEQ

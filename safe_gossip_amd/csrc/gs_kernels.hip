@@ -288,6 +288,9 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     uint4 stv = {0u, 0u, 0u, 0u};
     if (TRANSITION && valid && (SMALL || L.j == 0)) stv = reinterpret_cast<const uint4 *>(a.st32)[x];
 #endif
+    // rumor slice: an earlier round's network empty counts (pull | push << 8)
+    uint32_t eadd = 0;
+    if (TRANSITION && a.eadd && valid && (SMALL || L.j == 0)) eadd = reinterpret_cast<const uint16_t *>(a.eadd)[x];
     uint4 in = {0, 0, 0, 0};   // SHARD: {first, k|zi<<16, e0, e1}
     InRec in8 = {};            // {first << 5 | k, s0..s2}
     SibRec sb8 = {};           // {serial<<8 | rank of x in in(z), e0..e2}; stale unless rank >= 1
@@ -1117,13 +1120,10 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         uint4 v = stv;
 #endif
         const uint32_t d_empty_push = (on_next && live_new == 0u) ? 1u : 0u;
-        if (a.emin) {  // rumor slice: empty only if empty in every slice (MIN, caller)
-            a.emin[x] = (uint8_t)min(d_empty_pull, 255u);
-            a.emin[(u64)g.n + x] = (uint8_t)d_empty_push;
-            if (a.eadd) {  // an earlier round's network counts (reduced by the caller)
-                v.x += a.eadd[x];
-                v.y += a.eadd[(u64)g.n + x];
-            }
+        if (a.emin) {  // rumor slice: empty only if empty in every slice (MIN per byte, caller)
+            reinterpret_cast<uint16_t *>(a.emin)[x] = (uint16_t)(min(d_empty_pull, 255u) | (d_empty_push << 8));
+            v.x += eadd & 0xFFu;  // an earlier round's network counts (reduced by the caller)
+            v.y += eadd >> 8;
         } else {
             v.x += d_empty_pull;                   // empty_pull_sent
             v.y += d_empty_push;                   // empty_push_sent
@@ -1181,8 +1181,8 @@ __global__ __launch_bounds__(256) void slice_apply(uint32_t *st32, const uint8_t
     if (x >= n) return;
     uint2 *p = reinterpret_cast<uint2 *>(st32 + 4u * (u64)x);
     uint2 v = *p;
-    v.x += emin[x];                 // empty_pull_sent
-    v.y += emin[(u64)n + x];        // empty_push_sent
+    v.x += emin[2u * (u64)x];       // empty_pull_sent
+    v.y += emin[2u * (u64)x + 1u];  // empty_push_sent
     *p = v;
 }
 
