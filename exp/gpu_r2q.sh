@@ -1,12 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
-rm -rf gpurun_out/prof_r2q gpurun_out/prof_r2q_cfg5
-timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || exit 1
-timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 1
-timeout -k 10 400 python -u bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || exit 1
-timeout -k 10 400 python -u bench.py --config cfg5 > gpurun_out/bench_cfg5.json 2> gpurun_out/bench_cfg5.err || exit 1
-timeout -k 10 400 python -u bench.py --config cfg3 > gpurun_out/bench_cfg3.json 2> gpurun_out/bench_cfg3.err || exit 1
-timeout -k 10 400 python -u bench.py --config cfg2 > gpurun_out/bench_cfg2.json 2> gpurun_out/bench_cfg2.err || exit 1
-timeout -k 10 300 python -u bench.py --gpus 2 --dist-backend gloo --steps 5 --warmup 1 --no-cpu-baseline --no-spread > gpurun_out/bench2_gloo.json 2> gpurun_out/bench2_gloo.err || exit 1
-timeout -k 10 700 bash profiles/rocprof_r2.sh r2q > gpurun_out/prof_r2q.log 2>&1 || exit 1
-timeout -k 10 700 bash profiles/rocprof_r2.sh r2q_cfg5 --config cfg5 > gpurun_out/prof_r2q_cfg5.log 2>&1 || exit 1
+ROOT=$(pwd)
+timeout -k 10 200 python -u bench.py --sharded --parts 2 --no-cpu-baseline --no-spread > gpurun_out/bench_sh2_q.log 2>&1 &&
+timeout -k 10 200 python -u bench.py --sharded --parts 4 --no-cpu-baseline --no-spread > gpurun_out/bench_sh4_q.log 2>&1 &&
+cd /tmp && export TMPDIR=/tmp &&
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $ROOT/gpurun_out/prof_sh2 -o run -- python3 $ROOT/bench.py --sharded --parts 2 --steps 6 --warmup 1 --no-cpu-baseline --no-spread > $ROOT/gpurun_out/prof_sh2.log 2>&1

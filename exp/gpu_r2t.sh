@@ -1,9 +1,5 @@
-set -o pipefail
-mkdir -p gpurun_out/r2t
-timeout -k 10 400 python -u -m pytest tests/test_gpu_sliced.py -q --timeout 240 --timeout-method thread > gpurun_out/r2t/gpu_tests_sliced.log 2>&1 || exit 1
-for i in 1 2; do
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-spread > gpurun_out/r2t/bench_default_$i.json 2> gpurun_out/r2t/err || exit 1
-timeout -k 10 300 python -u bench.py --sharded --mode slices --no-cpu-baseline --no-spread > gpurun_out/r2t/bench_slices_x1_rccl_$i.json 2>> gpurun_out/r2t/err || exit 1
-timeout -k 10 300 python -u bench.py --rumors 32 --no-cpu-baseline --no-spread > gpurun_out/r2t/bench_R32_$i.json 2>> gpurun_out/r2t/err || exit 1
-timeout -k 10 300 python -u bench.py --rumors 32 --sharded --mode slices --no-cpu-baseline --no-spread > gpurun_out/r2t/bench_R32_slices_x1_rccl_$i.json 2>> gpurun_out/r2t/err || exit 1
+mkdir -p gpurun_out
+for c in "2000 1 trickle 0.5 0.2 0.2" "2000 1 trickle 0 0 0" "2000 1 origins 0 0 0" "1030 1 origins 0 0 0" "2000 16 origins 0 0 0" "2000 1 trickle 0.5 0 0" "2000 1 trickle 0 0.2 0.2"; do
+echo "== $c" >> gpurun_out/dlv4_debug.log
+timeout -k 10 60 python -u exp/dlv4_debug.py $c >> gpurun_out/dlv4_debug.log 2>&1 || exit 1
 done
