@@ -42,7 +42,7 @@ constexpr uint32_t kBinLog = GS_INL_BINLOG;
 constexpr uint32_t kBin = 1u << kBinLog;          // targets per bin
 constexpr uint32_t kBinCap = kBin + kBin / 4;     // region capacity per bin
 #ifndef GS_INL_CHUNK
-#define GS_INL_CHUNK 16384
+#define GS_INL_CHUNK 8192
 #endif
 constexpr uint32_t kChunk = GS_INL_CHUNK;         // sources per inl_bin block
 constexpr uint32_t kInlThreads = 1024;
