@@ -382,7 +382,10 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
 constexpr uint32_t kCoarseBins = 128;
 constexpr uint32_t kCoarseLog = kBinLog + 7;
 constexpr uint32_t kCoarseCap = (1u << kCoarseLog) + (1u << (kCoarseLog - 4));
-constexpr uint32_t kPartChunk = 8192;
+#ifndef GS_PART_CHUNK
+#define GS_PART_CHUNK 4096
+#endif
+constexpr uint32_t kPartChunk = GS_PART_CHUNK;
 constexpr uint32_t kPartPer = kPartChunk / kInlThreads;
 constexpr uint32_t kMaxCoarse = 64;  // n <= 2^27
 
