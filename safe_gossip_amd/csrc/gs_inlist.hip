@@ -268,35 +268,48 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
 GS_DEV uint32_t half_of(const uint32_t *h, uint32_t i) { return (h[i >> 1] >> ((i & 1u) << 4)) & 0xFFFFu; }
 
 constexpr uint32_t kSortPer = (kBinCap + kInlThreads - 1) / kInlThreads;  // region entries per thread
+#ifndef GS_SORT_SPLIT_LOG
+#define GS_SORT_SPLIT_LOG 0
+#endif
+constexpr uint32_t kSortSplitLog = GS_SORT_SPLIT_LOG;  // inl_sort blocks per bin = 2^kSortSplitLog
 
+// SPLITLOG > 0: 2^SPLITLOG blocks per bin (blockIdx.y = part), each sorting the
+// targets of its part from the whole bin region; half the LDS, so two blocks
+// share a CU (the fill counts are then cleared by the launcher, not here).
+template <uint32_t SPLITLOG>
 __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
+    constexpr uint32_t kPartLog = kBinLog - SPLITLOG;
+    constexpr uint32_t kPart = 1u << kPartLog;             // targets per block
+    constexpr uint32_t kPartCap = kBinCap >> SPLITLOG;     // sorted entries per block
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     const CsrPlan &p = a.p;
-    uint32_t *h = sh;                  // [kBin/2] packed per-target counters
-    uint32_t *sorted = sh + kBin / 2;  // [kBinCap]
+    uint32_t *h = sh;                   // [kPart/2] packed per-target counters
+    uint32_t *sorted = sh + kPart / 2;  // [kPartCap]
     __shared__ uint32_t lds_scan[kInlThreads / 64];
-    const uint32_t b = blockIdx.x;
+    const uint32_t b = blockIdx.x, hh = blockIdx.y;
     const uint32_t cnt = min(a.scratch[b], kBinCap);
-    const uint32_t t0 = b << kBinLog;
-    const uint32_t nodes = min(kBin, p.n - t0);
-    // the bin's entries, held in registers (coalesced loads, issued first)
+    const uint32_t t0 = (b << kBinLog) + (hh << kPartLog);
+    const uint32_t nodes = t0 < p.n ? min(kPart, p.n - t0) : 0u;
+    if (nodes == 0) return;  // a part past the last node (uniform per block)
+    // the bin's entries of this part, held in registers (coalesced loads, issued first)
     uint32_t ex[kSortPer], el[kSortPer];
 #pragma unroll
     for (uint32_t q = 0; q < kSortPer; ++q) {
         const uint32_t i = threadIdx.x + q * kInlThreads;
         const bool ok = i < cnt;
         ex[q] = ok ? a.region[(u64)b * kBinCap + i] : 0u;
-        el[q] = ok ? (uint32_t)a.region_lt[(u64)b * kBinCap + i] : kNone;
+        const uint32_t lt = ok ? (uint32_t)a.region_lt[(u64)b * kBinCap + i] : kNone;
+        el[q] = (ok && (lt >> kPartLog) == hh) ? (lt & (kPart - 1u)) : kNone;
     }
-    for (uint32_t i = threadIdx.x; i < kBin / 2; i += kInlThreads) h[i] = 0u;
-    // live-filtered gathers: the bin's "complete" bits (coalesced) and the
+    for (uint32_t i = threadIdx.x; i < kPart / 2; i += kInlThreads) h[i] = 0u;
+    // live-filtered gathers: the part's "complete" bits (coalesced) and the
     // live bit of every entry (L2-resident map lookups, issued together),
     // carried as bit 31 of the sorted ids (kLiveTag)
-    __shared__ uint32_t cpl[kBin / 32], lvl[kBin / 32];
+    __shared__ uint32_t cpl[kPart / 32], lvl[kPart / 32];
     const bool filt = a.lvm != nullptr;
     uint32_t lt_tag[kSortPer];
     if (filt) {
-        for (uint32_t i = threadIdx.x; i < kBin / 32; i += kInlThreads) {
+        for (uint32_t i = threadIdx.x; i < kPart / 32; i += kInlThreads) {
             const bool in = t0 + 32u * i < p.n;
             cpl[i] = in ? reinterpret_cast<const uint32_t *>(a.cpm)[(t0 >> 5) + i] : 0u;
             lvl[i] = in ? reinterpret_cast<const uint32_t *>(a.lvm)[(t0 >> 5) + i] : 0u;
@@ -306,13 +319,13 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
             lt_tag[q] = (el[q] != kNone && map_test(a.lvm, ex[q])) ? kLiveTag : 0u;
     }
     __syncthreads();
-    if (threadIdx.x == 0) a.scratch[b] = 0u;  // ready for the next build of this set
+    if (SPLITLOG == 0 && threadIdx.x == 0) a.scratch[b] = 0u;  // ready for the next build of this set
 #pragma unroll
     for (uint32_t q = 0; q < kSortPer; ++q)
         if (el[q] != kNone) atomicAdd(&h[el[q] >> 1], 1u << ((el[q] & 1u) << 4));
     __syncthreads();
-    // exclusive scan over the kBin targets, kBin/kInlThreads per thread
-    constexpr uint32_t per = kBin / kInlThreads;
+    // exclusive scan over the kPart targets, kPart/kInlThreads per thread
+    constexpr uint32_t per = kPart / kInlThreads;
     const uint32_t i0 = threadIdx.x * per;
     uint32_t sum = 0;
 #pragma unroll
@@ -326,27 +339,29 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
         run += c0 + c1;
     }
     __syncthreads();
+    if (SPLITLOG > 0 && threadIdx.x == 0 && total > kPartCap) atomicOr(&a.flags[2], kFlagLimit);
 #pragma unroll
     for (uint32_t q = 0; q < kSortPer; ++q) {
         if (el[q] != kNone) {
             const uint32_t shf = (el[q] & 1u) << 4;
             const uint32_t old = atomicAdd(&h[el[q] >> 1], 1u << shf);
-            // DLV: the entry's index in the region (its id and code are
-            // re-read from there, an L2-resident window)
-            sorted[(old >> shf) & 0xFFFFu] = ex[q] | (filt ? lt_tag[q] : 0u);
+            const uint32_t pos = (old >> shf) & 0xFFFFu;
+            if (pos < kPartCap) sorted[pos] = ex[q] | (filt ? lt_tag[q] : 0u);
         }
     }
     __syncthreads();
     // counters are now the ends of each target's run; lanes take consecutive
-    // targets so the InRec stores are coalesced
+    // targets so the InRec stores are coalesced (an overflowing part, flagged
+    // above, keeps only the entries that fit)
+    auto end_of = [&](uint32_t lt) { return min(half_of(h, lt), kPartCap); };
     uint32_t mine = 0;
     for (uint32_t lt = threadIdx.x; lt < nodes; lt += kInlThreads)
-        mine += tail_len<>(half_of(h, lt) - (lt ? half_of(h, lt - 1) : 0u));
+        mine += tail_len<>(end_of(lt) - (lt ? end_of(lt - 1) : 0u));
     uint32_t cur = reserve_tails<kInlThreads>(a, mine, &a.scratch[p.nb], lds_scan);
     uint32_t rows = 0;  // filtered: class rows left to gather (traffic accounting)
     for (uint32_t lt = threadIdx.x; lt < nodes; lt += kInlThreads) {
-        const uint32_t e = half_of(h, lt);
-        const uint32_t s = lt ? half_of(h, lt - 1) : 0u;
+        const uint32_t e = end_of(lt);
+        const uint32_t s = lt ? end_of(lt - 1) : 0u;
         uint32_t *lst = sorted + s;
         const uint32_t k = e - s;
         for (uint32_t q = 1; q < k; ++q) {  // Poisson(1)-sized: insertion sort (by id)
@@ -1027,9 +1042,9 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
     if (p.binned) {
         const size_t lds_bin = ((size_t)kChunk + kChunk / 2 + (p.nb + 1) / 2) * sizeof(uint32_t) +
                                (size_t)2 * p.nb * sizeof(uint16_t);
-        const size_t lds_sort = ((size_t)kBin / 2 + kBinCap) * sizeof(uint32_t);
+        const size_t lds_sort = ((size_t)(kBin >> kSortSplitLog) / 2 + (kBinCap >> kSortSplitLog)) * sizeof(uint32_t);
         const size_t lds_dlv = ((size_t)kHalf / 2 + 2 * (size_t)kHalfCap) * sizeof(uint32_t);
-        const void *ks = p.dlv ? (const void *)inl_sort_dlv : (const void *)inl_sort;
+        const void *ks = p.dlv ? (const void *)inl_sort_dlv : (const void *)inl_sort<kSortSplitLog>;
         hipError_t e = hipFuncSetAttribute((const void *)inl_bin, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)lds_bin);
         if (e == hipSuccess)
@@ -1064,8 +1079,13 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
             hipLaunchKernelGGL(pb_fine, dim3((1u << kCoarseLog) / kPartChunk, nc), dim3(kInlThreads), lds_pb, s, ab);
             hipLaunchKernelGGL(pb_place, dim3(p.nb), dim3(kInlThreads), 0, s, ab);
         } else {
+            if (kSortSplitLog > 0) {  // the split sort cannot clear the fill counts itself
+                e = hipMemsetAsync(a.scratch, 0, (size_t)p.nb * sizeof(uint32_t), s);
+                if (e != hipSuccess) return e;
+            }
             hipLaunchKernelGGL(inl_bin, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
-            hipLaunchKernelGGL(inl_sort, dim3(p.nb), dim3(kInlThreads), lds_sort, s, ab);
+            hipLaunchKernelGGL(inl_sort<kSortSplitLog>, dim3(p.nb, 1u << kSortSplitLog), dim3(kInlThreads), lds_sort,
+                               s, ab);
         }
         return hipGetLastError();
     }
