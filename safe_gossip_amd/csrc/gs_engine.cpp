@@ -1186,6 +1186,7 @@ gs_status gs_slice_bind(gs_engine *e, void *buf0, void *buf1, void *buf2, void *
 
 gs_status gs_slice_defer(gs_engine *e, uint32_t which) {
     if (!e || !e->slice || which > 2 || !e->eb[which]) return GS_ERR_INVALID_ARGUMENT;
+    if (e->eb_defer == (int)which) return GS_ERR_INVALID_ARGUMENT;  // would be added twice
     gs_status st = set_device(e);
     if (st != GS_OK) return st;
     if (e->eb_defer >= 0)  // one deferred buffer at a time: add the older one now
@@ -1200,6 +1201,7 @@ gs_status gs_slice_apply(gs_engine *e, uint32_t which) {
     gs_status st = set_device(e);
     if (st != GS_OK) return st;
     if (!e->eb[which]) return GS_ERR_INVALID_ARGUMENT;
+    if (e->eb_defer == (int)which) e->eb_defer = -1;  // deferred: added now instead, once
     GS_HIP(gs::launch_slice_apply(e->st32, e->eb[which], e->g.n, e->stream));
     e->obs_valid = false;
     return GS_OK;

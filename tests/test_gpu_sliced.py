@@ -111,6 +111,18 @@ def test_slice_engine_refusals(engine):
     frame = sg.rpc_encode(False, b"\x04\x00\x00\x00\x00\x00\x00\x00\x00\x00\x00\x05", 1)
     with pytest.raises(sg.GossipError):
         net.slices[0].net.handle_received(3, 1000, frame)  # no external RPCs on a slice
+    s = net.slices[0]
+    assert s.lib.gs_slice_defer(s.h, 3) != 0            # no such round buffer
+    net.next_round()                                     # round 3: buffer 0 deferred
+    assert s.lib.gs_slice_defer(s.h, 0) != 0            # deferring it twice would add it twice
+    assert s.lib.gs_slice_apply(s.h, 0) == 0            # applying it now cancels the deferral
+    orc = OracleNet(100, 8)
+    orc.send_new(3, 5)
+    for _ in range(3):
+        orc.next_round(SCHED_2P)
+    got = net.statistics_all()
+    np.testing.assert_array_equal(got, orc.statistics())  # added exactly once
+    orc.close()
     net.close()
 
 
