@@ -268,10 +268,18 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
 GS_DEV uint32_t half_of(const uint32_t *h, uint32_t i) { return (h[i >> 1] >> ((i & 1u) << 4)) & 0xFFFFu; }
 
 constexpr uint32_t kSortPer = (kBinCap + kInlThreads - 1) / kInlThreads;  // region entries per thread
-#ifndef GS_SORT_SPLIT_LOG
-#define GS_SORT_SPLIT_LOG 0
+// inl_sort blocks per bin = 2^split: one while there are enough bins to fill
+// the chip (two per bin measured slower at 1024 bins: every block reads the
+// whole bin region), more for small networks (2^20 nodes = 64 bins), whose
+// regions stay in L2.  GS_SORT_SPLIT_LOG forces one value (A/B).
+inline uint32_t sort_split_log(uint32_t nb) {
+#ifdef GS_SORT_SPLIT_LOG
+    (void)nb;
+    return GS_SORT_SPLIT_LOG;
+#else
+    return nb >= 512u ? 0u : (nb >= 128u ? 1u : 2u);
 #endif
-constexpr uint32_t kSortSplitLog = GS_SORT_SPLIT_LOG;  // inl_sort blocks per bin = 2^kSortSplitLog
+}
 
 // SPLITLOG > 0: 2^SPLITLOG blocks per bin (blockIdx.y = part), each sorting the
 // targets of its part from the whole bin region; half the LDS, so two blocks
@@ -1042,9 +1050,12 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
     if (p.binned) {
         const size_t lds_bin = ((size_t)kChunk + kChunk / 2 + (p.nb + 1) / 2) * sizeof(uint32_t) +
                                (size_t)2 * p.nb * sizeof(uint16_t);
-        const size_t lds_sort = ((size_t)(kBin >> kSortSplitLog) / 2 + (kBinCap >> kSortSplitLog)) * sizeof(uint32_t);
+        const uint32_t sl = sort_split_log(p.nb);
+        const size_t lds_sort = ((size_t)(kBin >> sl) / 2 + (kBinCap >> sl)) * sizeof(uint32_t);
         const size_t lds_dlv = ((size_t)kHalf / 2 + 2 * (size_t)kHalfCap) * sizeof(uint32_t);
-        const void *ks = p.dlv ? (const void *)inl_sort_dlv : (const void *)inl_sort<kSortSplitLog>;
+        const void *ks = p.dlv ? (const void *)inl_sort_dlv
+                               : (sl == 0 ? (const void *)inl_sort<0> : sl == 1 ? (const void *)inl_sort<1>
+                                                                               : (const void *)inl_sort<2>);
         hipError_t e = hipFuncSetAttribute((const void *)inl_bin, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)lds_bin);
         if (e == hipSuccess)
@@ -1079,13 +1090,15 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
             hipLaunchKernelGGL(pb_fine, dim3((1u << kCoarseLog) / kPartChunk, nc), dim3(kInlThreads), lds_pb, s, ab);
             hipLaunchKernelGGL(pb_place, dim3(p.nb), dim3(kInlThreads), 0, s, ab);
         } else {
-            if (kSortSplitLog > 0) {  // the split sort cannot clear the fill counts itself
+            if (sl > 0) {  // the split sort cannot clear the fill counts itself
                 e = hipMemsetAsync(a.scratch, 0, (size_t)p.nb * sizeof(uint32_t), s);
                 if (e != hipSuccess) return e;
             }
             hipLaunchKernelGGL(inl_bin, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
-            hipLaunchKernelGGL(inl_sort<kSortSplitLog>, dim3(p.nb, 1u << kSortSplitLog), dim3(kInlThreads), lds_sort,
-                               s, ab);
+            const dim3 gs(p.nb, 1u << sl);
+            if (sl == 0) hipLaunchKernelGGL(inl_sort<0>, gs, dim3(kInlThreads), lds_sort, s, ab);
+            else if (sl == 1) hipLaunchKernelGGL(inl_sort<1>, gs, dim3(kInlThreads), lds_sort, s, ab);
+            else hipLaunchKernelGGL(inl_sort<2>, gs, dim3(kInlThreads), lds_sort, s, ab);
         }
         return hipGetLastError();
     }
