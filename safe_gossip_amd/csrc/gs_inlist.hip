@@ -593,13 +593,22 @@ __global__ __launch_bounds__(kInlThreads) void dl_fine(InListArgs a) {
 #ifndef GS_DLV_SPLIT_LOG
 #define GS_DLV_SPLIT_LOG 1
 #endif
-constexpr uint32_t kSplitLog = GS_DLV_SPLIT_LOG;   // sort blocks per bin = 2^kSplitLog
-constexpr uint32_t kHalfLog = kBinLog - kSplitLog;
-constexpr uint32_t kHalf = 1u << kHalfLog;
-constexpr uint32_t kHalfCap = kBinCap >> kSplitLog;
-constexpr uint32_t kHalfPer = kHalf / kInlThreads;  // targets per thread
+constexpr uint32_t kSplitLog = GS_DLV_SPLIT_LOG;   // sort blocks per bin = 2^kSplitLog (large n)
+// Small networks (few bins) sort with more blocks per bin, so the chip fills;
+// their bin regions stay in L2 (config 2: 64 bins).
+inline uint32_t dlv_split_log(uint32_t nb) {
+#ifdef GS_DLV_SPLIT_FIXED
+    return (void)nb, kSplitLog;  // A/B: the large-n split everywhere
+#endif
+    return nb >= 512u ? kSplitLog : (nb >= 128u ? kSplitLog + 1u : kSplitLog + 2u);
+}
 
+template <uint32_t SL>
 __global__ __launch_bounds__(kInlThreads) void inl_sort_dlv(InListArgs a) {
+    constexpr uint32_t kHalfLog = kBinLog - SL;  // (a "half": one of the 2^SL parts of a bin)
+    constexpr uint32_t kHalf = 1u << kHalfLog;
+    constexpr uint32_t kHalfCap = kBinCap >> SL;
+    constexpr uint32_t kHalfPer = kHalf / kInlThreads;  // targets per thread
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     const CsrPlan &p = a.p;
     uint32_t *h = sh;                   // [kHalf/2] packed per-target counters
@@ -1052,8 +1061,11 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
                                (size_t)2 * p.nb * sizeof(uint16_t);
         const uint32_t sl = sort_split_log(p.nb);
         const size_t lds_sort = ((size_t)(kBin >> sl) / 2 + (kBinCap >> sl)) * sizeof(uint32_t);
-        const size_t lds_dlv = ((size_t)kHalf / 2 + 2 * (size_t)kHalfCap) * sizeof(uint32_t);
-        const void *ks = p.dlv ? (const void *)inl_sort_dlv
+        const uint32_t dsl = dlv_split_log(p.nb);
+        const size_t lds_dlv = ((size_t)(kBin >> dsl) / 2 + 2 * (size_t)(kBinCap >> dsl)) * sizeof(uint32_t);
+        const void *ks = p.dlv ? (dsl == kSplitLog       ? (const void *)inl_sort_dlv<kSplitLog>
+                                  : dsl == kSplitLog + 1u ? (const void *)inl_sort_dlv<kSplitLog + 1u>
+                                                          : (const void *)inl_sort_dlv<kSplitLog + 2u>)
                                : (sl == 0 ? (const void *)inl_sort<0> : sl == 1 ? (const void *)inl_sort<1>
                                                                                : (const void *)inl_sort<2>);
         hipError_t e = hipFuncSetAttribute((const void *)inl_bin, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1083,7 +1095,11 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
             hipLaunchKernelGGL(dl_coarse, dim3(p.ba), dim3(kInlThreads), lds_c, s, ab);
             hipLaunchKernelGGL(dl_fine, dim3((kCoarseCap + kPartChunk - 1) / kPartChunk, nc), dim3(kInlThreads),
                                lds_f, s, ab);
-            hipLaunchKernelGGL(inl_sort_dlv, dim3(p.nb, 1u << kSplitLog), dim3(kInlThreads), lds_dlv, s, ab);
+            const dim3 gd(p.nb, 1u << dsl);
+            if (dsl == kSplitLog) hipLaunchKernelGGL(inl_sort_dlv<kSplitLog>, gd, dim3(kInlThreads), lds_dlv, s, ab);
+            else if (dsl == kSplitLog + 1u)
+                hipLaunchKernelGGL(inl_sort_dlv<kSplitLog + 1u>, gd, dim3(kInlThreads), lds_dlv, s, ab);
+            else hipLaunchKernelGGL(inl_sort_dlv<kSplitLog + 2u>, gd, dim3(kInlThreads), lds_dlv, s, ab);
             const size_t lds_pb = ((size_t)kPartChunk + kPartChunk / 2 + kPartChunk / 4) * sizeof(uint32_t);
             e = hipFuncSetAttribute((const void *)pb_fine, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_pb);
             if (e != hipSuccess) return e;
