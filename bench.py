@@ -330,8 +330,9 @@ def main():
                 "parallelism": ((f"rumor slices x{dist.get_world_size()} (all {n} nodes, "
                                  f"{R // world}-{-(-R // world)} rumors per rank), "
                                  + ("RCCL" if args.dist_backend == "nccl" else args.dist_backend)
-                                 + " all_reduce(MIN) of 2 B/node empty-RPC counts per round, "
-                                   "overlapped with the next round")
+                                 + " all_reduce(MIN) of 2 B/node empty-RPC counts per round"
+                                 + (", overlapped with the next round" if args.dist_backend == "nccl"
+                                    else ", host-staged"))
                                 if args.mode == "slices" else
                                 (f"node-range shards x{dist.get_world_size()}, "
                                  + ("RCCL" if args.dist_backend == "nccl" else args.dist_backend)
