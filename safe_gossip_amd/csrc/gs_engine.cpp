@@ -49,7 +49,14 @@ struct gs_engine {
         uint32_t *pull = nullptr;  // DLV path: PULL[x]
         u64 *zl = nullptr;         // live-filtered gathers: per source "t(x) is live"
         uint32_t serial = 0;
+        uint32_t wraps = 0;        // serial wraps this set's SibRecs were cleared for
     } csr[2];
+    uint32_t serial_wraps = 0;
+    // Two-phase build (SAFE_GOSSIP_AMD_SPLIT_BUILD=1, filtered 2P gather path):
+    // inl_bin of round t+1 on cstream beside round t's kernel, then the zl map
+    // and inl_sort on the round stream after it (ev_binned[set]: phase A done).
+    bool split_build = false;
+    hipEvent_t ev_binned[2] = {nullptr, nullptr};
     // Live-filtered gathers (gs_common.h kSkipBit): node maps "live" and
     // "complete" of the planes the last transition launch wrote, read by the
     // in-list build that follows it on the same stream.  On for the 2P gather
@@ -206,6 +213,7 @@ void release(gs_engine *e) {
     for (int i = 0; i < 2; ++i) {
         if (e->ev_built[i]) (void)hipEventDestroy(e->ev_built[i]);
         if (e->ev_read[i]) (void)hipEventDestroy(e->ev_read[i]);
+        if (e->ev_binned[i]) (void)hipEventDestroy(e->ev_binned[i]);
     }
     for (int i = 0; i < 3; ++i) {
         if (e->planw[i]) (void)hipFree(e->planw[i]);
@@ -693,6 +701,10 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         e->filt = !off && !e->shard && !e->seq && !e->dlv && !e->spr && !e->concurrent_inlists &&
                   e->plan.binned && (g.small || g.W <= 8);
     }
+    {
+        const char *v = std::getenv("SAFE_GOSSIP_AMD_SPLIT_BUILD");
+        e->split_build = v && *v && *v != '0' && e->filt;
+    }
     // Per round a node's u32 Statistics deltas grow by at most 32*R_pad + 32
     // (in-degree <= 30 is enforced); fold them into u64 well before a wrap.
     e->fold_every = (uint32_t)std::max<uint64_t>(1, 0xFFFFFFFFull / (32ull * g.rpad + 32) / 2);
@@ -727,6 +739,7 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         auto &c = e->csr[i];
         ok = hipEventCreateWithFlags(&e->ev_built[i], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&e->ev_read[i], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&e->ev_binned[i], hipEventDisableTiming) == hipSuccess &&
              dalloc(&c.src, isz.src_words) == hipSuccess && dalloc(&c.tg, n) == hipSuccess &&
              dalloc(&c.region, isz.region_words) == hipSuccess &&
              dalloc(&c.scratch, isz.scratch_words) == hipSuccess &&
@@ -938,6 +951,56 @@ namespace {
 // node-range parts of gs_shard_create_parts; otherwise one part = the whole
 // grid): round_begin sequences the round and fixes its arguments, launch_part
 // launches one part's blocks, round_end does the bookkeeping after the last.
+// A new build serial for in-list set c (SibRecs of older builds read as
+// stale).  When the 24-bit serial wraps, every set's SibRecs are cleared at
+// that set's next build, on the build stream, after its last reader.
+gs_status next_serial(gs_engine *e, gs_engine::CsrSet &c, hipStream_t bs) {
+    c.serial = ++e->build_serial & gs::kSerialMask;
+    if (c.serial == 0) {
+        ++e->serial_wraps;
+        c.serial = ++e->build_serial & gs::kSerialMask;
+    }
+    if (c.wraps != e->serial_wraps) {
+        if (c.SIB8) GS_HIP(hipMemsetAsync(c.SIB8, 0, (size_t)e->g.n * sizeof(gs::SibRec), bs));
+        c.wraps = e->serial_wraps;
+    }
+    return GS_OK;
+}
+
+// Arguments of the build of round `round`'s in-lists into set c.
+gs::InListArgs inlist_args(gs_engine *e, gs_engine::CsrSet &c, uint32_t round) {
+    gs::InListArgs la{};
+    la.p = e->plan;
+    la.tg = c.tg;
+    la.IN8 = c.IN8;
+    la.SIB8 = c.SIB8;
+    la.src = c.src;
+    la.region = c.region;
+    la.scratch = c.scratch;
+    la.flags = e->flags;
+    la.serial = c.serial;
+    la.seed = e->seed;
+    la.epoch = e->epoch;
+    la.round = round;
+    la.f = e->faults;
+    if (e->filt) {  // skip flags from the maps the round kernel just wrote
+        la.lvm = e->lvm;
+        la.cpm = e->cpm;
+        la.zl = c.zl;
+        la.rows = e->rows_dev + (round & 1u);
+    }
+    if (e->dlv) {  // records carry the push codes of the new round's planes
+        la.dlv = 1;
+        la.S = e->S[e->cur];
+        la.PC = e->pc;
+        la.g = e->g;
+        la.DR = c.DR;
+        la.dtail = c.src;
+        la.pull = c.pull;
+    }
+    return la;
+}
+
 gs_status round_begin(gs_engine *e) {
     gs_status st = GS_OK;
     if (e->shard) {
@@ -1004,6 +1067,18 @@ gs_status round_begin(gs_engine *e) {
         GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[rs], 0));
         st = seq_prepare(e);  // SEQ: pull batches of round t (no-op for 2P)
         if (st != GS_OK) return st;
+    }
+    if (e->split_build) {
+        // phase A of round t+1's in-lists (targets, bin partition) on the side
+        // stream beside this round's kernel; the set's last reader was the
+        // kernel of round t-1
+        const uint32_t ns = (R0 + 1u) & 1u;
+        auto &c = e->csr[ns];
+        GS_HIP(hipStreamWaitEvent(e->cstream, e->ev_read[ns], 0));
+        st = next_serial(e, c, e->cstream);
+        if (st != GS_OK) return st;
+        GS_HIP(gs::launch_build_bins(inlist_args(e, c, R0 + 1u), e->cstream));
+        GS_HIP(hipEventRecord(e->ev_binned[ns], e->cstream));
     }
     e->ra = a;
     e->ra_mode = e->deliver_pending ? 1 : 0;
@@ -1086,45 +1161,21 @@ gs_status round_end(gs_engine *e, gs_round_report *report) {
         // measured slower than in sequence.
         // (DLV: the build reads the planes this round kernel writes: in sequence)
         hipStream_t bs = (e->concurrent_inlists && !e->dlv) ? e->cstream : e->stream;
-        GS_HIP(hipStreamWaitEvent(bs, e->ev_read[ns], 0));
-        c.serial = ++e->build_serial & gs::kSerialMask;
-        if (c.serial == 0) {  // 24-bit serial wrapped: no stale SibRec may match a new serial
-            GS_HIP(hipStreamSynchronize(e->stream));
-            for (auto &cc : e->csr)
-                if (cc.SIB8) GS_HIP(hipMemsetAsync(cc.SIB8, 0, (size_t)e->g.n * sizeof(gs::SibRec), bs));
-            c.serial = ++e->build_serial & gs::kSerialMask;
+        if (e->split_build) {
+            // phase A (inl_bin) ran beside this round kernel (round_begin);
+            // phase B needs the node maps this kernel wrote
+            GS_HIP(hipStreamWaitEvent(e->stream, e->ev_binned[ns], 0));
+            gs::InListArgs la = inlist_args(e, c, e->round);
+            GS_HIP(hipMemsetAsync(la.rows, 0, sizeof(u64), e->stream));
+            GS_HIP(gs::launch_build_sort(la, e->stream));
+        } else {
+            GS_HIP(hipStreamWaitEvent(bs, e->ev_read[ns], 0));
+            st = next_serial(e, c, bs);
+            if (st != GS_OK) return st;
+            gs::InListArgs la = inlist_args(e, c, e->round);
+            if (e->filt) GS_HIP(hipMemsetAsync(la.rows, 0, sizeof(u64), bs));
+            GS_HIP(gs::launch_build_inlists(la, bs));
         }
-        gs::InListArgs la{};
-        la.p = e->plan;
-        la.tg = c.tg;
-        la.IN8 = c.IN8;
-        la.SIB8 = c.SIB8;
-        la.src = c.src;
-        la.region = c.region;
-        la.scratch = c.scratch;
-        la.flags = e->flags;
-        la.serial = c.serial;
-        la.seed = e->seed;
-        la.epoch = e->epoch;
-        la.round = e->round;
-        la.f = e->faults;
-        if (e->filt) {  // skip flags from the maps the round kernel just wrote
-            la.lvm = e->lvm;
-            la.cpm = e->cpm;
-            la.zl = c.zl;
-            la.rows = e->rows_dev + ns;
-            GS_HIP(hipMemsetAsync(la.rows, 0, sizeof(u64), bs));
-        }
-        if (e->dlv) {  // records carry the push codes of the new round's planes
-            la.dlv = 1;
-            la.S = e->S[e->cur];
-            la.PC = e->pc;
-            la.g = e->g;
-            la.DR = c.DR;
-            la.dtail = c.src;
-            la.pull = c.pull;
-        }
-        GS_HIP(gs::launch_build_inlists(la, bs));
         GS_HIP(hipEventRecord(e->ev_built[ns], bs));
     }
     if (report) {

@@ -1053,6 +1053,77 @@ InListSizes inlist_sizes(const CsrPlan &p) {
     return z;
 }
 
+// zl = "t(x) is live" (and the rows it leaves to gather) from the targets
+// inl_bin wrote and the live map of the planes the round kernel just wrote:
+// a wave's 64 lanes are 64 consecutive sources, i.e. one zl word.
+constexpr uint32_t kZlPer = 4;  // sources per thread (strided by the block)
+__global__ __launch_bounds__(kInlThreads) void inl_zl(InListArgs a) {
+    __shared__ uint32_t zrows;
+    if (threadIdx.x == 0) zrows = 0u;
+    __syncthreads();
+    uint32_t zr = 0;  // (wave-uniform)
+#pragma unroll
+    for (uint32_t q = 0; q < kZlPer; ++q) {
+        const uint32_t x = (blockIdx.x * kZlPer + q) * kInlThreads + threadIdx.x;
+        bool l = false, np = true;
+        if (x < a.p.n) {
+            const uint32_t t = a.tg[x];
+            l = !(t & kTgDead) && map_test(a.lvm, t & kTgMask);
+            np = (t & kTgNoPull) != 0u;
+        }
+        const u64 b = __ballot(l);
+        if ((threadIdx.x & 63u) == 0u && x < a.p.n) a.zl[x >> 6] = b;
+        if (a.rows) zr += (uint32_t)__popcll(__ballot(l && !np));
+    }
+    if (a.rows && (threadIdx.x & 63u) == 0u && zr) atomicAdd(&zrows, zr);
+    __syncthreads();
+    if (a.rows && threadIdx.x == 0 && zrows) atomicAdd(a.rows, (u64)zrows);
+}
+
+hipError_t launch_build_bins(const InListArgs &a, hipStream_t s) {
+    const CsrPlan &p = a.p;
+    if (p.n == 0) return hipSuccess;
+    if (!p.binned || p.dlv) return hipErrorInvalidValue;
+    const size_t lds_bin = ((size_t)kChunk + kChunk / 2 + (p.nb + 1) / 2) * sizeof(uint32_t) +
+                           (size_t)2 * p.nb * sizeof(uint16_t);
+    hipError_t e = hipFuncSetAttribute((const void *)inl_bin, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds_bin);
+    if (e != hipSuccess) return e;
+    const uint32_t sl = sort_split_log(p.nb);
+    if (sl > 0) {  // the split sort cannot clear the fill counts itself
+        e = hipMemsetAsync(a.scratch, 0, (size_t)p.nb * sizeof(uint32_t), s);
+        if (e != hipSuccess) return e;
+    }
+    InListArgs ab = a;
+    ab.region_lt = reinterpret_cast<uint16_t *>(a.region + (size_t)p.nb * kBinCap);
+    ab.lvm = ab.cpm = nullptr;  // no node maps in this phase (inl_zl writes zl)
+    ab.zl = nullptr;
+    ab.rows = nullptr;
+    hipLaunchKernelGGL(inl_bin, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
+    return hipGetLastError();
+}
+
+hipError_t launch_build_sort(const InListArgs &a, hipStream_t s) {
+    const CsrPlan &p = a.p;
+    if (p.n == 0) return hipSuccess;
+    if (!p.binned || p.dlv || !a.lvm || !a.cpm || !a.zl) return hipErrorInvalidValue;
+    const uint32_t sl = sort_split_log(p.nb);
+    const size_t lds_sort = ((size_t)(kBin >> sl) / 2 + (kBinCap >> sl)) * sizeof(uint32_t);
+    const void *ks = sl == 0 ? (const void *)inl_sort<0> : sl == 1 ? (const void *)inl_sort<1>
+                                                                   : (const void *)inl_sort<2>;
+    hipError_t e = hipFuncSetAttribute(ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sort);
+    if (e != hipSuccess) return e;
+    InListArgs ab = a;
+    ab.region_lt = reinterpret_cast<uint16_t *>(a.region + (size_t)p.nb * kBinCap);
+    const uint32_t zb = (uint32_t)(((u64)p.n + kZlPer * kInlThreads - 1) / (kZlPer * kInlThreads));
+    hipLaunchKernelGGL(inl_zl, dim3(zb), dim3(kInlThreads), 0, s, ab);
+    const dim3 gs(p.nb, 1u << sl);
+    if (sl == 0) hipLaunchKernelGGL(inl_sort<0>, gs, dim3(kInlThreads), lds_sort, s, ab);
+    else if (sl == 1) hipLaunchKernelGGL(inl_sort<1>, gs, dim3(kInlThreads), lds_sort, s, ab);
+    else hipLaunchKernelGGL(inl_sort<2>, gs, dim3(kInlThreads), lds_sort, s, ab);
+    return hipGetLastError();
+}
+
 hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
     const CsrPlan &p = a.p;
     if (p.n == 0) return hipSuccess;

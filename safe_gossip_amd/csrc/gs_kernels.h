@@ -174,6 +174,11 @@ struct InListArgs {
 // `serial`).  Depends on nothing but the Philox stream, so it runs on its own
 // stream concurrently with the round kernel of the round before.
 hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s);
+// The filtered binned build in two phases (2P gather path): phase A (inl_bin:
+// targets and the bin partition, no node maps) can run beside the previous
+// round kernel; phase B (the zl map from lvm, then inl_sort) runs after it.
+hipError_t launch_build_bins(const InListArgs &a, hipStream_t s);
+hipError_t launch_build_sort(const InListArgs &a, hipStream_t s);
 hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, hipStream_t s);
 // Rumor slices: st32 empty_pull / empty_push += emin[2x] / emin[2x + 1].
 hipError_t launch_slice_apply(uint32_t *st32, const uint8_t *emin, uint32_t n, hipStream_t s);
