@@ -46,8 +46,9 @@ constexpr uint32_t kBinCap = kBin + kBin / 4;     // region capacity per bin
 #endif
 constexpr uint32_t kChunk = GS_INL_CHUNK;         // sources per inl_bin block
 constexpr uint32_t kInlThreads = 1024;
-constexpr uint32_t kBinPer = kChunk / kInlThreads;  // sources per inl_bin thread
 static_assert(kChunk % kInlThreads == 0, "inl_bin: whole sources per thread");
+constexpr uint32_t kChunkSmall = 2048;            // sources per inl_bin block below 2^22 nodes
+static_assert(kChunkSmall % kInlThreads == 0, "inl_bin: whole sources per thread");
 constexpr uint32_t kBinnedMaxBins = 8192;         // n <= 2^27 (per-bin LDS state is 6 B)
 constexpr uint32_t kFlagLimit = 2u;               // flags[2] bit: a device limit was hit
 
@@ -155,7 +156,10 @@ GS_DEV uint32_t emit_tail(const InListArgs &a, const uint32_t *lst, uint32_t k, 
 // the bin (u16) at region_lt[b*kBinCap ...].  Each target is drawn once, here:
 // a Philox4x32-10 draw is ~40 quarter-rate multiplies, so redrawing it in
 // inl_sort would cost more than carrying 2 bytes.
+template <uint32_t CHUNK>
 __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
+    constexpr uint32_t kChunk = CHUNK;                 // sources of this block
+    constexpr uint32_t kBinPer = kChunk / kInlThreads;  // per thread
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     const CsrPlan &p = a.p;
     // Per-bin state is 16-bit (every count, start and cursor is <= kChunk,
@@ -1017,8 +1021,10 @@ CsrPlan csr_plan(uint32_t n) {
         p.bin = kBin;
         p.logbin = kBinLog;
         p.nb = nb_binned;
-        p.ba = (uint32_t)(((u64)n + kChunk - 1) / kChunk);
-        p.chunk = kChunk;
+        // small networks: shorter chunks, so the partition fills the chip
+        // (2^20 nodes: 512 blocks instead of 128)
+        p.chunk = n >= (1u << 22) ? kChunk : kChunkSmall;
+        p.ba = (uint32_t)(((u64)n + p.chunk - 1) / p.chunk);
         p.tailcap = n / 32u + 1024u;
         return p;
     }
@@ -1084,10 +1090,10 @@ hipError_t launch_build_bins(const InListArgs &a, hipStream_t s) {
     const CsrPlan &p = a.p;
     if (p.n == 0) return hipSuccess;
     if (!p.binned || p.dlv) return hipErrorInvalidValue;
-    const size_t lds_bin = ((size_t)kChunk + kChunk / 2 + (p.nb + 1) / 2) * sizeof(uint32_t) +
+    const size_t lds_bin = ((size_t)p.chunk + p.chunk / 2 + (p.nb + 1) / 2) * sizeof(uint32_t) +
                            (size_t)2 * p.nb * sizeof(uint16_t);
-    hipError_t e = hipFuncSetAttribute((const void *)inl_bin, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds_bin);
+    const void *kb = p.chunk == kChunk ? (const void *)inl_bin<kChunk> : (const void *)inl_bin<kChunkSmall>;
+    hipError_t e = hipFuncSetAttribute(kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bin);
     if (e != hipSuccess) return e;
     const uint32_t sl = sort_split_log(p.nb);
     if (sl > 0) {  // the split sort cannot clear the fill counts itself
@@ -1099,7 +1105,8 @@ hipError_t launch_build_bins(const InListArgs &a, hipStream_t s) {
     ab.lvm = ab.cpm = nullptr;  // no node maps in this phase (inl_zl writes zl)
     ab.zl = nullptr;
     ab.rows = nullptr;
-    hipLaunchKernelGGL(inl_bin, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
+    if (p.chunk == kChunk) hipLaunchKernelGGL(inl_bin<kChunk>, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
+    else hipLaunchKernelGGL(inl_bin<kChunkSmall>, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
     return hipGetLastError();
 }
 
@@ -1128,8 +1135,9 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
     const CsrPlan &p = a.p;
     if (p.n == 0) return hipSuccess;
     if (p.binned) {
-        const size_t lds_bin = ((size_t)kChunk + kChunk / 2 + (p.nb + 1) / 2) * sizeof(uint32_t) +
+        const size_t lds_bin = ((size_t)p.chunk + p.chunk / 2 + (p.nb + 1) / 2) * sizeof(uint32_t) +
                                (size_t)2 * p.nb * sizeof(uint16_t);
+        const void *kb = p.chunk == kChunk ? (const void *)inl_bin<kChunk> : (const void *)inl_bin<kChunkSmall>;
         const uint32_t sl = sort_split_log(p.nb);
         const size_t lds_sort = ((size_t)(kBin >> sl) / 2 + (kBinCap >> sl)) * sizeof(uint32_t);
         const uint32_t dsl = dlv_split_log(p.nb);
@@ -1139,8 +1147,7 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
                                                           : (const void *)inl_sort_dlv<kSplitLog + 2u>)
                                : (sl == 0 ? (const void *)inl_sort<0> : sl == 1 ? (const void *)inl_sort<1>
                                                                                : (const void *)inl_sort<2>);
-        hipError_t e = hipFuncSetAttribute((const void *)inl_bin, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)lds_bin);
+        hipError_t e = hipFuncSetAttribute(kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bin);
         if (e == hipSuccess)
             e = hipFuncSetAttribute(ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(p.dlv ? lds_dlv : lds_sort));
         if (e != hipSuccess) return e;
@@ -1181,7 +1188,8 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
                 e = hipMemsetAsync(a.scratch, 0, (size_t)p.nb * sizeof(uint32_t), s);
                 if (e != hipSuccess) return e;
             }
-            hipLaunchKernelGGL(inl_bin, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
+            if (p.chunk == kChunk) hipLaunchKernelGGL(inl_bin<kChunk>, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
+            else hipLaunchKernelGGL(inl_bin<kChunkSmall>, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
             const dim3 gs(p.nb, 1u << sl);
             if (sl == 0) hipLaunchKernelGGL(inl_sort<0>, gs, dim3(kInlThreads), lds_sort, s, ab);
             else if (sl == 1) hipLaunchKernelGGL(inl_sort<1>, gs, dim3(kInlThreads), lds_sort, s, ab);
