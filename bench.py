@@ -230,6 +230,8 @@ def main():
     fk = dict(churn=args.faults[0], drop_push=args.faults[1], drop_pull=args.faults[2])
     if args.schedule != "2P":
         fk["schedule"] = args.schedule
+    if dist is not None and args.mode == "slices" and R < world:
+        args.mode = "nodes"  # fewer rumors than ranks: slice the nodes instead
     if dist is not None and args.mode == "slices":
         from safe_gossip_amd.sliced import SlicedNetwork
         net = SlicedNetwork(n, R, world, seed=args.seed, epoch=0, device=local, transport="dist", **fk)
