@@ -372,6 +372,11 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
     uint4 stv[kNpl];
 #pragma unroll
     for (uint32_t q = 0; q < kNpl; ++q) stv[q] = q < nv ? st[q] : make_uint4(0u, 0u, 0u, 0u);
+    // rumor slice: an earlier round's network empty counts (pull | push << 8)
+    uint32_t eav[kNpl];
+#pragma unroll
+    for (uint32_t q = 0; q < kNpl; ++q)
+        eav[q] = (a.eadd && q < nv) ? reinterpret_cast<const uint16_t *>(a.eadd)[x0 + q] : 0u;
 
     // ---- push codes of round t+1 for the in-list build (4 B per node)
     {
@@ -438,8 +443,16 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
         if (q >= nv) break;
         const bool on = (onM & M[q]) != 0;
         uint4 v = stv[q];
-        v.x += d_empty_pull[q];                       // empty_pull_sent
-        v.y += (on && live[q] == 0u) ? 1u : 0u;       // empty_push_sent
+        const uint32_t d_empty_push = (on && live[q] == 0u) ? 1u : 0u;
+        if (a.emin) {  // rumor slice: empty only if empty in every slice (MIN per byte, caller)
+            reinterpret_cast<uint16_t *>(a.emin)[x0 + q] =
+                (uint16_t)(min(d_empty_pull[q], 255u) | (d_empty_push << 8));
+            v.x += eav[q] & 0xFFu;
+            v.y += eav[q] >> 8;
+        } else {
+            v.x += d_empty_pull[q];                   // empty_pull_sent
+            v.y += d_empty_push;                      // empty_push_sent
+        }
         v.z += live[q] + d_full[q];                   // full_message_sent
         v.w += recv[q];                               // full_message_received
         st[q] = v;

@@ -660,8 +660,7 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         // build.  SAFE_GOSSIP_AMD_NO_DLV=1 forces gathers.
         const char *v = std::getenv("SAFE_GOSSIP_AMD_NO_DLV");
         const bool off = v && *v && *v != '0';
-        // (not in a rumor slice: its kernels count empty RPCs in place)
-        e->dlv = !off && !e->seq && !e->shard && !e->slice && g.small && g.rpad <= 16 && gs::dlv_plan(n).binned;
+        e->dlv = !off && !e->seq && !e->shard && g.small && g.rpad <= 16 && gs::dlv_plan(n).binned;
     }
     {
         const char *v = std::getenv("SAFE_GOSSIP_AMD_DLV_PACK");

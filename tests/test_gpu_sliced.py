@@ -69,6 +69,16 @@ def test_sliced_larger(engine, world, R):
     run_parity(engine, 20000, R, "origins", check_every=4, make_net=_maker(world))
 
 
+@pytest.mark.parametrize("pack", ["0", "u64", "u32x1", "default"])
+def test_sliced_delivery_records(engine, monkeypatch, pack):
+    # slices of R_g <= 16 run the delivery-record kernels (gs_dlv4.hip, and the
+    # node-per-lane DLV kernel); config-5 faults
+    if pack != "default":
+        monkeypatch.setenv("SAFE_GOSSIP_AMD_DLV_PACK", pack)
+    run_parity(engine, 700, 24, "origins", make_net=_maker(3), faults=(0.05, 0.05, 0.05))
+    run_parity(engine, 2000, 16, "reinject", make_net=_maker(2))
+
+
 def test_sliced_clear_and_counts(engine):
     from safe_gossip_amd.sliced import SlicedNetwork
     n, R = 500, 40
