@@ -42,6 +42,21 @@ import numpy as np
 from . import GossipError, Network, NoPeers, RoundReport, Statistics, _check
 
 
+def merge_known(per, bounds, n: int, kw: int) -> np.ndarray:
+    """Known-rumor words of the network (n x kw) from each slice's words
+    (slice g: rumors [bounds[g], bounds[g+1]) as its bits 0..), each word
+    shifted to its rumor offset -- no per-bit expansion."""
+    out = np.zeros((n, kw), dtype=np.uint64)
+    for k, lo in zip(per, bounds[:-1]):
+        sh = np.uint64(lo % 64)
+        for w in range(k.shape[1]):
+            j = lo // 64 + w
+            out[:, j] |= k[:, w] << sh
+            if sh and j + 1 < kw:
+                out[:, j + 1] |= k[:, w] >> (np.uint64(64) - sh)
+    return out
+
+
 class _Slice:
     """One rank's engine (rumors [lo, hi)) and its empty-count buffers."""
 
@@ -297,12 +312,7 @@ class SlicedNetwork:
     def known_all(self) -> np.ndarray:
         self._flush()
         per = self._gather([s.net.known_all() for s in self.slices])
-        bits = [np.unpackbits(k.view(np.uint8), axis=1, bitorder="little")[:, :s1 - s0]
-                for k, s0, s1 in zip(per, self.bounds[:-1], self.bounds[1:])]
-        allb = np.concatenate(bits, axis=1)
-        pad = np.zeros((self.n, self.kw * 64), dtype=np.uint8)
-        pad[:, :self.R] = allb
-        return np.packbits(pad, axis=1, bitorder="little").view(np.uint64)
+        return merge_known(per, self.bounds, self.n, self.kw)
 
     def known_counts(self, min_known: Optional[int] = None):
         """(known node-rumor pairs, nodes knowing >= min_known rumors; default R)."""
