@@ -218,4 +218,37 @@ GS_DEV uint32_t block_exclusive_scan_t(uint32_t v, uint32_t *lds, uint32_t &tota
     return wbase + inc - v;
 }
 
+// Keep the bits of m at multiples of W = 2^logw (W <= 8), packed to the bottom.
+GS_DEV u64 compress_stride(u64 m, uint32_t logw) {
+    if (logw == 1u) {
+        m &= 0x5555555555555555ull;
+        m = (m | (m >> 1)) & 0x3333333333333333ull;
+        m = (m | (m >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+        m = (m | (m >> 4)) & 0x00FF00FF00FF00FFull;
+        m = (m | (m >> 8)) & 0x0000FFFF0000FFFFull;
+        m = (m | (m >> 16)) & 0x00000000FFFFFFFFull;
+    } else if (logw == 2u) {
+        m &= 0x1111111111111111ull;
+        m = (m | (m >> 3)) & 0x0303030303030303ull;
+        m = (m | (m >> 6)) & 0x000F000F000F000Full;
+        m = (m | (m >> 12)) & 0x000000FF000000FFull;
+        m = (m | (m >> 24)) & 0x000000000000FFFFull;
+    } else if (logw == 3u) {
+        m &= 0x0101010101010101ull;
+        m = (m | (m >> 7)) & 0x0003000300030003ull;
+        m = (m | (m >> 14)) & 0x0000000F0000000Full;
+        m = (m | (m >> 28)) & 0x00000000000000FFull;
+    }
+    return m;
+}
+// OR / AND of each aligned group of W bits, into the group's lowest bit.
+GS_DEV u64 group_or_bits(u64 m, uint32_t logw) {
+    for (uint32_t o = 1; o < (1u << logw); o <<= 1) m |= m >> o;
+    return m;
+}
+GS_DEV u64 group_and_bits(u64 m, uint32_t logw) {
+    for (uint32_t o = 1; o < (1u << logw); o <<= 1) m &= m >> o;
+    return m;
+}
+
 }  // namespace gs

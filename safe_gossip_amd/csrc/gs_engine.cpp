@@ -70,6 +70,10 @@ struct gs_engine {
     // SAFE_GOSSIP_AMD_DLV_PACK = 0 one node per lane, u64 four 16-bit nodes
     // per 64-bit lane word, otherwise (default) a 32-bit lane word
     uint32_t dlv_pack = 1;
+    // SAFE_GOSSIP_AMD_PIPE=1: the wide 2P gather path runs the pipelined
+    // round kernel (gs_pipe.hip) instead of round_kernel
+    bool no_pipe = false;
+    uint32_t pipe_grid = 0;  // SAFE_GOSSIP_AMD_PIPE_GRID: fewer blocks (tests: many tiles per block)
     // Sparse records (wide 2P engine, W <= 8; gs_kernels.h RoundArgs): maps of
     // plane buffer i, the accounting words and MODE-1 launches counted in them
     // The sparse variant runs while the input planes are at least a quarter
@@ -362,6 +366,8 @@ gs::RoundArgs base_args(gs_engine *e) {
     }
     a.obs_only = 0xFFFFFFFFu;
     a.dlv_pack = e->dlv_pack;
+    a.no_pipe = e->no_pipe ? 1u : 0u;
+    a.pipe_grid = e->pipe_grid;
     a.g = e->g;
     a.seed = e->seed;
     a.epoch = e->epoch;
@@ -653,7 +659,6 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         g.units = (n + npu - 1) / npu;
         g.nseg = n;
     }
-    const size_t sw = (size_t)g.units * gs::kPlanes * g.W;
     {
         // Delivery records (DLV) for small R in the 2P schedule: every
         // class-plane gather but one is replaced by records of the in-list
@@ -689,6 +694,12 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         e->keys[r] = std::string(k, 12);
         e->key_rumor[e->keys[r]] = r;
         e->key_order[r] = r;
+    }
+    {
+        const char *v = std::getenv("SAFE_GOSSIP_AMD_PIPE");
+        e->no_pipe = !(v && *v == '1');  // opt-in: measured slower than round_kernel
+        const char *gv = std::getenv("SAFE_GOSSIP_AMD_PIPE_GRID");
+        e->pipe_grid = gv ? (uint32_t)std::strtoul(gv, nullptr, 10) : 0u;
     }
     {
         const char *v = std::getenv("SAFE_GOSSIP_AMD_CONCURRENT_INLISTS");
@@ -734,25 +745,28 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
     }
     if (ok && e->shard) ok = hipEventCreateWithFlags(&e->ev_main, hipEventDisableTiming) == hipSuccess;
     const gs::InListSizes isz = gs::inlist_sizes(e->plan);
+    // per-node arrays the pipelined round kernel reads by whole 64-node tiles
+    const size_t npad = gs::pipe_padded(n);
+    const size_t sw_pad = (size_t)gs::pipe_padded(g.units) * gs::kPlanes * g.W;
     for (int i = 0; i < 2 && ok && !e->shard; ++i) {
         auto &c = e->csr[i];
         ok = hipEventCreateWithFlags(&e->ev_built[i], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&e->ev_read[i], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&e->ev_binned[i], hipEventDisableTiming) == hipSuccess &&
-             dalloc(&c.src, isz.src_words) == hipSuccess && dalloc(&c.tg, n) == hipSuccess &&
+             dalloc(&c.src, isz.src_words) == hipSuccess && dalloc(&c.tg, npad) == hipSuccess &&
              dalloc(&c.region, isz.region_words) == hipSuccess &&
              dalloc(&c.scratch, isz.scratch_words) == hipSuccess &&
              hipMemset(c.scratch, 0, std::max<size_t>(isz.scratch_words, 1) * sizeof(uint32_t)) == hipSuccess;
         if (ok && e->dlv) {
             ok = dalloc(&c.DR, n) == hipSuccess && dalloc(&c.pull, n) == hipSuccess;
         } else if (ok) {
-            ok = dalloc(&c.IN8, n) == hipSuccess && dalloc(&c.SIB8, n) == hipSuccess &&
+            ok = dalloc(&c.IN8, npad) == hipSuccess && dalloc(&c.SIB8, npad) == hipSuccess &&
                  hipMemset(c.SIB8, 0, std::max<size_t>(n, 1) * sizeof(gs::SibRec)) == hipSuccess;
             if (ok && e->filt) ok = dalloc(&c.zl, gs::node_map_words(n)) == hipSuccess;
         }
     }
-    ok = ok && dalloc(&e->S[0], sw) == hipSuccess && dalloc(&e->S[1], sw) == hipSuccess &&
-         dalloc(&e->flags, 4) == hipSuccess && dalloc(&e->st32, (size_t)4 * n) == hipSuccess &&
+    ok = ok && dalloc(&e->S[0], sw_pad) == hipSuccess && dalloc(&e->S[1], sw_pad) == hipSuccess &&
+         dalloc(&e->flags, 4) == hipSuccess && dalloc(&e->st32, (size_t)4 * npad) == hipSuccess &&
          dalloc(&e->st64, (size_t)4 * n) == hipSuccess;
     if (ok && e->dlv) ok = dalloc(&e->pc, n) == hipSuccess;
     if (ok && e->filt)
@@ -1629,6 +1643,9 @@ gs_status gs_handle_received(gs_engine *e, uint32_t node, uint32_t peer, const u
     if (empty) {
         info |= gs::kExtEmpty;
     } else {
+        // the copy creates or updates an entry: messages() is no longer empty,
+        // so Gossiper::add_peer refuses from now on (src/gossiper.rs:45-52)
+        e->started = true;
         info |= rumor | ((uint32_t)counter << 12) | gs::kExtRec;
         // only the last copy from a peer is kept in peer_counters (BTreeMap::insert)
         for (auto &x : e->ext)

@@ -92,6 +92,8 @@ struct RoundArgs {
     // transition launch (gs_slice_defer: no separate apply pass).
     uint8_t *emin;
     const uint8_t *eadd;
+    uint32_t no_pipe;         // 1: the wide 2P path runs round_kernel instead of round_pipe
+    uint32_t pipe_grid;       // round_pipe's block count (0: every resident block)
     uint32_t dlv_pack;        // DLV transition launches: 0 one node per lane, 1 a 32-bit lane
                               // word of several nodes, 2 a 64-bit one (gs_dlv4.hip)
     Geometry g;
@@ -117,6 +119,15 @@ hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s);
 // DLV transition launches (modes 0 and 1, no external RPCs) with four nodes
 // per lane (gs_dlv4.hip).
 hipError_t launch_round_dlv4(const RoundArgs &a, int mode, hipStream_t s);
+// The pipelined round kernel of the wide 2P gather path (gs_pipe.hip): modes
+// 0 and 1, W = 2 / 4 / 8, the whole grid, no sparse records.
+bool pipe_eligible(const RoundArgs &a, int mode);
+// Its tiles are 64 nodes; every per-node array it reads (planes, InRec,
+// SibRec, target words, Statistics deltas) is allocated for n rounded up to
+// whole tiles, since the last tile's DMA reads past n.
+constexpr uint32_t kPipeTileNodes = 64;
+inline uint64_t pipe_padded(uint64_t n) { return (n + kPipeTileNodes - 1) / kPipeTileNodes * kPipeTileNodes; }
+hipError_t launch_round_pipe(const RoundArgs &a, int mode, hipStream_t s);
 
 // Plan of the in-list build (gs_inlist.hip).
 struct CsrPlan {

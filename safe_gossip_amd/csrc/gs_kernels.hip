@@ -25,111 +25,13 @@
 // all issued together, one dependent level after the coalesced reads.
 #include "gs_kernels.h"
 #include "gs_device.h"
+#include "gs_recv.h"
 
 namespace gs {
 
 // Words of planes one 256-lane block owns (its records are contiguous).
 constexpr uint32_t kBlockWords = 256u * kPlanes;
 constexpr uint32_t kStageIters = kBlockWords / 2u / 256u;  // uint4 loads per thread
-
-// Gathers issued in the first batch: pushers (in-degree is Poisson(1): <= 3
-// for 98% of nodes) and pushers of t(x) ahead of x (rank <= 2 for 98.6%).
-#ifndef GS_BATCH_K
-#define GS_BATCH_K 3
-#endif
-#ifndef GS_BATCH_E
-#define GS_BATCH_E 2
-#endif
-static_assert(GS_BATCH_E <= kSibInline, "SIB records hold kSibInline pushers");
-constexpr uint32_t kBatchK = GS_BATCH_K;
-constexpr uint32_t kBatchE = GS_BATCH_E;
-
-// Receiver-side state of phases 1-2 at x for one segment.  The transition
-// path keeps one bit-sliced counter of the recorded counters that vote ">= own"
-// (MessageState::next_round's greater_or_equal, src/message_state.rs:118-129);
-// the observation path (OBS) keeps the two counters the parity dumps report.
-template <bool OBS>
-struct Recv {
-    u64 notyet;          // still absent: the next live copy creates the entry
-    u64 recB;            // entries in state B (existing or created): record copies
-    u64 oc1;             // B entries whose our_counter is 1 (created ones included)
-    u64 crB, crC;        // created this round as B{0,1} / C{0,0}
-    u64 anyC;            // a recorded counter >= counter_max
-    u64 cv[5];           // #recorded counters >= our_counter (and < counter_max)
-    u64 c1[5];           // OBS only: #recorded counters in [1, counter_max)
-    u64 c2[5];           // OBS only: #recorded counters == 2 (< counter_max)
-    uint32_t part_cw;    // sum over pushers i of (k-1-i) * |created by i|
-    uint32_t first_create;
-    uint32_t recv;       // copies received (push rows + pull row)
-
-    GS_DEV void init(u64 A, u64 B, u64 Boc1) {
-        notyet = A;
-        recB = B;
-        oc1 = Boc1;
-        crB = crC = anyC = 0;
-#pragma unroll
-        for (int i = 0; i < 5; ++i) cv[i] = 0;
-        if constexpr (OBS) {
-#pragma unroll
-            for (int i = 0; i < 5; ++i) c1[i] = c2[i] = 0;
-        }
-        part_cw = 0;
-        first_create = kNone;
-        recv = 0;
-    }
-    // Record copies `rec` of class (vB: a B counter, v2: counter 2, vC: 255).
-    GS_DEV void record(u64 rec, u64 vB, u64 v2, u64 vC) {
-        anyC |= rec & vC;
-        add5(cv, rec & vB & (v2 | oc1));
-        if constexpr (OBS) {
-            add5(c1, rec & vB);
-            add5(c2, rec & v2);
-        }
-    }
-    GS_DEV void create(u64 newc, u64 vC) {
-        crB |= newc & ~vC;
-        crC |= newc & vC;
-        recB |= newc & ~vC;
-        oc1 |= newc & ~vC;
-        notyet &= ~newc;
-    }
-    // One batch x absorbs (Gossip::receive, src/gossip.rs:153-163) with
-    // copies of class vB (counter < counter_max; v2: counter 2) or vC (255).
-    // `rafter` = pull rows x sends after it (they include what it creates),
-    // `ev` = its position among x's batches; `recm` masks out the rumors whose
-    // copy a later copy from the same peer overwrites (message_state.rs:79).
-    GS_DEV void absorb(u64 vB, u64 v2, u64 vC, uint32_t rafter, uint32_t ev, u64 recm) {
-        const u64 sl = vB | vC;                // the batch
-        const u64 newc = notyet & sl;          // new_from_peer: not recorded
-        record(recB & sl & recm, vB, v2, vC);  // MessageState::receive on B
-        create(newc, vC);
-        const uint32_t pc = popc(newc);
-        part_cw += rafter * pc;
-        if (pc && first_create == kNone) first_create = ev;
-        recv += popc(sl);
-    }
-    // Push batch of pusher i of k (2P: pushers in ascending order, all
-    // answered; `rec_on` is false for t(x)'s own push, superseded by its pull).
-    GS_DEV void push(const Cls &q, uint32_t i, uint32_t k, bool rec_on) {
-        const u64 vC = q.c & ~(q.a0 & q.a1);   // C: counter 255
-        const u64 vB = ~q.c & (q.a0 | q.a1);   // B: counter = our_counter
-        const u64 v2 = vB & q.a1 & ~q.a0;      // B with our_counter 2
-        const u64 sl = vB | vC;                // the push batch
-        const u64 newc = notyet & sl;          // new_from_peer: not recorded
-        if (rec_on) record(recB & sl, vB, v2, vC);  // MessageState::receive on B
-        create(newc, vC);
-        const uint32_t pc = popc(newc);
-        part_cw += (k - 1u - i) * pc;  // later pushers' pull rows include it
-        if (pc && first_create == kNone) first_create = i;
-        recv += popc(sl);
-    }
-    GS_DEV void absorb_cls(const Cls &q, uint32_t rafter, uint32_t ev, bool rec_on) {
-        const u64 vC = q.c & ~(q.a0 & q.a1);   // C: counter 255
-        const u64 vB = ~q.c & (q.a0 | q.a1);   // B: counter = our_counter
-        const u64 v2 = vB & q.a1 & ~q.a0;      // B with our_counter 2
-        absorb(vB, v2, vC, rafter, ev, rec_on ? ~0ull : 0ull);
-    }
-};
 
 #ifndef GS_RK_MINW
 #define GS_RK_MINW 1
@@ -181,39 +83,6 @@ GS_DEV bool chunk_zero(u64 word, uint32_t bit, uint32_t logw) {
     const u64 m = logw ? 3ull : 1ull;
     return ((word >> bit) & m) == m;
 }
-// Keep the bits of m at multiples of W = 2^logw (W <= 8), packed to the bottom.
-GS_DEV u64 compress_stride(u64 m, uint32_t logw) {
-    if (logw == 1u) {
-        m &= 0x5555555555555555ull;
-        m = (m | (m >> 1)) & 0x3333333333333333ull;
-        m = (m | (m >> 2)) & 0x0F0F0F0F0F0F0F0Full;
-        m = (m | (m >> 4)) & 0x00FF00FF00FF00FFull;
-        m = (m | (m >> 8)) & 0x0000FFFF0000FFFFull;
-        m = (m | (m >> 16)) & 0x00000000FFFFFFFFull;
-    } else if (logw == 2u) {
-        m &= 0x1111111111111111ull;
-        m = (m | (m >> 3)) & 0x0303030303030303ull;
-        m = (m | (m >> 6)) & 0x000F000F000F000Full;
-        m = (m | (m >> 12)) & 0x000000FF000000FFull;
-        m = (m | (m >> 24)) & 0x000000000000FFFFull;
-    } else if (logw == 3u) {
-        m &= 0x0101010101010101ull;
-        m = (m | (m >> 7)) & 0x0003000300030003ull;
-        m = (m | (m >> 14)) & 0x0000000F0000000Full;
-        m = (m | (m >> 28)) & 0x00000000000000FFull;
-    }
-    return m;
-}
-// OR / AND of each aligned group of W bits, into the group's lowest bit.
-GS_DEV u64 group_or_bits(u64 m, uint32_t logw) {
-    for (uint32_t o = 1; o < (1u << logw); o <<= 1) m |= m >> o;
-    return m;
-}
-GS_DEV u64 group_and_bits(u64 m, uint32_t logw) {
-    for (uint32_t o = 1; o < (1u << logw); o <<= 1) m &= m >> o;
-    return m;
-}
-
 // SPRK: the sparse-records variant (wide 2P engine, transition modes), launched
 // while a dissemination is young (gs_engine.cpp picks it per round).
 template <bool SMALL, int MODE, bool SHARD, bool SEQ, bool DLV, bool SPRK = false>
@@ -851,100 +720,25 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     u64 Bn = 0, Cn = 0;
     bool on_next = true;
     if (!wtriv) {
-            // Gossip::new_message (insert = replace with MessageState::new, records
+        // Gossip::new_message (insert = replace with MessageState::new, records
         // dropped) for the rumors injected at x this round.
         u64 inj = 0;
-        if (a.n_inj && valid) {
-            const u64 key = SMALL ? (u64)x : seg;
-            uint32_t lo = 0, hi = a.n_inj;
-            while (lo < hi) {
-                uint32_t mid = (lo + hi) >> 1;
-                if (a.inj_key[mid] < key) lo = mid + 1; else hi = mid;
-            }
-            if (lo < a.n_inj && a.inj_key[lo] == key) inj = a.inj_mask[lo] & L.m;
-        }
-        const u64 ninj = ~inj;
-        const u64 Bold = B & ninj, Cold = C & ninj, Dold = D & ninj;
-        const u64 cB = crB & ninj, cC = crC & ninj;
-        const u64 Bf = Bold | cB | inj;  // entries in state B entering next_round
-        const u64 Cf = Cold | cC;        // entries in state C entering next_round
-
-        // B (src/message_state.rs:94-147).  0-filled peers vote "less", so with
-        // no C copy the median rule is: bump iff 2*ge > |P| iff ge >= |P|/2+1.
-        const u64 oc1 = (Bold & a0 & ~a1) | cB | inj;
-        const u64 oc2 = Bold & a1 & ~a0;
-        const uint32_t thr = psize / 2u + 1u;
-        // Churn: a node offline in round t+1 skips next_round; it keeps its
-        // pre-transition state (created entries folded in as B{0,1} / C{0,0}) and
-        // the two per-rumor votes next_round will use (bump, anyC) in `pend`.  A
-        // node returning from offline (off_t) takes its votes from there.
+        if (a.n_inj && valid) inj = find_injection(a, SMALL ? (u64)x : seg) & L.m;
+        // Churn: a node offline in round t+1 skips next_round (its votes go to
+        // `pend`); a node returning from offline (off_t) takes them from there.
         on_next = !(a.f.churn && valid && offline_of(a.seed, a.epoch, a.round_new, a.node_lo + x, a.f.churn));
-        u64 bump, anyCe;
-        if (off_t && valid) {
-            const u64 pidx = ((u64)x * 2u) * g.W + L.j;
-            bump = a.pend[pidx] & Bold;
-            anyCe = a.pend[pidx + g.W] & ninj;
-        } else {
-            bump = ge_k<5>(rv.cv, thr) & (Bold | cB);  // cv counts only B entries' votes
-            anyCe = anyC & ninj;
-        }
-        u64 nr[6];  // round + 1
-        {
-            u64 carry = ~0ull;
-    #pragma unroll
-            for (int i = 0; i < 5; ++i) {
-                const u64 rb = P[3 + i] & Bold;
-                nr[i] = rb ^ carry;
-                carry &= rb;
-            }
-            nr[5] = carry;
-        }
-        const u64 toD = ge_u<6>(nr, a.maxr);
-        const u64 oc1n = oc1 & ~bump;
-        const u64 oc2n = (oc1 & bump) | (oc2 & ~bump);
-        const u64 oc3n = oc2 & bump;
-        const u64 ocge = a.cmax <= 1u ? ~0ull : (a.cmax == 2u ? (oc2n | oc3n) : oc3n);
-        const u64 toC = anyCe | ocge;
-        const u64 BD = Bf & toD, BC = Bf & ~toD & toC, BB = Bf & ~toD & ~toC;
-
-        // C (src/message_state.rs:148-168): round+1; D if round+rib >= max_rounds
-        // or round >= max_c_rounds.
-        const u64 cr0 = a0 & Cold, cr1 = a1 & Cold;
-        const u64 d[3] = {~cr0, cr1 ^ cr0, cr1 & cr0};
-        u64 rib[5];
-    #pragma unroll
-        for (int i = 0; i < 5; ++i) rib[i] = P[3 + i] & Cold;
-        u64 sum[6];
-        {
-            u64 c = 0;
-    #pragma unroll
-            for (int i = 0; i < 5; ++i) {
-                const u64 di = i < 3 ? d[i] : 0ull;
-                sum[i] = rib[i] ^ di ^ c;
-                c = (rib[i] & di) | (c & (rib[i] ^ di));
-            }
-            sum[5] = c;
-        }
-        const u64 CtoD = ge_u<6>(sum, a.maxr) | ge_u<3>(d, a.maxc);
-        const u64 CD = Cf & CtoD, CC = Cf & ~CtoD;
-
-        const u64 Dn = BD | CD | Dold;
-        Cn = BC | CC;
-        Bn = BB;
-        N[0] = Cn | Dn;
-        N[1] = (Bn & oc1n) | (CC & d[0]) | Dn;
-        N[2] = (Bn & oc2n) | (CC & d[1]) | Dn;
-    #pragma unroll
-        for (int i = 0; i < 5; ++i) N[3 + i] = ((Bn | BC) & nr[i]) | (CC & rib[i]);
+        const u64 pidx = ((u64)x * 2u) * g.W + L.j;
+        const bool pending = off_t && valid;
+        const u64 pb = pending ? a.pend[pidx] : 0ull, pa = pending ? a.pend[pidx + g.W] : 0ull;
+        NextOut o;
+        next_round_seg(P, rv, inj, psize, pending, pb, pa, on_next, a.cmax, a.maxc, a.maxr, o);
+#pragma unroll
+        for (int p = 0; p < kPlanes; ++p) N[p] = o.N[p];
+        Bn = o.Bn;
+        Cn = o.Cn;
         if (!on_next) {  // frozen: pre-transition planes + votes (the lane is valid)
-            N[0] = (isC & ninj) | cC;
-            N[1] = (a0 & ninj) | cB | inj;
-            N[2] = a1 & ninj;
-    #pragma unroll
-            for (int i = 0; i < 5; ++i) N[3 + i] = P[3 + i] & ninj;
-            const u64 pidx = ((u64)x * 2u) * g.W + L.j;
-            a.pend[pidx] = bump;
-            a.pend[pidx + g.W] = anyCe & (Bold | cB);
+            a.pend[pidx] = o.bump;
+            a.pend[pidx + g.W] = o.anyC;
         }
     }
 
@@ -1171,6 +965,7 @@ hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s) {
         if (a.dlv_pack && (mode == 0 || mode == 1) && a.n_ext == 0) return launch_round_dlv4(a, mode, s);
         return launch_mode<true, false, false, true>(a, mode, s);
     }
+    if (!a.no_pipe && pipe_eligible(a, mode)) return launch_round_pipe(a, mode, s);  // gs_pipe.hip
     return a.g.small ? launch_mode<true, false, false>(a, mode, s) : launch_mode<false, false, false>(a, mode, s);
 }
 

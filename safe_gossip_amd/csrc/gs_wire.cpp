@@ -53,13 +53,15 @@ gs_status gs_rpc_encode(int pull, const uint8_t *msg, uint32_t msg_len, uint8_t 
 gs_status gs_rpc_decode(const uint8_t *buf, uint32_t len, int *pull, uint32_t *msg_off, uint32_t *msg_len,
                         uint8_t *counter) {
     if (!buf || !pull || !msg_off || !msg_len || !counter) return GS_ERR_INVALID_ARGUMENT;
-    // Message::deserialise (cfg(test)) = bincode::deserialize::<GossipRpc>:
-    // an unknown variant or a short buffer is a serialisation error
+    // Message::deserialise (cfg(test)) = maidsafe_utilities::serialisation::
+    // deserialise::<GossipRpc> (src/messages.rs:53): an unknown variant or a
+    // short buffer is a serialisation error, and so are bytes left over after
+    // the RPC (that crate's DeserialiseExtraBytes; recalled, not vendored here)
     if (len < 13) return GS_ERR_SERIALISATION;
     const uint32_t v = get_u32(buf);
     if (v > 1) return GS_ERR_SERIALISATION;
     const uint64_t m = get_u64(buf + 4);
-    if (m > (uint64_t)len - 13) return GS_ERR_SERIALISATION;
+    if (m != (uint64_t)len - 13) return GS_ERR_SERIALISATION;
     *pull = (int)v;
     *msg_off = 12;
     *msg_len = (uint32_t)m;
@@ -84,11 +86,13 @@ gs_status gs_message_wrap(const uint8_t *payload, uint32_t len, const uint8_t si
 gs_status gs_message_unwrap(const uint8_t *buf, uint32_t len, uint32_t *payload_off, uint32_t *payload_len,
                             uint32_t *signature_off) {
     if (!buf || !payload_off || !payload_len || !signature_off) return GS_ERR_INVALID_ARGUMENT;
+    // serialisation::deserialise::<Message> (src/messages.rs:37): exactly one
+    // wrapper, no bytes after the signature
     if (len < 16) return GS_ERR_SERIALISATION;
     const uint64_t m = get_u64(buf);
     if (m > (uint64_t)len - 16) return GS_ERR_SERIALISATION;
     const uint64_t s = get_u64(buf + 8 + m);
-    if (s != 64 || (uint64_t)len < 16 + m + 64) return GS_ERR_SERIALISATION;
+    if (s != 64 || (uint64_t)len != 16 + m + 64) return GS_ERR_SERIALISATION;
     *payload_off = 8;
     *payload_len = (uint32_t)m;
     *signature_off = (uint32_t)(16 + m);

@@ -158,8 +158,8 @@ def _worker(rank, world, port, cases, q, backend="gloo"):
         def make(n, R, seed, epoch, params, **faults):
             return SlicedNetwork(n, R, world, seed=seed, epoch=epoch, params=params, device=0,
                                  transport="dist", **faults)
-        for n, R, kind, faults in cases:
-            run_parity(sg, n, R, kind, make_net=make, faults=faults)
+        for n, R, kind, faults, *every in cases:
+            run_parity(sg, n, R, kind, make_net=make, faults=faults, check_every=every[0] if every else 1)
         q.put(("ok", rank))
     except BaseException as e:
         q.put(("fail", f"rank {rank}: {type(e).__name__}: {e}"))
@@ -197,3 +197,12 @@ def test_sliced_dist_rccl_single_rank(engine):
     # one RCCL rank: the all-reduce runs asynchronously on the process group's
     # stream and is applied on the engine stream a round later
     _spawn(1, [(300, 64, "trickle", None), (600, 16, "origins", (0.05, 0.05, 0.05))], "nccl")
+
+
+def test_sliced_dist_rccl_deferred(engine):
+    # the bench's path: rounds run unobserved, so each round's all-reduce is
+    # folded into a later round kernel (gs_slice_defer, _apply_pending(keep=1))
+    # instead of being applied by an observer; Statistics checked every 3rd /
+    # 5th round against the oracle
+    _spawn(1, [(300, 64, "trickle", None, 3), (600, 16, "origins", (0.05, 0.05, 0.05), 5),
+               (130, 256, "origins", None, 4)], "nccl")

@@ -52,7 +52,7 @@ def _worker(rank, world, port, n, R, params, kind, q, faults=None):
             if kind == "reinject" and rnd in (1, 2, 4):
                 inj = [(int(rng.integers(n)), int(rng.integers(R))) for _ in range(R)]
             for x, r in inj:
-                if lo <= x < n and lo <= r < hi:
+                if 0 <= x < n and lo <= r < hi:
                     sl.send_new(x, r - lo)
                 if orc:
                     orc.send_new(x, r)
