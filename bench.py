@@ -10,7 +10,8 @@ region).
 value  = n * R * K / wall seconds of K timed rounds (summed over ranks).
 roofline: algorithmic HBM bytes of the round kernel (DESIGN.md "Roofline") per
           launch / its average duration measured with HIP events on the
-          engine's stream over the timed rounds; peak 8.0 TB/s.
+          engine's stream over the timed rounds; peak 8.0 TB/s.  step_frac:
+          the same bytes over the whole step (round kernel + in-list build).
 cpu_baseline: the CPU oracle (reference-faithful port: per-node ordered maps,
           one thread, same 2P schedule) on a bounded sample of the same
           workload (fewer nodes, same R and injection), rank 0 at N=1 only.
@@ -22,15 +23,16 @@ cfg4, the configuration the metric is quoted on that fits one GPU.
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N, or plain
 `python bench.py --gpus N`, which starts that launcher itself): ONE network
-of the same n x R over the N ranks.  Default --mode slices: every rank holds
-all n nodes and R/N of the rumors (safe_gossip_amd.sliced, DESIGN.md section
-7b); rumors evolve independently, so a round's only exchange is one RCCL
-all_reduce(MIN) of 2 bytes per node (the empty-RPC Statistics), overlapped
-with the next round.  --mode nodes: the node range sharded over the ranks
-(safe_gossip_amd.sharded), push and pull rows exchanged
-with RCCL all_to_all_single every round.  Total work is fixed, so "scaling"
-is "strong".  Barrier + synchronize around the timed region, time = max over
-ranks.  The roofline line describes rank 0's round kernel.
+of the same n x R over the N ranks, measured in both multi-GPU modes one after
+the other, and the faster is the headline (the other under "alternative"):
+rumor slices (every rank holds all n nodes and R/N of the rumors,
+safe_gossip_amd.sliced; rumors evolve independently, so
+a round's only exchange is one RCCL all_reduce(MIN) of 2 bytes per node, the
+empty-RPC Statistics, overlapped with the next round) and node-range shards
+(safe_gossip_amd.sharded, DESIGN.md section 7: push and pull rows exchanged
+with RCCL all_to_all_single every round).  --mode slices|nodes measures one.
+Total work is fixed, so "scaling" is "strong".  Barrier + synchronize around
+the timed region, time = max over ranks.  The roofline line describes rank 0's round kernel.
 """
 import argparse
 import json
@@ -75,11 +77,13 @@ def parse():
     p.add_argument("--parts", type=int, default=None,
                    help="pipeline parts per rank (N>1; default 4 with RCCL: the exchanges of one "
                         "part overlap the round kernel of another)")
-    p.add_argument("--mode", default="slices", choices=["slices", "nodes"],
-                   help="N>1 (or --sharded): rumor slices per rank (default) or node-range shards")
+    p.add_argument("--mode", default="both", choices=["both", "slices", "nodes"],
+                   help="N>1: measure both multi-GPU modes and report the faster (default), or only "
+                        "rumor slices per rank / node-range shards; with --sharded at N=1 the "
+                        "default is node shards")
     p.add_argument("--sharded", action="store_true",
-                   help="run the sharded engine even at N=1 (one RCCL rank: exchanges are "
-                        "self-copies; measures the sharded path's overhead and overlap)")
+                   help="run a multi-GPU mode even at N=1 (one RCCL rank: node-shard exchanges are "
+                        "self-copies, the slice all-reduce a no-op; measures that path's overhead)")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (RCCL, one GPU per rank) or gloo (host-staged rows; rehearsal of "
                         "the N>1 path with several ranks on one GPU)")
@@ -193,49 +197,19 @@ def self_launch(args):
     sys.exit(subprocess.run(cmd).returncode)
 
 
-def main():
-    args = parse()
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        self_launch(args)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus:
-        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
-        sys.exit(2)
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    dist = None
-    if world > 1 or args.sharded:
-        if world == 1:
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", "29517")
-            os.environ.setdefault("RANK", "0")
-            os.environ.setdefault("WORLD_SIZE", "1")
-        import torch.distributed as dist
-        if args.dist_backend == "gloo":
-            local = local % torch.cuda.device_count()
-        torch.cuda.set_device(local)
-        dist.init_process_group(args.dist_backend)
-        if dist.get_world_size() != args.gpus:
-            print(f"bench.py: process group of {dist.get_world_size()} ranks, --gpus {args.gpus}",
-                  file=sys.stderr)
-            sys.exit(2)
-    else:
-        torch.cuda.set_device(0)
-
-    import numpy as np
-    import safe_gossip_amd as sg
-
+def run_mode(args, mode, world, rank, local, dist, sg, np, torch, with_spread):
+    """Build the network for `mode` ("single", "slices" or "nodes"), run W
+    warmup rounds of one dissemination, then time exactly K rounds of a fresh
+    one (barrier + synchronize on both sides, max over ranks).  Returns the
+    measurements; the network is closed."""
     n, R = args.nodes, args.rumors
     fk = dict(churn=args.faults[0], drop_push=args.faults[1], drop_pull=args.faults[2])
     if args.schedule != "2P":
         fk["schedule"] = args.schedule
-    if dist is not None and args.mode == "slices" and R < world:
-        args.mode = "nodes"  # fewer rumors than ranks: slice the nodes instead
-    if dist is not None and args.mode == "slices":
+    if mode == "slices":
         from safe_gossip_amd.sliced import SlicedNetwork
         net = SlicedNetwork(n, R, world, seed=args.seed, epoch=0, device=local, transport="dist", **fk)
-    elif dist is not None:
+    elif mode == "nodes":
         from safe_gossip_amd.sharded import ShardedNetwork
         net = ShardedNetwork(n, R, world, seed=args.seed, epoch=0, device=local,
                              transport="dist", parts=args.parts, **fk)
@@ -271,27 +245,103 @@ def main():
                          device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-
     # rounds 2.. run the fused deliver+transition kernel (round 1 has nothing
     # to deliver); that is the dominant kernel the roofline describes.
     kt = ktimes[1:] if len(ktimes) > 1 else ktimes
-    kernel_ms = float(np.mean(kt)) if len(kt) else float("nan")
-    bytes_dense = net.round_kernel_bytes()
-    # algorithmic bytes the timed launches had to move: with sparse records
-    # (wide 2P engine) words known to be zero are neither read nor rewritten
-    # and empty pushes are not gathered, so this is counted by the kernels
-    bytes_per, launches = (net.round_traffic() if hasattr(net, "round_traffic")
-                           else (bytes_dense, 0))
-    achieved = bytes_per / (kernel_ms * 1e-3) / 1e9
+    out = dict(mode=mode, elapsed=elapsed, kt=kt, name=net.round_kernel_name(),
+               bytes_dense=net.round_kernel_bytes(), params=list(net.params),
+               parts=getattr(net, "parts", None))
+    # algorithmic bytes the timed launches had to move: with live-filtered
+    # gathers, only the class rows the flags leave are gathered, so this is
+    # counted by the kernels
+    out["bytes_per"], out["launches"] = (net.round_traffic() if hasattr(net, "round_traffic")
+                                         else (out["bytes_dense"], 0))
+    out["spread"] = spread_run(net, epoch) if with_spread else None
+    net.close()
+    return out
 
-    spread = None if args.no_spread else spread_run(net, epoch)
+
+def parallelism(args, mode, world, parts):
+    backend = "RCCL" if args.dist_backend == "nccl" else args.dist_backend
+    n, R = args.nodes, args.rumors
+    if mode == "slices":
+        return (f"rumor slices x{world} (all {n} nodes, {R // world}-{-(-R // world)} rumors per rank), "
+                + backend + " all_reduce(MIN) of 2 B/node empty-RPC counts per round"
+                + (", overlapped with the next round" if args.dist_backend == "nccl" else ", host-staged"))
+    if mode == "nodes":
+        return (f"node-range shards x{world}, " + backend
+                + f" all-to-all push/pull rows, {parts} pipeline part(s) per rank")
+    return "single-gpu"
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        self_launch(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1 or args.sharded:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29517")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+        import torch.distributed as dist
+        if args.dist_backend == "gloo":
+            local = local % torch.cuda.device_count()
+        torch.cuda.set_device(local)
+        dist.init_process_group(args.dist_backend)
+        if dist.get_world_size() != args.gpus:
+            print(f"bench.py: process group of {dist.get_world_size()} ranks, --gpus {args.gpus}",
+                  file=sys.stderr)
+            sys.exit(2)
+    else:
+        torch.cuda.set_device(0)
+
+    import numpy as np
+    import safe_gossip_amd as sg
+
+    n, R = args.nodes, args.rumors
+    # Modes measured: one GPU runs the single engine; several ranks run both
+    # multi-GPU modes (rumor slices, node shards) one after the other and the
+    # faster is the headline, unless --mode picks one;
+    # --sharded at N = 1 runs the node shards (self-copy exchanges).
+    if dist is None:
+        modes = ["single"]
+    elif args.mode != "both":
+        modes = [args.mode]
+    elif world == 1:
+        modes = ["nodes"]
+    else:
+        modes = ["slices", "nodes"]
+    if R < world:  # fewer rumors than ranks: no rumor slices
+        modes = [m for m in modes if m != "slices"] or ["nodes"]
+    runs = [run_mode(args, m, world, rank, local, dist, sg, np, torch, with_spread=(i == 0 and not args.no_spread))
+            for i, m in enumerate(modes)]
+    best = min(runs, key=lambda r: r["elapsed"])
+    spread = runs[0]["spread"]
+
+    kt = best["kt"]
+    kernel_ms = float(np.mean(kt)) if len(kt) else float("nan")
+    achieved = best["bytes_per"] / (kernel_ms * 1e-3) / 1e9
+    elapsed = best["elapsed"]
+    ms_per_step = elapsed / args.steps * 1e3
+    # the whole step's algorithmic bytes over its wall time: the round kernel's
+    # bytes against the time of the round kernel AND the in-list build
+    step_frac = best["bytes_per"] / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS
 
     # PMC traffic of the same kernel from the committed rocprofv3 run of this
     # workload (profiles/summarize.py writes one file per (nodes, rumors))
     traffic = None
     for name in (f"pmc_n{n}_r{R}.json", "pmc_latest.json"):
         pmc_path = os.path.join(REPO, "profiles", name)
-        if traffic is None and os.path.exists(pmc_path) and world == 1:
+        if traffic is None and os.path.exists(pmc_path) and world == 1 and best["mode"] == "single":
             try:
                 pmc = json.load(open(pmc_path))
                 if pmc.get("nodes") == n and pmc.get("rumors") == R:
@@ -299,11 +349,11 @@ def main():
             except Exception:
                 traffic = None
 
-    cpu = best = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    cpu = cpu_best_line = None
+    if rank == 0 and world == 1 and dist is None and not args.no_cpu_baseline:
         cpu = cpu_baseline(R, args.seed, args.cpu_seconds, args.faults, args.schedule)
         if args.schedule == "2P" and not any(args.faults):
-            best = cpu_best(R, args.seed, args.cpu_seconds)
+            cpu_best_line = cpu_best(R, args.seed, args.cpu_seconds)
 
     if rank == 0:
         total_updates = float(n) * R * args.steps
@@ -314,7 +364,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -328,35 +378,33 @@ def main():
                 "n_nodes": n, "n_rumors": R, "seed": hex(args.seed),
                 "faults": {"churn": args.faults[0], "drop_push": args.faults[1],
                            "drop_pull": args.faults[2]},
-                "params": list(net.params),
-                "parallelism": ((f"rumor slices x{dist.get_world_size()} (all {n} nodes, "
-                                 f"{R // world}-{-(-R // world)} rumors per rank), "
-                                 + ("RCCL" if args.dist_backend == "nccl" else args.dist_backend)
-                                 + " all_reduce(MIN) of 2 B/node empty-RPC counts per round"
-                                 + (", overlapped with the next round" if args.dist_backend == "nccl"
-                                    else ", host-staged"))
-                                if args.mode == "slices" else
-                                (f"node-range shards x{dist.get_world_size()}, "
-                                 + ("RCCL" if args.dist_backend == "nccl" else args.dist_backend)
-                                 + f" all-to-all push/pull rows, {net.parts} pipeline part(s) per rank"))
-                               if dist is not None else "single-gpu",
+                "params": best["params"],
+                "parallelism": parallelism(args, best["mode"], world, best["parts"])
+                               + (" (faster of: " + "; ".join(f"{r['mode']} {r['elapsed'] / args.steps * 1e3:.3f} ms/step"
+                                                               for r in runs) + ")" if len(runs) > 1 else ""),
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": net.round_kernel_name() + " (deliver round t + transition to t+1)",
-                "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": bytes_per,
+                "step_frac": step_frac,
+                "kernel": best["name"] + " (deliver round t + transition to t+1)",
+                "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": best["bytes_per"],
                 "bytes_counted_by": ("kernels (rows actually gathered + planes moved), %d launches"
-                                     % launches) if launches else "static model",
-                "dense_model_bytes_per_launch": bytes_dense,
+                                     % best["launches"]) if best["launches"] else "static model",
+                "dense_model_bytes_per_launch": best["bytes_dense"],
                 "kernel_ms_per_round": [round(float(v), 4) for v in kt],
             },
             "cpu_baseline": cpu,
-            "cpu_best": best,
+            "cpu_best": cpu_best_line,
             "spread": spread,
         }
+        if len(runs) > 1:
+            line["alternative"] = [{
+                "mode": r["mode"], "parallelism": parallelism(args, r["mode"], world, r["parts"]),
+                "value": total_updates / r["elapsed"], "ms_per_step": r["elapsed"] / args.steps * 1e3,
+                "kernel": r["name"], "kernel_ms": float(np.mean(r["kt"])) if len(r["kt"]) else None,
+            } for r in runs if r is not best]
         print(json.dumps(line), flush=True)
-    net.close()
     if dist is not None:
         dist.destroy_process_group()
 

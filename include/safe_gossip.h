@@ -48,7 +48,7 @@ typedef enum {
     GS_OK = 0,
     GS_ERR_NO_PEERS = 1,          /* Error::NoPeers         */
     GS_ERR_ALREADY_STARTED = 2,   /* Error::AlreadyStarted  */
-    GS_ERR_SIG_FAILURE = 3,       /* Error::SigFailure (reserved: signatures are not verified) */
+    GS_ERR_SIG_FAILURE = 3,       /* Error::SigFailure: a signed frame failed verification */
     GS_ERR_IO = 4,                /* Error::Io (reserved)   */
     GS_ERR_SERIALISATION = 5,     /* Error::Serialisation: undecodable RPC bytes, buffer too small */
     GS_ERR_INVALID_ARGUMENT = -1,
@@ -217,6 +217,8 @@ gs_status   gs_shard_round_part(gs_engine *e, uint32_t part);
 gs_status   gs_shard_pull(gs_engine *e);
 /* The engine's HIP stream (hipStream_t), to order collectives on it. */
 uint64_t    gs_stream(const gs_engine *e);
+/* The HIP device the engine runs on (gs_config.device). */
+int         gs_device(const gs_engine *e);
 
 /* ---- Rumor-sliced network (multi-GPU): rank g holds
  * ALL n nodes and the rumors [lo_g, lo_g + R_g) as a plain engine of R_g
@@ -256,10 +258,11 @@ gs_status   gs_slice_defer(gs_engine *e, uint32_t which);
  * GossipRpc as maidsafe_utilities::serialisation (bincode, fixed-width little
  * endian) writes it: u32 variant (0 Push, 1 Pull) | u64 msg length | msg |
  * u8 counter.  The signed Message(Vec<u8>, Signature) wrapper used outside
- * cfg(test) (src/messages.rs:26-44) is framed but NOT signed or verified
- * (ed25519 over SHA3-512 is parity-unpinned here): callers pass frames
- * through, as the reference's own cfg(test) simulation does (:46-55).
- * Size errors return GS_ERR_SERIALISATION with *out_len = the size needed. */
+ * cfg(test) (src/messages.rs:26-44) = u64 payload length | payload | u64 64 |
+ * 64 signature bytes; gs_message_wrap / _unwrap only frame it, the signed
+ * entry points below (gs_handle_received_signed, gs_push_batch_signed) also
+ * verify / sign it on the GPU.  Size errors return GS_ERR_SERIALISATION with
+ * *out_len = the size needed. */
 gs_status   gs_rpc_encode(int pull, const uint8_t *msg, uint32_t msg_len, uint8_t counter, uint8_t *out,
                           uint32_t cap, uint32_t *out_len);
 gs_status   gs_rpc_decode(const uint8_t *buf, uint32_t len, int *pull, uint32_t *msg_off, uint32_t *msg_len,
@@ -293,6 +296,40 @@ gs_status   gs_push_batch(gs_engine *e, uint32_t node, uint8_t *out, uint32_t ca
 gs_status   gs_handle_received(gs_engine *e, uint32_t node, uint32_t peer, const uint8_t *msg,
                                uint32_t msg_len, uint8_t *out, uint32_t cap, uint32_t *out_len,
                                uint32_t *out_count);
+
+/* ---- Signatures (src/messages.rs:28-44): ed25519 over SHA3-512 ----------
+ * As ed25519-dalek ~0.6.1 with sha3 ~0.7.2 (not vendored in the reference;
+ * restated from their published algorithms, gs_verify.hip): Keypair::sign::
+ * <Sha3_512> and PublicKey::verify::<Sha3_512> for batches, one signature per
+ * GPU lane.  Messages are packed in one buffer: item i is
+ * msgs[off[i] .. off[i] + len[i]).  Host buffers; each call copies them to
+ * `device`, runs there and waits.  The curve results are parity-unpinned
+ * against a real ed25519-dalek run (oracle/ed25519_sha3.py is pinned by RFC
+ * 8032's SHA-512 vectors). */
+/* SHA3-512 digests (64 bytes each) of count byte strings. */
+gs_status   gs_sha3_512(int device, uint32_t count, const uint8_t *data, const uint32_t *off,
+                        const uint32_t *len, uint8_t *out);
+/* Message::deserialise's check (src/messages.rs:38): ok[i] = 1 iff sigs[i]
+ * (64 bytes) is a valid signature of message i under pubs[i] (32 bytes, the
+ * peer's Id). */
+gs_status   gs_ed25519_verify(int device, uint32_t count, const uint8_t *pubs, const uint8_t *sigs,
+                              const uint8_t *msgs, const uint32_t *off, const uint32_t *len, uint8_t *ok);
+/* Message::serialise's signature (src/messages.rs:32) for 32-byte secret
+ * seeds (Gossiper::default's Keypair): pubs[i] (32) and sigs[i] (64) out. */
+gs_status   gs_ed25519_sign(int device, uint32_t count, const uint8_t *seeds, const uint8_t *msgs,
+                            const uint32_t *off, const uint32_t *len, uint8_t *pubs, uint8_t *sigs);
+/* gs_handle_received for a SIGNED frame (Message wrapper): the signature is
+ * verified under peer_key (the peer's Id = its public key,
+ * src/gossiper.rs:84-88); a bad one returns GS_ERR_SIG_FAILURE and applies
+ * nothing (handle_received_message drops the frame).  With node_seed (the
+ * node's secret seed; NULL: unsigned responses) the Pull responses come back
+ * signed by the node, as Gossiper::prepare_to_send does (src/gossiper.rs:117-127). */
+gs_status   gs_handle_received_signed(gs_engine *e, uint32_t node, uint32_t peer, const uint8_t peer_key[32],
+                                      const uint8_t node_seed[32], const uint8_t *msg, uint32_t msg_len,
+                                      uint8_t *out, uint32_t cap, uint32_t *out_len, uint32_t *out_count);
+/* gs_push_batch with every Push frame signed by the node (node_seed). */
+gs_status   gs_push_batch_signed(gs_engine *e, uint32_t node, const uint8_t node_seed[32], uint8_t *out,
+                                 uint32_t cap, uint32_t *len, uint32_t *count);
 
 /* Injected peer schedule: the peer node `node` chooses in `round`. */
 uint32_t    gs_peer(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node, uint32_t n);

@@ -18,7 +18,7 @@ from __future__ import annotations
 import ctypes
 import os
 from dataclasses import dataclass
-from typing import List, Optional
+from typing import List, Optional, Sequence
 
 import numpy as np
 
@@ -28,7 +28,7 @@ __all__ = [
     "Network", "Gossiper", "Statistics", "RoundReport", "GossipError", "NoPeers",
     "AlreadyStarted", "DeviceError", "derive_params", "peer_of", "origin_of", "coin_of",
     "send_messages", "load_library", "SYMBOLS", "rpc_encode", "rpc_decode", "message_wrap",
-    "message_unwrap", "split_frames",
+    "message_unwrap", "split_frames", "SigFailure", "sha3_512", "ed25519_sign", "ed25519_verify",
 ]
 
 # ----------------------------------------------------------------- errors
@@ -50,11 +50,17 @@ class AlreadyStarted(GossipError):
     code = 2
 
 
+class SigFailure(GossipError):
+    """``Error::SigFailure``: a signed frame failed verification."""
+
+    code = 3
+
+
 class DeviceError(GossipError):
     """Engine-side failure (no library, no GPU, HIP error, device limit)."""
 
 
-_ERRORS = {1: NoPeers, 2: AlreadyStarted}
+_ERRORS = {1: NoPeers, 2: AlreadyStarted, 3: SigFailure}
 
 # ------------------------------------------------------------------ ctypes
 class _Config(ctypes.Structure):
@@ -112,6 +118,13 @@ SYMBOLS = {
     "gs_push_batch": (ctypes.c_int, [_P, ctypes.c_uint32, _U8P, ctypes.c_uint32, _U32P, _U32P]),
     "gs_handle_received": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_uint32, _U8P, ctypes.c_uint32,
                                           _U8P, ctypes.c_uint32, _U32P, _U32P]),
+    "gs_device": (ctypes.c_int, [_P]),
+    "gs_sha3_512": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, _U8P, _U32P, _U32P, _U8P]),
+    "gs_ed25519_verify": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, _U8P, _U8P, _U8P, _U32P, _U32P, _U8P]),
+    "gs_ed25519_sign": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, _U8P, _U8P, _U32P, _U32P, _U8P, _U8P]),
+    "gs_handle_received_signed": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_uint32, _U8P, _U8P, _U8P,
+                                                 ctypes.c_uint32, _U8P, ctypes.c_uint32, _U32P, _U32P]),
+    "gs_push_batch_signed": (ctypes.c_int, [_P, ctypes.c_uint32, _U8P, _U8P, ctypes.c_uint32, _U32P, _U32P]),
     "gs_dump_state": (ctypes.c_int, [_P, _U16P]),
     "gs_dump_records": (ctypes.c_int, [_P, _U16P, _U32P]),
     "gs_clear": (ctypes.c_int, [_P, ctypes.c_uint32]),
@@ -313,7 +326,7 @@ def rpc_decode(data: bytes):
 
 def message_wrap(payload: bytes, signature: bytes) -> bytes:
     """bincode of ``Message(payload, signature)`` (src/messages.rs:26-34); the
-    signature is not computed here (ed25519/SHA3-512 is out of scope)."""
+    signature is given (``ed25519_sign`` computes one)."""
     assert len(signature) == 64
     lib = load_library()
     n = ctypes.c_uint32()
@@ -325,11 +338,60 @@ def message_wrap(payload: bytes, signature: bytes) -> bytes:
 
 
 def message_unwrap(data: bytes):
-    """-> ``(payload, signature)`` of a bincode ``Message`` (not verified)."""
+    """-> ``(payload, signature)`` of a bincode ``Message`` (framing only;
+    ``ed25519_verify`` checks the signature)."""
     lib = load_library()
     po, pl, so = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
     _check(lib.gs_message_unwrap(_buf(data), len(data), ctypes.byref(po), ctypes.byref(pl), ctypes.byref(so)))
     return bytes(data[po.value:po.value + pl.value]), bytes(data[so.value:so.value + 64])
+
+
+def _pack(msgs: Sequence[bytes]):
+    off, ln, at = [], [], 0
+    for m in msgs:
+        off.append(at)
+        ln.append(len(m))
+        at += len(m)
+    return (_buf(b"".join(msgs)), (ctypes.c_uint32 * max(1, len(msgs)))(*off),
+            (ctypes.c_uint32 * max(1, len(msgs)))(*ln))
+
+
+def sha3_512(msgs: Sequence[bytes], device: int = 0) -> List[bytes]:
+    """SHA3-512 of each message, on the GPU (gs_verify.hip)."""
+    lib = load_library()
+    data, off, ln = _pack(msgs)
+    out = (ctypes.c_uint8 * max(1, 64 * len(msgs)))()
+    _check(lib.gs_sha3_512(device, len(msgs), data, off, ln, out))
+    raw = bytes(out)
+    return [raw[64 * i:64 * i + 64] for i in range(len(msgs))]
+
+
+def ed25519_sign(seeds: Sequence[bytes], msgs: Sequence[bytes], device: int = 0):
+    """``Keypair::sign::<Sha3_512>`` (ed25519-dalek 0.6, src/messages.rs:32) for
+    32-byte secret seeds, on the GPU -> (public keys, 64-byte signatures)."""
+    assert len(seeds) == len(msgs) and all(len(s) == 32 for s in seeds)
+    lib = load_library()
+    data, off, ln = _pack(msgs)
+    k = len(msgs)
+    pub, sig = (ctypes.c_uint8 * max(1, 32 * k))(), (ctypes.c_uint8 * max(1, 64 * k))()
+    _check(lib.gs_ed25519_sign(device, k, _buf(b"".join(seeds)), data, off, ln, pub, sig))
+    p, s = bytes(pub), bytes(sig)
+    return [p[32 * i:32 * i + 32] for i in range(k)], [s[64 * i:64 * i + 64] for i in range(k)]
+
+
+def ed25519_verify(pubs: Sequence[bytes], msgs: Sequence[bytes], sigs: Sequence[bytes],
+                   device: int = 0) -> List[bool]:
+    """``PublicKey::verify::<Sha3_512>`` (ed25519-dalek 0.6, the check of
+    ``Message::deserialise``, src/messages.rs:38) of each (key, message,
+    signature), on the GPU."""
+    assert len(pubs) == len(msgs) == len(sigs)
+    assert all(len(p) == 32 for p in pubs) and all(len(s) == 64 for s in sigs)
+    lib = load_library()
+    data, off, ln = _pack(msgs)
+    k = len(msgs)
+    ok = (ctypes.c_uint8 * max(1, k))()
+    _check(lib.gs_ed25519_verify(device, k, _buf(b"".join(pubs)), _buf(b"".join(sigs)), data, off, ln, ok))
+    return [bool(v) for v in bytes(ok)[:k]]
 
 
 def split_frames(data: bytes) -> List[bytes]:
@@ -502,6 +564,37 @@ class Network:
                 continue
             _check(st)
             return split_frames(bytes(out)[:n.value])
+
+    def handle_received_signed(self, node: int, peer: int, peer_key: bytes, message: bytes,
+                               node_seed: Optional[bytes] = None) -> List[bytes]:
+        """``handle_received`` for a signed ``Message`` frame (the reference's
+        non-test path, src/messages.rs:36-43): verified on the GPU under
+        ``peer_key`` (the peer's Id); raises ``SigFailure`` on a bad signature
+        (the reference drops the frame).  With ``node_seed`` the Pull
+        responses are signed by the node."""
+        assert len(peer_key) == 32 and (node_seed is None or len(node_seed) == 32)
+        cap = 4096
+        while True:
+            out = (ctypes.c_uint8 * cap)()
+            n, c = ctypes.c_uint32(), ctypes.c_uint32()
+            st = self._lib.gs_handle_received_signed(self._h, node, peer, _buf(peer_key),
+                                                     _buf(node_seed) if node_seed else None, _buf(message),
+                                                     len(message), out, cap, ctypes.byref(n), ctypes.byref(c))
+            if st == 5 and n.value > cap:
+                cap = n.value
+                continue
+            _check(st)
+            return split_frames(bytes(out)[:n.value])
+
+    def push_batch_signed(self, node: int, node_seed: bytes) -> List[bytes]:
+        """``push_batch`` with every Push signed by the node (``Message::serialise``)."""
+        assert len(node_seed) == 32
+        n, c = ctypes.c_uint32(), ctypes.c_uint32()
+        self._lib.gs_push_batch_signed(self._h, node, _buf(node_seed), None, 0, ctypes.byref(n), ctypes.byref(c))
+        out = (ctypes.c_uint8 * max(1, n.value))()
+        _check(self._lib.gs_push_batch_signed(self._h, node, _buf(node_seed), out, n.value, ctypes.byref(n),
+                                              ctypes.byref(c)))
+        return split_frames(bytes(out)[:n.value])
 
     def known_popcounts(self) -> np.ndarray:
         """``Gossiper::messages().len()`` of every node (device popcount)."""

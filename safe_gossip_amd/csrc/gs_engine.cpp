@@ -911,6 +911,8 @@ gs_status gs_shard_pull(gs_engine *e) {
 
 uint64_t gs_stream(const gs_engine *e) { return e ? (uint64_t)(uintptr_t)e->stream : 0; }
 
+int gs_device(const gs_engine *e) { return e ? e->device : 0; }
+
 void gs_destroy(gs_engine *e) { release(e); }
 
 gs_status gs_get_params(const gs_engine *e, uint8_t out[3]) {

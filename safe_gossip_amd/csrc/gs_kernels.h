@@ -311,6 +311,16 @@ struct PullArgs {
 };
 hipError_t launch_pull(const PullArgs &a, hipStream_t s);
 
+// ---------------------------------------------------------------- signatures
+// gs_verify.hip: SHA3-512 and ed25519 over SHA3-512, one item per lane;
+// item i's bytes are data[off[i] .. off[i] + len[i]) (device buffers).
+hipError_t launch_sha3_512(const uint8_t *data, const uint32_t *off, const uint32_t *len, uint32_t count,
+                           uint8_t *out, hipStream_t s);
+hipError_t launch_ed25519_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *msg, const uint32_t *off,
+                                 const uint32_t *len, uint32_t count, uint8_t *ok, hipStream_t s);
+hipError_t launch_ed25519_sign(const uint8_t *seed, const uint8_t *msg, const uint32_t *off, const uint32_t *len,
+                               uint32_t count, uint8_t *pub, uint8_t *sig, hipStream_t s);
+
 // Reductions for observers.
 // nodes_complete counts nodes knowing >= min_known rumors.
 hipError_t launch_known_reduce(const u64 *known, uint32_t n, uint32_t KW, uint32_t min_known,

@@ -39,7 +39,8 @@ def test_config5_full_size(engine, faults):
         prev_known = net.known_all()
         prev = net.statistics_reduce("sum")
         online_total = 0
-        for rnd in range(1, 7):
+        prev_cnt = net.known_popcounts()
+        for rnd in range(1, 23):
             rep = net.next_round()
             assert rep.round == rnd
             if thr:
@@ -57,14 +58,22 @@ def test_config5_full_size(engine, faults):
                 assert st.full_message_received > prev.full_message_received
             else:
                 assert st.full_message_received == st.full_message_sent, f"round {rnd}"
-            known = net.known_all()
-            assert not np.any(prev_known & ~known), f"round {rnd}: a known rumor was lost"
+            cnt = net.known_popcounts()
+            assert np.all(cnt >= prev_cnt), f"round {rnd}: a node's known set shrank"
+            if rnd % 7 == 0:  # whole known sets (800 MB) every 7th round
+                known = net.known_all()
+                assert not np.any(prev_known & ~known), f"round {rnd}: a known rumor was lost"
+                prev_known = known
             tot, _ = net.known_counts(min_known=1)
-            assert tot > 0
-            prev_known, prev = known, st
-        # the rumors spread: more node-rumor pairs known than injected
-        t, _ = net.known_counts()
-        assert t > 16 * 4 ** 3
+            assert tot == int(cnt.sum(dtype=np.uint64)) and tot > 0
+            prev_cnt, prev = cnt, st
+        # 22 rounds: well past Karp's log3(n) + ln ln n ~ 19.7 rounds, so
+        # nearly every node knows every rumor (exactly every one without faults)
+        t, complete = net.known_counts()
+        if thr:
+            assert t > 0.99 * N5 * R5
+        else:
+            assert (t, complete) == (N5 * R5, N5)
         net.sync()   # no device limit hit in any round
     finally:
         net.close()
