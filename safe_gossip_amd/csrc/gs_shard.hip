@@ -272,7 +272,7 @@ __global__ __launch_bounds__(256) void edge_bin_sort(const u64 *__restrict__ pai
                                                      const uint32_t *__restrict__ tot, uint32_t *EP,
                                                      uint4 *IN, uint32_t *IN2,
                                                      const uint32_t *__restrict__ E_id,
-                                                     const uint32_t *__restrict__ tg) {
+                                                     const uint32_t *__restrict__ tg, uint32_t *flags) {
     extern __shared__ __attribute__((aligned(16))) uint32_t h[];
     uint32_t *lds_scan = h + p.bin;
     const uint32_t b = blockIdx.x;
@@ -302,7 +302,15 @@ __global__ __launch_bounds__(256) void edge_bin_sort(const u64 *__restrict__ pai
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nodes; i += blockDim.x) {
-        const uint32_t a = start + (i ? h[i - 1] : 0u), e = start + h[i];
+        const uint32_t a = start + (i ? h[i - 1] : 0u);
+        uint32_t e = start + h[i];
+        if (e - a > kMaxIn) {
+            // in-degree above the limit (probability ~1e-34 per node, or a
+            // corrupted exchange): a device limit, reported by gs_sync; the
+            // list is cut so that the insertion sort stays O(kMaxIn^2)
+            atomicOr(&flags[2], 1u);
+            e = a + kMaxIn;
+        }
         for (uint32_t q = a + 1; q < e; ++q) {  // slot keys ascending = pushers ascending
             const uint32_t v = EP[q];
             uint32_t r = q;
@@ -440,7 +448,7 @@ hipError_t launch_shard_edges(const ShardPlan &P, const ShardEdgeLayout &L, uint
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(edge_bin_sort, dim3(c.nb), dim3(256), lds_sort, s, pairs, c, P, P.m, base, tot, EP, IN,
-                       IN2, E_id, tg);
+                       IN2, E_id, tg, flags);
     return hipGetLastError();
 }
 

@@ -34,12 +34,17 @@ work runs in the engine's gfx950 kernels.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 import numpy as np
 
 from . import (DeviceError, GossipError, NoPeers, RoundReport, _check, _Config, _Report,
                fault_threshold, load_library)
+
+# RCCL's all_to_all_single is exact up to 2^30 bytes per rank (DESIGN.md
+# section 7, "The single-part stall").
+RCCL_MAX_BYTES = 1 << 30
 
 _P = ctypes.c_void_p
 _U32P = ctypes.POINTER(ctypes.c_uint32)
@@ -123,6 +128,8 @@ class ShardedNetwork:
         cfg.churn, cfg.drop_push, cfg.drop_pull = self.faults
         self._cfg = cfg
         self.host_staged = False
+        # largest RCCL collective issued at once (bytes per rank; tests lower it)
+        self.max_collective_bytes = int(os.environ.get("SAFE_GOSSIP_AMD_RCCL_MAX_BYTES", RCCL_MAX_BYTES))
         if transport == "local":
             self.parts = 1 if parts is None else parts
             self.shards = [_Shard(self.lib, cfg, r, world, self.parts, torch, device) for r in range(world)]
@@ -133,10 +140,15 @@ class ShardedNetwork:
             assert dist.get_world_size(group) == world
             self.host_staged = dist.get_backend(group) == "gloo"
             # four parts overlap the RCCL exchanges with the round kernel
-            # (and keep each collective small: a 1.1 GB self-exchange of one
-            # part was seen to stall RCCL on a single rank)
             self.parts = (1 if self.host_staged else 4) if parts is None else parts
             self.shards = [_Shard(self.lib, cfg, self.rank, world, self.parts, torch, device)]
+            s = self.shards[0]
+            biggest = max(world * s.region(which, h)[1] * 8 for which in "AB" for h in range(s.parts))
+            if not self.host_staged and world > 1 and biggest > self.max_collective_bytes:
+                for sh in self.shards:
+                    sh.close()
+                raise ValueError(f"an exchange of {biggest} B per rank exceeds the {self.max_collective_bytes} B "
+                                 f"RCCL all_to_all limit; use more pipeline parts (parts={self.parts})")
         else:
             raise ValueError(transport)
         self.round = 0
@@ -212,14 +224,31 @@ class ShardedNetwork:
             return None
         # RCCL: the collective waits for the engine stream's work so far and
         # runs on the process group's stream; the engine stream waits for it
-        # only when its rows are needed (_wait)
+        # only when its rows are needed (_wait).  RCCL 2.26's all_to_all_single
+        # returns wrong bytes past 2^30 per rank (measured on one rank,
+        # exp/r3/rccl_size.py: 1024 MiB exact, 1025 MiB not), so a larger
+        # exchange moves in pieces of at most RCCL_MAX_BYTES (one rank: the
+        # span is its own single block, cut anywhere); with several ranks the
+        # parts keep every exchange far below it (constructor check).
+        limit = self.max_collective_bytes
+        if self.world * w * 8 <= limit:
+            with torch.cuda.stream(s.stream):
+                return dist.all_to_all_single(recv[span], send[span], group=self.group, async_op=True)
+        assert self.world == 1, "multi-rank exchange above the RCCL size limit (constructor check)"
+        step = max(1, limit // 8)
+        works = []
         with torch.cuda.stream(s.stream):
-            return dist.all_to_all_single(recv[span], send[span], group=self.group, async_op=True)
+            for a in range(off, off + w, step):
+                b = min(a + step, off + w)
+                works.append(dist.all_to_all_single(recv[a:b], send[a:b], group=self.group, async_op=True))
+        return works
 
     def _wait(self, work):
-        if work is not None:
-            with self.torch.cuda.stream(self.shards[0].stream):
-                work.wait()
+        if work is None:
+            return
+        with self.torch.cuda.stream(self.shards[0].stream):
+            for wk in (work if isinstance(work, list) else [work]):
+                wk.wait()
 
     def _wait_all(self):
         for w in self._pendA:

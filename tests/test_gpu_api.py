@@ -76,6 +76,7 @@ def test_add_peer_already_started(engine):
         assert net.params == (2, 2, 5)
         # a message received from an outside peer creates an entry too
         net.clear()
+        net.next_round()  # (external RPCs join a round after its deliveries)
         net.handle_received(7, 100, engine.rpc_encode(False, b"", 0))  # empty push: no entry
         net.set_params((2, 2, 6))
         net.handle_received(7, 100, engine.rpc_encode(False, net.rumor_key(2), 1))

@@ -22,10 +22,10 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, cases, q, backend="gloo", parts=None):
+def _worker(rank, world, port, cases, q, backend="gloo", parts=None, env=None):
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **(env or {}))
     import torch
     import torch.distributed as dist
     if backend == "nccl":
@@ -91,3 +91,36 @@ def test_sharded_dist_rccl_single_rank(engine, parts):
     while not q.empty():
         msgs.append(q.get())
     assert msgs == [("ok", 0)], msgs
+
+
+def test_sharded_dist_rccl_chunked_exchange(engine):
+    # RCCL's all_to_all_single is exact only up to 2^30 bytes per rank
+    # (exp/r3/rccl_size.py): one rank's larger exchange moves in pieces.  The
+    # piece limit is lowered to 4 KiB so the chunked path runs at oracle sizes.
+    import torch.multiprocessing as mp
+    cases = [(700, 256, "reinject"), (1000, 3, "trickle")]
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    p = ctx.Process(target=_worker, args=(0, 1, _free_port(), cases, q, "nccl", 1,
+                                          {"SAFE_GOSSIP_AMD_RCCL_MAX_BYTES": "4096"}))
+    p.start()
+    p.join(timeout=200)
+    if p.is_alive():
+        p.kill()
+    msgs = []
+    while not q.empty():
+        msgs.append(q.get())
+    assert msgs == [("ok", 0)], msgs
+
+
+def test_sharded_single_part_full_size_rccl(engine):
+    # the formerly stalling shape: one RCCL rank, ONE part, 2^24 x 256: each
+    # exchange is ~1.1 GB, past RCCL's 2^30-byte limit; unchunked, the id rows
+    # at its end arrived corrupted and one node's in-list grew to millions of
+    # pushers (an O(k^2) insertion sort that ran for minutes).  Chunked, the
+    # rounds complete and obey the accounting laws.
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(HERE), "exp", "r3", "rccl_p1.py"),
+                        "24", "1", "256", "nccl"], capture_output=True, text=True, timeout=250,
+                       env=dict(os.environ, MASTER_PORT=str(_free_port())))
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
