@@ -33,8 +33,15 @@ __host__ __device__ __forceinline__ Ph4 philox4(uint32_t c0, uint32_t c1, uint32
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
+#ifdef GS_PHILOX_MULHI
         uint32_t hi0 = mulhi32(kPhM0, c0), lo0 = kPhM0 * c0;
         uint32_t hi1 = mulhi32(kPhM1, c2), lo1 = kPhM1 * c2;
+#else
+        // one v_mad_u64_u32 per product instead of a mul_hi + mul_lo pair
+        const uint64_t p0 = (uint64_t)kPhM0 * c0, p1 = (uint64_t)kPhM1 * c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+#endif
         uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
         k0 += kPhW0; k1 += kPhW1;

@@ -8,6 +8,15 @@ namespace gs {
 
 GS_DEV uint32_t popc(u64 v) { return (uint32_t)__popcll(v); }
 
+// Round kernels clear the next in-list build's counters (RoundArgs::zero_*)
+// instead of a memset launch: grid-stride vector stores of buf[0, words), and
+// *one = 0 from the first thread.
+GS_DEV void zero_for_build(uint32_t *buf, uint32_t words, u64 *one) {
+    const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint32_t i = gt; i < words; i += gridDim.x * blockDim.x) buf[i] = 0u;
+    if (one && gt == 0u) *one = 0ull;
+}
+
 // c += in (bit-sliced 5-bit counters, one per rumor).
 GS_DEV void add5(u64 (&c)[5], u64 in) {
 #pragma unroll

@@ -71,6 +71,7 @@ template <int MODE, typename T, uint32_t kNpl>
 __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(RoundArgs a) {
     constexpr bool DELIVER = MODE == 1;
     const Geometry &g = a.g;
+    if (a.zero_buf || a.zero_rows) zero_for_build(a.zero_buf, a.zero_words, a.zero_rows);
     const uint32_t n_nodes = g.n;
     const uint32_t rp = g.rpad, lr = g.logr, lognpu = g.lognpu;  // rp <= 16: npu >= 4
     const uint32_t lane = blockIdx.x * kDlv4Threads + threadIdx.x;

@@ -133,6 +133,7 @@ struct gs_engine {
     gs::RoundArgs ra{};
     int ra_mode = 0;
     bool ra_sparse = false;
+    bool ra_prezeroed = false;  // the round kernel clears the next build's counters
     uint32_t *st32 = nullptr;  // [n][4] u32 deltas
     u64 *st64 = nullptr;       // [n][4] folded totals
     uint32_t fold_every = 1, since_fold = 0;
@@ -1095,6 +1096,19 @@ gs_status round_begin(gs_engine *e) {
         GS_HIP(gs::launch_build_bins(inlist_args(e, c, R0 + 1u), e->cstream));
         GS_HIP(hipEventRecord(e->ev_binned[ns], e->cstream));
     }
+    // the build of round t+1 runs right behind this kernel on its stream: the
+    // kernel clears that build's counters (no memset launch)
+    e->ra_prezeroed = !e->shard && !e->split_build && !(e->concurrent_inlists && !e->dlv);
+    if (e->ra_prezeroed) {
+        auto &c = e->csr[(R0 + 1u) & 1u];
+        size_t first = 0, words = 0;
+        gs::inlist_zero_range(e->plan, &first, &words);
+        if (words) {
+            a.zero_buf = c.scratch + first;
+            a.zero_words = (uint32_t)words;
+        }
+        if (e->filt) a.zero_rows = e->rows_dev + ((R0 + 1u) & 1u);
+    }
     e->ra = a;
     e->ra_mode = e->deliver_pending ? 1 : 0;
     e->ra_sparse = sparse;
@@ -1188,7 +1202,8 @@ gs_status round_end(gs_engine *e, gs_round_report *report) {
             st = next_serial(e, c, bs);
             if (st != GS_OK) return st;
             gs::InListArgs la = inlist_args(e, c, e->round);
-            if (e->filt) GS_HIP(hipMemsetAsync(la.rows, 0, sizeof(u64), bs));
+            la.prezeroed = e->ra_prezeroed ? 1u : 0u;
+            if (e->filt && !e->ra_prezeroed) GS_HIP(hipMemsetAsync(la.rows, 0, sizeof(u64), bs));
             GS_HIP(gs::launch_build_inlists(la, bs));
         }
         GS_HIP(hipEventRecord(e->ev_built[ns], bs));

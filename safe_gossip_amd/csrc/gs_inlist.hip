@@ -49,7 +49,7 @@ constexpr uint32_t kInlThreads = 1024;
 static_assert(kChunk % kInlThreads == 0, "inl_bin: whole sources per thread");
 constexpr uint32_t kChunkSmall = 2048;            // sources per inl_bin block below 2^22 nodes
 static_assert(kChunkSmall % kInlThreads == 0, "inl_bin: whole sources per thread");
-constexpr uint32_t kBinnedMaxBins = 8192;         // n <= 2^27 (per-bin LDS state is 6 B)
+constexpr uint32_t kBinnedMaxBins = 1u << (27 - kBinLog);  // n <= 2^27 (per-bin LDS state is 6 B)
 constexpr uint32_t kFlagLimit = 2u;               // flags[2] bit: a device limit was hit
 
 // Target word (target + delivery flags, gs_common.h); edges flagged kTgDead
@@ -167,15 +167,18 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
     // LDS atomics, so 8192 bins fit beside the stage.
     uint32_t *stage = sh;                                      // [kChunk] sources by bin
     uint16_t *stage_lt = reinterpret_cast<uint16_t *>(sh + kChunk);  // [kChunk]
-    uint32_t *cnt = sh + kChunk + kChunk / 2;  // [nb/2] counts, then cursors (2 x u16 per word)
+    // partitions: bins, or 2^sub parts per bin (small networks)
+    const uint32_t np = p.nb << p.sub, plog = kBinLog - p.sub, pcap = kBinCap >> p.sub;
+    uint32_t *fill = a.scratch + p.fill_off;
+    uint32_t *cnt = sh + kChunk + kChunk / 2;  // [np/2] counts, then cursors (2 x u16 per word)
     uint16_t *cnt16 = reinterpret_cast<uint16_t *>(cnt);
-    uint16_t *off = reinterpret_cast<uint16_t *>(cnt + (p.nb + 1) / 2);  // [nb] chunk-local bin starts
-    uint16_t *res = off + p.nb;                // [nb] reserved start in the bin's region
+    uint16_t *off = reinterpret_cast<uint16_t *>(cnt + (np + 1) / 2);  // [np] chunk-local starts
+    uint16_t *res = off + np;                  // [np] reserved start in the part's region
     __shared__ uint32_t lds_scan[kInlThreads / 64];
     __shared__ uint32_t zrows;  // filtered: t(x) rows the zl bits leave to gather
     if (blockIdx.x == 0 && threadIdx.x == 0) a.scratch[p.nb] = 0u;  // tail count; inl_sort runs after
     if (threadIdx.x == 0) zrows = 0u;
-    for (uint32_t i = threadIdx.x; i < (p.nb + 1) / 2; i += kInlThreads) cnt[i] = 0u;
+    for (uint32_t i = threadIdx.x; i < (np + 1) / 2; i += kInlThreads) cnt[i] = 0u;
     __syncthreads();
     const uint32_t lo = blockIdx.x * kChunk;
     const uint32_t hi = min(p.n, lo + kChunk);
@@ -190,7 +193,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
             tq[q] = target_of(a, x);
             a.tg[x] = tq[q];
             if (!(tq[q] & kTgDead)) {
-                const uint32_t b = (tq[q] & kTgMask) >> kBinLog;
+                const uint32_t b = (tq[q] & kTgMask) >> plog;
                 atomicAdd(&cnt[b >> 1], 1u << ((b & 1u) << 4));
             }
         }
@@ -214,24 +217,24 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
     __syncthreads();
     if (a.rows && threadIdx.x == 0 && zrows) atomicAdd(a.rows, (u64)zrows);
     // exclusive scan of the bin counts: thread i owns bins [i*per, i*per + per)
-    const uint32_t per = (p.nb + kInlThreads - 1) / kInlThreads;
+    const uint32_t per = (np + kInlThreads - 1) / kInlThreads;
     const uint32_t b0 = threadIdx.x * per;
     uint32_t sum = 0;
     for (uint32_t q = 0; q < per; ++q)
-        if (b0 + q < p.nb) sum += cnt16[b0 + q];
+        if (b0 + q < np) sum += cnt16[b0 + q];
     uint32_t total;
     uint32_t run = block_exclusive_scan_t<kInlThreads>(sum, lds_scan, total);
     for (uint32_t q = 0; q < per; ++q) {
         const uint32_t b = b0 + q;
-        if (b >= p.nb) break;
+        if (b >= np) break;
         const uint32_t c = cnt16[b];
         off[b] = (uint16_t)run;
         uint32_t r0 = 0;
         if (c) {
-            r0 = atomicAdd(&a.scratch[b], c);
-            if (r0 + c > kBinCap) {
+            r0 = atomicAdd(&fill[b], c);
+            if (r0 + c > pcap) {
                 atomicOr(&a.flags[2], kFlagLimit);
-                r0 = kBinCap;  // drop this run; the round reports the limit
+                r0 = pcap;  // drop this run; the round reports the limit
             }
         }
         res[b] = (uint16_t)r0;
@@ -243,27 +246,27 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
     for (uint32_t q = 0; q < kBinPer; ++q) {
         const uint32_t t = tq[q];
         if (t & kTgDead) continue;  // (also every slot past hi)
-        const uint32_t b = (t & kTgMask) >> kBinLog, sh16 = (b & 1u) << 4;
+        const uint32_t b = (t & kTgMask) >> plog, sh16 = (b & 1u) << 4;
         const uint32_t pos = (atomicAdd(&cnt[b >> 1], 1u << sh16) >> sh16) & 0xFFFFu;
         stage[pos] = lo + threadIdx.x + q * kInlThreads;
-        stage_lt[pos] = (uint16_t)(t & (kBin - 1u));
+        stage_lt[pos] = (uint16_t)(t & (kBin - 1u));  // (relative to the bin)
     }
     __syncthreads();
     // Consecutive stage entries of one bin go to consecutive region slots; the
     // bin of entry i is found by a binary search over the chunk-local starts.
     for (uint32_t i = threadIdx.x; i < total; i += kInlThreads) {  // delivered edges of the chunk
-        uint32_t lo_b = 0, hi_b = p.nb;  // last bin with off[b] <= i and a non-empty run
+        uint32_t lo_b = 0, hi_b = np;  // last part with off[b] <= i and a non-empty run
         while (hi_b - lo_b > 1) {
             const uint32_t mid = (lo_b + hi_b) >> 1;
             if (off[mid] <= i) lo_b = mid; else hi_b = mid;
         }
-        // (empty bins share their start with the next bin, so the last bin
+        // (empty parts share their start with the next part, so the last part
         // whose start is <= i is the one whose run holds entry i)
         const uint32_t b = lo_b;
         const uint32_t slot = res[b] + (i - off[b]);
-        if (slot < kBinCap) {
-            a.region[(u64)b * kBinCap + slot] = stage[i];
-            a.region_lt[(u64)b * kBinCap + slot] = stage_lt[i];
+        if (slot < pcap) {
+            a.region[(u64)b * pcap + slot] = stage[i];
+            a.region_lt[(u64)b * pcap + slot] = stage_lt[i];
         }
     }
 }
@@ -271,7 +274,6 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
 // Packed 16-bit counter `i` of h (two per word).
 GS_DEV uint32_t half_of(const uint32_t *h, uint32_t i) { return (h[i >> 1] >> ((i & 1u) << 4)) & 0xFFFFu; }
 
-constexpr uint32_t kSortPer = (kBinCap + kInlThreads - 1) / kInlThreads;  // region entries per thread
 // inl_sort blocks per bin = 2^split: one while there are enough bins to fill
 // the chip (two per bin measured slower at 1024 bins: every block reads the
 // whole bin region), more for small networks (2^20 nodes = 64 bins), whose
@@ -293,24 +295,28 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
     constexpr uint32_t kPartLog = kBinLog - SPLITLOG;
     constexpr uint32_t kPart = 1u << kPartLog;             // targets per block
     constexpr uint32_t kPartCap = kBinCap >> SPLITLOG;     // sorted entries per block
+    // SPLITLOG > 0: inl_bin wrote this part's own region (p.sub == SPLITLOG)
+    constexpr bool own = SPLITLOG > 0;
+    constexpr uint32_t kPer = (kPartCap + kInlThreads - 1) / kInlThreads;  // region entries per thread
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     const CsrPlan &p = a.p;
     uint32_t *h = sh;                   // [kPart/2] packed per-target counters
     uint32_t *sorted = sh + kPart / 2;  // [kPartCap]
     __shared__ uint32_t lds_scan[kInlThreads / 64];
     const uint32_t b = blockIdx.x, hh = blockIdx.y;
-    const uint32_t cnt = min(a.scratch[b], kBinCap);
+    const uint32_t cnt = own ? min(a.scratch[p.fill_off + (b << SPLITLOG) + hh], kPartCap) : min(a.scratch[b], kBinCap);
+    const u64 rb = own ? (u64)((b << SPLITLOG) + hh) * kPartCap : (u64)b * kBinCap;
     const uint32_t t0 = (b << kBinLog) + (hh << kPartLog);
     const uint32_t nodes = t0 < p.n ? min(kPart, p.n - t0) : 0u;
     if (nodes == 0) return;  // a part past the last node (uniform per block)
     // the bin's entries of this part, held in registers (coalesced loads, issued first)
-    uint32_t ex[kSortPer], el[kSortPer];
+    uint32_t ex[kPer], el[kPer];
 #pragma unroll
-    for (uint32_t q = 0; q < kSortPer; ++q) {
+    for (uint32_t q = 0; q < kPer; ++q) {
         const uint32_t i = threadIdx.x + q * kInlThreads;
         const bool ok = i < cnt;
-        ex[q] = ok ? a.region[(u64)b * kBinCap + i] : 0u;
-        const uint32_t lt = ok ? (uint32_t)a.region_lt[(u64)b * kBinCap + i] : kNone;
+        ex[q] = ok ? a.region[rb + i] : 0u;
+        const uint32_t lt = ok ? (uint32_t)a.region_lt[rb + i] : kNone;
         el[q] = (ok && (lt >> kPartLog) == hh) ? (lt & (kPart - 1u)) : kNone;
     }
     for (uint32_t i = threadIdx.x; i < kPart / 2; i += kInlThreads) h[i] = 0u;
@@ -319,7 +325,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
     // carried as bit 31 of the sorted ids (kLiveTag)
     __shared__ uint32_t cpl[kPart / 32], lvl[kPart / 32];
     const bool filt = a.lvm != nullptr;
-    uint32_t lt_tag[kSortPer];
+    uint32_t lt_tag[kPer];
     if (filt) {
         for (uint32_t i = threadIdx.x; i < kPart / 32; i += kInlThreads) {
             const bool in = t0 + 32u * i < p.n;
@@ -327,13 +333,13 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
             lvl[i] = in ? reinterpret_cast<const uint32_t *>(a.lvm)[(t0 >> 5) + i] : 0u;
         }
 #pragma unroll
-        for (uint32_t q = 0; q < kSortPer; ++q)
+        for (uint32_t q = 0; q < kPer; ++q)
             lt_tag[q] = (el[q] != kNone && map_test(a.lvm, ex[q])) ? kLiveTag : 0u;
     }
     __syncthreads();
     if (SPLITLOG == 0 && threadIdx.x == 0) a.scratch[b] = 0u;  // ready for the next build of this set
 #pragma unroll
-    for (uint32_t q = 0; q < kSortPer; ++q)
+    for (uint32_t q = 0; q < kPer; ++q)
         if (el[q] != kNone) atomicAdd(&h[el[q] >> 1], 1u << ((el[q] & 1u) << 4));
     __syncthreads();
     // exclusive scan over the kPart targets, kPart/kInlThreads per thread
@@ -353,7 +359,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
     __syncthreads();
     if (SPLITLOG > 0 && threadIdx.x == 0 && total > kPartCap) atomicOr(&a.flags[2], kFlagLimit);
 #pragma unroll
-    for (uint32_t q = 0; q < kSortPer; ++q) {
+    for (uint32_t q = 0; q < kPer; ++q) {
         if (el[q] != kNone) {
             const uint32_t shf = (el[q] & 1u) << 4;
             const uint32_t old = atomicAdd(&h[el[q] >> 1], 1u << shf);
@@ -414,9 +420,9 @@ constexpr uint32_t kCoarseCap = (1u << kCoarseLog) + (1u << (kCoarseLog - 4));
 #endif
 constexpr uint32_t kPartChunk = GS_PART_CHUNK;
 constexpr uint32_t kPartPer = kPartChunk / kInlThreads;
-constexpr uint32_t kMaxCoarse = 64;  // n <= 2^27
+constexpr uint32_t kMaxCoarse = 1u << (27 - kCoarseLog);  // n <= 2^27
 
-GS_DEV uint32_t n_coarse(uint32_t nb) { return (nb + kCoarseBins - 1) / kCoarseBins; }
+__host__ __device__ inline uint32_t n_coarse(uint32_t nb) { return (nb + kCoarseBins - 1) / kCoarseBins; }
 
 // Coarse-bucket arrays inside the region buffer, after the bin regions.
 struct CoarseArrays {
@@ -515,20 +521,25 @@ __global__ __launch_bounds__(kInlThreads) void dl_coarse(InListArgs a) {
     }
 }
 
+constexpr uint32_t kFineParts = 2 * kCoarseBins;  // parts per coarse bucket (sub <= 1)
 __global__ __launch_bounds__(kInlThreads) void dl_fine(InListArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     uint32_t *sx = sh, *sc = sh + kPartChunk;
     uint16_t *slt = reinterpret_cast<uint16_t *>(sh + 2 * kPartChunk);
-    __shared__ uint32_t cnt[kCoarseBins], off[kCoarseBins], res[kCoarseBins];
+    __shared__ uint32_t cnt[kFineParts], off[kFineParts], res[kFineParts];
     __shared__ uint32_t lds_scan[kInlThreads / 64];
     const CsrPlan &p = a.p;
+    // the 2^sub parts of each bin inl_sort_dlv sorts: a coarse bucket's
+    // kCoarseBins << sub parts, each in its own region of kBinCap >> sub slots
+    const uint32_t fp = kCoarseBins << p.sub, plog = kBinLog - p.sub, pcap = kBinCap >> p.sub;
+    uint32_t *pfill = p.sub ? a.scratch + p.fill_off : a.scratch;
     const uint32_t cb = blockIdx.y;
     const uint32_t fill = min(a.scratch[p.nb + 1 + cb], kCoarseCap);
     const uint32_t lo = blockIdx.x * kPartChunk;
     if (lo >= fill) return;  // uniform per block
     const uint32_t hi = min(fill, lo + kPartChunk);
     const CoarseArrays ca = coarse_arrays(a.region, p.nb);
-    if (threadIdx.x < kCoarseBins) cnt[threadIdx.x] = 0u;
+    if (threadIdx.x < fp) cnt[threadIdx.x] = 0u;
     __syncthreads();
     uint32_t xv[kPartPer], tv[kPartPer], cv[kPartPer];
 #pragma unroll
@@ -539,20 +550,20 @@ __global__ __launch_bounds__(kInlThreads) void dl_fine(InListArgs a) {
         xv[q] = ca.x[o];
         tv[q] = ok ? ca.t[o] : kNone;
         cv[q] = ca.c[o];
-        if (ok) atomicAdd(&cnt[(tv[q] >> kBinLog) & (kCoarseBins - 1u)], 1u);
+        if (ok) atomicAdd(&cnt[(tv[q] >> plog) & (fp - 1u)], 1u);
     }
     __syncthreads();
-    {  // exclusive scan of the kCoarseBins counts, reservations in the bin regions
-        const uint32_t c = threadIdx.x < kCoarseBins ? cnt[threadIdx.x] : 0u;
+    {  // exclusive scan of the part counts, reservations in the part regions
+        const uint32_t c = threadIdx.x < fp ? cnt[threadIdx.x] : 0u;
         uint32_t total;
         const uint32_t ex = block_exclusive_scan_t<kInlThreads>(c, lds_scan, total);
-        if (threadIdx.x < kCoarseBins) {
-            const uint32_t b = cb * kCoarseBins + threadIdx.x;
+        if (threadIdx.x < fp) {
+            const uint32_t b = cb * fp + threadIdx.x;
             off[threadIdx.x] = ex;
-            uint32_t r0 = c ? atomicAdd(&a.scratch[b], c) : 0u;
-            if (r0 + c > kBinCap) {
+            uint32_t r0 = c ? atomicAdd(&pfill[b], c) : 0u;
+            if (r0 + c > pcap) {
                 atomicOr(&a.flags[2], kFlagLimit);
-                r0 = kBinCap;
+                r0 = pcap;
             }
             res[threadIdx.x] = r0;
             cnt[threadIdx.x] = ex;  // cursor
@@ -562,23 +573,97 @@ __global__ __launch_bounds__(kInlThreads) void dl_fine(InListArgs a) {
 #pragma unroll
     for (uint32_t q = 0; q < kPartPer; ++q) {
         if (tv[q] == kNone) continue;
-        const uint32_t fb = (tv[q] >> kBinLog) & (kCoarseBins - 1u);
+        const uint32_t fb = (tv[q] >> plog) & (fp - 1u);
         const uint32_t pos = atomicAdd(&cnt[fb], 1u);
         sx[pos] = xv[q];
         sc[pos] = cv[q];
-        slt[pos] = (uint16_t)(tv[q] & (kBin - 1u));  // (its fine bin is found from off[] below)
+        slt[pos] = (uint16_t)(tv[q] & (kBin - 1u));  // (relative to the bin; its part is found from off[] below)
     }
     __syncthreads();
     const uint32_t n_here = hi - lo;
     for (uint32_t i = threadIdx.x; i < n_here; i += kInlThreads) {
-        uint32_t lo_b = 0, hi_b = kCoarseBins;  // last bin whose run starts at or before i
+        uint32_t lo_b = 0, hi_b = fp;  // last part whose run starts at or before i
         while (hi_b - lo_b > 1) {
             const uint32_t mid = (lo_b + hi_b) >> 1;
             if (off[mid] <= i) lo_b = mid; else hi_b = mid;
         }
         const uint32_t slot = res[lo_b] + (i - off[lo_b]);
-        if (slot < kBinCap) {
-            const u64 o = (u64)(cb * kCoarseBins + lo_b) * kBinCap + slot;
+        if (slot < pcap) {
+            const u64 o = (u64)(cb * fp + lo_b) * pcap + slot;
+            a.region[o] = sx[i];
+            a.region_lt[o] = slt[i];
+            a.region_code[o] = sc[i];
+        }
+    }
+}
+
+// Small networks (one coarse bucket, n <= kCoarseBins bins): the targets and
+// one LDS counting sort of each chunk of sources straight into the regions of
+// the 2^sub parts of every bin that inl_sort_dlv sorts (dl_coarse + dl_fine in
+// one pass; the regions stay in cache at this size).
+constexpr uint32_t kDirectParts = kInlThreads;  // nb << sub <= 1024 (one scan slot per part)
+__global__ __launch_bounds__(kInlThreads) void dl_direct(InListArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
+    uint32_t *sx = sh, *sc = sh + kPartChunk;
+    uint16_t *slt = reinterpret_cast<uint16_t *>(sh + 2 * kPartChunk);
+    uint16_t *sb = slt + kPartChunk;
+    __shared__ uint32_t cnt[kDirectParts], off[kDirectParts], res[kDirectParts + 1];
+    __shared__ uint32_t lds_scan[kInlThreads / 64];
+    const CsrPlan &p = a.p;
+    const uint32_t np = p.nb << p.sub, plog = kBinLog - p.sub, pcap = kBinCap >> p.sub;
+    uint32_t *fill = a.scratch + p.fill_off;
+    for (uint32_t i = threadIdx.x; i < np; i += kInlThreads) cnt[i] = 0u;
+    __syncthreads();
+    const uint32_t lo = blockIdx.x * kPartChunk;
+    uint32_t tv[kPartPer], cv[kPartPer];
+#pragma unroll
+    for (uint32_t q = 0; q < kPartPer; ++q) {
+        const uint32_t x = lo + threadIdx.x + q * kInlThreads;
+        tv[q] = kTgDead;
+        cv[q] = 0u;
+        if (x < p.n) {
+            const uint32_t t = target_of(a, x);
+            a.tg[x] = t;
+            tv[q] = t;
+            cv[q] = a.PC[x];
+            if (!(t & kTgDead)) atomicAdd(&cnt[(t & kTgMask) >> plog], 1u);
+        }
+    }
+    __syncthreads();
+    {
+        const uint32_t c = threadIdx.x < np ? cnt[threadIdx.x] : 0u;
+        uint32_t total;
+        const uint32_t ex = block_exclusive_scan_t<kInlThreads>(c, lds_scan, total);
+        if (threadIdx.x < np) {
+            off[threadIdx.x] = ex;
+            uint32_t r0 = c ? atomicAdd(&fill[threadIdx.x], c) : 0u;
+            if (r0 + c > pcap) {
+                atomicOr(&a.flags[2], kFlagLimit);
+                r0 = pcap;
+            }
+            res[threadIdx.x] = r0;
+            cnt[threadIdx.x] = ex;  // cursor
+        }
+        if (threadIdx.x == 0) res[kDirectParts] = total;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < kPartPer; ++q) {
+        if (tv[q] & kTgDead) continue;
+        const uint32_t t = tv[q] & kTgMask, b = t >> plog;
+        const uint32_t pos = atomicAdd(&cnt[b], 1u);
+        sx[pos] = lo + threadIdx.x + q * kInlThreads;
+        sc[pos] = cv[q];
+        slt[pos] = (uint16_t)(t & (kBin - 1u));  // (relative to the bin)
+        sb[pos] = (uint16_t)b;
+    }
+    __syncthreads();
+    const uint32_t total = res[kDirectParts];
+    for (uint32_t i = threadIdx.x; i < total; i += kInlThreads) {
+        const uint32_t b = sb[i];
+        const uint32_t slot = res[b] + (i - off[b]);
+        if (slot < pcap) {
+            const u64 o = (u64)b * pcap + slot;
             a.region[o] = sx[i];
             a.region_lt[o] = slt[i];
             a.region_code[o] = sc[i];
@@ -607,12 +692,14 @@ inline uint32_t dlv_split_log(uint32_t nb) {
     return nb >= 512u ? kSplitLog : (nb >= 128u ? kSplitLog + 1u : kSplitLog + 2u);
 }
 
-template <uint32_t SL>
+template <uint32_t SL, bool OWN>
 __global__ __launch_bounds__(kInlThreads) void inl_sort_dlv(InListArgs a) {
     constexpr uint32_t kHalfLog = kBinLog - SL;  // (a "half": one of the 2^SL parts of a bin)
     constexpr uint32_t kHalf = 1u << kHalfLog;
     constexpr uint32_t kHalfCap = kBinCap >> SL;
     constexpr uint32_t kHalfPer = kHalf / kInlThreads;  // targets per thread
+    // region entries per thread: the half's own region (OWN: p.sub == SL) or the whole bin's
+    constexpr uint32_t kPer = ((OWN ? kHalfCap : kBinCap) + kInlThreads - 1) / kInlThreads;
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     const CsrPlan &p = a.p;
     uint32_t *h = sh;                   // [kHalf/2] packed per-target counters
@@ -621,19 +708,25 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort_dlv(InListArgs a) {
     __shared__ uint32_t lds_scan[kInlThreads / 64];
     __shared__ uint32_t pcnt[kMaxCoarse], pres[kMaxCoarse];
     const uint32_t b = blockIdx.x, hh = blockIdx.y;
-    const uint32_t cnt = min(a.scratch[b], kBinCap);
     const uint32_t t0 = (b << kBinLog) + (hh << kHalfLog);
     const uint32_t nodes = t0 < p.n ? min(kHalf, p.n - t0) : 0u;
     if (nodes == 0) return;  // a half past the last node (uniform per block)
     const uint32_t nc = n_coarse(p.nb);
+    // p.sub == SL: dl_fine / dl_direct wrote this half's own region; small
+    // networks (one coarse bucket) write every pull straight to PULL (no
+    // pass-back partition)
+    constexpr bool own = OWN;
+    const bool direct = nc == 1u;
+    const uint32_t cnt = own ? min(a.scratch[p.fill_off + (b << SL) + hh], kHalfCap) : min(a.scratch[b], kBinCap);
+    const u64 rb = own ? (u64)((b << SL) + hh) * kHalfCap : (u64)b * kBinCap;
     uint32_t *pcfill = a.scratch + p.nb + 1 + nc;
     const PullArrays pa = pull_arrays(a.region, p.nb);
-    uint32_t ex[kSortPer], ec[kSortPer], el[kSortPer];
+    uint32_t ex[kPer], ec[kPer], el[kPer];
 #pragma unroll
-    for (uint32_t q = 0; q < kSortPer; ++q) {
+    for (uint32_t q = 0; q < kPer; ++q) {
         const uint32_t i = threadIdx.x + q * kInlThreads;
         const bool ok = i < cnt;
-        const u64 ri = (u64)b * kBinCap + (ok ? i : 0u);
+        const u64 ri = rb + (ok ? i : 0u);
         const uint32_t lt = ok ? (uint32_t)a.region_lt[ri] : kNone;
         ex[q] = a.region[ri];
         ec[q] = a.region_code[ri];
@@ -643,7 +736,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort_dlv(InListArgs a) {
     if (threadIdx.x < kMaxCoarse) pcnt[threadIdx.x] = 0u;
     __syncthreads();
 #pragma unroll
-    for (uint32_t q = 0; q < kSortPer; ++q)
+    for (uint32_t q = 0; q < kPer; ++q)
         if (el[q] != kNone) atomicAdd(&h[el[q] >> 1], 1u << ((el[q] & 1u) << 4));
     __syncthreads();
     const uint32_t i0 = threadIdx.x * kHalfPer;
@@ -661,7 +754,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort_dlv(InListArgs a) {
     __syncthreads();
     if (threadIdx.x == 0 && total > kHalfCap) atomicOr(&a.flags[2], kFlagLimit);
 #pragma unroll
-    for (uint32_t q = 0; q < kSortPer; ++q) {
+    for (uint32_t q = 0; q < kPer; ++q) {
         if (el[q] != kNone) {
             const uint32_t shf = (el[q] & 1u) << 4;
             const uint32_t pos = (atomicAdd(&h[el[q] >> 1], 1u << shf) >> shf) & 0xFFFFu;
@@ -747,10 +840,15 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort_dlv(InListArgs a) {
             pC |= nw & vC;
             pnot &= ~sl;
             // an empty pull batch is not passed back: PULL[] reads 0 for it
-            if (scd[j]) atomicAdd(&pcnt[sid[j] >> kCoarseLog], 1u);
+            if (!direct && scd[j]) atomicAdd(&pcnt[sid[j] >> kCoarseLog], 1u);
         }
     }
     __syncthreads();
+    if (direct) {  // one coarse bucket: every pull straight into PULL (cache-resident)
+        const uint32_t placed = min(total, kHalfCap);
+        for (uint32_t j = threadIdx.x; j < placed; j += kInlThreads) a.pull[sid[j]] = scd[j];
+        return;
+    }
     // the (pusher, pull) pairs into the pushers' coarse source buckets
     if (threadIdx.x < nc) {
         const uint32_t c = pcnt[threadIdx.x];
@@ -1009,6 +1107,15 @@ CsrPlan dlv_plan(uint32_t n) {
     p.chunk = kPartChunk;
     // pushers beyond kDlvInline: E[max(k - 2, 0)] = 3/e - 1 = 10.4 % of n
     p.tailcap = n / 8u + 4096u;  // (the tails hold push codes only: src_words = tailcap)
+    // the partition writes the sort blocks' parts (one coarse bucket:
+    // dl_direct; dl_fine: at most two parts per bin)
+    const uint32_t nc = n_coarse(p.nb);
+    p.sub = dlv_split_log(p.nb);
+#ifdef GS_DLV_BIN_REGIONS  // (A/B: whole-bin regions, each sort block filters by part)
+    if (nc > 1u) p.sub = 0u;
+#endif
+    if (nc > 1u && p.sub > 1u) p.sub = 0u;  // (kFineParts)
+    p.fill_off = p.sub ? 2 * p.nb + 1 + 2 * nc : 0u;  // after fill[nb], tailcnt, coarse fills, pull fills
     return p;
 }
 
@@ -1026,6 +1133,9 @@ CsrPlan csr_plan(uint32_t n) {
         p.chunk = n >= (1u << 22) ? kChunk : kChunkSmall;
         p.ba = (uint32_t)(((u64)n + p.chunk - 1) / p.chunk);
         p.tailcap = n / 32u + 1024u;
+        // several sort blocks per bin: inl_bin partitions into their parts
+        p.sub = sort_split_log(p.nb);
+        p.fill_off = p.sub ? p.nb + 1 : 0u;  // after fill[nb], tailcnt
         return p;
     }
     uint32_t bin = 4096;
@@ -1041,6 +1151,20 @@ CsrPlan csr_plan(uint32_t n) {
     return p;
 }
 
+// The counters a binned build needs cleared before it runs, as one range of
+// scratch (words == 0: none; the whole-bin sort clears its own).
+void inlist_zero_range(const CsrPlan &p, size_t *first, size_t *words) {
+    *first = 0;
+    *words = 0;
+    if (!p.binned) return;
+    if (p.dlv) {
+        *words = inlist_sizes(p).scratch_words;
+    } else if (p.sub) {
+        *first = p.fill_off;
+        *words = (size_t)p.nb << p.sub;
+    }
+}
+
 InListSizes inlist_sizes(const CsrPlan &p) {
     InListSizes z{};
     if (p.binned) {
@@ -1051,6 +1175,7 @@ InListSizes inlist_sizes(const CsrPlan &p) {
         if (p.dlv) z.region_words += 3 * nc * kCoarseCap + pull_words(p.nb);
         // fill[nb], tailcnt[, coarse fill[nc], pull coarse fill[nc], pull bin fill[nb]]
         z.scratch_words = (size_t)p.nb + 1 + (p.dlv ? 2 * nc + p.nb : 0);
+        if (p.sub) z.scratch_words = (size_t)p.fill_off + ((size_t)p.nb << p.sub);  // part fills
     } else {
         z.src_words = p.tailcap;
         z.region_words = 3 * (size_t)p.n;  // u64 pairs + the CSR
@@ -1090,14 +1215,16 @@ hipError_t launch_build_bins(const InListArgs &a, hipStream_t s) {
     const CsrPlan &p = a.p;
     if (p.n == 0) return hipSuccess;
     if (!p.binned || p.dlv) return hipErrorInvalidValue;
-    const size_t lds_bin = ((size_t)p.chunk + p.chunk / 2 + (p.nb + 1) / 2) * sizeof(uint32_t) +
-                           (size_t)2 * p.nb * sizeof(uint16_t);
+    const uint32_t np = p.nb << p.sub;
+    const size_t lds_bin = ((size_t)p.chunk + p.chunk / 2 + (np + 1) / 2) * sizeof(uint32_t) +
+                           (size_t)2 * np * sizeof(uint16_t);
     const void *kb = p.chunk == kChunk ? (const void *)inl_bin<kChunk> : (const void *)inl_bin<kChunkSmall>;
     hipError_t e = hipFuncSetAttribute(kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bin);
     if (e != hipSuccess) return e;
     const uint32_t sl = sort_split_log(p.nb);
     if (sl > 0) {  // the split sort cannot clear the fill counts itself
-        e = hipMemsetAsync(a.scratch, 0, (size_t)p.nb * sizeof(uint32_t), s);
+        if (p.sub != sl) return hipErrorInvalidValue;
+        e = hipMemsetAsync(a.scratch + p.fill_off, 0, ((size_t)p.nb << p.sub) * sizeof(uint32_t), s);
         if (e != hipSuccess) return e;
     }
     InListArgs ab = a;
@@ -1135,16 +1262,23 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
     const CsrPlan &p = a.p;
     if (p.n == 0) return hipSuccess;
     if (p.binned) {
-        const size_t lds_bin = ((size_t)p.chunk + p.chunk / 2 + (p.nb + 1) / 2) * sizeof(uint32_t) +
-                               (size_t)2 * p.nb * sizeof(uint16_t);
+        const uint32_t np = p.nb << p.sub;
+        const size_t lds_bin = ((size_t)p.chunk + p.chunk / 2 + (np + 1) / 2) * sizeof(uint32_t) +
+                               (size_t)2 * np * sizeof(uint16_t);
         const void *kb = p.chunk == kChunk ? (const void *)inl_bin<kChunk> : (const void *)inl_bin<kChunkSmall>;
         const uint32_t sl = sort_split_log(p.nb);
         const size_t lds_sort = ((size_t)(kBin >> sl) / 2 + (kBinCap >> sl)) * sizeof(uint32_t);
         const uint32_t dsl = dlv_split_log(p.nb);
         const size_t lds_dlv = ((size_t)(kBin >> dsl) / 2 + 2 * (size_t)(kBinCap >> dsl)) * sizeof(uint32_t);
-        const void *ks = p.dlv ? (dsl == kSplitLog       ? (const void *)inl_sort_dlv<kSplitLog>
-                                  : dsl == kSplitLog + 1u ? (const void *)inl_sort_dlv<kSplitLog + 1u>
-                                                          : (const void *)inl_sort_dlv<kSplitLog + 2u>)
+        const bool own = p.sub != 0u;
+        const void *kd = dsl == kSplitLog
+                             ? (own ? (const void *)inl_sort_dlv<kSplitLog, true> : (const void *)inl_sort_dlv<kSplitLog, false>)
+                         : dsl == kSplitLog + 1u
+                             ? (own ? (const void *)inl_sort_dlv<kSplitLog + 1u, true>
+                                    : (const void *)inl_sort_dlv<kSplitLog + 1u, false>)
+                             : (own ? (const void *)inl_sort_dlv<kSplitLog + 2u, true>
+                                    : (const void *)inl_sort_dlv<kSplitLog + 2u, false>);
+        const void *ks = p.dlv ? kd
                                : (sl == 0 ? (const void *)inl_sort<0> : sl == 1 ? (const void *)inl_sort<1>
                                                                                : (const void *)inl_sort<2>);
         hipError_t e = hipFuncSetAttribute(kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bin);
@@ -1160,7 +1294,7 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
             // fill counts (both half-bin blocks of a bin read them, so they are
             // cleared here rather than by the sort), tail count, coarse fills
             const uint32_t nc = (p.nb + kCoarseBins - 1) / kCoarseBins;
-            e = hipMemsetAsync(a.scratch, 0, ((size_t)2 * p.nb + 1 + 2 * nc) * sizeof(uint32_t), s);
+            if (!a.prezeroed) e = hipMemsetAsync(a.scratch, 0, inlist_sizes(p).scratch_words * sizeof(uint32_t), s);
             const size_t lds_c = 3 * (size_t)kPartChunk * sizeof(uint32_t);
             const size_t lds_f = (2 * (size_t)kPartChunk + kPartChunk / 2) * sizeof(uint32_t);
             if (e == hipSuccess)
@@ -1170,22 +1304,38 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
                 e = hipFuncSetAttribute((const void *)dl_fine, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)lds_f);
             if (e != hipSuccess) return e;
-            hipLaunchKernelGGL(dl_coarse, dim3(p.ba), dim3(kInlThreads), lds_c, s, ab);
-            hipLaunchKernelGGL(dl_fine, dim3((kCoarseCap + kPartChunk - 1) / kPartChunk, nc), dim3(kInlThreads),
-                               lds_f, s, ab);
+            const bool direct = nc == 1u;  // small n: one pass into the parts, pulls written directly
+            if ((p.sub && p.sub != dsl) || (direct && (!p.sub || (p.nb << p.sub) > kDirectParts)) ||
+                (!direct && p.sub > 1u))
+                return hipErrorInvalidValue;
+            if (direct) {
+                const size_t lds_d = (2 * (size_t)kPartChunk + kPartChunk) * sizeof(uint32_t);
+                e = hipFuncSetAttribute((const void *)dl_direct, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)lds_d);
+                if (e != hipSuccess) return e;
+                hipLaunchKernelGGL(dl_direct, dim3(p.ba), dim3(kInlThreads), lds_d, s, ab);
+            } else {
+                hipLaunchKernelGGL(dl_coarse, dim3(p.ba), dim3(kInlThreads), lds_c, s, ab);
+                hipLaunchKernelGGL(dl_fine, dim3((kCoarseCap + kPartChunk - 1) / kPartChunk, nc),
+                                   dim3(kInlThreads), lds_f, s, ab);
+            }
             const dim3 gd(p.nb, 1u << dsl);
-            if (dsl == kSplitLog) hipLaunchKernelGGL(inl_sort_dlv<kSplitLog>, gd, dim3(kInlThreads), lds_dlv, s, ab);
-            else if (dsl == kSplitLog + 1u)
-                hipLaunchKernelGGL(inl_sort_dlv<kSplitLog + 1u>, gd, dim3(kInlThreads), lds_dlv, s, ab);
-            else hipLaunchKernelGGL(inl_sort_dlv<kSplitLog + 2u>, gd, dim3(kInlThreads), lds_dlv, s, ab);
+            void *kargs[] = {&ab};
+            e = hipLaunchKernel(kd, gd, dim3(kInlThreads), kargs, lds_dlv, s);
+            if (e != hipSuccess) return e;
             const size_t lds_pb = ((size_t)kPartChunk + kPartChunk / 2 + kPartChunk / 4) * sizeof(uint32_t);
             e = hipFuncSetAttribute((const void *)pb_fine, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_pb);
             if (e != hipSuccess) return e;
-            hipLaunchKernelGGL(pb_fine, dim3((1u << kCoarseLog) / kPartChunk, nc), dim3(kInlThreads), lds_pb, s, ab);
-            hipLaunchKernelGGL(pb_place, dim3(p.nb), dim3(kInlThreads), 0, s, ab);
+            if (!direct) {
+                hipLaunchKernelGGL(pb_fine, dim3((1u << kCoarseLog) / kPartChunk, nc), dim3(kInlThreads), lds_pb, s,
+                                   ab);
+                hipLaunchKernelGGL(pb_place, dim3(p.nb), dim3(kInlThreads), 0, s, ab);
+            }
         } else {
             if (sl > 0) {  // the split sort cannot clear the fill counts itself
-                e = hipMemsetAsync(a.scratch, 0, (size_t)p.nb * sizeof(uint32_t), s);
+                if (p.sub != sl) return hipErrorInvalidValue;
+                if (!a.prezeroed)
+                    e = hipMemsetAsync(a.scratch + p.fill_off, 0, ((size_t)p.nb << p.sub) * sizeof(uint32_t), s);
                 if (e != hipSuccess) return e;
             }
             if (p.chunk == kChunk) hipLaunchKernelGGL(inl_bin<kChunk>, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);

@@ -13,6 +13,11 @@ struct RoundArgs {
     const uint32_t *dtail;    //   push codes of pushers >= kDlvInline
     const uint32_t *pull;     //   PULL[x]: the pull batch t(x) returned to x
     uint32_t *pc_out;         // DLV: push code of every node's round-(t+1) push batch
+    // counters of the in-list build that follows this kernel on its stream,
+    // cleared here (grid-stride) instead of by a memset launch (null: none)
+    uint32_t *zero_buf;
+    uint32_t zero_words;
+    u64 *zero_rows;
     const uint4 *IN;          // shard engine: per node {first edge, k | zi<<16, e0, e1}
     const uint32_t *IN2;      // shard engine: per node e2 (third pusher's receive row)
     const uint32_t *src;      // round t in-list tails (shard engine: receive rows)
@@ -140,6 +145,12 @@ struct CsrPlan {
     uint32_t chunk;   // sources per chunk
     uint32_t tailcap; // binned: capacity of the in-degree > kInline tail list
     uint32_t dlv;     // delivery records (DlvRec) instead of InRec / SibRec
+    // binned, small networks: the partition writes 2^sub parts per bin, each
+    // in its own region of kBinCap >> sub slots with its fill count at
+    // scratch[fill_off + part], so each sort block reads only its part
+    // (sub = 0: whole bins, fills at scratch[0, nb))
+    uint32_t sub;
+    uint32_t fill_off;
 };
 CsrPlan csr_plan(uint32_t n);
 // The plan of the DLV path (binned only; tails sized for kDlvInline), or one
@@ -149,6 +160,7 @@ struct InListSizes {
     size_t src_words, region_words, scratch_words;  // u32 words
 };
 InListSizes inlist_sizes(const CsrPlan &p);
+void inlist_zero_range(const CsrPlan &p, size_t *first, size_t *words);
 
 struct InListArgs {
     CsrPlan p;
@@ -158,6 +170,7 @@ struct InListArgs {
     uint32_t dlv;
     const u64 *S;
     const uint32_t *PC;     // push codes of the round (written by the round kernel)
+    uint32_t prezeroed;     // 1: the round kernel before cleared the counters (RoundArgs::zero_*)
     Geometry g;
     DlvRec *DR;         // [n]
     uint32_t *dtail;    // [tailcap] push codes of pushers >= kDlvInline

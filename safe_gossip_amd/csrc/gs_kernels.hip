@@ -90,6 +90,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     constexpr bool DELIVER = (MODE == 1 || MODE == 2);
     constexpr bool TRANSITION = (MODE == 0 || MODE == 1);
     const Geometry &g = a.g;
+    if (a.zero_buf || a.zero_rows) zero_for_build(a.zero_buf, a.zero_words, a.zero_rows);
     const uint32_t bid = blockIdx.x + a.blk_off;
     const u64 seg = (u64)bid * blockDim.x + threadIdx.x;
     const bool valid = seg < g.nseg;
