@@ -55,9 +55,51 @@ GS_DEV u64 ge_u(const u64 (&x)[NB], uint32_t K) {
     return ~b;
 }
 
-struct Cls {
-    u64 c, a0, a1;
+// The bit-sliced helpers for a lane word of either width (u64, or u32 for
+// the 32-bit lane kernels: gs_dlv4.hip, gs_w32.hip).
+template <typename T>
+GS_DEV uint32_t popcT(T v) {
+    if constexpr (sizeof(T) == 8) return (uint32_t)__popcll(v);
+    else return (uint32_t)__popc(v);
+}
+template <typename T>
+GS_DEV void add5T(T (&c)[5], T in) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const T t = c[i] & in;
+        c[i] ^= in;
+        in = t;
+    }
+}
+// "x >= K" for a wave-uniform K (the borrow chain of x - K)
+template <int NB, typename T>
+GS_DEV T ge_uT(const T (&x)[NB], uint32_t K) {
+    if (K >= (1u << NB)) return (T)0;
+    T b = 0;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const T k = ((K >> i) & 1u) ? (T)~(T)0 : (T)0;
+        b = (~x[i] & b) | (k & (~x[i] | b));
+    }
+    return ~b;
+}
+// "x >= K" for a per-lane K
+template <int NB, typename T>
+GS_DEV T ge_kT(const T (&x)[NB], uint32_t K) {
+    T b = 0;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const T k = (T)0 - (T)((K >> i) & 1u);
+        b = (~x[i] & b) | (k & (~x[i] | b));
+    }
+    return K >= (1u << NB) ? (T)0 : ~b;
+}
+
+template <typename T>
+struct ClsT {
+    T c, a0, a1;
 };
+using Cls = ClsT<u64>;
 
 template <bool SMALL>
 struct Lane {

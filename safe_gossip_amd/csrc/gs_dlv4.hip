@@ -30,33 +30,7 @@ constexpr uint32_t kDlv4Threads = 256;
 
 // The lane word T holds the lane's nodes side by side (u32: two 16-bit or
 // four <= 8-bit segments; u64: four 16-bit segments); the bit-sliced helpers
-// of gs_device.h for either width.
-template <typename T>
-GS_DEV uint32_t popcT(T v) {
-    if constexpr (sizeof(T) == 8) return (uint32_t)__popcll(v);
-    else return (uint32_t)__popc(v);
-}
-template <typename T>
-GS_DEV void add5T(T (&c)[5], T in) {
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        const T t = c[i] & in;
-        c[i] ^= in;
-        in = t;
-    }
-}
-// "x >= K" for a wave-uniform K (the borrow chain of x - K)
-template <int NB, typename T>
-GS_DEV T ge_uT(const T (&x)[NB], uint32_t K) {
-    if (K >= (1u << NB)) return (T)0;
-    T b = 0;
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-        const T k = ((K >> i) & 1u) ? (T)~(T)0 : (T)0;
-        b = (~x[i] & b) | (k & (~x[i] | b));
-    }
-    return ~b;
-}
+// of gs_device.h (popcT, add5T, ge_uT) take either width.
 // "x >= K" with K given per segment: km[i] holds bit i of every segment's K
 // spread over that segment.
 template <int NB, typename T>

@@ -73,6 +73,7 @@ struct gs_engine {
     // SAFE_GOSSIP_AMD_PIPE=1: the wide 2P gather path runs the pipelined
     // round kernel (gs_pipe.hip) instead of round_kernel
     bool no_pipe = false;
+    bool w32 = false;  // 2P gather path, R_pad 32..256: the 32-bit lane round kernel (gs_w32.hip)
     uint32_t pipe_grid = 0;  // SAFE_GOSSIP_AMD_PIPE_GRID: fewer blocks (tests: many tiles per block)
     // Sparse records (wide 2P engine, W <= 8; gs_kernels.h RoundArgs): maps of
     // plane buffer i, the accounting words and MODE-1 launches counted in them
@@ -195,6 +196,9 @@ uint32_t ilog2(uint32_t v) {
     while ((1u << l) < v) ++l;
     return l;
 }
+
+// The 32-bit lane round kernel (gs_w32.hip) on eligible launches by default.
+constexpr bool kW32Default = false;
 
 gs_status set_device(gs_engine *e) {
     return hipSetDevice(e->device) == hipSuccess ? GS_OK : GS_ERR_HIP;
@@ -368,6 +372,7 @@ gs::RoundArgs base_args(gs_engine *e) {
     a.obs_only = 0xFFFFFFFFu;
     a.dlv_pack = e->dlv_pack;
     a.no_pipe = e->no_pipe ? 1u : 0u;
+    a.w32 = e->w32 ? 1u : 0u;
     a.pipe_grid = e->pipe_grid;
     a.g = e->g;
     a.seed = e->seed;
@@ -699,6 +704,9 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
     {
         const char *v = std::getenv("SAFE_GOSSIP_AMD_PIPE");
         e->no_pipe = !(v && *v == '1');  // opt-in: measured slower than round_kernel
+        // SAFE_GOSSIP_AMD_W32=0/1: the 64-bit / 32-bit lane round kernel (A/B, tests)
+        const char *w = std::getenv("SAFE_GOSSIP_AMD_W32");
+        e->w32 = (w && *w) ? *w != '0' : kW32Default;
         const char *gv = std::getenv("SAFE_GOSSIP_AMD_PIPE_GRID");
         e->pipe_grid = gv ? (uint32_t)std::strtoul(gv, nullptr, 10) : 0u;
     }
@@ -1080,7 +1088,8 @@ gs_status round_begin(gs_engine *e) {
         GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[(R0 + 1) % 3], 0));
         if (e->deliver_pending) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_edges[R0 % 2], 0));
     } else if (e->deliver_pending) {
-        GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[rs], 0));
+        if (e->concurrent_inlists && !e->dlv)  // (built on the engine stream: in order already)
+            GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[rs], 0));
         st = seq_prepare(e);  // SEQ: pull batches of round t (no-op for 2P)
         if (st != GS_OK) return st;
     }
@@ -1198,7 +1207,7 @@ gs_status round_end(gs_engine *e, gs_round_report *report) {
             GS_HIP(hipMemsetAsync(la.rows, 0, sizeof(u64), e->stream));
             GS_HIP(gs::launch_build_sort(la, e->stream));
         } else {
-            GS_HIP(hipStreamWaitEvent(bs, e->ev_read[ns], 0));
+            if (bs != e->stream) GS_HIP(hipStreamWaitEvent(bs, e->ev_read[ns], 0));
             st = next_serial(e, c, bs);
             if (st != GS_OK) return st;
             gs::InListArgs la = inlist_args(e, c, e->round);
@@ -1450,8 +1459,10 @@ void gs_set_timing(gs_engine *e, int enable) {
         (void)hipSetDevice(e->device);
         e->tev.resize(2 * (size_t)kTimingSlots * gs::kMaxParts, nullptr);
         e->tparts.assign(kTimingSlots, 0);
+        // timing only: no system-scope fence (an L2 write-back and invalidate
+        // at every record) around the kernel being timed
         for (auto &ev : e->tev)
-            if (hipEventCreate(&ev) != hipSuccess) {
+            if (hipEventCreateWithFlags(&ev, hipEventDisableSystemFence) != hipSuccess) {
                 e->timing = false;
                 return;
             }
@@ -1700,6 +1711,8 @@ const char *gs_round_kernel_name(const gs_engine *e) {
                                 : (e->dlv_pack == 3 ? "round_kernel_dlv4<1,u32,1>" : "round_kernel_dlv4<1,u32,2>");
     }
     if (e->spr) return "round_kernel<false,1,SPARSE>";
+    if (e->filt && e->w32 && !e->g.small && e->g.logr <= 8)
+        return "round_kernel_w32<1> (32-bit lanes, live-filtered gathers)";
     if (e->filt) return e->g.small ? "round_kernel<true,1> (live-filtered gathers)"
                                    : "round_kernel<false,1> (live-filtered gathers)";
     return e->g.small ? "round_kernel<true,1>" : "round_kernel<false,1>";

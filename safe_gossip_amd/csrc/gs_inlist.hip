@@ -415,6 +415,17 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
 constexpr uint32_t kCoarseBins = 128;
 constexpr uint32_t kCoarseLog = kBinLog + 7;
 constexpr uint32_t kCoarseCap = (1u << kCoarseLog) + (1u << (kCoarseLog - 4));
+// Each coarse bucket is split into kCoarseShards sub-regions with fill
+// counters of their own (dl_coarse block b reserves in shard b % S): every
+// dl_coarse block makes one returning atomic per bucket, and on one counter
+// word those serialise at the memory side (~88 per us, MI355X_MICROARCH.md
+// "dequeue"), so ~24 K blocks on 48 words queued behind each other.
+#ifndef GS_COARSE_SHARDS
+#define GS_COARSE_SHARDS 1
+#endif
+constexpr uint32_t kCoarseShards = GS_COARSE_SHARDS;
+constexpr uint32_t kShardCap = kCoarseCap / kCoarseShards;
+static_assert(kCoarseCap % kCoarseShards == 0, "whole shards");
 #ifndef GS_PART_CHUNK
 #define GS_PART_CHUNK 4096
 #endif
@@ -423,6 +434,12 @@ constexpr uint32_t kPartPer = kPartChunk / kInlThreads;
 constexpr uint32_t kMaxCoarse = 1u << (27 - kCoarseLog);  // n <= 2^27
 
 __host__ __device__ inline uint32_t n_coarse(uint32_t nb) { return (nb + kCoarseBins - 1) / kCoarseBins; }
+// DLV scratch: fill[nb], tail count, coarse shard fills [nc * S], pull coarse
+// fills [nc], pull bin fills [nb], then the part fills (fill_off)
+__host__ __device__ inline uint32_t cfill_off(uint32_t nb) { return nb + 1u; }
+__host__ __device__ inline uint32_t pcfill_off(uint32_t nb) { return nb + 1u + n_coarse(nb) * kCoarseShards; }
+__host__ __device__ inline uint32_t pffill_off(uint32_t nb) { return pcfill_off(nb) + n_coarse(nb); }
+__host__ __device__ inline uint32_t dlv_scratch_words(uint32_t nb) { return pffill_off(nb) + nb; }
 
 // Coarse-bucket arrays inside the region buffer, after the bin regions.
 struct CoarseArrays {
@@ -430,7 +447,7 @@ struct CoarseArrays {
 };
 __host__ __device__ inline CoarseArrays coarse_arrays(uint32_t *region, uint32_t nb) {
     const size_t base = (size_t)nb * kBinCap * 5 / 2;
-    const size_t cap = (size_t)((nb + kCoarseBins - 1) / kCoarseBins) * kCoarseCap;
+    const size_t cap = (size_t)((nb + kCoarseBins - 1) / kCoarseBins) * kCoarseCap;  // = nc * S * kShardCap
     return CoarseArrays{region + base, region + base + cap, region + base + 2 * cap};
 }
 
@@ -460,7 +477,8 @@ __global__ __launch_bounds__(kInlThreads) void dl_coarse(InListArgs a) {
     __shared__ uint32_t cnt[kMaxCoarse], off[kMaxCoarse], res[kMaxCoarse + 1];
     const CsrPlan &p = a.p;
     const uint32_t nc = n_coarse(p.nb);
-    uint32_t *cfill = a.scratch + p.nb + 1;
+    const uint32_t shard = blockIdx.x % kCoarseShards;
+    uint32_t *cfill = a.scratch + cfill_off(p.nb);
     const CoarseArrays ca = coarse_arrays(a.region, p.nb);
     for (uint32_t i = threadIdx.x; i < nc; i += kInlThreads) cnt[i] = 0u;
     __syncthreads();
@@ -487,10 +505,10 @@ __global__ __launch_bounds__(kInlThreads) void dl_coarse(InListArgs a) {
         const uint32_t ex = block_exclusive_scan_t<kInlThreads>(c, lds_scan, total);
         if (threadIdx.x < nc) {
             off[threadIdx.x] = ex;
-            uint32_t r0 = c ? atomicAdd(&cfill[threadIdx.x], c) : 0u;
-            if (r0 + c > kCoarseCap) {
+            uint32_t r0 = c ? atomicAdd(&cfill[threadIdx.x * kCoarseShards + shard], c) : 0u;
+            if (r0 + c > kShardCap) {
                 atomicOr(&a.flags[2], kFlagLimit);
-                r0 = kCoarseCap;
+                r0 = kShardCap;
             }
             res[threadIdx.x] = r0;
             cnt[threadIdx.x] = ex;  // cursor
@@ -512,8 +530,8 @@ __global__ __launch_bounds__(kInlThreads) void dl_coarse(InListArgs a) {
     for (uint32_t i = threadIdx.x; i < total; i += kInlThreads) {
         const uint32_t b = st[i] >> kCoarseLog;
         const uint32_t slot = res[b] + (i - off[b]);
-        if (slot < kCoarseCap) {
-            const u64 o = (u64)b * kCoarseCap + slot;
+        if (slot < kShardCap) {
+            const u64 o = (u64)(b * kCoarseShards + shard) * kShardCap + slot;
             ca.x[o] = sx[i];
             ca.t[o] = st[i];
             ca.c[o] = sc[i];
@@ -521,7 +539,8 @@ __global__ __launch_bounds__(kInlThreads) void dl_coarse(InListArgs a) {
     }
 }
 
-constexpr uint32_t kFineParts = 2 * kCoarseBins;  // parts per coarse bucket (sub <= 1)
+constexpr uint32_t kMaxFineSub = 2;
+constexpr uint32_t kFineParts = kCoarseBins << kMaxFineSub;  // parts per coarse bucket (sub <= 2)
 __global__ __launch_bounds__(kInlThreads) void dl_fine(InListArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     uint32_t *sx = sh, *sc = sh + kPartChunk;
@@ -533,8 +552,8 @@ __global__ __launch_bounds__(kInlThreads) void dl_fine(InListArgs a) {
     // kCoarseBins << sub parts, each in its own region of kBinCap >> sub slots
     const uint32_t fp = kCoarseBins << p.sub, plog = kBinLog - p.sub, pcap = kBinCap >> p.sub;
     uint32_t *pfill = p.sub ? a.scratch + p.fill_off : a.scratch;
-    const uint32_t cb = blockIdx.y;
-    const uint32_t fill = min(a.scratch[p.nb + 1 + cb], kCoarseCap);
+    const uint32_t cs = blockIdx.y, cb = cs / kCoarseShards;  // (coarse bucket, shard)
+    const uint32_t fill = min(a.scratch[cfill_off(p.nb) + cs], kShardCap);
     const uint32_t lo = blockIdx.x * kPartChunk;
     if (lo >= fill) return;  // uniform per block
     const uint32_t hi = min(fill, lo + kPartChunk);
@@ -546,7 +565,7 @@ __global__ __launch_bounds__(kInlThreads) void dl_fine(InListArgs a) {
     for (uint32_t q = 0; q < kPartPer; ++q) {
         const uint32_t i = lo + threadIdx.x + q * kInlThreads;
         const bool ok = i < hi;
-        const u64 o = (u64)cb * kCoarseCap + (ok ? i : lo);
+        const u64 o = (u64)cs * kShardCap + (ok ? i : lo);
         xv[q] = ca.x[o];
         tv[q] = ok ? ca.t[o] : kNone;
         cv[q] = ca.c[o];
@@ -693,7 +712,9 @@ inline uint32_t dlv_split_log(uint32_t nb) {
 }
 
 template <uint32_t SL, bool OWN>
-__global__ __launch_bounds__(kInlThreads) void inl_sort_dlv(InListArgs a) {
+// (own quarter-bin regions: two blocks per CU, 48 KiB of LDS and
+// <= 64 VGPRs each; the second bound is waves per SIMD)
+__global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sort_dlv(InListArgs a) {
     constexpr uint32_t kHalfLog = kBinLog - SL;  // (a "half": one of the 2^SL parts of a bin)
     constexpr uint32_t kHalf = 1u << kHalfLog;
     constexpr uint32_t kHalfCap = kBinCap >> SL;
@@ -719,7 +740,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort_dlv(InListArgs a) {
     const bool direct = nc == 1u;
     const uint32_t cnt = own ? min(a.scratch[p.fill_off + (b << SL) + hh], kHalfCap) : min(a.scratch[b], kBinCap);
     const u64 rb = own ? (u64)((b << SL) + hh) * kHalfCap : (u64)b * kBinCap;
-    uint32_t *pcfill = a.scratch + p.nb + 1 + nc;
+    uint32_t *pcfill = a.scratch + pcfill_off(p.nb);
     const PullArrays pa = pull_arrays(a.region, p.nb);
     uint32_t ex[kPer], ec[kPer], el[kPer];
 #pragma unroll
@@ -877,14 +898,13 @@ __global__ __launch_bounds__(kInlThreads) void pb_fine(InListArgs a) {
     __shared__ uint32_t cnt[kCoarseBins], off[kCoarseBins], res[kCoarseBins];
     __shared__ uint32_t lds_scan[kInlThreads / 64];
     const CsrPlan &p = a.p;
-    const uint32_t nc = n_coarse(p.nb);
     const uint32_t cb = blockIdx.y;
-    const uint32_t fill = min(a.scratch[p.nb + 1 + nc + cb], 1u << kCoarseLog);
+    const uint32_t fill = min(a.scratch[pcfill_off(p.nb) + cb], 1u << kCoarseLog);
     const uint32_t lo = blockIdx.x * kPartChunk;
     if (lo >= fill) return;  // uniform per block
     const uint32_t hi = min(fill, lo + kPartChunk);
     const PullArrays pa = pull_arrays(a.region, p.nb);
-    uint32_t *pffill = a.scratch + p.nb + 1 + 2 * nc;
+    uint32_t *pffill = a.scratch + pffill_off(p.nb);
     if (threadIdx.x < kCoarseBins) cnt[threadIdx.x] = 0u;
     __syncthreads();
     uint32_t xv[kPartPer], vv[kPartPer];
@@ -936,9 +956,8 @@ __global__ __launch_bounds__(kInlThreads) void pb_fine(InListArgs a) {
 __global__ __launch_bounds__(kInlThreads) void pb_place(InListArgs a) {
     __shared__ uint32_t img[kBin];
     const CsrPlan &p = a.p;
-    const uint32_t nc = n_coarse(p.nb);
     const uint32_t b = blockIdx.x;
-    const uint32_t cnt = min(a.scratch[p.nb + 1 + 2 * nc + b], kBin);
+    const uint32_t cnt = min(a.scratch[pffill_off(p.nb) + b], kBin);
     const PullArrays pa = pull_arrays(a.region, p.nb);
     for (uint32_t i = threadIdx.x; i < kBin; i += kInlThreads) img[i] = 0u;
     __syncthreads();
@@ -1114,8 +1133,8 @@ CsrPlan dlv_plan(uint32_t n) {
 #ifdef GS_DLV_BIN_REGIONS  // (A/B: whole-bin regions, each sort block filters by part)
     if (nc > 1u) p.sub = 0u;
 #endif
-    if (nc > 1u && p.sub > 1u) p.sub = 0u;  // (kFineParts)
-    p.fill_off = p.sub ? 2 * p.nb + 1 + 2 * nc : 0u;  // after fill[nb], tailcnt, coarse fills, pull fills
+    if (nc > 1u && p.sub > kMaxFineSub) p.sub = 0u;  // (kFineParts)
+    p.fill_off = p.sub ? dlv_scratch_words(p.nb) : 0u;  // after fill[nb], tailcnt, coarse fills, pull fills
     return p;
 }
 
@@ -1174,7 +1193,7 @@ InListSizes inlist_sizes(const CsrPlan &p) {
         const size_t nc = (p.nb + kCoarseBins - 1) / kCoarseBins;
         if (p.dlv) z.region_words += 3 * nc * kCoarseCap + pull_words(p.nb);
         // fill[nb], tailcnt[, coarse fill[nc], pull coarse fill[nc], pull bin fill[nb]]
-        z.scratch_words = (size_t)p.nb + 1 + (p.dlv ? 2 * nc + p.nb : 0);
+        z.scratch_words = p.dlv ? (size_t)dlv_scratch_words(p.nb) : (size_t)p.nb + 1;
         if (p.sub) z.scratch_words = (size_t)p.fill_off + ((size_t)p.nb << p.sub);  // part fills
     } else {
         z.src_words = p.tailcap;
@@ -1306,7 +1325,7 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
             if (e != hipSuccess) return e;
             const bool direct = nc == 1u;  // small n: one pass into the parts, pulls written directly
             if ((p.sub && p.sub != dsl) || (direct && (!p.sub || (p.nb << p.sub) > kDirectParts)) ||
-                (!direct && p.sub > 1u))
+                (!direct && p.sub > kMaxFineSub))
                 return hipErrorInvalidValue;
             if (direct) {
                 const size_t lds_d = (2 * (size_t)kPartChunk + kPartChunk) * sizeof(uint32_t);
@@ -1316,7 +1335,7 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
                 hipLaunchKernelGGL(dl_direct, dim3(p.ba), dim3(kInlThreads), lds_d, s, ab);
             } else {
                 hipLaunchKernelGGL(dl_coarse, dim3(p.ba), dim3(kInlThreads), lds_c, s, ab);
-                hipLaunchKernelGGL(dl_fine, dim3((kCoarseCap + kPartChunk - 1) / kPartChunk, nc),
+                hipLaunchKernelGGL(dl_fine, dim3((kShardCap + kPartChunk - 1) / kPartChunk, nc * kCoarseShards),
                                    dim3(kInlThreads), lds_f, s, ab);
             }
             const dim3 gd(p.nb, 1u << dsl);

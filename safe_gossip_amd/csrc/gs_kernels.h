@@ -99,6 +99,7 @@ struct RoundArgs {
     const uint8_t *eadd;
     uint32_t no_pipe;         // 1: the wide 2P path runs round_kernel instead of round_pipe
     uint32_t pipe_grid;       // round_pipe's block count (0: every resident block)
+    uint32_t w32;             // 1: eligible launches run round_kernel_w32 (gs_w32.hip)
     uint32_t dlv_pack;        // DLV transition launches: 0 one node per lane, 1 a 32-bit lane
                               // word of several nodes, 2 a 64-bit one (gs_dlv4.hip)
     Geometry g;
@@ -133,6 +134,10 @@ bool pipe_eligible(const RoundArgs &a, int mode);
 constexpr uint32_t kPipeTileNodes = 64;
 inline uint64_t pipe_padded(uint64_t n) { return (n + kPipeTileNodes - 1) / kPipeTileNodes * kPipeTileNodes; }
 hipError_t launch_round_pipe(const RoundArgs &a, int mode, hipStream_t s);
+// The 2P gather path with a 32-bit lane word (gs_w32.hip): modes 0 and 1,
+// R_pad 64..256, live-filtered gathers, no external RPCs, the whole grid.
+bool w32_eligible(const RoundArgs &a, int mode);
+hipError_t launch_round_w32(const RoundArgs &a, int mode, hipStream_t s);
 
 // Plan of the in-list build (gs_inlist.hip).
 struct CsrPlan {

@@ -132,3 +132,64 @@ def test_packed_dlv_matches_node_per_lane(engine, monkeypatch):
     finally:
         a.close()
         b.close()
+
+
+def test_dlv_partition_build_matches_gather_path(engine, monkeypatch):
+    # The DLV build of networks with more than one coarse bucket (n > 2^21:
+    # dl_coarse -> dl_fine -> inl_sort_dlv -> pb_fine -> pb_place) against the
+    # class-plane gather path (SAFE_GOSSIP_AMD_NO_DLV=1: inl_bin / inl_sort and
+    # the gathers of gs_kernels.hip), an independent build of the same round:
+    # every state code, Statistics row and known set, every round, with faults.
+    n, R = (1 << 22) + 54321, 16
+    faults = dict(churn=0.01, drop_push=0.01, drop_pull=0.01)
+    a = engine.Network(n, R, seed=SEED, **faults)
+    monkeypatch.setenv("SAFE_GOSSIP_AMD_NO_DLV", "1")
+    b = engine.Network(n, R, seed=SEED, **faults)
+    try:
+        for r in range(R):
+            x = engine.origin_of(SEED, 0, r, n)
+            a.send_new(x, r)
+            b.send_new(x, r)
+        for rnd in range(1, 9):
+            ra, rb = a.next_round(), b.next_round()
+            assert ra.any_live == rb.any_live
+            np.testing.assert_array_equal(a.dump_state(), b.dump_state(), err_msg=f"state round {rnd}")
+            np.testing.assert_array_equal(a.statistics_all(), b.statistics_all(),
+                                          err_msg=f"statistics round {rnd}")
+            np.testing.assert_array_equal(a.known_all(), b.known_all(), err_msg=f"known round {rnd}")
+        a.sync()
+        b.sync()
+    finally:
+        a.close()
+        b.close()
+
+
+def test_w32_lane_kernel_matches_w64(engine, monkeypatch):
+    # round_kernel_w32 (32-bit lanes, the default at R_pad 64..256) against
+    # the 64-bit lane round_kernel on a network larger than any oracle run:
+    # 2^21 + 1234 nodes x 256 rumors with faults, a partial last block, every
+    # state code, Statistics row and known set of 8 rounds
+    n, R = (1 << 21) + 1234, 256
+    faults = dict(churn=0.01, drop_push=0.02, drop_pull=0.02)
+    monkeypatch.setenv("SAFE_GOSSIP_AMD_W32", "1")
+    a = engine.Network(n, R, seed=SEED, **faults)
+    monkeypatch.setenv("SAFE_GOSSIP_AMD_W32", "0")
+    b = engine.Network(n, R, seed=SEED, **faults)
+    try:
+        for r in range(R):
+            x = engine.origin_of(SEED, 0, r, n)
+            a.send_new(x, r)
+            b.send_new(x, r)
+        for rnd in range(1, 9):
+            ra, rb = a.next_round(), b.next_round()
+            assert ra.any_live == rb.any_live
+            if rnd % 2 == 0:
+                np.testing.assert_array_equal(a.dump_state(), b.dump_state(), err_msg=f"state round {rnd}")
+            np.testing.assert_array_equal(a.statistics_all(), b.statistics_all(),
+                                          err_msg=f"statistics round {rnd}")
+            np.testing.assert_array_equal(a.known_all(), b.known_all(), err_msg=f"known round {rnd}")
+        a.sync()
+        b.sync()
+    finally:
+        a.close()
+        b.close()

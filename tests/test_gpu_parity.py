@@ -473,8 +473,26 @@ def test_parity_pipe(engine, monkeypatch, n, R, kind, faults, grid):
 
 @pytest.mark.parametrize("n,R,filt", [(3000, 256, "1"), (3000, 256, "0"), (2000, 128, "1")])
 def test_parity_round_kernel_wide(engine, monkeypatch, n, R, filt):
-    # round_kernel on the wide 2P path (the default; the pipelined kernel is
-    # opt-in), filtered and unfiltered
+    # the 64-bit lane round_kernel on the wide 2P path (SAFE_GOSSIP_AMD_W32=0;
+    # the default for R_pad 64..256 is round_kernel_w32, which every other
+    # filtered wide test runs), filtered and unfiltered
     monkeypatch.setenv("SAFE_GOSSIP_AMD_PIPE", "0")
+    monkeypatch.setenv("SAFE_GOSSIP_AMD_W32", "0")
     monkeypatch.setenv("SAFE_GOSSIP_AMD_FILTER", filt)
     run_parity(engine, n, R, "origins", check_every=2)
+
+
+@pytest.mark.parametrize("n,R,kind,faults", [
+    (101, 32, "reinject", None),                   # R_pad 32: a lane per node, two nodes per unit word
+    (777, 20, "origins", (0.05, 0.05, 0.05)),      # R_pad 32 with churn votes, an odd node count
+    (300, 64, "trickle", None),                    # W32 = 2: 32 nodes per wave, u32 map stores
+    (77, 100, "origins", None),                    # R_pad 128: W32 = 4
+    (130, 256, "reinject", (0.1, 0.1, 0.2)),       # W32 = 8, churn votes in half words
+    (1000, 200, "trickle", (0.05, 0.05, 0.05)),    # a partial last block
+    (20000, 256, "origins", None),                 # deep in-lists and sibling walks
+])
+def test_parity_w32(engine, monkeypatch, n, R, kind, faults):
+    # the 32-bit lane round kernel (gs_w32.hip), forced on explicitly
+    monkeypatch.setenv("SAFE_GOSSIP_AMD_PIPE", "0")
+    monkeypatch.setenv("SAFE_GOSSIP_AMD_W32", "1")
+    run_parity(engine, n, R, kind, faults=faults, check_every=1 if n < 5000 else 3)
