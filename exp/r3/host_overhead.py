@@ -34,4 +34,4 @@ for n, R in ((1 << 20, 1), (1 << 20, 64)):
         net.close()
         print(json.dumps(dict(n=n, R=R, timing=timing, enqueue_us=(t1 - t0) / K * 1e6,
                               total_us=(t2 - t0) / K * 1e6,
-                              kernel_us=(sum(kt[1:]) / max(1, len(kt) - 1) * 1e3) if len(kt) else None)), flush=True)
+                              kernel_us=float(sum(kt[1:]) / max(1, len(kt) - 1) * 1e3) if len(kt) else None)), flush=True)

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -73,7 +74,7 @@ struct gs_engine {
     // SAFE_GOSSIP_AMD_PIPE=1: the wide 2P gather path runs the pipelined
     // round kernel (gs_pipe.hip) instead of round_kernel
     bool no_pipe = false;
-    bool w32 = false;  // 2P gather path, R_pad 32..256: the 32-bit lane round kernel (gs_w32.hip)
+    bool w32 = false;  // 2P gather path: the 32-bit lane round kernel on eligible launches (gs_w32.hip)
     uint32_t pipe_grid = 0;  // SAFE_GOSSIP_AMD_PIPE_GRID: fewer blocks (tests: many tiles per block)
     // Sparse records (wide 2P engine, W <= 8; gs_kernels.h RoundArgs): maps of
     // plane buffer i, the accounting words and MODE-1 launches counted in them
@@ -180,10 +181,23 @@ namespace {
 constexpr uint32_t kReduceBlocks = 1024;
 constexpr uint32_t kTimingSlots = 4096;
 
+// A failing HIP call returns GS_ERR_HIP; SAFE_GOSSIP_AMD_DEBUG=1 also names
+// it on stderr (call, line, HIP error).
+void report_hip(hipError_t err, const char *what, int line) {
+    static const bool on = [] {
+        const char *v = std::getenv("SAFE_GOSSIP_AMD_DEBUG");
+        return v && *v && *v != '0';
+    }();
+    if (on) std::fprintf(stderr, "safe_gossip_amd: %s failed at gs_engine.cpp:%d: %s\n", what, line,
+                         hipGetErrorString(err));
+}
 #define GS_HIP(expr)                                   \
     do {                                               \
         hipError_t _e = (expr);                        \
-        if (_e != hipSuccess) return GS_ERR_HIP;       \
+        if (_e != hipSuccess) {                        \
+            report_hip(_e, #expr, __LINE__);           \
+            return GS_ERR_HIP;                         \
+        }                                              \
     } while (0)
 
 uint32_t next_pow2(uint32_t v) {
@@ -196,9 +210,6 @@ uint32_t ilog2(uint32_t v) {
     while ((1u << l) < v) ++l;
     return l;
 }
-
-// The 32-bit lane round kernel (gs_w32.hip) on eligible launches by default.
-constexpr bool kW32Default = false;
 
 gs_status set_device(gs_engine *e) {
     return hipSetDevice(e->device) == hipSuccess ? GS_OK : GS_ERR_HIP;
@@ -704,9 +715,13 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
     {
         const char *v = std::getenv("SAFE_GOSSIP_AMD_PIPE");
         e->no_pipe = !(v && *v == '1');  // opt-in: measured slower than round_kernel
-        // SAFE_GOSSIP_AMD_W32=0/1: the 64-bit / 32-bit lane round kernel (A/B, tests)
+        // The 32-bit lane round kernel (gs_w32.hip) by default where a lane
+        // holds one node (R_pad 32: 2^24 x 32, 1.24 -> 1.10 ms/step); at R_pad
+        // 64..256 its duplicated per-node work costs more than its occupancy
+        // gains (config 4: 2.61 -> 3.03 ms per launch).
+        // SAFE_GOSSIP_AMD_W32=0/1 forces the 64-bit / 32-bit lane kernel.
         const char *w = std::getenv("SAFE_GOSSIP_AMD_W32");
-        e->w32 = (w && *w) ? *w != '0' : kW32Default;
+        e->w32 = (w && *w) ? *w != '0' : (e->g.small && e->g.rpad == 32u);
         const char *gv = std::getenv("SAFE_GOSSIP_AMD_PIPE_GRID");
         e->pipe_grid = gv ? (uint32_t)std::strtoul(gv, nullptr, 10) : 0u;
     }
@@ -1711,7 +1726,7 @@ const char *gs_round_kernel_name(const gs_engine *e) {
                                 : (e->dlv_pack == 3 ? "round_kernel_dlv4<1,u32,1>" : "round_kernel_dlv4<1,u32,2>");
     }
     if (e->spr) return "round_kernel<false,1,SPARSE>";
-    if (e->filt && e->w32 && !e->g.small && e->g.logr <= 8)
+    if (e->filt && e->w32 && (e->g.small ? e->g.rpad == 32 : e->g.logr <= 8))
         return "round_kernel_w32<1> (32-bit lanes, live-filtered gathers)";
     if (e->filt) return e->g.small ? "round_kernel<true,1> (live-filtered gathers)"
                                    : "round_kernel<false,1> (live-filtered gathers)";

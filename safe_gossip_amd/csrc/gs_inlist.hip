@@ -174,6 +174,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
     uint16_t *cnt16 = reinterpret_cast<uint16_t *>(cnt);
     uint16_t *off = reinterpret_cast<uint16_t *>(cnt + (np + 1) / 2);  // [np] chunk-local starts
     uint16_t *res = off + np;                  // [np] reserved start in the part's region
+    uint16_t *stage_b = res + np;              // [kChunk] part of each stage entry
     __shared__ uint32_t lds_scan[kInlThreads / 64];
     __shared__ uint32_t zrows;  // filtered: t(x) rows the zl bits leave to gather
     if (blockIdx.x == 0 && threadIdx.x == 0) a.scratch[p.nb] = 0u;  // tail count; inl_sort runs after
@@ -250,19 +251,13 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
         const uint32_t pos = (atomicAdd(&cnt[b >> 1], 1u << sh16) >> sh16) & 0xFFFFu;
         stage[pos] = lo + threadIdx.x + q * kInlThreads;
         stage_lt[pos] = (uint16_t)(t & (kBin - 1u));  // (relative to the bin)
+        stage_b[pos] = (uint16_t)b;
     }
     __syncthreads();
-    // Consecutive stage entries of one bin go to consecutive region slots; the
-    // bin of entry i is found by a binary search over the chunk-local starts.
+    // Consecutive stage entries of one part go to consecutive region slots
+    // (the part of each entry is kept beside it: no search over the starts).
     for (uint32_t i = threadIdx.x; i < total; i += kInlThreads) {  // delivered edges of the chunk
-        uint32_t lo_b = 0, hi_b = np;  // last part with off[b] <= i and a non-empty run
-        while (hi_b - lo_b > 1) {
-            const uint32_t mid = (lo_b + hi_b) >> 1;
-            if (off[mid] <= i) lo_b = mid; else hi_b = mid;
-        }
-        // (empty parts share their start with the next part, so the last part
-        // whose start is <= i is the one whose run holds entry i)
-        const uint32_t b = lo_b;
+        const uint32_t b = stage_b[i];
         const uint32_t slot = res[b] + (i - off[b]);
         if (slot < pcap) {
             a.region[(u64)b * pcap + slot] = stage[i];
@@ -545,6 +540,7 @@ __global__ __launch_bounds__(kInlThreads) void dl_fine(InListArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     uint32_t *sx = sh, *sc = sh + kPartChunk;
     uint16_t *slt = reinterpret_cast<uint16_t *>(sh + 2 * kPartChunk);
+    uint16_t *sb = slt + kPartChunk;  // part of each stage entry
     __shared__ uint32_t cnt[kFineParts], off[kFineParts], res[kFineParts];
     __shared__ uint32_t lds_scan[kInlThreads / 64];
     const CsrPlan &p = a.p;
@@ -596,16 +592,13 @@ __global__ __launch_bounds__(kInlThreads) void dl_fine(InListArgs a) {
         const uint32_t pos = atomicAdd(&cnt[fb], 1u);
         sx[pos] = xv[q];
         sc[pos] = cv[q];
-        slt[pos] = (uint16_t)(tv[q] & (kBin - 1u));  // (relative to the bin; its part is found from off[] below)
+        slt[pos] = (uint16_t)(tv[q] & (kBin - 1u));  // (relative to the bin)
+        sb[pos] = (uint16_t)fb;
     }
     __syncthreads();
     const uint32_t n_here = hi - lo;
     for (uint32_t i = threadIdx.x; i < n_here; i += kInlThreads) {
-        uint32_t lo_b = 0, hi_b = fp;  // last part whose run starts at or before i
-        while (hi_b - lo_b > 1) {
-            const uint32_t mid = (lo_b + hi_b) >> 1;
-            if (off[mid] <= i) lo_b = mid; else hi_b = mid;
-        }
+        const uint32_t lo_b = sb[i];
         const uint32_t slot = res[lo_b] + (i - off[lo_b]);
         if (slot < pcap) {
             const u64 o = (u64)(cb * fp + lo_b) * pcap + slot;
@@ -702,6 +695,9 @@ __global__ __launch_bounds__(kInlThreads) void dl_direct(InListArgs a) {
 #define GS_DLV_SPLIT_LOG 1
 #endif
 constexpr uint32_t kSplitLog = GS_DLV_SPLIT_LOG;   // sort blocks per bin = 2^kSplitLog (large n)
+#ifndef GS_DLV_PP
+#define GS_DLV_PP 0  // 1: inl_sort_dlv as a persistent walk with the next part's loads in flight
+#endif
 // Small networks (few bins) sort with more blocks per bin, so the chip fills;
 // their bin regions stay in L2 (config 2: 64 bins).
 inline uint32_t dlv_split_log(uint32_t nb) {
@@ -711,10 +707,16 @@ inline uint32_t dlv_split_log(uint32_t nb) {
     return nb >= 512u ? kSplitLog : (nb >= 128u ? kSplitLog + 1u : kSplitLog + 2u);
 }
 
-template <uint32_t SL, bool OWN>
+// PP (persistent, own regions, several coarse buckets): a resident grid walks
+// the parts in order, and each block issues the region loads of its NEXT part
+// while the current one's records and pulls are computed (one block per CU
+// holds the LDS of a half bin, so without this a CU's loads and its LDS work
+// take turns).
+template <uint32_t SL, bool OWN, bool PP = false>
 // (own quarter-bin regions: two blocks per CU, 48 KiB of LDS and
 // <= 64 VGPRs each; the second bound is waves per SIMD)
 __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sort_dlv(InListArgs a) {
+    static_assert(!PP || OWN, "the persistent walk reads own part regions");
     constexpr uint32_t kHalfLog = kBinLog - SL;  // (a "half": one of the 2^SL parts of a bin)
     constexpr uint32_t kHalf = 1u << kHalfLog;
     constexpr uint32_t kHalfCap = kBinCap >> SL;
@@ -728,31 +730,40 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
     uint32_t *scd = sid + kHalfCap;     // [kHalfCap] their push codes, then their pulls
     __shared__ uint32_t lds_scan[kInlThreads / 64];
     __shared__ uint32_t pcnt[kMaxCoarse], pres[kMaxCoarse];
-    const uint32_t b = blockIdx.x, hh = blockIdx.y;
-    const uint32_t t0 = (b << kBinLog) + (hh << kHalfLog);
-    const uint32_t nodes = t0 < p.n ? min(kHalf, p.n - t0) : 0u;
-    if (nodes == 0) return;  // a half past the last node (uniform per block)
     const uint32_t nc = n_coarse(p.nb);
     // p.sub == SL: dl_fine / dl_direct wrote this half's own region; small
     // networks (one coarse bucket) write every pull straight to PULL (no
     // pass-back partition)
     constexpr bool own = OWN;
-    const bool direct = nc == 1u;
-    const uint32_t cnt = own ? min(a.scratch[p.fill_off + (b << SL) + hh], kHalfCap) : min(a.scratch[b], kBinCap);
-    const u64 rb = own ? (u64)((b << SL) + hh) * kHalfCap : (u64)b * kBinCap;
+    const bool direct = !PP && nc == 1u;
     uint32_t *pcfill = a.scratch + pcfill_off(p.nb);
     const PullArrays pa = pull_arrays(a.region, p.nb);
+    // part w = (bin b, half hh) = w >> SL, w & (2^SL - 1); PP: the parts
+    // holding nodes, blockIdx.x, + gridDim.x, ...
+    const uint32_t items = PP ? (p.n + kHalf - 1u) / kHalf : 0u;
+    uint32_t w = PP ? blockIdx.x : (blockIdx.x << SL) + blockIdx.y;
+    if (PP && w >= items) return;  // (uniform per block)
     uint32_t ex[kPer], ec[kPer], el[kPer];
+    auto load_part = [&](uint32_t wp) {
+        const uint32_t bp = wp >> SL, hp = wp & ((1u << SL) - 1u);
+        const uint32_t cnt = own ? min(a.scratch[p.fill_off + wp], kHalfCap) : min(a.scratch[bp], kBinCap);
+        const u64 rb = own ? (u64)wp * kHalfCap : (u64)bp * kBinCap;
 #pragma unroll
-    for (uint32_t q = 0; q < kPer; ++q) {
-        const uint32_t i = threadIdx.x + q * kInlThreads;
-        const bool ok = i < cnt;
-        const u64 ri = rb + (ok ? i : 0u);
-        const uint32_t lt = ok ? (uint32_t)a.region_lt[ri] : kNone;
-        ex[q] = a.region[ri];
-        ec[q] = a.region_code[ri];
-        el[q] = (ok && (lt >> kHalfLog) == hh) ? (lt & (kHalf - 1u)) : kNone;
-    }
+        for (uint32_t q = 0; q < kPer; ++q) {
+            const uint32_t i = threadIdx.x + q * kInlThreads;
+            const bool ok = i < cnt;
+            const u64 ri = rb + (ok ? i : 0u);
+            const uint32_t lt = ok ? (uint32_t)a.region_lt[ri] : kNone;
+            ex[q] = a.region[ri];
+            ec[q] = a.region_code[ri];
+            el[q] = (ok && (lt >> kHalfLog) == hp) ? (lt & (kHalf - 1u)) : kNone;
+        }
+    };
+    load_part(w);
+    for (;;) {
+    const uint32_t t0 = w << kHalfLog;
+    const uint32_t nodes = t0 < p.n ? min(kHalf, p.n - t0) : 0u;
+    if (nodes == 0) return;  // a half past the last node (uniform per block; not PP)
     for (uint32_t i = threadIdx.x; i < kHalf / 2; i += kInlThreads) h[i] = 0u;
     if (threadIdx.x < kMaxCoarse) pcnt[threadIdx.x] = 0u;
     __syncthreads();
@@ -787,22 +798,30 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
     }
     __syncthreads();
     // the targets' own target words and class planes, loads issued together
+    // (R_pad <= 16: a node's segment lies in one 32-bit half of its plane word)
     uint32_t tgv[kHalfPer];
-    u64 w0[kHalfPer], w1[kHalfPer], w2[kHalfPer];
+    uint32_t w0[kHalfPer], w1[kHalfPer], w2[kHalfPer];
+    const uint32_t *S32 = reinterpret_cast<const uint32_t *>(a.S);
 #pragma unroll
     for (uint32_t q = 0; q < kHalfPer; ++q) {
         const uint32_t lt = threadIdx.x + q * kInlThreads;
         const uint32_t y = t0 + (lt < nodes ? lt : 0u);
-        const u64 rb = (u64)(y >> a.g.lognpu) * kPlanes;
+        const uint32_t ysh = (y & ((1u << a.g.lognpu) - 1u)) << a.g.logr;
+        const u64 rb = (u64)(y >> a.g.lognpu) * kPlanes * 2u + (ysh >> 5);
         tgv[q] = a.tg[y];
-        w0[q] = a.S[rb];
-        w1[q] = a.S[rb + 1];
-        w2[q] = a.S[rb + 2];
+        w0[q] = S32[rb];
+        w1[q] = S32[rb + 2];
+        w2[q] = S32[rb + 4];
     }
     uint32_t mine = 0;
     for (uint32_t lt = threadIdx.x; lt < nodes; lt += kInlThreads)
         mine += tail_len<kDlvInline>(min(half_of(h, lt), kHalfCap) - (lt ? min(half_of(h, lt - 1), kHalfCap) : 0u));
     uint32_t cur = reserve_tails<kInlThreads>(a, mine, &a.scratch[p.nb], lds_scan);
+    // PP: the next part's region loads, issued after every load and returning
+    // atomic this part still waits for (vmcnt counts in issue order), so
+    // they stay in flight through the record and pull work below
+    const uint32_t wnext = w + gridDim.x;
+    if (PP && wnext < items) load_part(wnext);
     const uint32_t m = (uint32_t)((1ull << a.g.rpad) - 1ull);
 #pragma unroll
     for (uint32_t q = 0; q < kHalfPer; ++q) {
@@ -844,9 +863,8 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
         // the pull batch of each pusher, in place of its push code: y's live
         // set (B with our_counter, C as 255) plus the entries y created from
         // the pushers ahead of it (first carrier B -> counter 1, C -> 255)
-        const uint32_t ysh = ((t0 + lt) & ((1u << a.g.lognpu) - 1u)) << a.g.logr;
-        const uint32_t c = (uint32_t)(w0[q] >> ysh) & m, a0 = (uint32_t)(w1[q] >> ysh) & m,
-                       a1 = (uint32_t)(w2[q] >> ysh) & m;
+        const uint32_t ysh = (((t0 + lt) & ((1u << a.g.lognpu) - 1u)) << a.g.logr) & 31u;
+        const uint32_t c = (w0[q] >> ysh) & m, a0 = (w1[q] >> ysh) & m, a1 = (w2[q] >> ysh) & m;
         const uint32_t zB = ~c & (a0 | a1), zC = c & ~(a0 & a1);
         const uint32_t zB1 = zB & a0 & ~a1, zB2 = zB & a1 & ~a0;
         uint32_t pnot = ~c & ~a0 & ~a1 & m, pB = 0, pC = 0;
@@ -885,6 +903,10 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
         const u64 o = ((u64)cb << kCoarseLog) + slot;
         pa.x[o] = x;
         pa.v[o] = scd[j];
+    }
+    if (!PP || wnext >= items) return;
+    w = wnext;
+    __syncthreads();  // every thread is done with this part's LDS (h, sid, scd, pcnt, pres)
     }
 }
 
@@ -1236,7 +1258,7 @@ hipError_t launch_build_bins(const InListArgs &a, hipStream_t s) {
     if (!p.binned || p.dlv) return hipErrorInvalidValue;
     const uint32_t np = p.nb << p.sub;
     const size_t lds_bin = ((size_t)p.chunk + p.chunk / 2 + (np + 1) / 2) * sizeof(uint32_t) +
-                           (size_t)2 * np * sizeof(uint16_t);
+                           ((size_t)2 * np + p.chunk) * sizeof(uint16_t);
     const void *kb = p.chunk == kChunk ? (const void *)inl_bin<kChunk> : (const void *)inl_bin<kChunkSmall>;
     hipError_t e = hipFuncSetAttribute(kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bin);
     if (e != hipSuccess) return e;
@@ -1283,7 +1305,7 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
     if (p.binned) {
         const uint32_t np = p.nb << p.sub;
         const size_t lds_bin = ((size_t)p.chunk + p.chunk / 2 + (np + 1) / 2) * sizeof(uint32_t) +
-                               (size_t)2 * np * sizeof(uint16_t);
+                               ((size_t)2 * np + p.chunk) * sizeof(uint16_t);
         const void *kb = p.chunk == kChunk ? (const void *)inl_bin<kChunk> : (const void *)inl_bin<kChunkSmall>;
         const uint32_t sl = sort_split_log(p.nb);
         const size_t lds_sort = ((size_t)(kBin >> sl) / 2 + (kBinCap >> sl)) * sizeof(uint32_t);
@@ -1300,7 +1322,9 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
         const void *ks = p.dlv ? kd
                                : (sl == 0 ? (const void *)inl_sort<0> : sl == 1 ? (const void *)inl_sort<1>
                                                                                : (const void *)inl_sort<2>);
-        hipError_t e = hipFuncSetAttribute(kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bin);
+        // (inl_bin is the gather path's partition: its LDS, sized by the parts,
+        // is not set for a DLV plan, whose part count it may not fit)
+        hipError_t e = p.dlv ? hipSuccess : hipFuncSetAttribute(kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bin);
         if (e == hipSuccess)
             e = hipFuncSetAttribute(ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(p.dlv ? lds_dlv : lds_sort));
         if (e != hipSuccess) return e;
@@ -1315,7 +1339,7 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
             const uint32_t nc = (p.nb + kCoarseBins - 1) / kCoarseBins;
             if (!a.prezeroed) e = hipMemsetAsync(a.scratch, 0, inlist_sizes(p).scratch_words * sizeof(uint32_t), s);
             const size_t lds_c = 3 * (size_t)kPartChunk * sizeof(uint32_t);
-            const size_t lds_f = (2 * (size_t)kPartChunk + kPartChunk / 2) * sizeof(uint32_t);
+            const size_t lds_f = (2 * (size_t)kPartChunk + kPartChunk) * sizeof(uint32_t);
             if (e == hipSuccess)
                 e = hipFuncSetAttribute((const void *)dl_coarse, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)lds_c);
@@ -1338,9 +1362,24 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
                 hipLaunchKernelGGL(dl_fine, dim3((kShardCap + kPartChunk - 1) / kPartChunk, nc * kCoarseShards),
                                    dim3(kInlThreads), lds_f, s, ab);
             }
-            const dim3 gd(p.nb, 1u << dsl);
             void *kargs[] = {&ab};
-            e = hipLaunchKernel(kd, gd, dim3(kInlThreads), kargs, lds_dlv, s);
+            if (GS_DLV_PP && own && !direct) {  // persistent walk over the parts (A/B)
+                const void *kp = dsl == kSplitLog        ? (const void *)inl_sort_dlv<kSplitLog, true, true>
+                                 : dsl == kSplitLog + 1u ? (const void *)inl_sort_dlv<kSplitLog + 1u, true, true>
+                                                         : (const void *)inl_sort_dlv<kSplitLog + 2u, true, true>;
+                e = hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dlv);
+                int dev = 0, cus = 0, per_cu = 0;
+                if (e == hipSuccess) e = hipGetDevice(&dev);
+                if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+                if (e == hipSuccess)
+                    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, kInlThreads, lds_dlv);
+                if (e != hipSuccess) return e;
+                const u64 items = ((u64)p.n + (kBin >> dsl) - 1) >> (kBinLog - dsl);
+                const uint32_t grid = (uint32_t)std::min<u64>(items, (u64)std::max(1, per_cu) * std::max(1, cus));
+                e = hipLaunchKernel(kp, dim3(grid), dim3(kInlThreads), kargs, lds_dlv, s);
+            } else {
+                e = hipLaunchKernel(kd, dim3(p.nb, 1u << dsl), dim3(kInlThreads), kargs, lds_dlv, s);
+            }
             if (e != hipSuccess) return e;
             const size_t lds_pb = ((size_t)kPartChunk + kPartChunk / 2 + kPartChunk / 4) * sizeof(uint32_t);
             e = hipFuncSetAttribute((const void *)pb_fine, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_pb);

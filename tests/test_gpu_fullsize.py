@@ -134,13 +134,15 @@ def test_packed_dlv_matches_node_per_lane(engine, monkeypatch):
         b.close()
 
 
-def test_dlv_partition_build_matches_gather_path(engine, monkeypatch):
+@pytest.mark.parametrize("n", [(1 << 22) + 54321, (1 << 23) + 4321])
+def test_dlv_partition_build_matches_gather_path(engine, monkeypatch, n):
     # The DLV build of networks with more than one coarse bucket (n > 2^21:
     # dl_coarse -> dl_fine -> inl_sort_dlv -> pb_fine -> pb_place) against the
     # class-plane gather path (SAFE_GOSSIP_AMD_NO_DLV=1: inl_bin / inl_sort and
     # the gathers of gs_kernels.hip), an independent build of the same round:
     # every state code, Statistics row and known set, every round, with faults.
-    n, R = (1 << 22) + 54321, 16
+    # 260 bins: quarter-bin sort parts; 513 bins: half bins, the config-5 shape.
+    R = 16
     faults = dict(churn=0.01, drop_push=0.01, drop_pull=0.01)
     a = engine.Network(n, R, seed=SEED, **faults)
     monkeypatch.setenv("SAFE_GOSSIP_AMD_NO_DLV", "1")
