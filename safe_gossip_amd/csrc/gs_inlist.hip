@@ -407,8 +407,13 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
 //   dl_fine   : per chunk of a coarse bucket: an LDS counting sort into its
 //               kCoarseBins bins of kBin targets, runs of ~64, into the bin
 //               regions inl_sort_dlv reads
-constexpr uint32_t kCoarseBins = 128;
-constexpr uint32_t kCoarseLog = kBinLog + 7;
+#ifndef GS_COARSE_BINS
+#define GS_COARSE_BINS 128
+#endif
+constexpr uint32_t kCoarseBins = GS_COARSE_BINS;  // bins per coarse bucket (a power of two)
+constexpr uint32_t ilog2c(uint32_t v) { return v <= 1u ? 0u : 1u + ilog2c(v >> 1); }
+static_assert((kCoarseBins & (kCoarseBins - 1u)) == 0 && kCoarseBins <= 256, "coarse bins: a power of two <= 256");
+constexpr uint32_t kCoarseLog = kBinLog + ilog2c(kCoarseBins);
 constexpr uint32_t kCoarseCap = (1u << kCoarseLog) + (1u << (kCoarseLog - 4));
 // Each coarse bucket is split into kCoarseShards sub-regions with fill
 // counters of their own (dl_coarse block b reserves in shard b % S): every
@@ -425,6 +430,10 @@ static_assert(kCoarseCap % kCoarseShards == 0, "whole shards");
 #define GS_PART_CHUNK 4096
 #endif
 constexpr uint32_t kPartChunk = GS_PART_CHUNK;
+#ifndef GS_COARSE_THREADS
+#define GS_COARSE_THREADS 1024
+#endif
+constexpr uint32_t kCoarseThreads = GS_COARSE_THREADS;
 constexpr uint32_t kPartPer = kPartChunk / kInlThreads;
 constexpr uint32_t kMaxCoarse = 1u << (27 - kCoarseLog);  // n <= 2^27
 
@@ -466,7 +475,11 @@ __host__ __device__ inline PullArrays pull_arrays(uint32_t *region, uint32_t nb)
                       base + 2 * pc + (size_t)nb * kBin / 2};
 }
 
-__global__ __launch_bounds__(kInlThreads) void dl_coarse(InListArgs a) {
+// NT threads per block (GS_COARSE_THREADS): 512 lets three blocks share a CU
+template <uint32_t NT>
+__global__ __launch_bounds__(NT) void dl_coarse(InListArgs a) {
+    constexpr uint32_t kPer = kPartChunk / NT;
+    static_assert(kPartChunk % NT == 0 && kMaxCoarse <= NT, "dl_coarse: whole sources, a scan slot per bucket");
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     uint32_t *sx = sh, *st = sh + kPartChunk, *sc = sh + 2 * kPartChunk;
     __shared__ uint32_t cnt[kMaxCoarse], off[kMaxCoarse], res[kMaxCoarse + 1];
@@ -475,13 +488,13 @@ __global__ __launch_bounds__(kInlThreads) void dl_coarse(InListArgs a) {
     const uint32_t shard = blockIdx.x % kCoarseShards;
     uint32_t *cfill = a.scratch + cfill_off(p.nb);
     const CoarseArrays ca = coarse_arrays(a.region, p.nb);
-    for (uint32_t i = threadIdx.x; i < nc; i += kInlThreads) cnt[i] = 0u;
+    for (uint32_t i = threadIdx.x; i < nc; i += NT) cnt[i] = 0u;
     __syncthreads();
     const uint32_t lo = blockIdx.x * kPartChunk;
-    uint32_t tv[kPartPer], cv[kPartPer];
+    uint32_t tv[kPer], cv[kPer];
 #pragma unroll
-    for (uint32_t q = 0; q < kPartPer; ++q) {
-        const uint32_t x = lo + threadIdx.x + q * kInlThreads;
+    for (uint32_t q = 0; q < kPer; ++q) {
+        const uint32_t x = lo + threadIdx.x + q * NT;
         tv[q] = kTgDead;
         cv[q] = 0u;
         if (x < p.n) {
@@ -494,10 +507,10 @@ __global__ __launch_bounds__(kInlThreads) void dl_coarse(InListArgs a) {
     }
     __syncthreads();
     {  // exclusive scan of the nc <= 64 bucket counts; one reservation per bucket
-        __shared__ uint32_t lds_scan[kInlThreads / 64];
+        __shared__ uint32_t lds_scan[NT / 64];
         const uint32_t c = threadIdx.x < nc ? cnt[threadIdx.x] : 0u;
         uint32_t total;
-        const uint32_t ex = block_exclusive_scan_t<kInlThreads>(c, lds_scan, total);
+        const uint32_t ex = block_exclusive_scan_t<NT>(c, lds_scan, total);
         if (threadIdx.x < nc) {
             off[threadIdx.x] = ex;
             uint32_t r0 = c ? atomicAdd(&cfill[threadIdx.x * kCoarseShards + shard], c) : 0u;
@@ -512,17 +525,17 @@ __global__ __launch_bounds__(kInlThreads) void dl_coarse(InListArgs a) {
     }
     __syncthreads();
 #pragma unroll
-    for (uint32_t q = 0; q < kPartPer; ++q) {
+    for (uint32_t q = 0; q < kPer; ++q) {
         if (tv[q] & kTgDead) continue;
         const uint32_t t = tv[q] & kTgMask;
         const uint32_t pos = atomicAdd(&cnt[t >> kCoarseLog], 1u);
-        sx[pos] = lo + threadIdx.x + q * kInlThreads;
+        sx[pos] = lo + threadIdx.x + q * NT;
         st[pos] = t;
         sc[pos] = cv[q];
     }
     __syncthreads();
     const uint32_t total = res[kMaxCoarse];
-    for (uint32_t i = threadIdx.x; i < total; i += kInlThreads) {
+    for (uint32_t i = threadIdx.x; i < total; i += NT) {
         const uint32_t b = st[i] >> kCoarseLog;
         const uint32_t slot = res[b] + (i - off[b]);
         if (slot < kShardCap) {
@@ -535,14 +548,24 @@ __global__ __launch_bounds__(kInlThreads) void dl_coarse(InListArgs a) {
 }
 
 constexpr uint32_t kMaxFineSub = 2;
+#ifndef GS_FINE_THREADS
+#define GS_FINE_THREADS 1024
+#endif
+constexpr uint32_t kFineThreads = GS_FINE_THREADS;
 constexpr uint32_t kFineParts = kCoarseBins << kMaxFineSub;  // parts per coarse bucket (sub <= 2)
-__global__ __launch_bounds__(kInlThreads) void dl_fine(InListArgs a) {
+// NT threads per block (GS_FINE_THREADS): 512 lets three blocks share a CU
+template <uint32_t NT>
+__global__ __launch_bounds__(NT) void dl_fine(InListArgs a) {
+    constexpr uint32_t kPer = kPartChunk / NT;
+    static_assert(kPartChunk % NT == 0 && kFineParts <= NT, "dl_fine: whole entries, a scan slot per part");
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     uint32_t *sx = sh, *sc = sh + kPartChunk;
     uint16_t *slt = reinterpret_cast<uint16_t *>(sh + 2 * kPartChunk);
     uint16_t *sb = slt + kPartChunk;  // part of each stage entry
-    __shared__ uint32_t cnt[kFineParts], off[kFineParts], res[kFineParts];
-    __shared__ uint32_t lds_scan[kInlThreads / 64];
+    __shared__ uint32_t cnt[kFineParts];
+    __shared__ uint16_t off[kFineParts], res[kFineParts];  // (<= kPartChunk, <= pcap: 16 bits)
+    static_assert(kPartChunk <= 65535u && kBinCap <= 65535u, "16-bit starts");
+    __shared__ uint32_t lds_scan[NT / 64];
     const CsrPlan &p = a.p;
     // the 2^sub parts of each bin inl_sort_dlv sorts: a coarse bucket's
     // kCoarseBins << sub parts, each in its own region of kBinCap >> sub slots
@@ -556,10 +579,10 @@ __global__ __launch_bounds__(kInlThreads) void dl_fine(InListArgs a) {
     const CoarseArrays ca = coarse_arrays(a.region, p.nb);
     if (threadIdx.x < fp) cnt[threadIdx.x] = 0u;
     __syncthreads();
-    uint32_t xv[kPartPer], tv[kPartPer], cv[kPartPer];
+    uint32_t xv[kPer], tv[kPer], cv[kPer];
 #pragma unroll
-    for (uint32_t q = 0; q < kPartPer; ++q) {
-        const uint32_t i = lo + threadIdx.x + q * kInlThreads;
+    for (uint32_t q = 0; q < kPer; ++q) {
+        const uint32_t i = lo + threadIdx.x + q * NT;
         const bool ok = i < hi;
         const u64 o = (u64)cs * kShardCap + (ok ? i : lo);
         xv[q] = ca.x[o];
@@ -571,22 +594,22 @@ __global__ __launch_bounds__(kInlThreads) void dl_fine(InListArgs a) {
     {  // exclusive scan of the part counts, reservations in the part regions
         const uint32_t c = threadIdx.x < fp ? cnt[threadIdx.x] : 0u;
         uint32_t total;
-        const uint32_t ex = block_exclusive_scan_t<kInlThreads>(c, lds_scan, total);
+        const uint32_t ex = block_exclusive_scan_t<NT>(c, lds_scan, total);
         if (threadIdx.x < fp) {
             const uint32_t b = cb * fp + threadIdx.x;
-            off[threadIdx.x] = ex;
+            off[threadIdx.x] = (uint16_t)ex;
             uint32_t r0 = c ? atomicAdd(&pfill[b], c) : 0u;
             if (r0 + c > pcap) {
                 atomicOr(&a.flags[2], kFlagLimit);
                 r0 = pcap;
             }
-            res[threadIdx.x] = r0;
+            res[threadIdx.x] = (uint16_t)r0;
             cnt[threadIdx.x] = ex;  // cursor
         }
     }
     __syncthreads();
 #pragma unroll
-    for (uint32_t q = 0; q < kPartPer; ++q) {
+    for (uint32_t q = 0; q < kPer; ++q) {
         if (tv[q] == kNone) continue;
         const uint32_t fb = (tv[q] >> plog) & (fp - 1u);
         const uint32_t pos = atomicAdd(&cnt[fb], 1u);
@@ -597,7 +620,7 @@ __global__ __launch_bounds__(kInlThreads) void dl_fine(InListArgs a) {
     }
     __syncthreads();
     const uint32_t n_here = hi - lo;
-    for (uint32_t i = threadIdx.x; i < n_here; i += kInlThreads) {
+    for (uint32_t i = threadIdx.x; i < n_here; i += NT) {
         const uint32_t lo_b = sb[i];
         const uint32_t slot = res[lo_b] + (i - off[lo_b]);
         if (slot < pcap) {
@@ -692,9 +715,13 @@ __global__ __launch_bounds__(kInlThreads) void dl_direct(InListArgs a) {
 // bucket for the pull pass-back (pb_fine, pb_place).  Halving the bin keeps
 // ids and codes in LDS.
 #ifndef GS_DLV_SPLIT_LOG
-#define GS_DLV_SPLIT_LOG 1
+#define GS_DLV_SPLIT_LOG 2
 #endif
-constexpr uint32_t kSplitLog = GS_DLV_SPLIT_LOG;   // sort blocks per bin = 2^kSplitLog (large n)
+// sort blocks per bin = 2^kSplitLog (n >= 2^21): quarter bins, whose 48 KiB of
+// LDS let two 1024-thread blocks share a CU (half bins took 96 KiB, so a CU's
+// loads and LDS work took turns: inl_sort_dlv 1.52 -> 1.09 ms, config 5
+// 5.19 -> 4.76 ms/step, profiles/r3/cfg5_build)
+constexpr uint32_t kSplitLog = GS_DLV_SPLIT_LOG;
 #ifndef GS_DLV_PP
 #define GS_DLV_PP 0  // 1: inl_sort_dlv as a persistent walk with the next part's loads in flight
 #endif
@@ -704,7 +731,7 @@ inline uint32_t dlv_split_log(uint32_t nb) {
 #ifdef GS_DLV_SPLIT_FIXED
     return (void)nb, kSplitLog;  // A/B: the large-n split everywhere
 #endif
-    return nb >= 512u ? kSplitLog : (nb >= 128u ? kSplitLog + 1u : kSplitLog + 2u);
+    return nb >= 128u ? kSplitLog : kSplitLog + 1u;
 }
 
 // PP (persistent, own regions, several coarse buckets): a resident grid walks
@@ -1341,11 +1368,11 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
             const size_t lds_c = 3 * (size_t)kPartChunk * sizeof(uint32_t);
             const size_t lds_f = (2 * (size_t)kPartChunk + kPartChunk) * sizeof(uint32_t);
             if (e == hipSuccess)
-                e = hipFuncSetAttribute((const void *)dl_coarse, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)lds_c);
+                e = hipFuncSetAttribute((const void *)dl_coarse<kCoarseThreads>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_c);
             if (e == hipSuccess)
-                e = hipFuncSetAttribute((const void *)dl_fine, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)lds_f);
+                e = hipFuncSetAttribute((const void *)dl_fine<kFineThreads>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f);
             if (e != hipSuccess) return e;
             const bool direct = nc == 1u;  // small n: one pass into the parts, pulls written directly
             if ((p.sub && p.sub != dsl) || (direct && (!p.sub || (p.nb << p.sub) > kDirectParts)) ||
@@ -1358,9 +1385,10 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
                 if (e != hipSuccess) return e;
                 hipLaunchKernelGGL(dl_direct, dim3(p.ba), dim3(kInlThreads), lds_d, s, ab);
             } else {
-                hipLaunchKernelGGL(dl_coarse, dim3(p.ba), dim3(kInlThreads), lds_c, s, ab);
-                hipLaunchKernelGGL(dl_fine, dim3((kShardCap + kPartChunk - 1) / kPartChunk, nc * kCoarseShards),
-                                   dim3(kInlThreads), lds_f, s, ab);
+                hipLaunchKernelGGL(dl_coarse<kCoarseThreads>, dim3(p.ba), dim3(kCoarseThreads), lds_c, s, ab);
+                hipLaunchKernelGGL(dl_fine<kFineThreads>,
+                                   dim3((kShardCap + kPartChunk - 1) / kPartChunk, nc * kCoarseShards),
+                                   dim3(kFineThreads), lds_f, s, ab);
             }
             void *kargs[] = {&ab};
             if (GS_DLV_PP && own && !direct) {  // persistent walk over the parts (A/B)
