@@ -389,6 +389,10 @@ def main():
                 "step_frac": step_frac,
                 "kernel": best["name"] + " (deliver round t + transition to t+1)",
                 "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": best["bytes_per"],
+                # the rest of a step: the next round's in-list build (the largest of
+                # its kernels is smaller than the round kernel at every config) and
+                # the launch gaps
+                "rest_of_step_ms": ms_per_step - kernel_ms,
                 "bytes_counted_by": ("kernels (rows actually gathered + planes moved), %d launches"
                                      % best["launches"]) if best["launches"] else "static model",
                 "dense_model_bytes_per_launch": best["bytes_dense"],

@@ -41,11 +41,13 @@ GS_DEV T ge_seg(const T (&x)[NB], const T (&km)[NB]) {
     return ~b;
 }
 
-template <int MODE, typename T, uint32_t kNpl>
+// FUSE: the launch also runs the next build's first partition (a.cp_x set)
+template <int MODE, typename T, uint32_t kNpl, bool FUSE>
 __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(RoundArgs a) {
     constexpr bool DELIVER = MODE == 1;
     const Geometry &g = a.g;
     if (a.zero_buf || a.zero_rows) zero_for_build(a.zero_buf, a.zero_words, a.zero_rows);
+    if (a.zero_buf2) zero_for_build(a.zero_buf2, a.zero_words2, nullptr);
     const uint32_t n_nodes = g.n;
     const uint32_t rp = g.rpad, lr = g.logr, lognpu = g.lognpu;  // rp <= 16: npu >= 4
     const uint32_t lane = blockIdx.x * kDlv4Threads + threadIdx.x;
@@ -353,15 +355,18 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
     for (uint32_t q = 0; q < kNpl; ++q)
         eav[q] = (a.eadd && q < nv) ? reinterpret_cast<const uint16_t *>(a.eadd)[x0 + q] : 0u;
 
-    // ---- push codes of round t+1 for the in-list build (4 B per node)
+    // ---- push codes of round t+1 for the in-list build (4 B per node; the
+    // fused partition below carries them itself)
+    uint32_t pc[kNpl];
     {
         const T vC = N[0] & ~(N[1] & N[2]), vB = ~N[0] & (N[1] | N[2]);
         const T b0 = (vB & N[1] & ~N[2]) | vC, b1 = (vB & N[2] & ~N[1]) | vC;
-        uint32_t pc[kNpl];
 #pragma unroll
         for (uint32_t q = 0; q < kNpl; ++q)
             pc[q] = (uint32_t)((b0 >> (q * rp)) & m1) | ((uint32_t)((b1 >> (q * rp)) & m1) << 16);
-        if (kNpl == 4 && nv == kNpl) {
+        if (FUSE) {
+            // (not stored)
+        } else if (kNpl == 4 && nv == kNpl) {
             *reinterpret_cast<uint4 *>(a.pc_out + x0) =
                 make_uint4(pc[0], pc[1], pc[kNpl > 2 ? 2 : 0], pc[kNpl > 3 ? 3 : 0]);
         } else if (kNpl == 2 && nv == kNpl) {
@@ -433,6 +438,78 @@ __global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(
         st[q] = v;
         if (!on) a.offc[x0 + q] += 1u;
     }
+
+    // ---- fused first partition of round t+1's build (dl_coarse's work,
+    // gs_inlist.hip): every node's round-(t+1) target word (peer choice and
+    // harness faults, src/gossiper.rs:71) and its (source, target, push code)
+    // entry into the coarse bucket of its target, one reservation per bucket
+    // in shard blockIdx.x % S of the next set's coarse regions
+    if constexpr (FUSE) {
+        constexpr uint32_t kMaxCp = 64;  // coarse buckets (the host fuses only nc <= 64)
+        constexpr uint32_t kBlkNodes = kDlv4Threads * kNpl;
+        __shared__ uint32_t ccnt[kMaxCp], coff[kMaxCp], cres[kMaxCp];
+        __shared__ uint32_t cx[kBlkNodes], ct[kBlkNodes], cc[kBlkNodes];
+        __shared__ uint32_t lds_scan[kDlv4Threads / 64];
+        const uint32_t nc = a.cp_nc, shard = blockIdx.x % a.cp_shards, cap = a.cp_shard_cap;
+        if (threadIdx.x < nc) ccnt[threadIdx.x] = 0u;
+        uint32_t tq[kNpl];
+#pragma unroll
+        for (uint32_t q = 0; q < kNpl; ++q)
+            tq[q] = q < nv ? target_word(a.seed, a.epoch, a.round_new, x0 + q, n_nodes, a.f) : kTgDead;
+        if (kNpl == 4 && nv == kNpl) {
+            *reinterpret_cast<uint4 *>(a.tg_out + x0) =
+                make_uint4(tq[0], tq[1], tq[kNpl > 2 ? 2 : 0], tq[kNpl > 3 ? 3 : 0]);
+        } else if (kNpl == 2 && nv == kNpl) {
+            *reinterpret_cast<uint2 *>(a.tg_out + x0) = make_uint2(tq[0], tq[1]);
+        } else {
+#pragma unroll
+            for (uint32_t q = 0; q < kNpl; ++q)
+                if (q < nv) a.tg_out[x0 + q] = tq[q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t q = 0; q < kNpl; ++q)
+            if (!(tq[q] & kTgDead)) atomicAdd(&ccnt[(tq[q] & kTgMask) >> a.cp_log], 1u);
+        __syncthreads();
+        {  // exclusive scan of the bucket counts; one reservation per bucket
+            const uint32_t c = threadIdx.x < nc ? ccnt[threadIdx.x] : 0u;
+            uint32_t total;
+            const uint32_t ex = block_exclusive_scan(c, lds_scan, total);
+            if (threadIdx.x < nc) {
+                coff[threadIdx.x] = ex;
+                uint32_t r0 = c ? atomicAdd(&a.cp_fill[threadIdx.x * a.cp_shards + shard], c) : 0u;
+                if (r0 + c > cap) {
+                    atomicOr(&a.flags[2], 2u);  // a device limit (coarse region full)
+                    r0 = cap;
+                }
+                cres[threadIdx.x] = r0;
+                ccnt[threadIdx.x] = ex;  // cursor
+            }
+        }
+        __syncthreads();
+        uint32_t total = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kNpl; ++q) {
+            if (tq[q] & kTgDead) continue;
+            const uint32_t t = tq[q] & kTgMask;
+            const uint32_t pos = atomicAdd(&ccnt[t >> a.cp_log], 1u);
+            cx[pos] = x0 + q;
+            ct[pos] = t;
+            cc[pos] = pc[q];
+        }
+        __syncthreads();
+        total = ccnt[nc - 1u];  // the last bucket's cursor ends the block's entries
+        for (uint32_t i = threadIdx.x; i < total; i += kDlv4Threads) {
+            const uint32_t b = ct[i] >> a.cp_log;
+            const uint32_t slot = cres[b] + (i - coff[b]);
+            if (slot < cap) {
+                const u64 o = (u64)(b * a.cp_shards + shard) * cap + slot;
+                a.cp_x[o] = cx[i];
+                a.cp_t[o] = ct[i];
+                a.cp_c[o] = cc[i];
+            }
+        }
+    }
 }
 
 template <typename T, uint32_t NPL>
@@ -440,10 +517,15 @@ static hipError_t launch_dlv4_t(const RoundArgs &a, int mode, hipStream_t s) {
     const u64 lanes = ((u64)a.g.n + NPL - 1) / NPL;
     const u64 grid = (lanes + kDlv4Threads - 1) / kDlv4Threads;
     if (grid == 0) return hipSuccess;
-    if (mode == 0)
-        hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL>), dim3((uint32_t)grid), dim3(kDlv4Threads), 0, s, a);
-    else
-        hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL>), dim3((uint32_t)grid), dim3(kDlv4Threads), 0, s, a);
+    if (a.cp_x && (a.cp_nc == 0 || a.cp_nc > 64 || a.cp_shards == 0 || !a.tg_out)) return hipErrorInvalidValue;
+    const dim3 gd((uint32_t)grid), bd(kDlv4Threads);
+    if (a.cp_x) {
+        if (mode == 0) hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL, true>), gd, bd, 0, s, a);
+        else hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, true>), gd, bd, 0, s, a);
+    } else {
+        if (mode == 0) hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL, false>), gd, bd, 0, s, a);
+        else hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, false>), gd, bd, 0, s, a);
+    }
     return hipGetLastError();
 }
 

@@ -136,6 +136,12 @@ struct gs_engine {
     int ra_mode = 0;
     bool ra_sparse = false;
     bool ra_prezeroed = false;  // the round kernel clears the next build's counters
+    // DLV: the transition launch runs the next build's first partition
+    // (opt-in SAFE_GOSSIP_AMD_FUSE_COARSE=1; measured slower: its 512-node
+    // blocks make 8x the coarse reservations of dl_coarse's 4 K-source
+    // chunks, config 5 4.62 -> 6.03 ms per step)
+    bool fuse_coarse = false;
+    bool ra_fused = false;  // this round's launch did
     uint32_t *st32 = nullptr;  // [n][4] u32 deltas
     u64 *st64 = nullptr;       // [n][4] folded totals
     uint32_t fold_every = 1, since_fold = 0;
@@ -278,6 +284,12 @@ gs_status reset_state(gs_engine *e) {
         }
         e->spr_active = true;
         e->dens_round[0] = e->dens_round[1] = 0;
+    }
+    if (e->dlv) {  // both sets' coarse fills (the round kernels clear them a round late)
+        size_t first = 0, words = 0;
+        gs::inlist_cfill_range(e->plan, &first, &words);
+        for (auto &c : e->csr)
+            if (words && c.scratch) GS_HIP(hipMemsetAsync(c.scratch + first, 0, words * sizeof(uint32_t), e->stream));
     }
     e->cur = 0;
     e->round = 0;
@@ -720,6 +732,8 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         // 64..256 its duplicated per-node work costs more than its occupancy
         // gains (config 4: 2.61 -> 3.03 ms per launch).
         // SAFE_GOSSIP_AMD_W32=0/1 forces the 64-bit / 32-bit lane kernel.
+        const char *fc = std::getenv("SAFE_GOSSIP_AMD_FUSE_COARSE");
+        e->fuse_coarse = fc && *fc == '1';
         const char *w = std::getenv("SAFE_GOSSIP_AMD_W32");
         e->w32 = (w && *w) ? *w != '0' : (e->g.small && e->g.rpad == 32u);
         const char *gv = std::getenv("SAFE_GOSSIP_AMD_PIPE_GRID");
@@ -1123,6 +1137,7 @@ gs_status round_begin(gs_engine *e) {
     // the build of round t+1 runs right behind this kernel on its stream: the
     // kernel clears that build's counters (no memset launch)
     e->ra_prezeroed = !e->shard && !e->split_build && !(e->concurrent_inlists && !e->dlv);
+    e->ra_fused = false;
     if (e->ra_prezeroed) {
         auto &c = e->csr[(R0 + 1u) & 1u];
         size_t first = 0, words = 0;
@@ -1132,6 +1147,29 @@ gs_status round_begin(gs_engine *e) {
             a.zero_words = (uint32_t)words;
         }
         if (e->filt) a.zero_rows = e->rows_dev + ((R0 + 1u) & 1u);
+        // DLV: the coarse fills of the set round t's build used (consumed by
+        // its dl_fine) are cleared now, a round before that set is
+        // partitioned into again; the next set's were cleared a round ago, so
+        // this launch may reserve in them
+        gs::inlist_cfill_range(e->plan, &first, &words);
+        if (words) {
+            a.zero_buf2 = e->csr[R0 & 1u].scratch + first;
+            a.zero_words2 = (uint32_t)words;
+        }
+        gs::CoarseTarget ct{};
+        if (e->dlv && e->fuse_coarse && e->dlv_pack && a.n_ext == 0 &&
+            gs::dlv_coarse_target(e->plan, c.region, c.scratch, &ct) && ct.nc <= 64) {
+            a.cp_x = ct.x;
+            a.cp_t = ct.t;
+            a.cp_c = ct.c;
+            a.cp_fill = ct.fill;
+            a.cp_nc = ct.nc;
+            a.cp_shards = ct.shards;
+            a.cp_shard_cap = ct.shard_cap;
+            a.cp_log = ct.log;
+            a.tg_out = c.tg;
+            e->ra_fused = true;
+        }
     }
     e->ra = a;
     e->ra_mode = e->deliver_pending ? 1 : 0;
@@ -1227,6 +1265,7 @@ gs_status round_end(gs_engine *e, gs_round_report *report) {
             if (st != GS_OK) return st;
             gs::InListArgs la = inlist_args(e, c, e->round);
             la.prezeroed = e->ra_prezeroed ? 1u : 0u;
+            la.coarse_done = e->ra_fused ? 1u : 0u;
             if (e->filt && !e->ra_prezeroed) GS_HIP(hipMemsetAsync(la.rows, 0, sizeof(u64), bs));
             GS_HIP(gs::launch_build_inlists(la, bs));
         }

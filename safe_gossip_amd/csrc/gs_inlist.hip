@@ -273,12 +273,15 @@ GS_DEV uint32_t half_of(const uint32_t *h, uint32_t i) { return (h[i >> 1] >> ((
 // the chip (two per bin measured slower at 1024 bins: every block reads the
 // whole bin region), more for small networks (2^20 nodes = 64 bins), whose
 // regions stay in L2.  GS_SORT_SPLIT_LOG forces one value (A/B).
+#ifndef GS_SORT_SMALL_LOG
+#define GS_SORT_SMALL_LOG 2u  // sort blocks per bin = 2^this below 128 bins (2^21 nodes)
+#endif
 inline uint32_t sort_split_log(uint32_t nb) {
 #ifdef GS_SORT_SPLIT_LOG
     (void)nb;
     return GS_SORT_SPLIT_LOG;
 #else
-    return nb >= 512u ? 0u : (nb >= 128u ? 1u : 2u);
+    return nb >= 512u ? 0u : (nb >= 128u ? 1u : GS_SORT_SMALL_LOG);
 #endif
 }
 
@@ -339,6 +342,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
     __syncthreads();
     // exclusive scan over the kPart targets, kPart/kInlThreads per thread
     constexpr uint32_t per = kPart / kInlThreads;
+    static_assert(per >= 2 && per % 2 == 0, "the scan walks packed counter pairs: >= 2048 targets");
     const uint32_t i0 = threadIdx.x * per;
     uint32_t sum = 0;
 #pragma unroll
@@ -416,12 +420,14 @@ static_assert((kCoarseBins & (kCoarseBins - 1u)) == 0 && kCoarseBins <= 256, "co
 constexpr uint32_t kCoarseLog = kBinLog + ilog2c(kCoarseBins);
 constexpr uint32_t kCoarseCap = (1u << kCoarseLog) + (1u << (kCoarseLog - 4));
 // Each coarse bucket is split into kCoarseShards sub-regions with fill
-// counters of their own (dl_coarse block b reserves in shard b % S): every
-// dl_coarse block makes one returning atomic per bucket, and on one counter
-// word those serialise at the memory side (~88 per us, MI355X_MICROARCH.md
-// "dequeue"), so ~24 K blocks on 48 words queued behind each other.
+// counters of their own (the partitioning block b reserves in shard b % S):
+// every block makes one returning atomic per bucket, and on one counter word
+// those serialise at the memory side (~88 per us, MI355X_MICROARCH.md
+// "dequeue").  dl_coarse's ~24 K blocks showed no queueing on 48 words (A/B
+// with 1 / 4 / 8 shards within noise); the transition launch that partitions
+// in its epilogue has 8x more blocks.
 #ifndef GS_COARSE_SHARDS
-#define GS_COARSE_SHARDS 1
+#define GS_COARSE_SHARDS 8
 #endif
 constexpr uint32_t kCoarseShards = GS_COARSE_SHARDS;
 constexpr uint32_t kShardCap = kCoarseCap / kCoarseShards;
@@ -438,12 +444,19 @@ constexpr uint32_t kPartPer = kPartChunk / kInlThreads;
 constexpr uint32_t kMaxCoarse = 1u << (27 - kCoarseLog);  // n <= 2^27
 
 __host__ __device__ inline uint32_t n_coarse(uint32_t nb) { return (nb + kCoarseBins - 1) / kCoarseBins; }
-// DLV scratch: fill[nb], tail count, coarse shard fills [nc * S], pull coarse
-// fills [nc], pull bin fills [nb], then the part fills (fill_off)
-__host__ __device__ inline uint32_t cfill_off(uint32_t nb) { return nb + 1u; }
-__host__ __device__ inline uint32_t pcfill_off(uint32_t nb) { return nb + 1u + n_coarse(nb) * kCoarseShards; }
+// DLV scratch: fill[nb], tail count, pull coarse fills [nc], pull bin fills
+// [nb], the part fills (fill_off, when sub > 0), then the coarse shard fills
+// [nc * S] last: the transition launch that partitions into a set reserves in
+// them while it clears the rest of that set's counters (RoundArgs::cp_*).
+__host__ __device__ inline uint32_t pcfill_off(uint32_t nb) { return nb + 1u; }
 __host__ __device__ inline uint32_t pffill_off(uint32_t nb) { return pcfill_off(nb) + n_coarse(nb); }
-__host__ __device__ inline uint32_t dlv_scratch_words(uint32_t nb) { return pffill_off(nb) + nb; }
+__host__ __device__ inline uint32_t dlv_head_words(uint32_t nb) { return pffill_off(nb) + nb; }
+__host__ __device__ inline uint32_t cfill_off(const CsrPlan &p) {
+    return dlv_head_words(p.nb) + (p.sub ? (p.nb << p.sub) : 0u);
+}
+__host__ __device__ inline uint32_t dlv_scratch_words(const CsrPlan &p) {
+    return cfill_off(p) + n_coarse(p.nb) * kCoarseShards;
+}
 
 // Coarse-bucket arrays inside the region buffer, after the bin regions.
 struct CoarseArrays {
@@ -486,7 +499,7 @@ __global__ __launch_bounds__(NT) void dl_coarse(InListArgs a) {
     const CsrPlan &p = a.p;
     const uint32_t nc = n_coarse(p.nb);
     const uint32_t shard = blockIdx.x % kCoarseShards;
-    uint32_t *cfill = a.scratch + cfill_off(p.nb);
+    uint32_t *cfill = a.scratch + cfill_off(p);
     const CoarseArrays ca = coarse_arrays(a.region, p.nb);
     for (uint32_t i = threadIdx.x; i < nc; i += NT) cnt[i] = 0u;
     __syncthreads();
@@ -552,19 +565,23 @@ constexpr uint32_t kMaxFineSub = 2;
 #define GS_FINE_THREADS 1024
 #endif
 constexpr uint32_t kFineThreads = GS_FINE_THREADS;
+#ifndef GS_FINE_CHUNK
+#define GS_FINE_CHUNK 4096  // coarse-bucket entries per dl_fine block
+#endif
+constexpr uint32_t kFineChunk = GS_FINE_CHUNK;
 constexpr uint32_t kFineParts = kCoarseBins << kMaxFineSub;  // parts per coarse bucket (sub <= 2)
 // NT threads per block (GS_FINE_THREADS): 512 lets three blocks share a CU
 template <uint32_t NT>
 __global__ __launch_bounds__(NT) void dl_fine(InListArgs a) {
-    constexpr uint32_t kPer = kPartChunk / NT;
-    static_assert(kPartChunk % NT == 0 && kFineParts <= NT, "dl_fine: whole entries, a scan slot per part");
+    constexpr uint32_t kPer = kFineChunk / NT;
+    static_assert(kFineChunk % NT == 0 && kFineParts <= NT, "dl_fine: whole entries, a scan slot per part");
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
-    uint32_t *sx = sh, *sc = sh + kPartChunk;
-    uint16_t *slt = reinterpret_cast<uint16_t *>(sh + 2 * kPartChunk);
-    uint16_t *sb = slt + kPartChunk;  // part of each stage entry
+    uint32_t *sx = sh, *sc = sh + kFineChunk;
+    uint16_t *slt = reinterpret_cast<uint16_t *>(sh + 2 * kFineChunk);
+    uint16_t *sb = slt + kFineChunk;  // part of each stage entry
     __shared__ uint32_t cnt[kFineParts];
-    __shared__ uint16_t off[kFineParts], res[kFineParts];  // (<= kPartChunk, <= pcap: 16 bits)
-    static_assert(kPartChunk <= 65535u && kBinCap <= 65535u, "16-bit starts");
+    __shared__ uint16_t off[kFineParts], res[kFineParts];  // (<= kFineChunk, <= pcap: 16 bits)
+    static_assert(kFineChunk <= 65535u && kBinCap <= 65535u, "16-bit starts");
     __shared__ uint32_t lds_scan[NT / 64];
     const CsrPlan &p = a.p;
     // the 2^sub parts of each bin inl_sort_dlv sorts: a coarse bucket's
@@ -572,10 +589,10 @@ __global__ __launch_bounds__(NT) void dl_fine(InListArgs a) {
     const uint32_t fp = kCoarseBins << p.sub, plog = kBinLog - p.sub, pcap = kBinCap >> p.sub;
     uint32_t *pfill = p.sub ? a.scratch + p.fill_off : a.scratch;
     const uint32_t cs = blockIdx.y, cb = cs / kCoarseShards;  // (coarse bucket, shard)
-    const uint32_t fill = min(a.scratch[cfill_off(p.nb) + cs], kShardCap);
-    const uint32_t lo = blockIdx.x * kPartChunk;
+    const uint32_t fill = min(a.scratch[cfill_off(p) + cs], kShardCap);
+    const uint32_t lo = blockIdx.x * kFineChunk;
     if (lo >= fill) return;  // uniform per block
-    const uint32_t hi = min(fill, lo + kPartChunk);
+    const uint32_t hi = min(fill, lo + kFineChunk);
     const CoarseArrays ca = coarse_arrays(a.region, p.nb);
     if (threadIdx.x < fp) cnt[threadIdx.x] = 0u;
     __syncthreads();
@@ -722,6 +739,10 @@ __global__ __launch_bounds__(kInlThreads) void dl_direct(InListArgs a) {
 // loads and LDS work took turns: inl_sort_dlv 1.52 -> 1.09 ms, config 5
 // 5.19 -> 4.76 ms/step, profiles/r3/cfg5_build)
 constexpr uint32_t kSplitLog = GS_DLV_SPLIT_LOG;
+#ifndef GS_DLV_SMALL_LOG
+#define GS_DLV_SMALL_LOG (kSplitLog + 1u)  // below 128 bins (one coarse bucket, cache-resident)
+#endif
+constexpr uint32_t kDlvSmallLog = GS_DLV_SMALL_LOG;
 #ifndef GS_DLV_PP
 #define GS_DLV_PP 0  // 1: inl_sort_dlv as a persistent walk with the next part's loads in flight
 #endif
@@ -731,7 +752,7 @@ inline uint32_t dlv_split_log(uint32_t nb) {
 #ifdef GS_DLV_SPLIT_FIXED
     return (void)nb, kSplitLog;  // A/B: the large-n split everywhere
 #endif
-    return nb >= 128u ? kSplitLog : kSplitLog + 1u;
+    return nb >= 128u ? kSplitLog : kDlvSmallLog;
 }
 
 // PP (persistent, own regions, several coarse buckets): a resident grid walks
@@ -748,6 +769,7 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
     constexpr uint32_t kHalf = 1u << kHalfLog;
     constexpr uint32_t kHalfCap = kBinCap >> SL;
     constexpr uint32_t kHalfPer = kHalf / kInlThreads;  // targets per thread
+    static_assert(kHalfPer >= 2 && kHalfPer % 2 == 0, "the scan walks packed counter pairs: >= 2048 targets");
     // region entries per thread: the half's own region (OWN: p.sub == SL) or the whole bin's
     constexpr uint32_t kPer = ((OWN ? kHalfCap : kBinCap) + kInlThreads - 1) / kInlThreads;
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
@@ -1183,7 +1205,7 @@ CsrPlan dlv_plan(uint32_t n) {
     if (nc > 1u) p.sub = 0u;
 #endif
     if (nc > 1u && p.sub > kMaxFineSub) p.sub = 0u;  // (kFineParts)
-    p.fill_off = p.sub ? dlv_scratch_words(p.nb) : 0u;  // after fill[nb], tailcnt, coarse fills, pull fills
+    p.fill_off = p.sub ? dlv_head_words(p.nb) : 0u;  // after fill[nb], tailcnt, pull fills
     return p;
 }
 
@@ -1226,11 +1248,30 @@ void inlist_zero_range(const CsrPlan &p, size_t *first, size_t *words) {
     *words = 0;
     if (!p.binned) return;
     if (p.dlv) {
-        *words = inlist_sizes(p).scratch_words;
+        *words = cfill_off(p);  // the coarse fills are cleared a round later (inlist_cfill_range)
     } else if (p.sub) {
         *first = p.fill_off;
         *words = (size_t)p.nb << p.sub;
     }
+}
+
+void inlist_cfill_range(const CsrPlan &p, size_t *first, size_t *words) {
+    *first = p.dlv && p.binned ? cfill_off(p) : 0u;
+    *words = p.dlv && p.binned ? (size_t)n_coarse(p.nb) * kCoarseShards : 0u;
+}
+
+bool dlv_coarse_target(const CsrPlan &p, uint32_t *region, uint32_t *scratch, CoarseTarget *out) {
+    if (!p.binned || !p.dlv || n_coarse(p.nb) < 2u) return false;  // (one coarse bucket: dl_direct)
+    const CoarseArrays ca = coarse_arrays(region, p.nb);
+    out->x = ca.x;
+    out->t = ca.t;
+    out->c = ca.c;
+    out->fill = scratch + cfill_off(p);
+    out->nc = n_coarse(p.nb);
+    out->shards = kCoarseShards;
+    out->shard_cap = kShardCap;
+    out->log = kCoarseLog;
+    return true;
 }
 
 InListSizes inlist_sizes(const CsrPlan &p) {
@@ -1242,8 +1283,12 @@ InListSizes inlist_sizes(const CsrPlan &p) {
         const size_t nc = (p.nb + kCoarseBins - 1) / kCoarseBins;
         if (p.dlv) z.region_words += 3 * nc * kCoarseCap + pull_words(p.nb);
         // fill[nb], tailcnt[, coarse fill[nc], pull coarse fill[nc], pull bin fill[nb]]
-        z.scratch_words = p.dlv ? (size_t)dlv_scratch_words(p.nb) : (size_t)p.nb + 1;
-        if (p.sub) z.scratch_words = (size_t)p.fill_off + ((size_t)p.nb << p.sub);  // part fills
+        if (p.dlv) {
+            z.scratch_words = dlv_scratch_words(p);
+        } else {
+            z.scratch_words = (size_t)p.nb + 1;
+            if (p.sub) z.scratch_words = (size_t)p.fill_off + ((size_t)p.nb << p.sub);  // part fills
+        }
     } else {
         z.src_words = p.tailcap;
         z.region_words = 3 * (size_t)p.n;  // u64 pairs + the CSR
@@ -1311,8 +1356,10 @@ hipError_t launch_build_sort(const InListArgs &a, hipStream_t s) {
     if (!p.binned || p.dlv || !a.lvm || !a.cpm || !a.zl) return hipErrorInvalidValue;
     const uint32_t sl = sort_split_log(p.nb);
     const size_t lds_sort = ((size_t)(kBin >> sl) / 2 + (kBinCap >> sl)) * sizeof(uint32_t);
-    const void *ks = sl == 0 ? (const void *)inl_sort<0> : sl == 1 ? (const void *)inl_sort<1>
-                                                                   : (const void *)inl_sort<2>;
+    const void *ks = sl == 0   ? (const void *)inl_sort<0>
+                     : sl == 1 ? (const void *)inl_sort<1>
+                     : sl == 2 ? (const void *)inl_sort<2>
+                               : (const void *)inl_sort<3>;
     hipError_t e = hipFuncSetAttribute(ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sort);
     if (e != hipSuccess) return e;
     InListArgs ab = a;
@@ -1322,7 +1369,8 @@ hipError_t launch_build_sort(const InListArgs &a, hipStream_t s) {
     const dim3 gs(p.nb, 1u << sl);
     if (sl == 0) hipLaunchKernelGGL(inl_sort<0>, gs, dim3(kInlThreads), lds_sort, s, ab);
     else if (sl == 1) hipLaunchKernelGGL(inl_sort<1>, gs, dim3(kInlThreads), lds_sort, s, ab);
-    else hipLaunchKernelGGL(inl_sort<2>, gs, dim3(kInlThreads), lds_sort, s, ab);
+    else if (sl == 2) hipLaunchKernelGGL(inl_sort<2>, gs, dim3(kInlThreads), lds_sort, s, ab);
+    else hipLaunchKernelGGL(inl_sort<3>, gs, dim3(kInlThreads), lds_sort, s, ab);
     return hipGetLastError();
 }
 
@@ -1341,14 +1389,13 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
         const bool own = p.sub != 0u;
         const void *kd = dsl == kSplitLog
                              ? (own ? (const void *)inl_sort_dlv<kSplitLog, true> : (const void *)inl_sort_dlv<kSplitLog, false>)
-                         : dsl == kSplitLog + 1u
-                             ? (own ? (const void *)inl_sort_dlv<kSplitLog + 1u, true>
-                                    : (const void *)inl_sort_dlv<kSplitLog + 1u, false>)
-                             : (own ? (const void *)inl_sort_dlv<kSplitLog + 2u, true>
-                                    : (const void *)inl_sort_dlv<kSplitLog + 2u, false>);
+                             : (own ? (const void *)inl_sort_dlv<kDlvSmallLog, true>
+                                    : (const void *)inl_sort_dlv<kDlvSmallLog, false>);
         const void *ks = p.dlv ? kd
-                               : (sl == 0 ? (const void *)inl_sort<0> : sl == 1 ? (const void *)inl_sort<1>
-                                                                               : (const void *)inl_sort<2>);
+                               : (sl == 0   ? (const void *)inl_sort<0>
+                                  : sl == 1 ? (const void *)inl_sort<1>
+                                  : sl == 2 ? (const void *)inl_sort<2>
+                                            : (const void *)inl_sort<3>);
         // (inl_bin is the gather path's partition: its LDS, sized by the parts,
         // is not set for a DLV plan, whose part count it may not fit)
         hipError_t e = p.dlv ? hipSuccess : hipFuncSetAttribute(kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bin);
@@ -1366,7 +1413,7 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
             const uint32_t nc = (p.nb + kCoarseBins - 1) / kCoarseBins;
             if (!a.prezeroed) e = hipMemsetAsync(a.scratch, 0, inlist_sizes(p).scratch_words * sizeof(uint32_t), s);
             const size_t lds_c = 3 * (size_t)kPartChunk * sizeof(uint32_t);
-            const size_t lds_f = (2 * (size_t)kPartChunk + kPartChunk) * sizeof(uint32_t);
+            const size_t lds_f = 3 * (size_t)kFineChunk * sizeof(uint32_t);
             if (e == hipSuccess)
                 e = hipFuncSetAttribute((const void *)dl_coarse<kCoarseThreads>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_c);
@@ -1385,16 +1432,16 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
                 if (e != hipSuccess) return e;
                 hipLaunchKernelGGL(dl_direct, dim3(p.ba), dim3(kInlThreads), lds_d, s, ab);
             } else {
-                hipLaunchKernelGGL(dl_coarse<kCoarseThreads>, dim3(p.ba), dim3(kCoarseThreads), lds_c, s, ab);
+                if (!a.coarse_done)  // (else the transition launch before partitioned the entries)
+                    hipLaunchKernelGGL(dl_coarse<kCoarseThreads>, dim3(p.ba), dim3(kCoarseThreads), lds_c, s, ab);
                 hipLaunchKernelGGL(dl_fine<kFineThreads>,
-                                   dim3((kShardCap + kPartChunk - 1) / kPartChunk, nc * kCoarseShards),
+                                   dim3((kShardCap + kFineChunk - 1) / kFineChunk, nc * kCoarseShards),
                                    dim3(kFineThreads), lds_f, s, ab);
             }
             void *kargs[] = {&ab};
             if (GS_DLV_PP && own && !direct) {  // persistent walk over the parts (A/B)
-                const void *kp = dsl == kSplitLog        ? (const void *)inl_sort_dlv<kSplitLog, true, true>
-                                 : dsl == kSplitLog + 1u ? (const void *)inl_sort_dlv<kSplitLog + 1u, true, true>
-                                                         : (const void *)inl_sort_dlv<kSplitLog + 2u, true, true>;
+                const void *kp = dsl == kSplitLog ? (const void *)inl_sort_dlv<kSplitLog, true, true>
+                                                  : (const void *)inl_sort_dlv<kDlvSmallLog, true, true>;
                 e = hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dlv);
                 int dev = 0, cus = 0, per_cu = 0;
                 if (e == hipSuccess) e = hipGetDevice(&dev);
@@ -1429,7 +1476,8 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
             const dim3 gs(p.nb, 1u << sl);
             if (sl == 0) hipLaunchKernelGGL(inl_sort<0>, gs, dim3(kInlThreads), lds_sort, s, ab);
             else if (sl == 1) hipLaunchKernelGGL(inl_sort<1>, gs, dim3(kInlThreads), lds_sort, s, ab);
-            else hipLaunchKernelGGL(inl_sort<2>, gs, dim3(kInlThreads), lds_sort, s, ab);
+            else if (sl == 2) hipLaunchKernelGGL(inl_sort<2>, gs, dim3(kInlThreads), lds_sort, s, ab);
+            else hipLaunchKernelGGL(inl_sort<3>, gs, dim3(kInlThreads), lds_sort, s, ab);
         }
         return hipGetLastError();
     }

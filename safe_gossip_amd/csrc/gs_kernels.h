@@ -100,6 +100,16 @@ struct RoundArgs {
     uint32_t no_pipe;         // 1: the wide 2P path runs round_kernel instead of round_pipe
     uint32_t pipe_grid;       // round_pipe's block count (0: every resident block)
     uint32_t w32;             // 1: eligible launches run round_kernel_w32 (gs_w32.hip)
+    // DLV transition launches (gs_dlv4.hip) may run the first partition of
+    // the next round's build in their epilogue, in place of dl_coarse: the
+    // round-(t+1) target words (tg_out) and the (source, target, push code)
+    // entries into the coarse shards of the next set (cp_x null: not fused)
+    uint32_t *cp_x, *cp_t, *cp_c, *cp_fill, *tg_out;
+    uint32_t cp_nc, cp_shards, cp_shard_cap, cp_log;
+    // a second range cleared at the start (the coarse fills of the set the
+    // previous round's build consumed)
+    uint32_t *zero_buf2;
+    uint32_t zero_words2;
     uint32_t dlv_pack;        // DLV transition launches: 0 one node per lane, 1 a 32-bit lane
                               // word of several nodes, 2 a 64-bit one (gs_dlv4.hip)
     Geometry g;
@@ -166,6 +176,14 @@ struct InListSizes {
 };
 InListSizes inlist_sizes(const CsrPlan &p);
 void inlist_zero_range(const CsrPlan &p, size_t *first, size_t *words);
+// DLV: the coarse shard fills (cleared one round later than the other counters).
+void inlist_cfill_range(const CsrPlan &p, size_t *first, size_t *words);
+// DLV with several coarse buckets: where a fused partition writes (false: none).
+struct CoarseTarget {
+    uint32_t *x, *t, *c, *fill;
+    uint32_t nc, shards, shard_cap, log;
+};
+bool dlv_coarse_target(const CsrPlan &p, uint32_t *region, uint32_t *scratch, CoarseTarget *out);
 
 struct InListArgs {
     CsrPlan p;
@@ -176,6 +194,7 @@ struct InListArgs {
     const u64 *S;
     const uint32_t *PC;     // push codes of the round (written by the round kernel)
     uint32_t prezeroed;     // 1: the round kernel before cleared the counters (RoundArgs::zero_*)
+    uint32_t coarse_done;   // 1: the round kernel before wrote tg and the coarse partition
     Geometry g;
     DlvRec *DR;         // [n]
     uint32_t *dtail;    // [tailcap] push codes of pushers >= kDlvInline

@@ -91,6 +91,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     constexpr bool TRANSITION = (MODE == 0 || MODE == 1);
     const Geometry &g = a.g;
     if (a.zero_buf || a.zero_rows) zero_for_build(a.zero_buf, a.zero_words, a.zero_rows);
+    if (a.zero_buf2) zero_for_build(a.zero_buf2, a.zero_words2, nullptr);
     const uint32_t bid = blockIdx.x + a.blk_off;
     const u64 seg = (u64)bid * blockDim.x + threadIdx.x;
     const bool valid = seg < g.nseg;

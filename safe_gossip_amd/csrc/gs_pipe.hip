@@ -153,6 +153,7 @@ __global__ __launch_bounds__(PipeTile<W>::kThreads) void round_pipe(RoundArgs a,
     const u64 *__restrict__ S = a.Scur;
     uint32_t *blk_any = reinterpret_cast<uint32_t *>(lds + T::oAny);
     if (a.zero_buf || a.zero_rows) zero_for_build(a.zero_buf, a.zero_words, a.zero_rows);
+    if (a.zero_buf2) zero_for_build(a.zero_buf2, a.zero_words2, nullptr);
     if (tid0 == 0) *blk_any = 0u;
     if (blockIdx.x == 0 && tid0 == 0) {
         // slot of round t, read by the host already

@@ -65,6 +65,7 @@ __global__ __launch_bounds__(kW32Threads, GS_W32_MINW) void round_kernel_w32(Rou
     constexpr bool DELIVER = MODE == 1;
     const Geometry &g = a.g;
     if (a.zero_buf || a.zero_rows) zero_for_build(a.zero_buf, a.zero_words, a.zero_rows);
+    if (a.zero_buf2) zero_for_build(a.zero_buf2, a.zero_words2, nullptr);
     const uint32_t lw = g.logr - 5u;  // log2 of the u32 words (lanes) per node plane: 0..3
     const uint32_t W32 = 1u << lw;
     const uint32_t bid = blockIdx.x;
