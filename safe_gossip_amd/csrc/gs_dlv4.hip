@@ -27,6 +27,9 @@ constexpr uint32_t kDlv4Threads = 256;
 #ifndef GS_DLV4_MINW
 #define GS_DLV4_MINW 4
 #endif
+#ifndef GS_DLV4_MINW_R16
+#define GS_DLV4_MINW_R16 GS_DLV4_MINW  // the config-5 kernel (R_pad 16, two nodes per u32 lane)
+#endif
 
 // The lane word T holds the lane's nodes side by side (u32: two 16-bit or
 // four <= 8-bit segments; u64: four 16-bit segments); the bit-sliced helpers
@@ -43,7 +46,8 @@ GS_DEV T ge_seg(const T (&x)[NB], const T (&km)[NB]) {
 
 // FUSE: the launch also runs the next build's first partition (a.cp_x set)
 template <int MODE, typename T, uint32_t kNpl, bool FUSE>
-__global__ __launch_bounds__(kDlv4Threads, GS_DLV4_MINW) void round_kernel_dlv4(RoundArgs a) {
+__global__ __launch_bounds__(kDlv4Threads, (kNpl == 2 && sizeof(T) == 4 && !FUSE) ? GS_DLV4_MINW_R16 : GS_DLV4_MINW)
+void round_kernel_dlv4(RoundArgs a) {
     constexpr bool DELIVER = MODE == 1;
     const Geometry &g = a.g;
     if (a.zero_buf || a.zero_rows) zero_for_build(a.zero_buf, a.zero_words, a.zero_rows);
