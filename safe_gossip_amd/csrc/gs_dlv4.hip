@@ -44,7 +44,7 @@ GS_DEV T ge_seg(const T (&x)[NB], const T (&km)[NB]) {
     return ~b;
 }
 
-// FUSE: the launch also runs the next build's first partition (a.cp_x set)
+// FUSE: the launch also runs the next build's first partition (a.cp_e set)
 template <int MODE, typename T, uint32_t kNpl, bool FUSE>
 __global__ __launch_bounds__(kDlv4Threads, (kNpl == 2 && sizeof(T) == 4 && !FUSE) ? GS_DLV4_MINW_R16 : GS_DLV4_MINW)
 void round_kernel_dlv4(RoundArgs a) {
@@ -507,10 +507,10 @@ void round_kernel_dlv4(RoundArgs a) {
             const uint32_t b = ct[i] >> a.cp_log;
             const uint32_t slot = cres[b] + (i - coff[b]);
             if (slot < cap) {
-                const u64 o = (u64)(b * a.cp_shards + shard) * cap + slot;
-                a.cp_x[o] = cx[i];
-                a.cp_t[o] = ct[i];
-                a.cp_c[o] = cc[i];
+                const u64 o = ((u64)(b * a.cp_shards + shard) * cap + slot) * 3u;
+                a.cp_e[o] = cx[i];
+                a.cp_e[o + 1] = ct[i];
+                a.cp_e[o + 2] = cc[i];
             }
         }
     }
@@ -521,9 +521,9 @@ static hipError_t launch_dlv4_t(const RoundArgs &a, int mode, hipStream_t s) {
     const u64 lanes = ((u64)a.g.n + NPL - 1) / NPL;
     const u64 grid = (lanes + kDlv4Threads - 1) / kDlv4Threads;
     if (grid == 0) return hipSuccess;
-    if (a.cp_x && (a.cp_nc == 0 || a.cp_nc > 64 || a.cp_shards == 0 || !a.tg_out)) return hipErrorInvalidValue;
+    if (a.cp_e && (a.cp_nc == 0 || a.cp_nc > 64 || a.cp_shards == 0 || !a.tg_out)) return hipErrorInvalidValue;
     const dim3 gd((uint32_t)grid), bd(kDlv4Threads);
-    if (a.cp_x) {
+    if (a.cp_e) {
         if (mode == 0) hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL, true>), gd, bd, 0, s, a);
         else hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, true>), gd, bd, 0, s, a);
     } else {

@@ -1159,9 +1159,7 @@ gs_status round_begin(gs_engine *e) {
         gs::CoarseTarget ct{};
         if (e->dlv && e->fuse_coarse && e->dlv_pack && a.n_ext == 0 &&
             gs::dlv_coarse_target(e->plan, c.region, c.scratch, &ct) && ct.nc <= 64) {
-            a.cp_x = ct.x;
-            a.cp_t = ct.t;
-            a.cp_c = ct.c;
+            a.cp_e = ct.e;
             a.cp_fill = ct.fill;
             a.cp_nc = ct.nc;
             a.cp_shards = ct.shards;

@@ -458,14 +458,19 @@ __host__ __device__ inline uint32_t dlv_scratch_words(const CsrPlan &p) {
     return cfill_off(p) + n_coarse(p.nb) * kCoarseShards;
 }
 
-// Coarse-bucket arrays inside the region buffer, after the bin regions.
-struct CoarseArrays {
-    uint32_t *x, *t, *c;
+// DLV partition entries are 12-byte records, one store stream per run: a
+// coarse entry (source, target, push code), a part entry (source, push code,
+// target within the bin).  (Three u32 / u16 arrays made three scattered
+// segments per run: dl_fine's runs are ~8 entries.)
+struct PEnt {
+    uint32_t a, b, c;
 };
-__host__ __device__ inline CoarseArrays coarse_arrays(uint32_t *region, uint32_t nb) {
-    const size_t base = (size_t)nb * kBinCap * 5 / 2;
-    const size_t cap = (size_t)((nb + kCoarseBins - 1) / kCoarseBins) * kCoarseCap;  // = nc * S * kShardCap
-    return CoarseArrays{region + base, region + base + cap, region + base + 2 * cap};
+// The bin (part) regions: [nb * kBinCap] part entries at the region base.
+__host__ __device__ inline PEnt *part_entries(uint32_t *region) { return reinterpret_cast<PEnt *>(region); }
+constexpr size_t kDlvRegionWords = 3;  // u32 words per part slot
+// Coarse-bucket entries inside the region buffer, after the bin regions.
+__host__ __device__ inline PEnt *coarse_entries(uint32_t *region, uint32_t nb) {
+    return reinterpret_cast<PEnt *>(region + (size_t)nb * kBinCap * kDlvRegionWords);
 }
 
 // Pull pass-back arrays, after the coarse buckets: per coarse source bucket
@@ -482,7 +487,7 @@ __host__ __device__ inline size_t pull_words(uint32_t nb) {
 }
 __host__ __device__ inline PullArrays pull_arrays(uint32_t *region, uint32_t nb) {
     const size_t nc = (nb + kCoarseBins - 1) / kCoarseBins;
-    uint32_t *base = region + (size_t)nb * kBinCap * 5 / 2 + 3 * nc * kCoarseCap;
+    uint32_t *base = region + (size_t)nb * kBinCap * kDlvRegionWords + 3 * nc * kCoarseCap;
     const size_t pc = nc << kCoarseLog;
     return PullArrays{base, base + pc, reinterpret_cast<uint16_t *>(base + 2 * pc),
                       base + 2 * pc + (size_t)nb * kBin / 2};
@@ -500,7 +505,7 @@ __global__ __launch_bounds__(NT) void dl_coarse(InListArgs a) {
     const uint32_t nc = n_coarse(p.nb);
     const uint32_t shard = blockIdx.x % kCoarseShards;
     uint32_t *cfill = a.scratch + cfill_off(p);
-    const CoarseArrays ca = coarse_arrays(a.region, p.nb);
+    PEnt *ce = coarse_entries(a.region, p.nb);
     for (uint32_t i = threadIdx.x; i < nc; i += NT) cnt[i] = 0u;
     __syncthreads();
     const uint32_t lo = blockIdx.x * kPartChunk;
@@ -553,9 +558,7 @@ __global__ __launch_bounds__(NT) void dl_coarse(InListArgs a) {
         const uint32_t slot = res[b] + (i - off[b]);
         if (slot < kShardCap) {
             const u64 o = (u64)(b * kCoarseShards + shard) * kShardCap + slot;
-            ca.x[o] = sx[i];
-            ca.t[o] = st[i];
-            ca.c[o] = sc[i];
+            ce[o] = PEnt{sx[i], st[i], sc[i]};
         }
     }
 }
@@ -593,7 +596,8 @@ __global__ __launch_bounds__(NT) void dl_fine(InListArgs a) {
     const uint32_t lo = blockIdx.x * kFineChunk;
     if (lo >= fill) return;  // uniform per block
     const uint32_t hi = min(fill, lo + kFineChunk);
-    const CoarseArrays ca = coarse_arrays(a.region, p.nb);
+    const PEnt *ce = coarse_entries(a.region, p.nb);
+    PEnt *pe = part_entries(a.region);
     if (threadIdx.x < fp) cnt[threadIdx.x] = 0u;
     __syncthreads();
     uint32_t xv[kPer], tv[kPer], cv[kPer];
@@ -601,10 +605,10 @@ __global__ __launch_bounds__(NT) void dl_fine(InListArgs a) {
     for (uint32_t q = 0; q < kPer; ++q) {
         const uint32_t i = lo + threadIdx.x + q * NT;
         const bool ok = i < hi;
-        const u64 o = (u64)cs * kShardCap + (ok ? i : lo);
-        xv[q] = ca.x[o];
-        tv[q] = ok ? ca.t[o] : kNone;
-        cv[q] = ca.c[o];
+        const PEnt en = ce[(u64)cs * kShardCap + (ok ? i : lo)];
+        xv[q] = en.a;
+        tv[q] = ok ? en.b : kNone;
+        cv[q] = en.c;
         if (ok) atomicAdd(&cnt[(tv[q] >> plog) & (fp - 1u)], 1u);
     }
     __syncthreads();
@@ -642,9 +646,7 @@ __global__ __launch_bounds__(NT) void dl_fine(InListArgs a) {
         const uint32_t slot = res[lo_b] + (i - off[lo_b]);
         if (slot < pcap) {
             const u64 o = (u64)(cb * fp + lo_b) * pcap + slot;
-            a.region[o] = sx[i];
-            a.region_lt[o] = slt[i];
-            a.region_code[o] = sc[i];
+            pe[o] = PEnt{sx[i], sc[i], slt[i]};
         }
     }
 }
@@ -715,10 +717,7 @@ __global__ __launch_bounds__(kInlThreads) void dl_direct(InListArgs a) {
         const uint32_t b = sb[i];
         const uint32_t slot = res[b] + (i - off[b]);
         if (slot < pcap) {
-            const u64 o = (u64)b * pcap + slot;
-            a.region[o] = sx[i];
-            a.region_lt[o] = slt[i];
-            a.region_code[o] = sc[i];
+            part_entries(a.region)[(u64)b * pcap + slot] = PEnt{sx[i], sc[i], slt[i]};
         }
     }
 }
@@ -801,10 +800,10 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
         for (uint32_t q = 0; q < kPer; ++q) {
             const uint32_t i = threadIdx.x + q * kInlThreads;
             const bool ok = i < cnt;
-            const u64 ri = rb + (ok ? i : 0u);
-            const uint32_t lt = ok ? (uint32_t)a.region_lt[ri] : kNone;
-            ex[q] = a.region[ri];
-            ec[q] = a.region_code[ri];
+            const PEnt en = part_entries(a.region)[rb + (ok ? i : 0u)];
+            const uint32_t lt = ok ? en.c : kNone;
+            ex[q] = en.a;
+            ec[q] = en.b;
             el[q] = (ok && (lt >> kHalfLog) == hp) ? (lt & (kHalf - 1u)) : kNone;
         }
     };
@@ -1262,10 +1261,7 @@ void inlist_cfill_range(const CsrPlan &p, size_t *first, size_t *words) {
 
 bool dlv_coarse_target(const CsrPlan &p, uint32_t *region, uint32_t *scratch, CoarseTarget *out) {
     if (!p.binned || !p.dlv || n_coarse(p.nb) < 2u) return false;  // (one coarse bucket: dl_direct)
-    const CoarseArrays ca = coarse_arrays(region, p.nb);
-    out->x = ca.x;
-    out->t = ca.t;
-    out->c = ca.c;
+    out->e = reinterpret_cast<uint32_t *>(coarse_entries(region, p.nb));
     out->fill = scratch + cfill_off(p);
     out->nc = n_coarse(p.nb);
     out->shards = kCoarseShards;
@@ -1279,7 +1275,7 @@ InListSizes inlist_sizes(const CsrPlan &p) {
     if (p.binned) {
         z.src_words = p.tailcap;  // ids (or DLV: push codes) of the in-list tails
         // sources (u32) + local targets (u16) [+ push codes (u32) + the coarse buckets]
-        z.region_words = (size_t)p.nb * kBinCap * (p.dlv ? 5 : 3) / 2;
+        z.region_words = p.dlv ? (size_t)p.nb * kBinCap * kDlvRegionWords : (size_t)p.nb * kBinCap * 3 / 2;
         const size_t nc = (p.nb + kCoarseBins - 1) / kCoarseBins;
         if (p.dlv) z.region_words += 3 * nc * kCoarseCap + pull_words(p.nb);
         // fill[nb], tailcnt[, coarse fill[nc], pull coarse fill[nc], pull bin fill[nb]]
@@ -1406,7 +1402,6 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
         if ((a.lvm == nullptr) != (a.zl == nullptr) || (a.lvm && !a.cpm)) return hipErrorInvalidValue;
         InListArgs ab = a;
         ab.region_lt = reinterpret_cast<uint16_t *>(a.region + (size_t)p.nb * kBinCap);
-        ab.region_code = a.region + (size_t)p.nb * kBinCap * 3 / 2;
         if (p.dlv) {
             // fill counts (both half-bin blocks of a bin read them, so they are
             // cleared here rather than by the sort), tail count, coarse fills

@@ -103,8 +103,8 @@ struct RoundArgs {
     // DLV transition launches (gs_dlv4.hip) may run the first partition of
     // the next round's build in their epilogue, in place of dl_coarse: the
     // round-(t+1) target words (tg_out) and the (source, target, push code)
-    // entries into the coarse shards of the next set (cp_x null: not fused)
-    uint32_t *cp_x, *cp_t, *cp_c, *cp_fill, *tg_out;
+    // entries into the coarse shards of the next set (cp_e null: not fused)
+    uint32_t *cp_e, *cp_fill, *tg_out;  // cp_e: 12-byte (source, target, code) entries
     uint32_t cp_nc, cp_shards, cp_shard_cap, cp_log;
     // a second range cleared at the start (the coarse fills of the set the
     // previous round's build consumed)
@@ -180,7 +180,7 @@ void inlist_zero_range(const CsrPlan &p, size_t *first, size_t *words);
 void inlist_cfill_range(const CsrPlan &p, size_t *first, size_t *words);
 // DLV with several coarse buckets: where a fused partition writes (false: none).
 struct CoarseTarget {
-    uint32_t *x, *t, *c, *fill;
+    uint32_t *e, *fill;  // e: the 12-byte coarse entries
     uint32_t nc, shards, shard_cap, log;
 };
 bool dlv_coarse_target(const CsrPlan &p, uint32_t *region, uint32_t *scratch, CoarseTarget *out);
@@ -199,7 +199,6 @@ struct InListArgs {
     DlvRec *DR;         // [n]
     uint32_t *dtail;    // [tailcap] push codes of pushers >= kDlvInline
     uint32_t *pull;     // [n] PULL: pull batch of every pusher
-    uint32_t *region_code;  // binned: [nb][cap] push codes of the region's sources (set internally)
     InRec *IN8;         // [n]
     SibRec *SIB8;       // [n]
     uint32_t *src;      // tails (binned) or the full CSR (generic)
