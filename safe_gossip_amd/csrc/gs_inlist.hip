@@ -152,8 +152,8 @@ GS_DEV uint32_t emit_tail(const InListArgs &a, const uint32_t *lst, uint32_t k, 
 }
 
 // ------------------------------------------------------------ binned path
-// Region of bin b: sources at region[b*kBinCap ...], their targets relative to
-// the bin (u16) at region_lt[b*kBinCap ...].  Each target is drawn once, here:
+// Region of bin b: 8-byte records (source, target relative to the bin) at
+// region[b*kBinCap ...] (one store stream per run).  Each target is drawn once, here:
 // a Philox4x32-10 draw is ~40 quarter-rate multiplies, so redrawing it in
 // inl_sort would cost more than carrying 2 bytes.
 template <uint32_t CHUNK>
@@ -260,8 +260,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_bin(InListArgs a) {
         const uint32_t b = stage_b[i];
         const uint32_t slot = res[b] + (i - off[b]);
         if (slot < pcap) {
-            a.region[(u64)b * pcap + slot] = stage[i];
-            a.region_lt[(u64)b * pcap + slot] = stage_lt[i];
+            reinterpret_cast<uint2 *>(a.region)[(u64)b * pcap + slot] = make_uint2(stage[i], stage_lt[i]);
         }
     }
 }
@@ -273,6 +272,10 @@ GS_DEV uint32_t half_of(const uint32_t *h, uint32_t i) { return (h[i >> 1] >> ((
 // the chip (two per bin measured slower at 1024 bins: every block reads the
 // whole bin region), more for small networks (2^20 nodes = 64 bins), whose
 // regions stay in L2.  GS_SORT_SPLIT_LOG forces one value (A/B).
+#ifndef GS_SORT_THREADS
+#define GS_SORT_THREADS 1024
+#endif
+constexpr uint32_t kSortThreads = GS_SORT_THREADS;
 #ifndef GS_SORT_SMALL_LOG
 #define GS_SORT_SMALL_LOG 2u  // sort blocks per bin = 2^this below 128 bins (2^21 nodes)
 #endif
@@ -288,19 +291,21 @@ inline uint32_t sort_split_log(uint32_t nb) {
 // SPLITLOG > 0: 2^SPLITLOG blocks per bin (blockIdx.y = part), each sorting the
 // targets of its part from the whole bin region; half the LDS, so two blocks
 // share a CU (the fill counts are then cleared by the launcher, not here).
-template <uint32_t SPLITLOG>
-__global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
+// NT threads per block (GS_SORT_THREADS, A/B): 512-thread blocks of half bins
+// let two share a CU (a whole bin's 112 KiB of LDS takes one)
+template <uint32_t SPLITLOG, uint32_t NT = kInlThreads>
+__global__ __launch_bounds__(NT, NT == kInlThreads ? 1 : 2 * NT / 256) void inl_sort(InListArgs a) {
     constexpr uint32_t kPartLog = kBinLog - SPLITLOG;
     constexpr uint32_t kPart = 1u << kPartLog;             // targets per block
     constexpr uint32_t kPartCap = kBinCap >> SPLITLOG;     // sorted entries per block
     // SPLITLOG > 0: inl_bin wrote this part's own region (p.sub == SPLITLOG)
     constexpr bool own = SPLITLOG > 0;
-    constexpr uint32_t kPer = (kPartCap + kInlThreads - 1) / kInlThreads;  // region entries per thread
+    constexpr uint32_t kPer = (kPartCap + NT - 1) / NT;  // region entries per thread
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     const CsrPlan &p = a.p;
     uint32_t *h = sh;                   // [kPart/2] packed per-target counters
     uint32_t *sorted = sh + kPart / 2;  // [kPartCap]
-    __shared__ uint32_t lds_scan[kInlThreads / 64];
+    __shared__ uint32_t lds_scan[NT / 64];
     const uint32_t b = blockIdx.x, hh = blockIdx.y;
     const uint32_t cnt = own ? min(a.scratch[p.fill_off + (b << SPLITLOG) + hh], kPartCap) : min(a.scratch[b], kBinCap);
     const u64 rb = own ? (u64)((b << SPLITLOG) + hh) * kPartCap : (u64)b * kBinCap;
@@ -311,13 +316,14 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
     uint32_t ex[kPer], el[kPer];
 #pragma unroll
     for (uint32_t q = 0; q < kPer; ++q) {
-        const uint32_t i = threadIdx.x + q * kInlThreads;
+        const uint32_t i = threadIdx.x + q * NT;
         const bool ok = i < cnt;
-        ex[q] = ok ? a.region[rb + i] : 0u;
-        const uint32_t lt = ok ? (uint32_t)a.region_lt[rb + i] : kNone;
+        const uint2 en = ok ? reinterpret_cast<const uint2 *>(a.region)[rb + i] : make_uint2(0u, 0u);
+        ex[q] = en.x;
+        const uint32_t lt = ok ? en.y : kNone;
         el[q] = (ok && (lt >> kPartLog) == hh) ? (lt & (kPart - 1u)) : kNone;
     }
-    for (uint32_t i = threadIdx.x; i < kPart / 2; i += kInlThreads) h[i] = 0u;
+    for (uint32_t i = threadIdx.x; i < kPart / 2; i += NT) h[i] = 0u;
     // live-filtered gathers: the part's "complete" bits (coalesced) and the
     // live bit of every entry (L2-resident map lookups, issued together),
     // carried as bit 31 of the sorted ids (kLiveTag)
@@ -325,7 +331,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
     const bool filt = a.lvm != nullptr;
     uint32_t lt_tag[kPer];
     if (filt) {
-        for (uint32_t i = threadIdx.x; i < kPart / 32; i += kInlThreads) {
+        for (uint32_t i = threadIdx.x; i < kPart / 32; i += NT) {
             const bool in = t0 + 32u * i < p.n;
             cpl[i] = in ? reinterpret_cast<const uint32_t *>(a.cpm)[(t0 >> 5) + i] : 0u;
             lvl[i] = in ? reinterpret_cast<const uint32_t *>(a.lvm)[(t0 >> 5) + i] : 0u;
@@ -340,15 +346,15 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
     for (uint32_t q = 0; q < kPer; ++q)
         if (el[q] != kNone) atomicAdd(&h[el[q] >> 1], 1u << ((el[q] & 1u) << 4));
     __syncthreads();
-    // exclusive scan over the kPart targets, kPart/kInlThreads per thread
-    constexpr uint32_t per = kPart / kInlThreads;
+    // exclusive scan over the kPart targets, kPart/NT per thread
+    constexpr uint32_t per = kPart / NT;
     static_assert(per >= 2 && per % 2 == 0, "the scan walks packed counter pairs: >= 2048 targets");
     const uint32_t i0 = threadIdx.x * per;
     uint32_t sum = 0;
 #pragma unroll
     for (uint32_t q = 0; q < per; ++q) sum += half_of(h, i0 + q);
     uint32_t total;
-    uint32_t run = block_exclusive_scan_t<kInlThreads>(sum, lds_scan, total);
+    uint32_t run = block_exclusive_scan_t<NT>(sum, lds_scan, total);
 #pragma unroll
     for (uint32_t q = 0; q < per; q += 2) {
         const uint32_t c0 = half_of(h, i0 + q), c1 = half_of(h, i0 + q + 1);
@@ -372,11 +378,11 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
     // above, keeps only the entries that fit)
     auto end_of = [&](uint32_t lt) { return min(half_of(h, lt), kPartCap); };
     uint32_t mine = 0;
-    for (uint32_t lt = threadIdx.x; lt < nodes; lt += kInlThreads)
+    for (uint32_t lt = threadIdx.x; lt < nodes; lt += NT)
         mine += tail_len<>(end_of(lt) - (lt ? end_of(lt - 1) : 0u));
-    uint32_t cur = reserve_tails<kInlThreads>(a, mine, &a.scratch[p.nb], lds_scan);
+    uint32_t cur = reserve_tails<NT>(a, mine, &a.scratch[p.nb], lds_scan);
     uint32_t rows = 0;  // filtered: class rows left to gather (traffic accounting)
-    for (uint32_t lt = threadIdx.x; lt < nodes; lt += kInlThreads) {
+    for (uint32_t lt = threadIdx.x; lt < nodes; lt += NT) {
         const uint32_t e = end_of(lt);
         const uint32_t s = lt ? end_of(lt - 1) : 0u;
         uint32_t *lst = sorted + s;
@@ -396,7 +402,7 @@ __global__ __launch_bounds__(kInlThreads) void inl_sort(InListArgs a) {
     }
     if (a.rows) {
         uint32_t total;
-        (void)block_exclusive_scan_t<kInlThreads>(rows, lds_scan, total);
+        (void)block_exclusive_scan_t<NT>(rows, lds_scan, total);
         if (threadIdx.x == 0 && total) atomicAdd(a.rows, (u64)total);
     }
 }
@@ -1275,7 +1281,8 @@ InListSizes inlist_sizes(const CsrPlan &p) {
     if (p.binned) {
         z.src_words = p.tailcap;  // ids (or DLV: push codes) of the in-list tails
         // sources (u32) + local targets (u16) [+ push codes (u32) + the coarse buckets]
-        z.region_words = p.dlv ? (size_t)p.nb * kBinCap * kDlvRegionWords : (size_t)p.nb * kBinCap * 3 / 2;
+        // (gather path: 8-byte (source, target within the bin) records)
+        z.region_words = p.dlv ? (size_t)p.nb * kBinCap * kDlvRegionWords : (size_t)p.nb * kBinCap * 2;
         const size_t nc = (p.nb + kCoarseBins - 1) / kCoarseBins;
         if (p.dlv) z.region_words += 3 * nc * kCoarseCap + pull_words(p.nb);
         // fill[nb], tailcnt[, coarse fill[nc], pull coarse fill[nc], pull bin fill[nb]]
@@ -1337,7 +1344,6 @@ hipError_t launch_build_bins(const InListArgs &a, hipStream_t s) {
         if (e != hipSuccess) return e;
     }
     InListArgs ab = a;
-    ab.region_lt = reinterpret_cast<uint16_t *>(a.region + (size_t)p.nb * kBinCap);
     ab.lvm = ab.cpm = nullptr;  // no node maps in this phase (inl_zl writes zl)
     ab.zl = nullptr;
     ab.rows = nullptr;
@@ -1352,21 +1358,20 @@ hipError_t launch_build_sort(const InListArgs &a, hipStream_t s) {
     if (!p.binned || p.dlv || !a.lvm || !a.cpm || !a.zl) return hipErrorInvalidValue;
     const uint32_t sl = sort_split_log(p.nb);
     const size_t lds_sort = ((size_t)(kBin >> sl) / 2 + (kBinCap >> sl)) * sizeof(uint32_t);
-    const void *ks = sl == 0   ? (const void *)inl_sort<0>
-                     : sl == 1 ? (const void *)inl_sort<1>
-                     : sl == 2 ? (const void *)inl_sort<2>
-                               : (const void *)inl_sort<3>;
+    const void *ks = sl == 0   ? (const void *)inl_sort<0, kSortThreads>
+                     : sl == 1 ? (const void *)inl_sort<1, kSortThreads>
+                     : sl == 2 ? (const void *)inl_sort<2, kSortThreads>
+                               : (const void *)inl_sort<3, kSortThreads>;
     hipError_t e = hipFuncSetAttribute(ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sort);
     if (e != hipSuccess) return e;
     InListArgs ab = a;
-    ab.region_lt = reinterpret_cast<uint16_t *>(a.region + (size_t)p.nb * kBinCap);
     const uint32_t zb = (uint32_t)(((u64)p.n + kZlPer * kInlThreads - 1) / (kZlPer * kInlThreads));
     hipLaunchKernelGGL(inl_zl, dim3(zb), dim3(kInlThreads), 0, s, ab);
     const dim3 gs(p.nb, 1u << sl);
-    if (sl == 0) hipLaunchKernelGGL(inl_sort<0>, gs, dim3(kInlThreads), lds_sort, s, ab);
-    else if (sl == 1) hipLaunchKernelGGL(inl_sort<1>, gs, dim3(kInlThreads), lds_sort, s, ab);
-    else if (sl == 2) hipLaunchKernelGGL(inl_sort<2>, gs, dim3(kInlThreads), lds_sort, s, ab);
-    else hipLaunchKernelGGL(inl_sort<3>, gs, dim3(kInlThreads), lds_sort, s, ab);
+    if (sl == 0) hipLaunchKernelGGL((inl_sort<0, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
+    else if (sl == 1) hipLaunchKernelGGL((inl_sort<1, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
+    else if (sl == 2) hipLaunchKernelGGL((inl_sort<2, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
+    else hipLaunchKernelGGL((inl_sort<3, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
     return hipGetLastError();
 }
 
@@ -1388,10 +1393,10 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
                              : (own ? (const void *)inl_sort_dlv<kDlvSmallLog, true>
                                     : (const void *)inl_sort_dlv<kDlvSmallLog, false>);
         const void *ks = p.dlv ? kd
-                               : (sl == 0   ? (const void *)inl_sort<0>
-                                  : sl == 1 ? (const void *)inl_sort<1>
-                                  : sl == 2 ? (const void *)inl_sort<2>
-                                            : (const void *)inl_sort<3>);
+                               : (sl == 0   ? (const void *)inl_sort<0, kSortThreads>
+                                  : sl == 1 ? (const void *)inl_sort<1, kSortThreads>
+                                  : sl == 2 ? (const void *)inl_sort<2, kSortThreads>
+                                            : (const void *)inl_sort<3, kSortThreads>);
         // (inl_bin is the gather path's partition: its LDS, sized by the parts,
         // is not set for a DLV plan, whose part count it may not fit)
         hipError_t e = p.dlv ? hipSuccess : hipFuncSetAttribute(kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bin);
@@ -1401,8 +1406,7 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
         if (p.dlv && (a.lvm || a.zl)) return hipErrorInvalidValue;  // DLV records gather nothing
         if ((a.lvm == nullptr) != (a.zl == nullptr) || (a.lvm && !a.cpm)) return hipErrorInvalidValue;
         InListArgs ab = a;
-        ab.region_lt = reinterpret_cast<uint16_t *>(a.region + (size_t)p.nb * kBinCap);
-        if (p.dlv) {
+            if (p.dlv) {
             // fill counts (both half-bin blocks of a bin read them, so they are
             // cleared here rather than by the sort), tail count, coarse fills
             const uint32_t nc = (p.nb + kCoarseBins - 1) / kCoarseBins;
@@ -1469,10 +1473,10 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
             if (p.chunk == kChunk) hipLaunchKernelGGL(inl_bin<kChunk>, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
             else hipLaunchKernelGGL(inl_bin<kChunkSmall>, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
             const dim3 gs(p.nb, 1u << sl);
-            if (sl == 0) hipLaunchKernelGGL(inl_sort<0>, gs, dim3(kInlThreads), lds_sort, s, ab);
-            else if (sl == 1) hipLaunchKernelGGL(inl_sort<1>, gs, dim3(kInlThreads), lds_sort, s, ab);
-            else if (sl == 2) hipLaunchKernelGGL(inl_sort<2>, gs, dim3(kInlThreads), lds_sort, s, ab);
-            else hipLaunchKernelGGL(inl_sort<3>, gs, dim3(kInlThreads), lds_sort, s, ab);
+            if (sl == 0) hipLaunchKernelGGL((inl_sort<0, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
+            else if (sl == 1) hipLaunchKernelGGL((inl_sort<1, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
+            else if (sl == 2) hipLaunchKernelGGL((inl_sort<2, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
+            else hipLaunchKernelGGL((inl_sort<3, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
         }
         return hipGetLastError();
     }

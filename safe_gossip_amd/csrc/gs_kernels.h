@@ -202,8 +202,7 @@ struct InListArgs {
     InRec *IN8;         // [n]
     SibRec *SIB8;       // [n]
     uint32_t *src;      // tails (binned) or the full CSR (generic)
-    uint32_t *region;   // binned: [nb][cap] sources by bin; generic: u64 pairs[n]
-    uint16_t *region_lt;  // binned: [nb][cap] their targets within the bin (set internally)
+    uint32_t *region;   // binned: [nb][cap] (source, target in the bin) records; generic: u64 pairs[n]
     uint32_t *scratch;  // binned: fill[nb], tailcnt (zero between builds); generic: M, tot, base
     uint32_t *flags;    // flags[2]: device-limit bit
     uint32_t serial;

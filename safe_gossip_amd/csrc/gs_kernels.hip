@@ -36,6 +36,9 @@ constexpr uint32_t kStageIters = kBlockWords / 2u / 256u;  // uint4 loads per th
 #ifndef GS_RK_MINW
 #define GS_RK_MINW 1
 #endif
+#ifndef GS_RK_LATE_B
+#define GS_RK_LATE_B 0
+#endif
 
 // MODE: 0 transition only (first round), 1 deliver round t + transition to
 // t+1, 2 deliver round t + observe, 3 observe only.
@@ -338,12 +341,18 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         dst4[threadIdx.x + 768u] = st3;
     }
     __syncthreads();
+    // GS_RK_LATE_B: the five b planes are read from the stage only for the
+    // transition (fewer registers live across the deliveries; A/B)
+    constexpr bool kLateB = GS_RK_LATE_B != 0;
     u64 P[kPlanes];
+    auto load_planes = [&](int p0, int p1) {
 #pragma unroll
-    for (int p = 0; p < kPlanes; ++p) {
-        u64 v = valid ? stage[L.plane_index(p) - blk_base] : 0ull;
-        P[p] = SMALL ? ((v >> L.sh) & L.m) : v;
-    }
+        for (int p = p0; p < p1; ++p) {
+            u64 v = valid ? stage[L.plane_index(p) - blk_base] : 0ull;
+            P[p] = SMALL ? ((v >> L.sh) & L.m) : v;
+        }
+    };
+    load_planes(0, (kLateB && !spr) ? 3 : kPlanes);
 
     // Sparse variant: a wave all of whose segments are unknown words that
     // receive nothing live (no live pusher, an all-A t(x), no live pusher of
@@ -643,6 +652,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
 
     if (!TRANSITION) {
         // ---------------- observation (post phase 2 of round t) -------------
+        if (kLateB) load_planes(3, kPlanes);
         if (!valid) return;
         if (a.obs_only != 0xFFFFFFFFu) {  // one node's state codes only (obs_state[0..R))
             if (x != a.obs_only) return;
@@ -733,6 +743,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         const bool pending = off_t && valid;
         const u64 pb = pending ? a.pend[pidx] : 0ull, pa = pending ? a.pend[pidx + g.W] : 0ull;
         NextOut o;
+        if (kLateB && !spr) load_planes(3, kPlanes);
         next_round_seg(P, rv, inj, psize, pending, pb, pa, on_next, a.cmax, a.maxc, a.maxr, o);
 #pragma unroll
         for (int p = 0; p < kPlanes; ++p) N[p] = o.N[p];
