@@ -288,7 +288,8 @@ gs_status   gs_push_batch(gs_engine *e, uint32_t node, uint8_t *out, uint32_t ca
  * first Push from the peer this round is answered with the node's live
  * entries as Pull frames (or one empty Pull); the copy is absorbed (a new
  * entry is created, or recorded on a B entry); peers_in_this_round and the
- * Statistics count it.  2P schedule, unsharded; after a gs_next_round.
+ * Statistics count it.  2P or SEQ schedule, one engine (not node shards or
+ * rumor slices: GS_ERR_UNSUPPORTED); after a gs_next_round.
  * Messages whose bytes are no rumor slot's key: GS_ERR_INVALID_ARGUMENT.
  * A node offline this round (churn) drops the RPC: GS_OK, no frames, no
  * effect.  Undecodable bytes: GS_ERR_SERIALISATION, nothing applied; so is a

@@ -1611,7 +1611,11 @@ gs_status observe_node(gs_engine *e, uint32_t node, std::vector<uint16_t> &codes
     const u64 seg0 = e->g.small ? (u64)node : (u64)node * e->g.W;
     a.blk_off = (uint32_t)(seg0 / 256);
     a.blk_count = 1;
-    if (e->deliver_pending) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
+    if (e->deliver_pending) {
+        GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
+        st = seq_prepare(e);  // SEQ: the round's pull batches (no-op for 2P)
+        if (st != GS_OK) return st;
+    }
     GS_HIP(gs::launch_round(a, e->deliver_pending ? 2 : 3, e->stream));
     codes.resize(e->g.R);
     GS_HIP(hipMemcpyAsync(codes.data(), e->node_state, e->g.R * sizeof(uint16_t), hipMemcpyDeviceToHost,
@@ -1673,7 +1677,7 @@ gs_status gs_handle_received(gs_engine *e, uint32_t node, uint32_t peer, const u
     if (!e || !msg || !out_len || !out_count || node >= e->g.n) return GS_ERR_INVALID_ARGUMENT;
     *out_len = 0;
     *out_count = 0;
-    if (e->shard || e->seq || e->slice) return GS_ERR_UNSUPPORTED;
+    if (e->shard || e->slice) return GS_ERR_UNSUPPORTED;
     if (peer < e->g.n) return GS_ERR_INVALID_ARGUMENT;  // peers outside the simulated network
     if (e->round == 0 || !e->deliver_pending) return GS_ERR_INVALID_ARGUMENT;  // after a next_round
     int pull = 0;

@@ -50,6 +50,9 @@ static_assert(kChunk % kInlThreads == 0, "inl_bin: whole sources per thread");
 constexpr uint32_t kChunkSmall = 2048;            // sources per inl_bin block below 2^22 nodes
 static_assert(kChunkSmall % kInlThreads == 0, "inl_bin: whole sources per thread");
 constexpr uint32_t kBinnedMaxBins = 1u << (27 - kBinLog);  // n <= 2^27 (per-bin LDS state is 6 B)
+#ifndef GS_DLV_OWN_TAILS
+#define GS_DLV_OWN_TAILS 1  // A/B: 0 = one shared tail counter (reserve_tails)
+#endif
 constexpr uint32_t kFlagLimit = 2u;               // flags[2] bit: a device limit was hit
 
 // Target word (target + delivery flags, gs_common.h); edges flagged kTgDead
@@ -870,7 +873,16 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
     uint32_t mine = 0;
     for (uint32_t lt = threadIdx.x; lt < nodes; lt += kInlThreads)
         mine += tail_len<kDlvInline>(min(half_of(h, lt), kHalfCap) - (lt ? min(half_of(h, lt - 1), kHalfCap) : 0u));
-    uint32_t cur = reserve_tails<kInlThreads>(a, mine, &a.scratch[p.nb], lds_scan);
+    uint32_t cur;
+    if (own && GS_DLV_OWN_TAILS) {  // the part's own tail region (dlv_part_tails): a block scan, no atomic
+        uint32_t tot;
+        const uint32_t offs = block_exclusive_scan_t<kInlThreads>(mine, lds_scan, tot);
+        constexpr uint32_t kPartTails = (kBin >> SL) / 4u + (kBin >> SL) / 16u;
+        if (tot > kPartTails && threadIdx.x == 0) atomicOr(&a.flags[2], kFlagLimit);
+        cur = tot > kPartTails ? kNone : w * kPartTails + offs;
+    } else {
+        cur = reserve_tails<kInlThreads>(a, mine, &a.scratch[p.nb], lds_scan);
+    }
     // PP: the next part's region loads, issued after every load and returning
     // atomic this part still waits for (vmcnt counts in issue order), so
     // they stay in flight through the record and pull work below
@@ -1188,6 +1200,16 @@ bool getenv_generic_inlists() {
 
 }  // namespace
 
+// Tail slots of one own sort part (kBin >> sub targets): pushers beyond
+// kDlvInline average 3/e - 1 = 0.104 per target with a variance of ~0.15, so
+// kHalf * 5/16 is 25-35 standard deviations above the mean (2048-4096
+// targets); the sort blocks then need no shared tail counter (one returning
+// atomic per block on one word queued ~6 us behind 512 small-network blocks).
+inline uint32_t dlv_part_tails(uint32_t sub) {
+    const uint32_t half = kBin >> sub;
+    return half / 4u + half / 16u;
+}
+
 CsrPlan dlv_plan(uint32_t n) {
     CsrPlan p{};
     p.n = n;
@@ -1211,6 +1233,8 @@ CsrPlan dlv_plan(uint32_t n) {
 #endif
     if (nc > 1u && p.sub > kMaxFineSub) p.sub = 0u;  // (kFineParts)
     p.fill_off = p.sub ? dlv_head_words(p.nb) : 0u;  // after fill[nb], tailcnt, pull fills
+    // own parts: a fixed tail region per part (dlv_part_tails), no shared counter
+    if (p.sub && GS_DLV_OWN_TAILS) p.tailcap = (uint32_t)std::min<u64>((u64)(p.nb << p.sub) * dlv_part_tails(p.sub), 0xFFFFFFFFu);
     return p;
 }
 

@@ -574,7 +574,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             rv.create(newc, pCl);
         }
         rv.recv += popc(pl);
-        if (!SHARD && !SEQ && a.n_ext) {
+        if (!SHARD && a.n_ext) {
             // External RPCs to x (gs_handle_received), after every internal
             // delivery of the round, in call order (Gossip::receive,
             // src/gossip.rs:118-163): a first RPC from a peer joins

@@ -11,7 +11,7 @@
 import numpy as np
 import pytest
 
-from oracle_lib import SCHED_2P, OracleNet
+from oracle_lib import SCHED_2P, SCHED_SEQ, OracleNet
 from test_gpu_parity import SEED
 
 pytestmark = pytest.mark.gpu
@@ -89,15 +89,29 @@ def test_handle_received_matches_oracle(engine, n, R, faults):
     _handle_received_case(engine, n, R, faults)
 
 
+@pytest.mark.parametrize("n,R,faults", [
+    (300, 16, None),                  # SEQ over R_pad 16 (gather path: DLV is 2P only)
+    (250, 64, None),
+    (120, 200, (0.05, 0.05, 0.05)),
+])
+def test_handle_received_seq(engine, n, R, faults):
+    # the SEQ schedule (the reference harness's literal order): external RPCs
+    # after the round's internal deliveries, as under 2P
+    _handle_received_case(engine, n, R, faults, schedule="SEQ")
+
+
 def test_handle_received_sparse_records(engine, monkeypatch):
     # the sparse-record variant of the round kernel applies external RPCs too
     monkeypatch.setenv("SAFE_GOSSIP_AMD_SPARSE", "on")
     _handle_received_case(engine, 250, 128, None)
 
 
-def _handle_received_case(engine, n, R, faults):
+def _handle_received_case(engine, n, R, faults, schedule="2P"):
     from oracle_lib import fault_threshold
     fk = dict(churn=faults[0], drop_push=faults[1], drop_pull=faults[2]) if faults else {}
+    if schedule != "2P":
+        fk["schedule"] = schedule
+    osched = SCHED_SEQ if schedule == "SEQ" else SCHED_2P
     net = engine.Network(n, R, seed=SEED, **fk)
     orc = OracleNet(n, R, seed=SEED, faults=[fault_threshold(p) for p in faults] if faults else None)
     rng = np.random.default_rng(7 * n + R)
@@ -109,7 +123,7 @@ def _handle_received_case(engine, n, R, faults):
             orc.send_new(x, r)
         for rnd in range(1, 10):
             net.next_round()
-            orc.next_round(SCHED_2P)
+            orc.next_round(osched)
             off = orc.offline(rnd) if faults else np.zeros(n, dtype=bool)
             if rnd in (2, 3, 5):
                 # external peers n+1.. push / pull single rumors (some twice,
