@@ -10,17 +10,18 @@ import safe_gossip_amd as sg  # noqa: E402
 from safe_gossip_amd.sharded import ShardedNetwork  # noqa: E402
 
 world = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+K = int(sys.argv[2]) if len(sys.argv) > 2 else 10   # timed rounds
+W0 = int(sys.argv[3]) if len(sys.argv) > 3 else 3   # rounds before them
 n, R = 1 << 24, 256
 torch.cuda.set_device(0)
 net = ShardedNetwork(n, R, world, transport="local")
 for r in range(R):
     x = sg.origin_of(net.seed, 0, r, n)
     net.send_new(x, r)
-for _ in range(3):
+for _ in range(W0):
     net.next_round(report=False)
 net.sync()
 t0 = time.perf_counter()
-K = 10
 for _ in range(K):
     net.next_round(report=False)
 net.sync()

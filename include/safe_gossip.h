@@ -180,13 +180,15 @@ gs_status   gs_round_traffic(gs_engine *e, double *bytes_per_launch, uint32_t *l
  * moves two sets of rows between ranks with FIXED-SIZE
  * all-to-all exchanges (equal splits: no row count ever reaches the host, a
  * round needs no host synchronisation).  Both buffers are part-major: part h's
- * region starts at row h*world*capP and holds one sub-block per rank, so the
- * exchange of one part is ONE equal-split all-to-all over a contiguous region:
- *   A_h(t): exchange-A buffer set t % 2, part h: world sub-blocks of capP rows
- *           (the last part: capP + idrows rows, the idrows carrying the source
+ * region starts at row h*world*blk and holds one sub-block per rank, so the
+ * exchange of one part is ONE equal-split all-to-all over a contiguous region
+ * (blk = the row slots plus, with SAFE_GOSSIP_AMD_SHARD_FLAGS=1, flag rows:
+ * one byte per slot telling the receiver which words of the row are nonzero):
+ *   A_h(t): exchange-A buffer set t % 2, part h: world sub-blocks of blk rows
+ *           (the last part: blk + idrows rows, the idrows carrying the source
  *           ids of round t+1 for the in-lists, built one round ahead) -- push
  *           rows of round t of the sources in part h;
- *   B_h(t): part h of sendB -> part h of recvB, world sub-blocks of capP rows.
+ *   B_h(t): part h of sendB -> part h of recvB, world sub-blocks of blk rows.
  * A row is `row words` u64.  Sequence per round t >= 1, after round t exists:
  *   [t == 1: A_{P-1}(0) on set 0] -> all A_h(t) -> gs_shard_pull -> B_h(t) ->
  *   for h < P-1: gs_shard_round_part(h) (needs B_h(t); its rows are A_h(t+1))
@@ -200,10 +202,11 @@ gs_status   gs_shard_create(const gs_config *cfg, uint32_t rank, uint32_t world,
 /* The same with `parts` (1..4) pipeline parts (gs_shard_create: 1). */
 gs_status   gs_shard_create_parts(const gs_config *cfg, uint32_t rank, uint32_t world, uint32_t parts,
                                   gs_engine **out);
-/* info = {lo, m, capP (row slots per rank sub-block of a part), idrows (id
- *         rows per sub-block of A's last part), row words, world, rank, nodes
- *         per rank, parts P, nodes per part mP, rows of an A buffer (world *
- *         (P*capP + idrows)), rows of a B buffer (world * P * capP)} */
+/* info = {lo, m, blk (rows per rank sub-block of a part: row slots + flag
+ *         rows), idrows (id rows per sub-block of A's last part), row words,
+ *         world, rank, nodes per rank, parts P, nodes per part mP, rows of an
+ *         A buffer (world * (P*blk + idrows)), rows of a B buffer (world * P *
+ *         blk)}.  Every rank must see the same SAFE_GOSSIP_AMD_SHARD_FLAGS. */
 gs_status   gs_shard_info(const gs_engine *e, uint32_t info[12]);
 /* Device buffers: sendA[2], recvA[2] (info[10] rows each), sendB, recvB
  * (info[11] rows each). */

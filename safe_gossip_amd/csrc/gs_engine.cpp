@@ -342,6 +342,11 @@ gs_status device_limit(gs_engine *e) {
     return fl ? GS_ERR_DEVICE_LIMIT : GS_OK;
 }
 
+// The in-lists of the next round are built on the side stream (opt-in
+// SAFE_GOSSIP_AMD_CONCURRENT_INLISTS, gather path): only then do the engine
+// stream's readers wait for ev_built (else stream order suffices).
+bool built_elsewhere(const gs_engine *e) { return e->concurrent_inlists && !e->dlv; }
+
 gs::RoundArgs base_args(gs_engine *e) {
     gs::RoundArgs a{};
     a.Scur = e->S[e->cur];
@@ -360,6 +365,7 @@ gs::RoundArgs base_args(gs_engine *e) {
         a.recvA = e->recvA[t % 2];
         a.recvB = e->recvB;
         a.sendA = e->sendA[(t + 1) % 2];
+        a.sp = gs::ShardRows{e->sp.G, e->sp.P, e->sp.W, e->sp.capP, e->sp.flagrows, e->sp.blk, e->sp.idrows};
     } else {
         const auto &cs = e->csr[e->round & 1u];  // round-t lists (t = e->round)
         a.IN8 = cs.IN8;
@@ -472,7 +478,7 @@ gs_status ensure_obs(gs_engine *e, bool dumps) {
 gs_status seq_prepare(gs_engine *e) {
     if (!e->seq || !e->deliver_pending || e->seq_round == e->round) return GS_OK;
     const auto &cs = e->csr[e->round & 1u];
-    GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
+    if (built_elsewhere(e)) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
     gs::SeqArgs sa{};
     sa.S = e->S[e->cur];
     sa.IN8 = cs.IN8;
@@ -529,7 +535,7 @@ gs_status observe(gs_engine *e, bool dumps) {
     if (e->slice) a.emin = e->eb[3];  // pending empty pulls of this slice
     if (e->deliver_pending) {
         if (e->shard) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_edges[e->round % 2], 0));
-        else GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
+        else if (built_elsewhere(e)) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
         st = seq_prepare(e);
         if (st != GS_OK) return st;
     }
@@ -632,7 +638,14 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
     if (nglob > gs::kTgMask + 1u) return GS_ERR_UNSUPPORTED;
     gs::ShardPlan sp{};
     if (world && (parts == 0 || parts > gs::kMaxParts)) return GS_ERR_INVALID_ARGUMENT;
-    if (world) sp = gs::shard_plan(nglob, world, rank, R >= 64 ? (next_pow2(R) / 64) : 1u, parts);
+    if (world) {
+        // row flags (receivers skip empty rows; A/B, measured slower: DESIGN.md
+        // section 7): SAFE_GOSSIP_AMD_SHARD_FLAGS=1; every rank must agree (it
+        // changes the layout)
+        const char *v = std::getenv("SAFE_GOSSIP_AMD_SHARD_FLAGS");
+        const bool flags = v && *v == '1';
+        sp = gs::shard_plan(nglob, world, rank, R >= 64 ? (next_pow2(R) / 64) : 1u, parts, flags);
+    }
     const uint32_t n = world ? sp.m : nglob;  // nodes owned by this engine
     uint8_t p[3];
     gs_derive_params(nglob, p);
@@ -883,7 +896,7 @@ gs_status gs_shard_info(const gs_engine *e, uint32_t info[12]) {
     const uint32_t wa = 2 * e->g.W;  // u64 words per row (2-plane class code)
     info[0] = e->sp.lo;
     info[1] = e->sp.m;
-    info[2] = e->sp.capP;
+    info[2] = e->sp.blk;  // rows per rank sub-block of a part: capP row slots + flag rows
     info[3] = e->sp.idrows;
     info[4] = wa;
     info[5] = e->sp.G;
@@ -892,7 +905,7 @@ gs_status gs_shard_info(const gs_engine *e, uint32_t info[12]) {
     info[8] = e->sp.P;
     info[9] = e->sp.mP;
     info[10] = gs::shard_slotsA(e->sp);  // rows of an exchange-A buffer
-    info[11] = e->sp.G * e->sp.P * e->sp.capP;  // rows of an exchange-B buffer
+    info[11] = gs::shard_slotsB(e->sp);  // rows of an exchange-B buffer
     return GS_OK;
 }
 
@@ -1117,7 +1130,7 @@ gs_status round_begin(gs_engine *e) {
         GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[(R0 + 1) % 3], 0));
         if (e->deliver_pending) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_edges[R0 % 2], 0));
     } else if (e->deliver_pending) {
-        if (e->concurrent_inlists && !e->dlv)  // (built on the engine stream: in order already)
+        if (built_elsewhere(e))  // (built on the engine stream: in order already)
             GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[rs], 0));
         st = seq_prepare(e);  // SEQ: pull batches of round t (no-op for 2P)
         if (st != GS_OK) return st;
@@ -1217,7 +1230,9 @@ gs_status round_end(gs_engine *e, gs_round_report *report) {
         GS_HIP(hipEventRecord(e->ev_dens[par], e->stream));
         e->dens_round[par] = R0 + 1;
     }
-    if (!e->shard) GS_HIP(hipEventRecord(e->ev_read[rs], e->stream));
+    // (read only by a build on the side stream; an event record costs the
+    // stream a few microseconds between kernels, ~8 us per round at config 2)
+    if (!e->shard && (e->split_build || built_elsewhere(e))) GS_HIP(hipEventRecord(e->ev_read[rs], e->stream));
     e->timed = e->timing;
     e->round += 1;
     e->cur ^= 1;
@@ -1249,7 +1264,7 @@ gs_status round_end(gs_engine *e, gs_round_report *report) {
         // threads, >100 KiB LDS), so running them beside the round kernel
         // measured slower than in sequence.
         // (DLV: the build reads the planes this round kernel writes: in sequence)
-        hipStream_t bs = (e->concurrent_inlists && !e->dlv) ? e->cstream : e->stream;
+        hipStream_t bs = built_elsewhere(e) ? e->cstream : e->stream;
         if (e->split_build) {
             // phase A (inl_bin) ran beside this round kernel (round_begin);
             // phase B needs the node maps this kernel wrote
@@ -1267,7 +1282,7 @@ gs_status round_end(gs_engine *e, gs_round_report *report) {
             if (e->filt && !e->ra_prezeroed) GS_HIP(hipMemsetAsync(la.rows, 0, sizeof(u64), bs));
             GS_HIP(gs::launch_build_inlists(la, bs));
         }
-        GS_HIP(hipEventRecord(e->ev_built[ns], bs));
+        if (bs != e->stream) GS_HIP(hipEventRecord(e->ev_built[ns], bs));  // (else: stream order)
     }
     if (report) {
         uint32_t fl[4];
@@ -1612,7 +1627,7 @@ gs_status observe_node(gs_engine *e, uint32_t node, std::vector<uint16_t> &codes
     a.blk_off = (uint32_t)(seg0 / 256);
     a.blk_count = 1;
     if (e->deliver_pending) {
-        GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
+        if (built_elsewhere(e)) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
         st = seq_prepare(e);  // SEQ: the round's pull batches (no-op for 2P)
         if (st != GS_OK) return st;
     }

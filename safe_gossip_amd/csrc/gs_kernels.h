@@ -4,6 +4,12 @@
 
 namespace gs {
 
+// The exchange layout a round kernel needs (ShardPlan's fields of the same
+// names; the slot helpers below take either).
+struct ShardRows {
+    uint32_t G, P, W, capP, flagrows, blk, idrows;
+};
+
 struct RoundArgs {
     const u64 *Scur;          // state planes, round t (post phase 0)
     u64 *Snext;               // state planes, round t+1 (post phase 0)
@@ -45,6 +51,7 @@ struct RoundArgs {
     u64 *sendA;               // round-(t+1) push rows of this shard's nodes [slot][2][W]
     const uint32_t *spos_cur; // slot of x in recvB (exchange B of round t)
     const uint32_t *spos_next;// slot of x in sendA (exchange A of round t+1)
+    ShardRows sp;             // its layout (row flags when sp.flagrows != 0)
     // harness-injected faults (gs_common.h); pend/offc exist iff f.churn != 0
     Faults f;
     u64 *pend;                // [n][2][W]: votes (bump, anyC) of nodes frozen offline
@@ -277,27 +284,40 @@ struct ShardPlan {
     // is ONE equal-split all-to-all over a contiguous region.
     uint32_t P, mP, bP; // parts, nodes per part, plan blocks per part
     uint32_t capP;      // row slots per (source rank, destination rank, part)
+    // Row flags: after its capP row slots every sub-block carries flagrows
+    // rows of one byte per slot, bit j = word j of that slot's row is nonzero
+    // (written by the row's producer), so a receiver skips empty rows
+    // without reading them (opt-in, SAFE_GOSSIP_AMD_SHARD_FLAGS=1: measured
+    // slower); flagrows = 0 when off or W > 8.  blk = capP + flagrows.
+    uint32_t flagrows, blk;
     uint32_t idrows;    // rows of u32 ids per block of the last part of A (P*capP ids)
     CsrPlan edges;      // counting sort of the A receive slots over the m targets
 };
 // Row slot of (rank block s, part h, index i) in an exchange-A / -B buffer.
-__host__ __device__ inline uint32_t shard_blockA(const ShardPlan &P, uint32_t h) {
-    return P.capP + (h + 1u == P.P ? P.idrows : 0u);
+template <class SP>
+__host__ __device__ inline uint32_t shard_blockA(const SP &P, uint32_t h) {
+    return P.blk + (h + 1u == P.P ? P.idrows : 0u);
 }
-__host__ __device__ inline uint32_t shard_a_slot(const ShardPlan &P, uint32_t s, uint32_t h, uint32_t i) {
-    return h * P.G * P.capP + s * shard_blockA(P, h) + i;
+template <class SP>
+__host__ __device__ inline uint32_t shard_a_slot(const SP &P, uint32_t s, uint32_t h, uint32_t i) {
+    return h * P.G * P.blk + s * shard_blockA(P, h) + i;
 }
-__host__ __device__ inline uint32_t shard_b_slot(const ShardPlan &P, uint32_t s, uint32_t h, uint32_t i) {
-    return (h * P.G + s) * P.capP + i;
+template <class SP>
+__host__ __device__ inline uint32_t shard_b_slot(const SP &P, uint32_t s, uint32_t h, uint32_t i) {
+    return (h * P.G + s) * P.blk + i;
 }
-__host__ __device__ inline uint32_t shard_slotsA(const ShardPlan &P) {
-    return P.G * (P.P * P.capP + P.idrows);
+template <class SP>
+__host__ __device__ inline uint32_t shard_slotsA(const SP &P) {
+    return P.G * (P.P * P.blk + P.idrows);
 }
+template <class SP>
+__host__ __device__ inline uint32_t shard_slotsB(const SP &P) { return P.G * P.P * P.blk; }
 struct SlotPos {
     uint32_t s, h, i;  // i >= capP: an id row
 };
-__host__ __device__ inline SlotPos shard_a_decode(const ShardPlan &P, uint32_t e) {
-    const uint32_t reg = P.G * P.capP;
+template <class SP>
+__host__ __device__ inline SlotPos shard_a_decode(const SP &P, uint32_t e) {
+    const uint32_t reg = P.G * P.blk;
     uint32_t h = e / reg;
     if (h > P.P - 1u) h = P.P - 1u;
     const uint32_t r = e - h * reg, ba = shard_blockA(P, h);
@@ -305,13 +325,28 @@ __host__ __device__ inline SlotPos shard_a_decode(const ShardPlan &P, uint32_t e
     return SlotPos{s, h, r - s * ba};
 }
 // Pushers are listed in ascending source order = ascending (s, h, i).
-__host__ __device__ inline uint32_t shard_slot_key(const ShardPlan &P, const SlotPos &q) {
+template <class SP>
+__host__ __device__ inline uint32_t shard_slot_key(const SP &P, const SlotPos &q) {
     return (q.s * P.P + q.h) * P.capP + q.i;
 }
-__host__ __device__ inline uint32_t shard_key_slot(const ShardPlan &P, uint32_t key) {
+template <class SP>
+__host__ __device__ inline uint32_t shard_key_slot(const SP &P, uint32_t key) {
     const uint32_t per = P.P * P.capP;
     const uint32_t s = key / per, r = key - s * per, h = r / P.capP;
     return shard_a_slot(P, s, h, r - h * P.capP);
+}
+// The flag byte of row slot e of an exchange buffer (A: sub-blocks of
+// shard_blockA rows, B: of blk rows): byte i of the flag rows after the
+// capP row slots of e's sub-block.
+template <class SP>
+__host__ __device__ inline u64 shard_flag_a(const SP &P, uint32_t e) {
+    const SlotPos q = shard_a_decode(P, e);
+    return (u64)(e - q.i + P.capP) * (16u * P.W) + q.i;
+}
+template <class SP>
+__host__ __device__ inline u64 shard_flag_b(const SP &P, uint32_t e) {
+    const uint32_t i = e % P.blk;
+    return (u64)(e - i + P.capP) * (16u * P.W) + i;
 }
 // u32-word offsets inside one plan set (round r: targets and send slots of
 // the owned sources) and one in-list set (round r: receive-slot in-lists).
@@ -321,7 +356,7 @@ struct ShardPlanLayout {
 struct ShardEdgeLayout {
     size_t E_id, E_key, M, tot, base, EP, IN, IN2, pairs;
 };
-ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t parts);
+ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t parts, bool row_flags = true);
 size_t shard_plan_words(const ShardPlan &P, ShardPlanLayout *L);
 size_t shard_edge_words(const ShardPlan &P, ShardEdgeLayout *L);
 // Plan of `round`: owned targets, send slots, and the ids of every block of

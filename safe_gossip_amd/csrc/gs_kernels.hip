@@ -253,16 +253,36 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         } else if (SHARD) {
             if (valid) {
                 static_assert(kBatchK == 3, "shard rows: three batched pushers");
-                // the first three pushers' rows together (unconditional: row 0
-                // stands in for a missing pusher)
-                q[0] = L.load_push_row(a.recvA, in.z);
-                q[1] = L.load_push_row(a.recvA, in.w);
-                q[2] = L.load_push_row(a.recvA, a.IN2[x]);
+                const uint32_t e2 = a.IN2[x];
                 const uint32_t sp = a.spos_cur[x];  // the slot of x's pull row (z's answer)
-                if (!(tgw & kTgNoPull) && sp != 0xFFFFFFFFu) {  // no slot: capacity overflow (flagged)
+                const bool pl = !(tgw & kTgNoPull) && sp != 0xFFFFFFFFu;  // no slot: capacity overflow (flagged)
+                if (a.sp.flagrows) {
+                    // row flags (one byte per slot, bit j = word j nonzero):
+                    // rows that carry nothing for this lane's word are not read
+                    const uint8_t *fa = reinterpret_cast<const uint8_t *>(a.recvA);
+                    const uint8_t *fb = reinterpret_cast<const uint8_t *>(a.recvB);
+                    gq[0] = k > 0 && ((fa[shard_flag_a(a.sp, in.z)] >> L.j) & 1u);
+                    gq[1] = k > 1 && ((fa[shard_flag_a(a.sp, in.w)] >> L.j) & 1u);
+                    gq[2] = k > 2 && ((fa[shard_flag_a(a.sp, e2)] >> L.j) & 1u);
+                    gz = pl && ((fb[shard_flag_b(a.sp, sp)] >> L.j) & 1u);
+                    if (gq[0]) q[0] = L.load_push_row(a.recvA, in.z);
+                    if (gq[1]) q[1] = L.load_push_row(a.recvA, in.w);
+                    if (gq[2]) q[2] = L.load_push_row(a.recvA, e2);
+                    ngath += (gq[0] ? 1u : 0u) + (gq[1] ? 1u : 0u) + (gq[2] ? 1u : 0u);
+                } else {
+                    // the first three pushers' rows together (unconditional:
+                    // row 0 stands in for a missing pusher)
+                    q[0] = L.load_push_row(a.recvA, in.z);
+                    q[1] = L.load_push_row(a.recvA, in.w);
+                    q[2] = L.load_push_row(a.recvA, e2);
+                    ngath += min(k, kBatchK);
+                    gz = pl;
+                }
+                if (gz) {
                     qz.c = a.recvB[L.row_index(sp, 2, 0)];
                     qz.a0 = a.recvB[L.row_index(sp, 2, 1)];
                     qz.a1 = 0;
+                    ++ngath;
                 }
             }
         } else if (gchk) {
@@ -425,7 +445,12 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
 #pragma unroll
             for (uint32_t i = 0; i < kBatchK; ++i)
                 if (i < k) rv.push(q[i], i, k, zs != i);
-            for (uint32_t i = kBatchK; i < k; ++i) rv.push(L.load_push_row(a.recvA, a.src[in.x + i]), i, k, zs != i);
+            for (uint32_t i = kBatchK; i < k; ++i) {
+                const uint32_t ei = a.src[in.x + i];
+                const bool gi = !a.sp.flagrows ||
+                                ((reinterpret_cast<const uint8_t *>(a.recvA)[shard_flag_a(a.sp, ei)] >> L.j) & 1u);
+                rv.push(gi ? L.load_push_row(a.recvA, ei) : Cls{0, 0, 0}, i, k, zs != i);
+            }
             // pull row code (b0, b1): 01 counter 1, 10 counter 2, 11 counter 255
             pv2 = qz.a0 & ~qz.c;
             pvB = qz.c ^ qz.a0;
@@ -898,13 +923,24 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             for (uint32_t i = threadIdx.x; i < blk_v4; i += blockDim.x) nt_store4(src4[i], &dst4[i]);
         }
     }
-    if (SHARD && valid && a.spos_next[x] != 0xFFFFFFFFu) {
+    if (SHARD) {
         // push row of round t+1: the push batch's class code, to owner(t_{t+1}(x))
         // (no slot: an undelivered edge, or a capacity overflow, flagged)
-        const uint32_t sp = a.spos_next[x];
+        const uint32_t sp = valid ? a.spos_next[x] : 0xFFFFFFFFu;
         const u64 vC = N[0] & ~(N[1] & N[2]), vB = ~N[0] & (N[1] | N[2]);
-        a.sendA[L.row_index(sp, 2, 0)] = ((vB & N[1] & ~N[2]) | vC) & L.m;  // code bit 0
-        a.sendA[L.row_index(sp, 2, 1)] = ((vB & N[2] & ~N[1]) | vC) & L.m;  // code bit 1
+        const u64 c0 = ((vB & N[1] & ~N[2]) | vC) & L.m;  // code bit 0
+        const u64 c1 = ((vB & N[2] & ~N[1]) | vC) & L.m;  // code bit 1
+        if (sp != 0xFFFFFFFFu) {
+            a.sendA[L.row_index(sp, 2, 0)] = c0;
+            a.sendA[L.row_index(sp, 2, 1)] = c1;
+        }
+        if (a.sp.flagrows) {  // the row's flag byte: bit j = word j nonzero (x's W lanes are adjacent)
+            const u64 bal = __ballot(sp != 0xFFFFFFFFu && (c0 | c1) != 0ull);
+            if (sp != 0xFFFFFFFFu && L.j == 0) {
+                const uint32_t bits = (uint32_t)(bal >> (threadIdx.x & 63u)) & ((1u << a.sp.W) - 1u);
+                reinterpret_cast<uint8_t *>(a.sendA)[shard_flag_a(a.sp, sp)] = (uint8_t)bits;
+            }
+        }
     }
 
     // ---- push list + Statistics (src/gossip.rs:80,103-111)

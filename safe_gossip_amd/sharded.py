@@ -83,6 +83,7 @@ class _Shard:
     def region(self, which: str, h: int):
         """Part h of an exchange buffer: (first u64 word, u64 words per rank
         sub-block); the part's world sub-blocks are contiguous."""
+        # (info[2] "capP" here = rows per sub-block: row slots + flag rows)
         rows = self.capP + (self.idrows if which == "A" and h == self.parts - 1 else 0)
         return h * self.world * self.capP * self.wa, rows * self.wa
 
