@@ -101,6 +101,9 @@ struct ClsT {
 };
 using Cls = ClsT<u64>;
 
+#ifndef GS_CLS_VEC
+#define GS_CLS_VEC 0  // A/B: 1 = 16-byte loads for a gathered row's planes 0-1 (no gain / slower)
+#endif
 template <bool SMALL>
 struct Lane {
     // segment geometry
@@ -152,12 +155,29 @@ struct Lane {
         if (SMALL) {
             u64 b = (u64)(s >> lognpu) * kPlanes;
             uint32_t ss = (s & ((1u << lognpu) - 1u)) << logr;
-            r.c = (S[b] >> ss) & m;
-            r.a0 = (S[b + 1] >> ss) & m;
+            if (GS_CLS_VEC) {  // planes 0-1 in one 16-byte load (a unit's planes are 64-B aligned)
+                const ulonglong2 v = *reinterpret_cast<const ulonglong2 *>(S + b);
+                r.c = (v.x >> ss) & m;
+                r.a0 = (v.y >> ss) & m;
+            } else {
+                r.c = (S[b] >> ss) & m;
+                r.a0 = (S[b + 1] >> ss) & m;
+            }
             r.a1 = (S[b + 2] >> ss) & m;
         } else {
             const uint32_t lw = logr - 6u;
             u64 b = ((u64)s << (lw + 3u)) + j;
+#if !defined(GS_EXP_G1) && !defined(GS_EXP_G2)
+            if (GS_CLS_VEC && lw == 0u) {
+                // one word per plane (64 rumors): planes 0-1 in one 16-byte
+                // load, two load requests per row instead of three
+                const ulonglong2 v = *reinterpret_cast<const ulonglong2 *>(S + b);
+                r.c = v.x;
+                r.a0 = v.y;
+                r.a1 = S[b + 2];
+                return r;
+            }
+#endif
             r.c = S[b];
 #if defined(GS_EXP_G1)
             r.a0 = r.c >> 1;

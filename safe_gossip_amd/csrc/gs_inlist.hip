@@ -50,6 +50,9 @@ static_assert(kChunk % kInlThreads == 0, "inl_bin: whole sources per thread");
 constexpr uint32_t kChunkSmall = 2048;            // sources per inl_bin block below 2^22 nodes
 static_assert(kChunkSmall % kInlThreads == 0, "inl_bin: whole sources per thread");
 constexpr uint32_t kBinnedMaxBins = 1u << (27 - kBinLog);  // n <= 2^27 (per-bin LDS state is 6 B)
+#ifndef GS_SORT_OWN_TAILS
+#define GS_SORT_OWN_TAILS 1  // A/B: 0 = one shared tail counter (reserve_tails)
+#endif
 #ifndef GS_DLV_OWN_TAILS
 #define GS_DLV_OWN_TAILS 1  // A/B: 0 = one shared tail counter (reserve_tails)
 #endif
@@ -120,10 +123,12 @@ GS_DEV uint32_t emit_target(const InListArgs &a, uint32_t y, const uint32_t *lst
     return rows;
 }
 
-// Pushers i >= kInline of a target go to the shared tail array.  A block
+// Pushers i >= kInline of a target go to the tail array.  The binned sorts
+// give every part a fixed region of it (GS_SORT_OWN_TAILS / GS_DLV_OWN_TAILS:
+// tail_len per target and a block scan, no atomic); otherwise a block
 // reserves the tail words of all its targets with ONE atomic (same-address
-// atomics serialise at the memory side): tail_len per target, a block scan,
-// then emit_tail at the thread's running cursor.
+// atomics serialise at the memory side) -- then emit_tail at the thread's
+// running cursor.
 template <uint32_t INL = kInline>
 GS_DEV uint32_t tail_len(uint32_t k) { return k > INL ? min(k, kMaxIn) - INL : 0u; }
 
@@ -383,7 +388,19 @@ __global__ __launch_bounds__(NT, NT == kInlThreads ? 1 : 2 * NT / 256) void inl_
     uint32_t mine = 0;
     for (uint32_t lt = threadIdx.x; lt < nodes; lt += NT)
         mine += tail_len<>(end_of(lt) - (lt ? end_of(lt - 1) : 0u));
-    uint32_t cur = reserve_tails<NT>(a, mine, &a.scratch[p.nb], lds_scan);
+    uint32_t cur;
+    if (GS_SORT_OWN_TAILS) {
+        // the part's own tail region (kPart / 8 slots: pushers beyond kInline
+        // average 0.023 per target, so the cap is >= 25 standard deviations
+        // above the mean for >= 2 K-target parts): a block scan, no atomic
+        constexpr uint32_t kPartTails = kPart / 8u;
+        uint32_t tot;
+        const uint32_t offs = block_exclusive_scan_t<NT>(mine, lds_scan, tot);
+        if (tot > kPartTails && threadIdx.x == 0) atomicOr(&a.flags[2], kFlagLimit);
+        cur = tot > kPartTails ? kNone : ((b << SPLITLOG) + hh) * kPartTails + offs;
+    } else {
+        cur = reserve_tails<NT>(a, mine, &a.scratch[p.nb], lds_scan);
+    }
     uint32_t rows = 0;  // filtered: class rows left to gather (traffic accounting)
     for (uint32_t lt = threadIdx.x; lt < nodes; lt += NT) {
         const uint32_t e = end_of(lt);
@@ -751,6 +768,9 @@ constexpr uint32_t kSplitLog = GS_DLV_SPLIT_LOG;
 #define GS_DLV_SMALL_LOG (kSplitLog + 1u)  // below 128 bins (one coarse bucket, cache-resident)
 #endif
 constexpr uint32_t kDlvSmallLog = GS_DLV_SMALL_LOG;
+#ifndef GS_DLV_EARLY_TARGETS
+#define GS_DLV_EARLY_TARGETS 0  // A/B: 1 = small parts issue their target loads with the region loads (slower)
+#endif
 #ifndef GS_DLV_PP
 #define GS_DLV_PP 0  // 1: inl_sort_dlv as a persistent walk with the next part's loads in flight
 #endif
@@ -816,7 +836,32 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
             el[q] = (ok && (lt >> kHalfLog) == hp) ? (lt & (kHalf - 1u)) : kNone;
         }
     };
+    // the targets' own target words and class planes (R_pad <= 16: a node's
+    // segment lies in one 32-bit half of its plane word); they depend on the
+    // part index only, so they are issued with the part's region loads
+    uint32_t tgv[kHalfPer];
+    uint32_t w0[kHalfPer], w1[kHalfPer], w2[kHalfPer];
+    const uint32_t *S32 = reinterpret_cast<const uint32_t *>(a.S);
+    auto load_targets = [&](uint32_t wp) {
+        const uint32_t t0p = wp << kHalfLog;
+        const uint32_t np = t0p < p.n ? min(kHalf, p.n - t0p) : 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < kHalfPer; ++q) {
+            const uint32_t lt = threadIdx.x + q * kInlThreads;
+            const uint32_t y = np ? t0p + (lt < np ? lt : 0u) : 0u;  // (a part past the last node: node 0)
+            const uint32_t ysh = (y & ((1u << a.g.lognpu) - 1u)) << a.g.logr;
+            const u64 rb = (u64)(y >> a.g.lognpu) * kPlanes * 2u + (ysh >> 5);
+            tgv[q] = a.tg[y];
+            w0[q] = S32[rb];
+            w1[q] = S32[rb + 2];
+            w2[q] = S32[rb + 4];
+        }
+    };
+    // (small parts only: at SL = 2 the registers they hold across the LDS
+    // sort spill under the two-blocks-per-CU bound)
+    constexpr bool kEarly = GS_DLV_EARLY_TARGETS && !PP && SL >= 3;
     load_part(w);
+    if (kEarly) load_targets(w);
     for (;;) {
     const uint32_t t0 = w << kHalfLog;
     const uint32_t nodes = t0 < p.n ? min(kHalf, p.n - t0) : 0u;
@@ -854,22 +899,7 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
         }
     }
     __syncthreads();
-    // the targets' own target words and class planes, loads issued together
-    // (R_pad <= 16: a node's segment lies in one 32-bit half of its plane word)
-    uint32_t tgv[kHalfPer];
-    uint32_t w0[kHalfPer], w1[kHalfPer], w2[kHalfPer];
-    const uint32_t *S32 = reinterpret_cast<const uint32_t *>(a.S);
-#pragma unroll
-    for (uint32_t q = 0; q < kHalfPer; ++q) {
-        const uint32_t lt = threadIdx.x + q * kInlThreads;
-        const uint32_t y = t0 + (lt < nodes ? lt : 0u);
-        const uint32_t ysh = (y & ((1u << a.g.lognpu) - 1u)) << a.g.logr;
-        const u64 rb = (u64)(y >> a.g.lognpu) * kPlanes * 2u + (ysh >> 5);
-        tgv[q] = a.tg[y];
-        w0[q] = S32[rb];
-        w1[q] = S32[rb + 2];
-        w2[q] = S32[rb + 4];
-    }
+    if (!kEarly) load_targets(w);
     uint32_t mine = 0;
     for (uint32_t lt = threadIdx.x; lt < nodes; lt += kInlThreads)
         mine += tail_len<kDlvInline>(min(half_of(h, lt), kHalfCap) - (lt ? min(half_of(h, lt - 1), kHalfCap) : 0u));
@@ -1251,7 +1281,8 @@ CsrPlan csr_plan(uint32_t n) {
         // (2^20 nodes: 512 blocks instead of 128)
         p.chunk = n >= (1u << 22) ? kChunk : kChunkSmall;
         p.ba = (uint32_t)(((u64)n + p.chunk - 1) / p.chunk);
-        p.tailcap = n / 32u + 1024u;
+        // GS_SORT_OWN_TAILS: kBin / 8 tail slots per bin, split over its parts
+        p.tailcap = GS_SORT_OWN_TAILS ? nb_binned * (kBin / 8u) : n / 32u + 1024u;
         // several sort blocks per bin: inl_bin partitions into their parts
         p.sub = sort_split_log(p.nb);
         p.fill_off = p.sub ? p.nb + 1 : 0u;  // after fill[nb], tailcnt

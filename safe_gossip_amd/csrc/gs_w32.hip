@@ -46,6 +46,16 @@ GS_DEV u64 rec32(uint32_t x, uint32_t p, uint32_t j, uint32_t lw) {
 }
 // Class planes (isC, a0, a1) of node s for u32 word j.
 GS_DEV Cls32 load_cls32(const u32 *__restrict__ S, uint32_t s, uint32_t j, uint32_t lw) {
+    if (GS_CLS_VEC && lw <= 1u) {
+        // planes 0-2 of the 64-B unit holding s lie in its first 24 bytes
+        // (plane p, word sel at 2p + sel): a 16-byte and an 8-byte load
+        // instead of three 4-byte ones
+        const u64 b0 = lw ? ((u64)s << 4) : ((u64)(s >> 1) << 4);
+        const uint32_t sel = lw ? j : (s & 1u);
+        const uint4 v = *reinterpret_cast<const uint4 *>(S + b0);
+        const uint2 w = *reinterpret_cast<const uint2 *>(S + b0 + 4);
+        return Cls32{sel ? v.y : v.x, sel ? v.w : v.z, sel ? w.y : w.x};
+    }
     const u64 b = rec32(s, 0, j, lw);
     const uint32_t ps = lw ? (1u << lw) : 2u;  // plane stride
     return Cls32{S[b], S[b + ps], S[b + 2u * ps]};
