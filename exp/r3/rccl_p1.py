@@ -25,8 +25,8 @@ n = 1 << lg
 t0 = time.time()
 net = ShardedNetwork(n, R, 1, transport="dist", parts=parts)
 s = net.shards[0]
-print(f"n=2^{lg} R={R} parts={parts}: created in {time.time() - t0:.1f}s; exchange A {s.rowsA * s.wa * 8 / 1e9:.2f} GB, "
-      f"B {s.rowsB * s.wa * 8 / 1e9:.2f} GB; engine stream {s.stream}", flush=True)
+print(f"n=2^{lg} R={R} parts={parts}: created in {time.time() - t0:.1f}s; exchange A {s.rowsA * s.wa * 4 / 1e9:.2f} GB, "
+      f"B {s.rowsB * s.wa * 4 / 1e9:.2f} GB; engine stream {s.stream}", flush=True)
 for r in range(R):
     net.send_new(sg.origin_of(net.seed, 0, r, n), r)
 

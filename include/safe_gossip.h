@@ -145,6 +145,15 @@ gs_status   gs_known_popcounts(gs_engine *e, uint32_t *counts);
  *   rec:   anyC<<15 | cnt2<<7 | cnt1 over B.peer_counters; psize: n. */
 gs_status   gs_dump_state(gs_engine *e, uint16_t *out);
 gs_status   gs_dump_records(gs_engine *e, uint16_t *rec, uint32_t *psize);
+/* A 64-bit digest per node of everything the parity dumps and gs_statistics_all
+ * report (n u64, 8 B per node instead of 4R + 44): the sum mod 2^64 of one
+ * SplitMix64-finaliser term per (64-rumor word, bit-plane) of the 20 bit
+ * planes of the state codes and record summaries, one for psize and one per
+ * Statistics counter (exact definition: safe_gossip_amd/csrc/gs_common.h
+ * digest_*).  For checking large networks against a CPU program that computes
+ * the same function (oracle/gs_dense.c dn_digest).  GS_ERR_INVALID_ARGUMENT
+ * while send_new calls are queued (call it before injecting). */
+gs_status   gs_state_digest(gs_engine *e, uint64_t *out);
 
 /* Gossiper::clear for every node.  Returns GS_ERR_DEVICE_LIMIT (after
  * clearing) when a device limit was hit since the previous clear. */

@@ -14,6 +14,18 @@
  * counters >= own, plus anyC), in-edge lists by a counting sort of the Philox
  * targets (pushers ascending, as the harness delivers them,
  * src/gossiper.rs:217-231).  One thread owns a node across all its words.
+ *
+ * Harness-injected faults (config 5) as the oracle's
+ * or_next_round applies them (gs_oracle.c: churn skips a node's next_round and
+ * every RPC to or from it, a dropped push is never answered, a dropped pull is
+ * answered but not delivered); a node the harness skipped keeps its
+ * pre-transition state and the two votes its skipped next_round would take
+ * from its peer_counters (bump, anyC), as the GPU engine does, so its state
+ * equals the oracle's when it returns.
+ *
+ * dn_digest: the per-node digest gs_state_digest computes on the GPU
+ * (safe_gossip_amd/csrc/gs_common.h digest_*), so networks too large for the
+ * oracle are checked node by node against this program.
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -38,6 +50,7 @@ int dn_threads(void)
 }
 
 enum { PLANES = 8 };
+enum { DN_DEAD = 1, DN_NOPULL = 2, DN_OFF = 4 };  /* delivery flags of x's edge in the pending round */
 
 typedef struct {
     uint32_t n, R, W;
@@ -50,7 +63,48 @@ typedef struct {
     u64 *st;            /* [n][4]: empty_pull, empty_push, full_sent, full_received */
     uint32_t *tg, *off, *src, *rank;  /* targets, CSR of in-edges, rank of x at t(x) */
     u64 *inj;           /* [n][W] rumors injected before the next round */
+    uint32_t f_churn, f_push, f_pull;  /* fault thresholds over 2^32 (0: none) */
+    uint8_t *fl;        /* [n] DN_* flags of x's edge in the pending round */
+    u64 *pend;          /* [n][2][W] votes (bump, anyC) of nodes frozen offline */
+    uint32_t *offc;     /* [n] rounds each node was offline */
 } dn_net;
+
+/* The GPU's state digest (safe_gossip_amd/csrc/gs_common.h digest_*,
+ * restated): per 64-rumor word j the 20 bit-planes of the state codes and
+ * record summaries, plus |P| and the five Statistics counters. */
+static u64 dg_mix(u64 z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static u64 dg_word(uint32_t j, u64 m, u64 B, u64 C, u64 D, u64 crB, u64 crC, u64 a0, u64 a1, const u64 *bp,
+                   u64 anyC, const u64 *c1, const u64 *c2)
+{
+    const u64 BC = B | C, E = B | crB;
+    u64 pl[20];
+    pl[0] = crB | B | D;
+    pl[1] = crC | C | D;
+    pl[2] = crB | (BC & a0);
+    pl[3] = BC & a1;
+    for (int i = 0; i < 5; ++i) pl[4 + i] = BC & bp[i];
+    pl[9] = E & anyC;
+    for (int i = 0; i < 5; ++i) {
+        pl[10 + i] = E & c1[i];
+        pl[15 + i] = E & c2[i];
+    }
+    u64 h = 0;
+    for (uint32_t p = 0; p < 20; ++p) h += dg_mix((pl[p] & m) ^ dg_mix((((u64)j << 8) | p) + 0x632BE59BD9B4E019ull));
+    return h;
+}
+
+static u64 dg_node(uint32_t psize, const u64 st5[5])
+{
+    u64 h = dg_mix((1ull << 63) | psize);
+    for (int i = 0; i < 5; ++i) h += dg_mix(st5[i] ^ (0x9E3779B97F4A7C15ull * (u64)(i + 1)));
+    return h;
+}
 
 static u64 wmask(const dn_net *d, uint32_t j)
 {
@@ -98,8 +152,27 @@ void *dn_create(uint32_t n, uint32_t R, uint64_t seed, uint32_t epoch)
     d->src = (uint32_t *)calloc(n, 4);
     d->rank = (uint32_t *)calloc(n, 4);
     d->inj = (u64 *)calloc((size_t)n * d->W, 8);
-    if (!d->S[0] || !d->S[1] || !d->st || !d->tg || !d->off || !d->src || !d->rank || !d->inj) abort();
+    d->fl = (uint8_t *)calloc(n, 1);
+    d->pend = (u64 *)calloc((size_t)n * 2 * d->W, 8);
+    d->offc = (uint32_t *)calloc(n, 4);
+    if (!d->S[0] || !d->S[1] || !d->st || !d->tg || !d->off || !d->src || !d->rank || !d->inj || !d->fl ||
+        !d->pend || !d->offc)
+        abort();
     return d;
+}
+
+/* Harness faults from the next round on (thresholds over 2^32, or_fault). */
+void dn_set_faults(void *h, uint32_t churn, uint32_t drop_push, uint32_t drop_pull)
+{
+    dn_net *d = (dn_net *)h;
+    d->f_churn = churn;
+    d->f_push = drop_push;
+    d->f_pull = drop_pull;
+}
+
+static int dn_offline(const dn_net *d, uint32_t round, uint32_t x)
+{
+    return d->f_churn && (or_fault(d->seed, d->epoch, round, x, d->f_churn, 0, 0) & OR_FAULT_OFFLINE);
 }
 
 void dn_destroy(void *h)
@@ -107,7 +180,7 @@ void dn_destroy(void *h)
     dn_net *d = (dn_net *)h;
     if (!d) return;
     free(d->S[0]); free(d->S[1]); free(d->st); free(d->tg); free(d->off);
-    free(d->src); free(d->rank); free(d->inj);
+    free(d->src); free(d->rank); free(d->inj); free(d->fl); free(d->pend); free(d->offc);
     free(d);
 }
 
@@ -117,18 +190,34 @@ void dn_send_new(void *h, uint32_t node, uint32_t rumor)
     d->inj[(size_t)node * d->W + rumor / 64] |= 1ull << (rumor % 64);
 }
 
-/* Targets of `round` and their in-lists (stable counting sort: pushers of a
- * node in ascending order), with every source's rank at its target. */
+/* Targets of `round`, the delivery flags of every edge (the oracle's
+ * edge_alive and pull drop), and the in-lists of the delivered edges (stable
+ * counting sort: pushers of a node in ascending order), with every delivered
+ * source's rank at its target. */
 static void build_lists(dn_net *d)
 {
     const uint32_t n = d->n;
+    const int faults = (d->f_churn | d->f_push | d->f_pull) != 0;
     #pragma omp parallel for schedule(static)
-    for (uint32_t x = 0; x < n; ++x) d->tg[x] = or_peer(d->seed, d->epoch, d->round, x, n);
+    for (uint32_t x = 0; x < n; ++x) {
+        const uint32_t t = or_peer(d->seed, d->epoch, d->round, x, n);
+        uint8_t f = 0;
+        if (faults) {
+            const uint32_t fx = or_fault(d->seed, d->epoch, d->round, x, d->f_churn, d->f_push, d->f_pull);
+            if (fx & OR_FAULT_OFFLINE) f = DN_DEAD | DN_NOPULL | DN_OFF;
+            else if ((fx & OR_FAULT_PUSH) || dn_offline(d, d->round, t)) f = DN_DEAD | DN_NOPULL;
+            else if (fx & OR_FAULT_PULL) f = DN_NOPULL;
+        }
+        d->tg[x] = t;
+        d->fl[x] = f;
+    }
     memset(d->off, 0, ((size_t)n + 1) * 4);
     memset(d->rank, 0, (size_t)n * 4);
-    for (uint32_t x = 0; x < n; ++x) d->off[d->tg[x] + 1]++;
+    for (uint32_t x = 0; x < n; ++x)
+        if (!(d->fl[x] & DN_DEAD)) d->off[d->tg[x] + 1]++;
     for (uint32_t y = 0; y < n; ++y) d->off[y + 1] += d->off[y];
     for (uint32_t x = 0; x < n; ++x) {
+        if (d->fl[x] & DN_DEAD) continue;
         const uint32_t y = d->tg[x];
         const uint32_t pos = d->off[y] + d->rank[y];  /* rank[] doubles as a cursor */
         d->src[pos] = x;
@@ -140,8 +229,10 @@ static void build_lists(dn_net *d)
 }
 
 /* Deliveries of the pending round at x and (transition) phase 0 of the next
- * round, or (observe) the u16 state codes after the deliveries. */
-static int process_node(dn_net *d, uint32_t x, int transition, uint16_t *codes, u64 *stout)
+ * round, or (observe) the u16 state codes / record summaries after the
+ * deliveries (NULL: not written) and the node's digest (dg: NULL = none). */
+static int process_node(dn_net *d, uint32_t x, int transition, uint16_t *codes, u64 *stout, uint16_t *recs,
+                        u64 *dg)
 {
     const uint32_t W = d->W;
     const u64 *S = d->S[d->cur];
@@ -151,11 +242,16 @@ static int process_node(dn_net *d, uint32_t x, int transition, uint16_t *codes, 
     const uint32_t k = deliver ? d->off[x + 1] - d->off[x] : 0;
     const uint32_t *ins = d->src + (deliver ? d->off[x] : 0);
     const uint32_t z = d->tg[x];
-    const uint32_t r = deliver ? d->rank[x] : 0;
-    const uint32_t *ahead = d->src + (deliver ? d->off[z] : 0);
+    const uint8_t fl = deliver ? d->fl[x] : 0;
+    const int pulled = deliver && !(fl & DN_NOPULL);  /* t(x) answered x and the batch is delivered */
+    const int pending_votes = deliver && (fl & DN_OFF);  /* back from offline: its kept votes */
+    const int on_next = !dn_offline(d, d->round + 1, x);
+    const uint32_t r = pulled ? d->rank[x] : 0;
+    const uint32_t *ahead = d->src + (pulled ? d->off[z] : 0);
     int zin = 0;
     for (uint32_t i = 0; i < k; ++i) zin |= ins[i] == z;
-    const uint32_t psize = deliver ? k + (zin ? 0u : 1u) : 0u;
+    const uint32_t psize = deliver ? k + ((pulled && !zin) ? 1u : 0u) : 0u;
+    u64 dgs = 0;
     uint32_t lc = 0, part_cw = 0, recv = 0, first_create = 0xffffffffu, live_new = 0;
     for (uint32_t j = 0; j < W; ++j) {
         const u64 m = wmask(d, j);
@@ -178,14 +274,14 @@ static int process_node(dn_net *d, uint32_t x, int transition, uint16_t *codes, 
             const u64 qc = Q[0], q0 = Q[W], q1 = Q[2 * W];
             const u64 vC = qc & ~(q0 & q1), vB = ~qc & (q0 | q1), v2 = vB & q1 & ~q0, sl = vB | vC;
             const u64 newc = notyet & sl;
-            if (ins[i] != z) RECORD(recB & sl, vB, v2, vC);
+            if (!(pulled && ins[i] == z)) RECORD(recB & sl, vB, v2, vC);  /* superseded by the pull copy */
             crB |= newc & ~vC; crC |= newc & vC; recB |= newc & ~vC; oc1r |= newc & ~vC; notyet &= ~newc;
             const uint32_t pc = (uint32_t)popc(newc);
             part_cw += (k - 1 - i) * pc;
             if (pc && first_create > i) first_create = i;
             recv += (uint32_t)popc(sl);
         }
-        if (deliver) {  /* the pull batch from z: its live set + what it created ahead of x */
+        if (pulled) {  /* the pull batch from z: its live set + what it created ahead of x */
             const u64 *Z = S + (size_t)z * PLANES * W + j;
             const u64 zc = Z[0], z0 = Z[W], z1 = Z[2 * W];
             const u64 zB = ~zc & (z0 | z1), zC = zc & ~(z0 & z1);
@@ -203,9 +299,12 @@ static int process_node(dn_net *d, uint32_t x, int transition, uint16_t *codes, 
             recv += (uint32_t)popc(pl);
         }
 #undef RECORD
-        if (!transition) {  /* observation: codes after the deliveries */
+        if (dg) dgs += dg_word(j, m, B, C, D, crB, crC, a0, a1, P + 3, anyC, c1, c2);
+        if (!transition && !codes && !recs) continue;
+        if (!transition) {  /* observation: codes and records after the deliveries */
             for (uint32_t b = 0; b < 64 && 64 * j + b < d->R; ++b) {
                 const u64 bit = 1ull << b;
+                const uint32_t rr = 64 * j + b;
                 uint32_t bf = 0, af = (uint32_t)((a0 >> b) & 1u) | ((uint32_t)((a1 >> b) & 1u) << 1);
                 for (int i = 0; i < 5; ++i) bf |= (uint32_t)((P[3 + i] >> b) & 1u) << i;
                 uint16_t code = 0;
@@ -214,7 +313,17 @@ static int process_node(dn_net *d, uint32_t x, int transition, uint16_t *codes, 
                 else if (B & bit) code = (uint16_t)((1u << 14) | (af << 7) | bf);
                 else if (C & bit) code = (uint16_t)((2u << 14) | (af << 7) | bf);
                 else if (D & bit) code = (uint16_t)(3u << 14);
-                codes[(size_t)x * d->R + 64 * j + b] = code;
+                uint16_t rec = 0;
+                if ((B | crB) & bit) {  /* anyC << 15 | #counters == 2 << 7 | #counters in [1, cmax) */
+                    uint32_t v1 = 0, v2 = 0;
+                    for (int i = 0; i < 5; ++i) {
+                        v1 |= (uint32_t)((c1[i] >> b) & 1u) << i;
+                        v2 |= (uint32_t)((c2[i] >> b) & 1u) << i;
+                    }
+                    rec = (uint16_t)((((anyC >> b) & 1u) << 15) | (v2 << 7) | v1);
+                }
+                if (codes) codes[(size_t)x * d->R + rr] = code;
+                if (recs) recs[(size_t)x * d->R + rr] = rec;
             }
             continue;
         }
@@ -223,8 +332,9 @@ static int process_node(dn_net *d, uint32_t x, int transition, uint16_t *codes, 
         const u64 Bold = B & ninj, Cold = C & ninj, Dold = D & ninj, cB = crB & ninj, cC = crC & ninj;
         const u64 Bf = Bold | cB | inj, Cf = Cold | cC;
         const u64 oc1 = (Bold & a0 & ~a1) | cB | inj, oc2 = Bold & a1 & ~a0;
-        const u64 bump = ge_k(cv, 5, psize / 2 + 1) & (Bold | cB);
-        const u64 anyCe = anyC & ninj;
+        u64 *pv = d->pend + (size_t)x * 2 * W + j;
+        const u64 bump = pending_votes ? (pv[0] & Bold) : (ge_k(cv, 5, psize / 2 + 1) & (Bold | cB));
+        const u64 anyCe = pending_votes ? (pv[W] & ninj) : (anyC & ninj);
         u64 nr[6], carry = ~0ull;
         for (int i = 0; i < 5; ++i) {
             const u64 rb = P[3 + i] & Bold;
@@ -251,6 +361,18 @@ static int process_node(dn_net *d, uint32_t x, int transition, uint16_t *codes, 
         const u64 CD = Cf & CtoD, CC = Cf & ~CtoD;
         const u64 Dn = BD | CD | Dold, Cn = BC | CC, Bn = BB;
         u64 *Nx = N + (size_t)x * PLANES * W + j;
+        if (!on_next) {
+            /* the harness skips x's next_round: pre-transition state (entries
+             * the deliveries created folded in as B{0,1} / C{0,0}, injections
+             * applied) and the votes the skipped next_round would have taken */
+            Nx[0] = ((isC & ninj) | cC) & m;
+            Nx[W] = ((a0 & ninj) | cB | inj) & m;
+            Nx[2 * W] = (a1 & ninj) & m;
+            for (int i = 0; i < 5; ++i) Nx[(size_t)(3 + i) * W] = P[3 + i] & ninj & m;
+            pv[0] = bump;
+            pv[W] = anyCe & (Bold | cB);
+            continue;
+        }
         Nx[0] = (Cn | Dn) & m;
         Nx[W] = ((Bn & oc1n) | (CC & dd[0]) | Dn) & m;
         Nx[2 * W] = ((Bn & oc2n) | (CC & dd[1]) | Dn) & m;
@@ -263,28 +385,35 @@ static int process_node(dn_net *d, uint32_t x, int transition, uint16_t *codes, 
         if (k > 0 && lc == 0) d_empty = first_create == 0xffffffffu ? k : first_create + 1;
     }
     u64 *st = d->st + (size_t)x * 4;
-    if (!transition) {
-        stout[0] = d->round;
-        stout[1] = st[0] + d_empty;
-        stout[2] = st[1];
-        stout[3] = st[2] + d_full;
-        stout[4] = st[3] + recv;
-        return 0;
+    if (!transition || dg) {  /* the observed Statistics (before this transition's updates) */
+        u64 o[5];
+        o[0] = d->round - d->offc[x];  /* next_round calls */
+        o[1] = st[0] + d_empty;
+        o[2] = st[1];
+        o[3] = st[2] + d_full;
+        o[4] = st[3] + recv;
+        if (stout) memcpy(stout, o, sizeof(o));
+        if (dg) *dg = dgs + dg_node(psize, o);
+        if (!transition) return (int)psize;
     }
     st[0] += d_empty;
-    st[1] += live_new == 0;
+    st[1] += on_next && live_new == 0;
     st[2] += live_new + d_full;
     st[3] += recv;
+    if (!on_next) d->offc[x] += 1;
     return live_new > 0;
 }
 
-/* One harness round for every node (2P); returns NoPeers as the oracle does. */
-int dn_next_round(void *h, uint32_t *any_live)
+/* One harness round for every node (2P); returns NoPeers as the oracle does.
+ * digest (n u64, or NULL): the dn_digest of the state before this call (the
+ * pending round's deliveries applied, no transition), computed on the way:
+ * the transition applies the same deliveries. */
+int dn_next_round_digest(void *h, uint32_t *any_live, uint64_t *digest)
 {
     dn_net *d = (dn_net *)h;
     int live = 0;
     #pragma omp parallel for schedule(static, 256) reduction(| : live)
-    for (uint32_t x = 0; x < d->n; ++x) live |= process_node(d, x, 1, NULL, NULL);
+    for (uint32_t x = 0; x < d->n; ++x) live |= process_node(d, x, 1, NULL, NULL, NULL, digest ? digest + x : NULL);
     memset(d->inj, 0, (size_t)d->n * d->W * 8);
     d->cur ^= 1;
     d->round += 1;
@@ -294,10 +423,31 @@ int dn_next_round(void *h, uint32_t *any_live)
     return 0;
 }
 
+int dn_next_round(void *h, uint32_t *any_live) { return dn_next_round_digest(h, any_live, NULL); }
+
 /* Observers after the last round's deliveries (oracle formats). */
 void dn_dump_state(void *h, uint16_t *codes, uint64_t *stats /* n*5 */)
 {
     dn_net *d = (dn_net *)h;
     #pragma omp parallel for schedule(static, 256)
-    for (uint32_t x = 0; x < d->n; ++x) process_node(d, x, 0, codes, stats + (size_t)x * 5);
+    for (uint32_t x = 0; x < d->n; ++x) process_node(d, x, 0, codes, stats + (size_t)x * 5, NULL, NULL);
+}
+
+/* Record summaries and |peers_in_this_round| (gs_dump_records' formats). */
+void dn_dump_records(void *h, uint16_t *recs /* n*R */, uint32_t *psize /* n */)
+{
+    dn_net *d = (dn_net *)h;
+    #pragma omp parallel for schedule(static, 256)
+    for (uint32_t x = 0; x < d->n; ++x) {
+        const int ps = process_node(d, x, 0, NULL, NULL, recs, NULL);
+        if (psize) psize[x] = (uint32_t)ps;
+    }
+}
+
+/* The per-node digest of gs_state_digest (n u64). */
+void dn_digest(void *h, uint64_t *out)
+{
+    dn_net *d = (dn_net *)h;
+    #pragma omp parallel for schedule(static, 256)
+    for (uint32_t x = 0; x < d->n; ++x) process_node(d, x, 0, NULL, NULL, NULL, out + x);
 }

@@ -131,6 +131,11 @@ void     dn_destroy(void *d);
 void     dn_send_new(void *d, uint32_t node, uint32_t rumor);
 int      dn_next_round(void *d, uint32_t *any_live);
 void     dn_dump_state(void *d, uint16_t *codes /* n*R */, uint64_t *stats /* n*5 */);
+void     dn_dump_records(void *d, uint16_t *recs /* n*R */, uint32_t *psize /* n */);
+void     dn_set_faults(void *d, uint32_t churn, uint32_t drop_push, uint32_t drop_pull);
+void     dn_digest(void *d, uint64_t *out /* n */);
+/* dn_next_round, also writing the dn_digest of the state before it (NULL: none). */
+int      dn_next_round_digest(void *d, uint32_t *any_live, uint64_t *digest /* n */);
 int      dn_threads(void);
 
 #ifdef __cplusplus

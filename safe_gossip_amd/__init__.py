@@ -127,6 +127,7 @@ SYMBOLS = {
     "gs_push_batch_signed": (ctypes.c_int, [_P, ctypes.c_uint32, _U8P, _U8P, ctypes.c_uint32, _U32P, _U32P]),
     "gs_dump_state": (ctypes.c_int, [_P, _U16P]),
     "gs_dump_records": (ctypes.c_int, [_P, _U16P, _U32P]),
+    "gs_state_digest": (ctypes.c_int, [_P, _U64P]),
     "gs_clear": (ctypes.c_int, [_P, ctypes.c_uint32]),
     "gs_sync": (ctypes.c_int, [_P]),
     "gs_round": (ctypes.c_uint32, [_P]),
@@ -613,6 +614,13 @@ class Network:
         _check(self._lib.gs_dump_records(self._h, rec.ctypes.data_as(_U16P),
                                          ps.ctypes.data_as(_U32P)))
         return rec, ps
+
+    def state_digest(self) -> np.ndarray:
+        """Per-node u64 digest of state codes, records, |P| and Statistics
+        (``gs_state_digest``; oracle/gs_dense.c computes the same)."""
+        out = np.zeros(self.n, dtype=np.uint64)
+        _check(self._lib.gs_state_digest(self._h, out.ctypes.data_as(_U64P)))
+        return out
 
     def clear(self, epoch: Optional[int] = None) -> None:
         """``Gossiper::clear`` for every node (src/gossiper.rs:111-115)."""

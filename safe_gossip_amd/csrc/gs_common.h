@@ -210,4 +210,49 @@ struct alignas(16) DlvRec {
 };
 static_assert(sizeof(DlvRec) == 16, "one delivery record is 16 bytes");
 
+// State digest (gs_state_digest; oracle/gs_dense.c and tests/oracle_lib.py
+// digest_of compute the same): per node, the sum mod 2^64 of
+//   * per 64-rumor word j < ceil(R/64), one term per bit-plane p of the 20
+//     bit-planes of what gs_dump_state and gs_dump_records report for those
+//     rumors (state code bits 14, 15, 7, 8, 0..4, then record bits 15,
+//     0..4, 7..11; bit b of plane p = that bit of rumor 64j + b);
+//   * one term for |peers_in_this_round| and one per Statistics counter.
+// Order-free, so the lanes holding the words of a node add their terms.
+__host__ __device__ inline u64 digest_mix(u64 z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__host__ __device__ inline u64 digest_plane(uint32_t j, uint32_t p, u64 w) {
+    return digest_mix(w ^ digest_mix((((u64)j << 8) | p) + 0x632BE59BD9B4E019ull));
+}
+// The 20 observation planes of word j (m: its valid rumor bits) from the
+// post-delivery bit-sliced state: entries in A/B/C/D before the deliveries
+// (B, C, D; a0, a1 and the five b planes bp), the entries the deliveries
+// created (crB: B{0,1}, crC: C{0,0}), and the record counters of B entries
+// (anyC; c1: #counters in [1, counter_max); c2: #counters == 2).
+__host__ __device__ inline u64 digest_word(uint32_t j, u64 m, u64 B, u64 C, u64 D, u64 crB, u64 crC, u64 a0,
+                                           u64 a1, const u64 *bp, u64 anyC, const u64 *c1, const u64 *c2) {
+    const u64 BC = B | C, E = B | crB;
+    u64 pl[20];
+    pl[0] = crB | B | D;          // code bit 14 (tag 1 or 3)
+    pl[1] = crC | C | D;          // code bit 15 (tag 2 or 3)
+    pl[2] = crB | (BC & a0);      // code bit 7 (f2 bit 0; a created B has our_counter 1)
+    pl[3] = BC & a1;              // code bit 8
+    for (int i = 0; i < 5; ++i) pl[4 + i] = BC & bp[i];  // code bits 0..4 (f1)
+    pl[9] = E & anyC;             // record bit 15
+    for (int i = 0; i < 5; ++i) {
+        pl[10 + i] = E & c1[i];   // record bits 0..4
+        pl[15 + i] = E & c2[i];   // record bits 7..11
+    }
+    u64 h = 0;
+    for (uint32_t p = 0; p < 20; ++p) h += digest_plane(j, p, pl[p] & m);
+    return h;
+}
+__host__ __device__ inline u64 digest_node(uint32_t psize, const u64 *st5) {
+    u64 h = digest_mix((1ull << 63) | psize);
+    for (int i = 0; i < 5; ++i) h += digest_mix(st5[i] ^ (0x9E3779B97F4A7C15ull * (u64)(i + 1)));
+    return h;
+}
+
 }  // namespace gs

@@ -44,17 +44,23 @@ GS_DEV T ge_seg(const T (&x)[NB], const T (&km)[NB]) {
     return ~b;
 }
 
-// FUSE: the launch also runs the next build's first partition (a.cp_e set)
-template <int MODE, typename T, uint32_t kNpl, bool FUSE>
+// FUSE: the launch also runs the next build's first partition (a.cp_e set).
+// SH: a code-row shard engine (gs_shard.hip, ShardPlan::codes): the pull code
+// x received is read from exchange B at x's slot (spos_cur) instead of
+// PULL[x], and its next push code goes to its exchange-A slot (spos_next)
+// instead of PC[x]; blocks [blk_off, blk_off + grid) (a pipeline part).
+template <int MODE, typename T, uint32_t kNpl, bool FUSE, bool SH = false>
 __global__ __launch_bounds__(kDlv4Threads, (kNpl == 2 && sizeof(T) == 4 && !FUSE) ? GS_DLV4_MINW_R16 : GS_DLV4_MINW)
 void round_kernel_dlv4(RoundArgs a) {
+    static_assert(!(FUSE && SH), "shards build their in-lists from the exchanged ids");
     constexpr bool DELIVER = MODE == 1;
     const Geometry &g = a.g;
     if (a.zero_buf || a.zero_rows) zero_for_build(a.zero_buf, a.zero_words, a.zero_rows);
     if (a.zero_buf2) zero_for_build(a.zero_buf2, a.zero_words2, nullptr);
     const uint32_t n_nodes = g.n;
     const uint32_t rp = g.rpad, lr = g.logr, lognpu = g.lognpu;  // rp <= 16: npu >= 4
-    const uint32_t lane = blockIdx.x * kDlv4Threads + threadIdx.x;
+    const uint32_t bid = blockIdx.x + a.blk_off;
+    const uint32_t lane = bid * kDlv4Threads + threadIdx.x;
     const uint32_t x0 = lane * kNpl;
     const uint32_t nv = x0 < n_nodes ? min(kNpl, n_nodes - x0) : 0u;  // valid nodes of the lane
     const T m1 = (1ull << rp) - 1ull;
@@ -73,7 +79,7 @@ void round_kernel_dlv4(RoundArgs a) {
     // ---- own round-t planes, staged through LDS (16-byte coalesced loads)
     __shared__ __attribute__((aligned(16))) u64 stage[kDlv4Threads * kNpl * kPlanes / 4];  // >= 8 words per unit
     const uint32_t units_blk = (kDlv4Threads * kNpl) >> lognpu;
-    const u64 unit0 = (u64)blockIdx.x * units_blk;
+    const u64 unit0 = (u64)bid * units_blk;
     const uint32_t blk_units = (uint32_t)min((u64)units_blk, g.units - min(g.units, unit0));
     const uint32_t blk_v4 = blk_units * (kPlanes / 2u);
     {
@@ -96,7 +102,26 @@ void round_kernel_dlv4(RoundArgs a) {
     uint32_t kk[kNpl], dzi[kNpl], dfirst[kNpl], c0[kNpl], c1[kNpl], tgw[kNpl], dp[kNpl];
 #pragma unroll
     for (uint32_t q = 0; q < kNpl; ++q) kk[q] = dzi[q] = dfirst[q] = c0[q] = c1[q] = tgw[q] = dp[q] = 0u;
-    if (DELIVER) {
+    if (DELIVER && SH) {
+        // the pull code at x's exchange-B slot (none: x's push was not
+        // delivered, so no pull either; kTgNoPull masks it below)
+        const uint32_t *rB = reinterpret_cast<const uint32_t *>(a.recvB);
+        uint32_t sp[kNpl];
+        if (kNpl == 2 && nv == kNpl) {
+            const uint2 t2 = *reinterpret_cast<const uint2 *>(a.tg + x0);
+            const uint2 s2 = *reinterpret_cast<const uint2 *>(a.spos_cur + x0);
+            tgw[0] = t2.x; tgw[1] = t2.y;
+            sp[0] = s2.x; sp[kNpl > 1 ? 1 : 0] = s2.y;
+        } else {
+#pragma unroll
+            for (uint32_t q = 0; q < kNpl; ++q) {
+                tgw[q] = q < nv ? a.tg[x0 + q] : 0u;
+                sp[q] = q < nv ? a.spos_cur[x0 + q] : 0xFFFFFFFFu;
+            }
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kNpl; ++q) dp[q] = sp[q] != 0xFFFFFFFFu ? rB[sp[q]] : 0u;
+    } else if (DELIVER) {
         if (kNpl == 4 && nv == kNpl) {
             const uint4 t4 = *reinterpret_cast<const uint4 *>(a.tg + x0);
             const uint4 p4 = *reinterpret_cast<const uint4 *>(a.pull + x0);
@@ -115,6 +140,8 @@ void round_kernel_dlv4(RoundArgs a) {
                     dp[q] = a.pull[x0 + q];
                 }
         }
+    }
+    if (DELIVER) {
 #pragma unroll
         for (uint32_t q = 0; q < kNpl; ++q) {
             const DlvRec r = a.DR[q < nv ? x0 + q : 0u];  // node 0: a harmless valid address
@@ -370,6 +397,15 @@ void round_kernel_dlv4(RoundArgs a) {
             pc[q] = (uint32_t)((b0 >> (q * rp)) & m1) | ((uint32_t)((b1 >> (q * rp)) & m1) << 16);
         if (FUSE) {
             // (not stored)
+        } else if (SH) {
+            // exchange A of round t+1: to owner(t_{t+1}(x)) (no slot: an
+            // undelivered edge, or a capacity overflow, flagged by the plan)
+            uint32_t *sA = reinterpret_cast<uint32_t *>(a.sendA);
+#pragma unroll
+            for (uint32_t q = 0; q < kNpl; ++q) {
+                const uint32_t sp = q < nv ? a.spos_next[x0 + q] : 0xFFFFFFFFu;
+                if (sp != 0xFFFFFFFFu) sA[sp] = pc[q];
+            }
         } else if (kNpl == 4 && nv == kNpl) {
             *reinterpret_cast<uint4 *>(a.pc_out + x0) =
                 make_uint4(pc[0], pc[1], pc[kNpl > 2 ? 2 : 0], pc[kNpl > 3 ? 3 : 0]);
@@ -416,7 +452,7 @@ void round_kernel_dlv4(RoundArgs a) {
     }
 
     // ---- any-live flag of round t+1, Statistics (src/gossip.rs:80,103-111)
-    if (blockIdx.x == 0 && threadIdx.x == 0)  // slot of round t, read by the host already
+    if (bid == 0 && threadIdx.x == 0)  // slot of round t, read by the host already
         __hip_atomic_store(&a.flags[(a.round_new + 1u) & 1u], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 0 && blk_any) {
         uint32_t *f = &a.flags[a.round_new & 1u];
@@ -519,11 +555,18 @@ void round_kernel_dlv4(RoundArgs a) {
 template <typename T, uint32_t NPL>
 static hipError_t launch_dlv4_t(const RoundArgs &a, int mode, hipStream_t s) {
     const u64 lanes = ((u64)a.g.n + NPL - 1) / NPL;
-    const u64 grid = (lanes + kDlv4Threads - 1) / kDlv4Threads;
+    const u64 nblk = (lanes + kDlv4Threads - 1) / kDlv4Threads;
+    const u64 grid = a.blk_count ? a.blk_count : nblk;
     if (grid == 0) return hipSuccess;
-    if (a.cp_e && (a.cp_nc == 0 || a.cp_nc > 64 || a.cp_shards == 0 || !a.tg_out)) return hipErrorInvalidValue;
+    if (a.blk_off + grid > nblk) return hipErrorInvalidValue;
+    if (a.cp_e && (a.cp_nc == 0 || a.cp_nc > 64 || a.cp_shards == 0 || !a.tg_out || a.recvA))
+        return hipErrorInvalidValue;
     const dim3 gd((uint32_t)grid), bd(kDlv4Threads);
-    if (a.cp_e) {
+    if (a.recvA) {  // code-row shard
+        if (!a.sp.codes || !a.recvB || !a.sendA || !a.spos_cur || !a.spos_next) return hipErrorInvalidValue;
+        if (mode == 0) hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL, false, true>), gd, bd, 0, s, a);
+        else hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, false, true>), gd, bd, 0, s, a);
+    } else if (a.cp_e) {
         if (mode == 0) hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL, true>), gd, bd, 0, s, a);
         else hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, true>), gd, bd, 0, s, a);
     } else {

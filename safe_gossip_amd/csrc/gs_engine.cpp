@@ -128,6 +128,11 @@ struct gs_engine {
     hipEvent_t ev_main = nullptr;                          // engine stream position (cstream waits)
     u64 *sendA[2] = {nullptr, nullptr}, *recvA[2] = {nullptr, nullptr};
     u64 *sendB = nullptr, *recvB = nullptr;
+    // code-row shards (dlv && shard: R_pad <= 16, 2P): round t's delivery
+    // records and tail codes, written by the pull kernel after exchange A
+    // (gs_shard.hip pull_codes), read by the packed round kernel
+    gs::DlvRec *sDR = nullptr;
+    uint32_t *sdtail = nullptr;
     uint32_t pulled_round = 0;  // round whose gs_shard_pull ran (its plan of t+2 is launched)
     // Pipeline parts of the round in progress (gs_shard_round_part): parts
     // [0, parts_done) are launched with the arguments `ra` (mode ra_mode).
@@ -168,6 +173,7 @@ struct gs_engine {
     u64 *obs_known = nullptr, *obs_stats = nullptr, *partials = nullptr;
     uint16_t *obs_state = nullptr, *obs_rec = nullptr;
     uint32_t *obs_psize = nullptr;
+    u64 *obs_digest = nullptr;
     u64 *obs_pend = nullptr;       // queued send_new (node << 32 | rumor) shown to observers
     uint32_t obs_pend_cap = 0;
     bool obs_valid = false;
@@ -254,8 +260,8 @@ void release(gs_engine *e) {
     for (int i = 0; i < 2; ++i)
         if (e->ev_dens[i]) (void)hipEventDestroy(e->ev_dens[i]);
     if (e->dens_host) (void)hipHostFree(e->dens_host);
-    void *bufs[] = {e->lvm, e->cpm, e->rows_dev, e->zb[0], e->zb[1], e->lb[0], e->lb[1], e->ab[0], e->ab[1], e->acct, e->dens, e->pc, e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
-                    e->partials, e->obs_state, e->obs_rec, e->obs_psize, e->obs_pend, e->ext_dev,
+    void *bufs[] = {e->lvm, e->cpm, e->rows_dev, e->zb[0], e->zb[1], e->lb[0], e->lb[1], e->ab[0], e->ab[1], e->acct, e->dens, e->pc, e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->sDR, e->sdtail, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
+                    e->partials, e->obs_state, e->obs_rec, e->obs_psize, e->obs_digest, e->obs_pend, e->ext_dev,
                     e->node_state};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -365,7 +371,12 @@ gs::RoundArgs base_args(gs_engine *e) {
         a.recvA = e->recvA[t % 2];
         a.recvB = e->recvB;
         a.sendA = e->sendA[(t + 1) % 2];
-        a.sp = gs::ShardRows{e->sp.G, e->sp.P, e->sp.W, e->sp.capP, e->sp.flagrows, e->sp.blk, e->sp.idrows};
+        a.sp = gs::ShardRows{e->sp.G,    e->sp.P,      e->sp.W,  e->sp.capP,  e->sp.flagrows,
+                             e->sp.blk,  e->sp.idrows, e->sp.rw, e->sp.codes};
+        if (e->dlv) {  // code rows: delivery records of the pull kernel
+            a.DR = e->sDR;
+            a.dtail = e->sdtail;
+        }
     } else {
         const auto &cs = e->csr[e->round & 1u];  // round-t lists (t = e->round)
         a.IN8 = cs.IN8;
@@ -514,14 +525,15 @@ gs_status seq_prepare(gs_engine *e) {
 }
 
 // Fill the observation buffers with the state after the last delivery.
-gs_status observe(gs_engine *e, bool dumps) {
-    if (e->obs_valid && !dumps) return GS_OK;
+gs_status observe(gs_engine *e, bool dumps, bool digest = false) {
+    if (e->obs_valid && !dumps && !digest) return GS_OK;
     if (e->slice && !e->eb[3]) return GS_ERR_INVALID_ARGUMENT;  // gs_slice_bind first
     if (e->slice && e->eb_defer >= 0) {  // a deferred reduced buffer: add it now
         GS_HIP(gs::launch_slice_apply(e->st32, e->eb[e->eb_defer], e->g.n, e->stream));
         e->eb_defer = -1;
     }
     gs_status st = ensure_obs(e, dumps);
+    if (st == GS_OK && digest && !e->obs_digest && dalloc(&e->obs_digest, e->g.n) != hipSuccess) st = GS_ERR_HIP;
     if (st == GS_OK && e->deliver_pending) st = upload_ext(e);
     if (st != GS_OK) return st;
     gs::RoundArgs a = base_args(e);
@@ -532,12 +544,23 @@ gs_status observe(gs_engine *e, bool dumps) {
         a.obs_state = e->obs_state;
         a.obs_rec = e->obs_rec;
     }
+    if (digest) a.obs_digest = e->obs_digest;
     if (e->slice) a.emin = e->eb[3];  // pending empty pulls of this slice
     if (e->deliver_pending) {
         if (e->shard) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_edges[e->round % 2], 0));
         else if (built_elsewhere(e)) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
         st = seq_prepare(e);
         if (st != GS_OK) return st;
+    }
+    if (e->shard && e->dlv) {
+        // code rows: the observation runs the per-node DLV kernel over the
+        // pull codes unpacked into node order (the delivery records are the
+        // pull kernel's)
+        if (e->deliver_pending)
+            GS_HIP(gs::launch_shard_pull_unpack(a.spos_cur, reinterpret_cast<const uint32_t *>(e->recvB), e->pc,
+                                                e->g.n, e->stream));
+        a.recvA = nullptr;
+        a.pull = e->pc;
     }
     GS_HIP(gs::launch_round(a, e->deliver_pending ? 2 : 3, e->stream));
     if (!e->pending.empty()) {
@@ -644,7 +667,12 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         // changes the layout)
         const char *v = std::getenv("SAFE_GOSSIP_AMD_SHARD_FLAGS");
         const bool flags = v && *v == '1';
-        sp = gs::shard_plan(nglob, world, rank, R >= 64 ? (next_pow2(R) / 64) : 1u, parts, flags);
+        // code rows (one u32 push / pull code per row, delivery records and
+        // the packed DLV round kernel) at R_pad <= 16 in the 2P schedule;
+        // SAFE_GOSSIP_AMD_NO_DLV=1 keeps class rows (every rank must agree)
+        const char *nd = std::getenv("SAFE_GOSSIP_AMD_NO_DLV");
+        const bool codes = !(nd && *nd && *nd != '0') && next_pow2(R) <= 16 && cfg->schedule == GS_SCHED_2P;
+        sp = gs::shard_plan(nglob, world, rank, R >= 64 ? (next_pow2(R) / 64) : 1u, parts, flags, codes);
     }
     const uint32_t n = world ? sp.m : nglob;  // nodes owned by this engine
     uint8_t p[3];
@@ -707,7 +735,8 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         // build.  SAFE_GOSSIP_AMD_NO_DLV=1 forces gathers.
         const char *v = std::getenv("SAFE_GOSSIP_AMD_NO_DLV");
         const bool off = v && *v && *v != '0';
-        e->dlv = !off && !e->seq && !e->shard && g.small && g.rpad <= 16 && gs::dlv_plan(n).binned;
+        e->dlv = e->shard ? e->sp.codes != 0
+                          : !off && !e->seq && g.small && g.rpad <= 16 && gs::dlv_plan(n).binned;
     }
     {
         const char *v = std::getenv("SAFE_GOSSIP_AMD_DLV_PACK");
@@ -795,6 +824,8 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
              dalloc(&e->edgew[i], words) == hipSuccess;
     }
     if (ok && e->shard) ok = hipEventCreateWithFlags(&e->ev_main, hipEventDisableTiming) == hipSuccess;
+    if (ok && e->shard && e->dlv)
+        ok = dalloc(&e->sDR, n) == hipSuccess && dalloc(&e->sdtail, gs::shard_slotsA(e->sp)) == hipSuccess;
     const gs::InListSizes isz = gs::inlist_sizes(e->plan);
     // per-node arrays the pipelined round kernel reads by whole 64-node tiles
     const size_t npad = gs::pipe_padded(n);
@@ -893,7 +924,9 @@ gs_status gs_shard_create_parts(const gs_config *cfg, uint32_t rank, uint32_t wo
 
 gs_status gs_shard_info(const gs_engine *e, uint32_t info[12]) {
     if (!e || !info || !e->shard) return GS_ERR_INVALID_ARGUMENT;
-    const uint32_t wa = 2 * e->g.W;  // u64 words per row (2-plane class code)
+    // u32 words per row: the 2-plane class code (2W u64 = 4W u32), or one u32
+    // push / pull code (code rows, R_pad <= 16)
+    const uint32_t wa = e->sp.rw;
     info[0] = e->sp.lo;
     info[1] = e->sp.m;
     info[2] = e->sp.blk;  // rows per rank sub-block of a part: capP row slots + flag rows
@@ -956,6 +989,8 @@ gs_status gs_shard_pull(gs_engine *e) {
     a.sendB = e->sendB;
     a.P = e->sp;
     a.g = e->g;
+    a.DR = e->sDR;
+    a.dtail = e->sdtail;
     GS_HIP(gs::launch_pull(a, e->stream));
     return GS_OK;
 }
@@ -1193,11 +1228,20 @@ gs_status round_begin(gs_engine *e) {
     return GS_OK;
 }
 
+// Nodes per lane of the packed DLV round kernel (gs_dlv4.hip launch_round_dlv4).
+uint32_t dlv_nodes_per_lane(const gs_engine *e) {
+    if (e->g.rpad < 16) return 4u;
+    return e->dlv_pack == 2 ? 4u : (e->dlv_pack == 3 ? 1u : 2u);
+}
+
 gs_status launch_part(gs_engine *e, uint32_t h) {
     gs::RoundArgs a = e->ra;
     if (e->shard && e->sp.P > 1) {  // blocks of part h (blk_count 0 would mean the whole grid)
-        const u64 nblk = (e->g.nseg + 255) / 256;
-        const u64 per = e->g.small ? (u64)e->sp.bP : (u64)e->sp.mP * e->g.W / 256;
+        // (code rows: the packed DLV kernel's blocks of 256 lanes of npl
+        // nodes; parts are whole 1024-node blocks, gs_shard.hip shard_plan)
+        const u64 bn = e->dlv ? 256ull * dlv_nodes_per_lane(e) : 256ull;
+        const u64 nblk = e->dlv ? ((u64)e->g.n + bn - 1) / bn : (e->g.nseg + 255) / 256;
+        const u64 per = e->dlv ? (u64)e->sp.mP / bn : e->g.small ? (u64)e->sp.bP : (u64)e->sp.mP * e->g.W / 256;
         const u64 b0 = std::min<u64>((u64)h * per, nblk), b1 = std::min<u64>(b0 + per, nblk);
         if (b1 == b0) return GS_OK;
         a.blk_off = (uint32_t)b0;
@@ -1484,6 +1528,16 @@ gs_status gs_dump_state(gs_engine *e, uint16_t *out) {
     return GS_OK;
 }
 
+gs_status gs_state_digest(gs_engine *e, uint64_t *out) {
+    if (!e || !out) return GS_ERR_INVALID_ARGUMENT;
+    if (!e->pending.empty()) return GS_ERR_INVALID_ARGUMENT;  // queued send_new: observe before injecting
+    gs_status st = set_device(e);
+    if (st == GS_OK) st = observe(e, false, true);
+    if (st != GS_OK) return st;
+    GS_HIP(hipMemcpy(out, e->obs_digest, (size_t)e->g.n * sizeof(u64), hipMemcpyDeviceToHost));
+    return GS_OK;
+}
+
 gs_status gs_dump_records(gs_engine *e, uint16_t *rec, uint32_t *psize) {
     if (!e || !rec) return GS_ERR_INVALID_ARGUMENT;
     gs_status st = set_device(e);
@@ -1767,12 +1821,21 @@ double gs_round_kernel_bytes(const gs_engine *e) {
     // DLV path: per slot 1 B planes read + 1 B written; per node its delivery
     // record 16 + its pull batch 4 + target word 4 + Statistics deltas 16 r +
     // 16 w + the next round's push code 4.
+    // Code-row shards: the same, with the pull code read at x's exchange-B
+    // slot (slot 4 + code 4 B) and the push code written to its exchange-A
+    // slot (slot 4 + code 4): 68 B per node.
+    if (e->dlv && e->shard) return n * (2.0 * rp + 68.0);
     if (e->dlv) return n * (2.0 * rp + 60.0);
     return n * (2.75 * rp + 68.0);
 }
 
 const char *gs_round_kernel_name(const gs_engine *e) {
     if (!e) return "";
+    if (e->shard && e->dlv) {
+        if (e->g.rpad < 16) return "round_kernel_dlv4<1,u32,4,SHARD>";
+        return e->dlv_pack == 2 ? "round_kernel_dlv4<1,u64,4,SHARD>"
+                                : (e->dlv_pack == 3 ? "round_kernel_dlv4<1,u32,1,SHARD>" : "round_kernel_dlv4<1,u32,2,SHARD>");
+    }
     if (e->shard) return e->g.small ? "round_kernel<true,1,SHARD>" : "round_kernel<false,1,SHARD>";
     if (e->seq) return e->g.small ? "round_kernel<true,1,SEQ>" : "round_kernel<false,1,SEQ>";
     if (e->dlv) {

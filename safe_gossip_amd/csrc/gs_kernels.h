@@ -7,7 +7,7 @@ namespace gs {
 // The exchange layout a round kernel needs (ShardPlan's fields of the same
 // names; the slot helpers below take either).
 struct ShardRows {
-    uint32_t G, P, W, capP, flagrows, blk, idrows;
+    uint32_t G, P, W, capP, flagrows, blk, idrows, rw, codes;
 };
 
 struct RoundArgs {
@@ -45,6 +45,7 @@ struct RoundArgs {
     uint16_t *obs_state;      // [n][R]
     uint16_t *obs_rec;        // [n][R]
     uint32_t *obs_psize;      // [n]
+    u64 *obs_digest;          // [n] state digest (gs_common.h digest_*)
     // shard engine only (null otherwise): exchange rows, see gs_shard.hip
     const u64 *recvA;         // round-t push rows of this shard's pushers [slot][2][W]
     const u64 *recvB;         // round-t pull rows for this shard's nodes [slot][2][W]
@@ -152,7 +153,9 @@ constexpr uint32_t kPipeTileNodes = 64;
 inline uint64_t pipe_padded(uint64_t n) { return (n + kPipeTileNodes - 1) / kPipeTileNodes * kPipeTileNodes; }
 hipError_t launch_round_pipe(const RoundArgs &a, int mode, hipStream_t s);
 // The 2P gather path with a 32-bit lane word (gs_w32.hip): modes 0 and 1,
-// R_pad 64..256, live-filtered gathers, no external RPCs, the whole grid.
+// R_pad 32 (a lane per node; the engine's default there) or 64..256 (half a
+// 64-rumor word per lane; only when SAFE_GOSSIP_AMD_W32=1 forces it),
+// live-filtered gathers, no external RPCs, the whole grid.
 bool w32_eligible(const RoundArgs &a, int mode);
 hipError_t launch_round_w32(const RoundArgs &a, int mode, hipStream_t s);
 
@@ -291,6 +294,11 @@ struct ShardPlan {
     // slower); flagrows = 0 when off or W > 8.  blk = capP + flagrows.
     uint32_t flagrows, blk;
     uint32_t idrows;    // rows of u32 ids per block of the last part of A (P*capP ids)
+    // Row format: u32 words per row.  Class rows (R_pad >= 32, or the gather
+    // shards): the 2-plane class code as 2W u64 words, rw = 4W.  Code rows
+    // (codes = 1: delivery-record shards, R_pad <= 16, 2P): the push / pull
+    // code itself, one u32 (b0 | b1 << 16, gs_common.h DlvRec), rw = 1.
+    uint32_t rw, codes;
     CsrPlan edges;      // counting sort of the A receive slots over the m targets
 };
 // Row slot of (rank block s, part h, index i) in an exchange-A / -B buffer.
@@ -356,7 +364,10 @@ struct ShardPlanLayout {
 struct ShardEdgeLayout {
     size_t E_id, E_key, M, tot, base, EP, IN, IN2, pairs;
 };
-ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t parts, bool row_flags = true);
+// codes: one u32 code per row (delivery-record shards; no row flags), and
+// parts of whole 1024-node blocks (the packed DLV round kernel's blocks)
+ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t parts, bool row_flags = true,
+                     bool codes = false);
 size_t shard_plan_words(const ShardPlan &P, ShardPlanLayout *L);
 size_t shard_edge_words(const ShardPlan &P, ShardEdgeLayout *L);
 // Plan of `round`: owned targets, send slots, and the ids of every block of
@@ -371,6 +382,11 @@ hipError_t launch_shard_edges(const ShardPlan &P, const ShardEdgeLayout &L, uint
 
 struct PullArgs {
     const u64 *S;          // round-t planes of the owned nodes
+    // code rows (P.codes): the delivery records of round t for the packed
+    // DLV round kernel (DR[z] with the pushers' codes; pushers >= 2 at
+    // dtail[DR[z].first + i - 2])
+    DlvRec *DR;
+    uint32_t *dtail;
     const uint4 *IN;       // round-t in-lists of receive slots
     const uint32_t *IN2;   // their third pushers
     const uint32_t *EP;
@@ -380,6 +396,10 @@ struct PullArgs {
     Geometry g;            // local geometry (n = m)
 };
 hipError_t launch_pull(const PullArgs &a, hipStream_t s);
+// Code-row shards, observers: pull[x] = the pull code x received in round t
+// (recvB at x's exchange-B slot spos[x]; 0 without one).
+hipError_t launch_shard_pull_unpack(const uint32_t *spos, const uint32_t *recvB, uint32_t *pull, uint32_t m,
+                                    hipStream_t s);
 
 // ---------------------------------------------------------------- signatures
 // gs_verify.hip: SHA3-512 and ed25519 over SHA3-512, one item per lane;

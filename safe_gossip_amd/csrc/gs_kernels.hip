@@ -704,18 +704,31 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         const u64 known = (~A | crB | crC) & L.m;
         if (a.obs_known && (SMALL || L.j < KW)) a.obs_known[(u64)x * KW + L.j] = known;
         if (leader) {
-            if (a.obs_stats) {
+            if (a.obs_stats || a.obs_digest) {
                 const uint4 d32 = reinterpret_cast<const uint4 *>(a.st32)[x];
                 const u64 *b64 = a.st64 + (u64)x * 4;
-                u64 *o = a.obs_stats + (u64)x * 5;
+                u64 o[5];
                 o[0] = a.obs_rounds - (a.offc ? a.offc[x] : 0u);  // next_round calls
                 if (a.emin) a.emin[x] = (uint8_t)min(d_empty_pull, 255u);  // slice: reduced by the caller
                 o[1] = b64[0] + d32.x + (a.emin ? 0u : d_empty_pull);
                 o[2] = b64[1] + d32.y;
                 o[3] = b64[2] + d32.z + d_full_sent;
                 o[4] = b64[3] + d32.w + d_recv;
+                if (a.obs_stats)
+                    for (int i = 0; i < 5; ++i) a.obs_stats[(u64)x * 5 + i] = o[i];
+                if (a.obs_digest) a.obs_digest[x] = digest_node(psize, o);  // + the rumor terms below
             }
             if (a.obs_psize) a.obs_psize[x] = psize;
+        }
+        if (a.obs_digest) {
+            // this lane's word (words past ceil(R/64) hold no rumor: no term);
+            // the node's lanes add their terms (W adjacent lanes), the leader
+            // wrote the node terms above
+            const uint32_t jw = SMALL ? 0u : L.j;
+            u64 dg = 64u * jw < g.R ? digest_word(jw, L.m, B, C, D, crB, crC, a0, a1, &P[3], anyC, rv.c1, rv.c2) : 0ull;
+            if (!SMALL)
+                for (uint32_t o = 1; o < g.W; o <<= 1) dg += __shfl_xor(dg, (int)o, 64);
+            if (leader) a.obs_digest[x] += dg;
         }
         if (a.obs_state || a.obs_rec) {
             const uint32_t nb = SMALL ? g.rpad : 64u;
@@ -1005,8 +1018,12 @@ static hipError_t launch_mode(const RoundArgs &a, int mode, hipStream_t s) {
 }
 
 hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s) {
-    if (a.recvA)  // shard engine (2P only)
+    if (a.recvA) {  // shard engine (2P only)
+        // code rows: the packed DLV round kernel for transitions; observers
+        // read the unpacked pull codes on the DLV path (gs_engine.cpp observe)
+        if (a.sp.codes) return (mode == 0 || mode == 1) ? launch_round_dlv4(a, mode, s) : hipErrorInvalidValue;
         return a.g.small ? launch_mode<true, true, false>(a, mode, s) : launch_mode<false, true, false>(a, mode, s);
+    }
     if (a.Wb)     // SEQ schedule
         return a.g.small ? launch_mode<true, false, true>(a, mode, s) : launch_mode<false, false, true>(a, mode, s);
     if (a.DR) {   // delivery records (2P, R_pad <= 16)

@@ -57,10 +57,10 @@ GS_DEV uint32_t dest_rank(const ShardPlan &P, uint32_t t) {
 // capP row slots and the flag rows of d's sub-block of the last part (P*capP ids; the id of
 // next round's source (part h, index i) at h*capP + i).
 GS_DEV uint32_t *id_slots(const ShardPlan &P, u64 *bufA, uint32_t d) {
-    return reinterpret_cast<uint32_t *>(bufA + (u64)shard_a_slot(P, d, P.P - 1u, P.blk) * (2u * P.W));
+    return reinterpret_cast<uint32_t *>(bufA) + (u64)shard_a_slot(P, d, P.P - 1u, P.blk) * P.rw;
 }
 GS_DEV const uint32_t *id_slots(const ShardPlan &P, const u64 *bufA, uint32_t d) {
-    return reinterpret_cast<const uint32_t *>(bufA + (u64)shard_a_slot(P, d, P.P - 1u, P.blk) * (2u * P.W));
+    return reinterpret_cast<const uint32_t *>(bufA) + (u64)shard_a_slot(P, d, P.P - 1u, P.blk) * P.rw;
 }
 
 __global__ __launch_bounds__(kPlanBlock) void plan_count(ShardPlan P, uint64_t seed, uint32_t epoch,
@@ -331,8 +331,11 @@ __global__ __launch_bounds__(256) void edge_bin_sort(const u64 *__restrict__ pai
     }
 }
 
-ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t parts, bool row_flags) {
+ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t parts, bool row_flags,
+                     bool codes) {
     ShardPlan P{};
+    P.codes = codes ? 1u : 0u;
+    P.rw = codes ? 1u : 4u * W;
     P.n = n;
     P.G = G;
     P.g = g;
@@ -346,18 +349,21 @@ ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t pa
     P.m = (uint32_t)(hi - lo);
     P.nblk_own = (uint32_t)(((u64)P.m + kPlanBlock - 1) / kPlanBlock);
     P.P = std::max<uint32_t>(1, std::min(parts, kMaxParts));
-    const u64 mp = ((chunk + P.P - 1) / P.P + kPlanBlock - 1) / kPlanBlock * kPlanBlock;
+    // (code rows: parts of whole 1024-node blocks, the packed DLV round
+    // kernel's blocks at <= 4 nodes per lane)
+    const u64 align = codes ? 1024u : kPlanBlock;
+    const u64 mp = ((chunk + P.P - 1) / P.P + align - 1) / align * align;
     P.mP = (uint32_t)mp;
     P.bP = (uint32_t)(mp / kPlanBlock);
     // rows from one part of one rank to one rank: ~Binomial(mP, chunk/(n-1));
     // 16 standard deviations (the same on every rank: equal exchange splits)
     const double mean = (double)mp * (double)chunk / std::max(1.0, (double)n - 1.0);
     double capd = std::min<double>((double)mp, mean + 16.0 * std::sqrt(mean + 1.0) + 64.0);
-    const u64 q = std::max<u64>(64, 4ull * W);  // P*capP u32 ids fill whole rows of 2W words
+    const u64 q = std::max<u64>(64, P.rw);  // P*capP u32 ids fill whole rows of rw u32 words
     P.capP = (uint32_t)(((u64)std::ceil(capd) + q - 1) / q * q);
-    P.idrows = P.P * P.capP / (4u * W);
+    P.idrows = P.P * P.capP / P.rw;
     // a flag byte per row slot (bit j: row word j), capP bytes in rows of 16W
-    P.flagrows = (row_flags && W <= 8u) ? (P.capP + 16u * W - 1u) / (16u * W) : 0u;
+    P.flagrows = (row_flags && !codes && W <= 8u) ? (P.capP + 16u * W - 1u) / (16u * W) : 0u;
     P.blk = P.capP + P.flagrows;
     // counting sort of the receive slots of A over the m local targets
     CsrPlan &c = P.edges;
@@ -504,9 +510,83 @@ __global__ __launch_bounds__(256) void pull_kernel(PullArgs a) {
     }
 }
 
+// ------------------------------------------------ code rows (R_pad <= 16)
+// The same response half at z over one-u32 rows (ShardPlan::codes): a push
+// row is the pusher's push code, a pull row the code of the batch z returns
+// (b0 | b1 << 16: 01 counter 1, 10 counter 2, 11 counter 255).  On the way z's
+// delivery record of round t is written for the packed round kernel
+// (gs_dlv4.hip), the input the single-GPU DLV build produces
+// (gs_inlist.hip inl_sort_dlv): the pushers' codes in ascending source order
+// (the receive slots' order), and t(z)'s index among them
+// (src/message_state.rs:79: its pull copy supersedes its push copy).
+__global__ __launch_bounds__(256) void pull_codes(PullArgs a) {
+    const uint32_t z = blockIdx.x * 256u + threadIdx.x;
+    if (z >= a.g.n) return;
+    const uint32_t *__restrict__ rA = reinterpret_cast<const uint32_t *>(a.recvA);
+    uint32_t *sB = reinterpret_cast<uint32_t *>(a.sendB);
+    const uint4 in = a.IN[z];
+    const uint32_t e2 = a.IN2[z];
+    const uint32_t k = in.y & 0xFFFFu, zi = in.y >> 16;
+    // z's class planes: its R_pad-bit segment lies in one 32-bit half of its
+    // unit word (R_pad <= 16), planes 0..2 at words 0, 2, 4 of the unit
+    const uint32_t sh = (z & ((1u << a.g.lognpu) - 1u)) << a.g.logr;
+    const u64 wb = (u64)(z >> a.g.lognpu) * kPlanes * 2u + (sh >> 5);
+    const uint32_t *S32 = reinterpret_cast<const uint32_t *>(a.S);
+    const uint32_t w0 = S32[wb], w1 = S32[wb + 2], w2 = S32[wb + 4];
+    uint32_t c[3];
+    c[0] = k > 0 ? rA[in.z] : 0u;
+    c[1] = k > 1 ? rA[in.w] : 0u;
+    c[2] = k > 2 ? rA[e2] : 0u;
+    const uint32_t m = (uint32_t)((1ull << a.g.rpad) - 1ull), s5 = sh & 31u;
+    const uint32_t cz = (w0 >> s5) & m, a0 = (w1 >> s5) & m, a1 = (w2 >> s5) & m;
+    const uint32_t zB = ~cz & (a0 | a1), zC = cz & ~(a0 & a1);
+    const uint32_t zB1 = zB & a0 & ~a1, zB2 = zB & a1 & ~a0;
+    uint32_t pnot = ~cz & ~a0 & ~a1 & m, pB = 0u, pC = 0u;
+    for (uint32_t i = 0; i < k; ++i) {
+        const uint32_t e = i == 0 ? in.z : (i == 1 ? in.w : (i == 2 ? e2 : a.EP[in.x + i]));
+        const uint32_t code = i < 3u ? c[i] : rA[e];
+        if (i >= kDlvInline) a.dtail[in.x + i - kDlvInline] = code;
+        const uint32_t pcl = zC | pC;
+        const SlotPos q = shard_a_decode(a.P, e);
+        sB[shard_b_slot(a.P, q.s, q.h, q.i)] = ((zB1 | pB | pcl) & 0xFFFFu) | ((zB2 | pcl) << 16);
+        const uint32_t b0 = code & 0xFFFFu, b1 = code >> 16;
+        const uint32_t vC = b0 & b1, sl = b0 | b1;  // the pusher's batch; C carries 255
+        const uint32_t nw = pnot & sl;
+        pB |= nw & ~vC;
+        pC |= nw & vC;
+        pnot &= ~sl;
+    }
+    DlvRec r;
+    r.meta = k | ((zi == 0xFFFFu ? kDlvNoZ : zi) << 5);
+    r.first = in.x;  // pusher i >= 2 at dtail[in.x + i - 2]
+    r.c[0] = c[0];
+    r.c[1] = c[1];
+    a.DR[z] = r;
+}
+
+__global__ __launch_bounds__(256) void pull_unpack(const uint32_t *__restrict__ spos, const uint32_t *__restrict__ recvB,
+                                                   uint32_t *pull, uint32_t m) {
+    const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+    if (x >= m) return;
+    const uint32_t sp = spos[x];
+    pull[x] = sp != kNoId ? recvB[sp] : 0u;
+}
+
+hipError_t launch_shard_pull_unpack(const uint32_t *spos, const uint32_t *recvB, uint32_t *pull, uint32_t m,
+                                    hipStream_t s) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(pull_unpack, dim3((m + 255u) / 256u), dim3(256), 0, s, spos, recvB, pull, m);
+    return hipGetLastError();
+}
+
 hipError_t launch_pull(const PullArgs &a, hipStream_t s) {
     const u64 grid = (a.g.nseg + 255) / 256;
     if (grid == 0) return hipSuccess;
+    if (a.P.codes) {
+        if (!a.g.small || a.g.rpad > 16 || !a.DR || !a.dtail) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(pull_codes, dim3((uint32_t)grid), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
     if (a.g.small) hipLaunchKernelGGL(pull_kernel<true>, dim3((uint32_t)grid), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(pull_kernel<false>, dim3((uint32_t)grid), dim3(256), 0, s, a);
     return hipGetLastError();

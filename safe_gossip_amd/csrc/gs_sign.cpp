@@ -73,12 +73,22 @@ std::vector<std::pair<uint32_t, uint32_t>> split_frames(const uint8_t *buf, uint
     return f;
 }
 
+// Bytes of the signed form of unsigned frames ("u32 length + RPC") totalling
+// `unsigned_len` over `count` frames: each becomes "u32 length + Message
+// wrapper" (u64 length, RPC, u64 64, 64 signature bytes).
+uint32_t signed_size(uint32_t unsigned_len, uint32_t count) { return unsigned_len + count * (8u + 8u + 64u); }
+
 // Replaces every frame of `frames` (RPC bytes) with its signed Message
-// wrapper, signed for `seed` on `device`; output frames in `out`.
+// wrapper, signed for `seed` on `device`; output frames in `out`.  The size
+// is checked before anything is signed (a size query signs nothing).
 gs_status sign_frames(int device, const uint8_t seed[32], const std::vector<uint8_t> &frames, uint8_t *out,
                       uint32_t cap, uint32_t *out_len) {
     const auto f = split_frames(frames.data(), (uint32_t)frames.size());
     const uint32_t n = (uint32_t)f.size();
+    const uint32_t need = signed_size((uint32_t)frames.size(), n);
+    *out_len = need;
+    if (!out || cap < need) return GS_ERR_SERIALISATION;
+    if (!n) return GS_OK;
     std::vector<uint8_t> seeds(32ull * n);
     std::vector<uint32_t> off(n), len(n);
     for (uint32_t i = 0; i < n; ++i) {
@@ -90,10 +100,6 @@ gs_status sign_frames(int device, const uint8_t seed[32], const std::vector<uint
     gs_status st = gs_ed25519_sign(device, n, seeds.data(), frames.data(), off.data(), len.data(), pub.data(),
                                    sig.data());
     if (st != GS_OK) return st;
-    uint32_t need = 0;
-    for (uint32_t i = 0; i < n; ++i) need += 4 + 8 + len[i] + 8 + 64;
-    *out_len = need;
-    if (!out || cap < need) return GS_ERR_SERIALISATION;
     uint32_t at = 0;
     for (uint32_t i = 0; i < n; ++i) {
         uint32_t w = 0;
@@ -193,16 +199,29 @@ gs_status gs_handle_received_signed(gs_engine *e, uint32_t node, uint32_t peer, 
     if (!ok) return GS_ERR_SIG_FAILURE;  // Error::SigFailure: the frame is dropped, nothing applied
     if (!node_seed) return gs_handle_received(e, node, peer, msg + po, pl, out, cap, out_len, out_count);
     // the Pull responses, signed by the node (Gossiper::prepare_to_send,
-    // src/gossiper.rs:117-127); the unsigned frames are sized first
+    // src/gossiper.rs:117-127).  A size query first: with no room for its
+    // responses gs_handle_received applies nothing and reports their unsigned
+    // size and count, so the signed size is checked against `cap` before the
+    // RPC is applied (nothing applied when it does not fit; call again).  An
+    // RPC without responses (a Pull, or a peer already heard from this round)
+    // is applied by the query itself, with nothing to sign.
     uint32_t need = 0, cnt = 0;
-    std::vector<uint8_t> frames(256);
-    for (;;) {
-        st = gs_handle_received(e, node, peer, msg + po, pl, frames.data(), (uint32_t)frames.size(), &need, &cnt);
-        if (st != GS_ERR_SERIALISATION || need <= frames.size()) break;
-        frames.resize(need);  // nothing was applied; call again with room
+    st = gs_handle_received(e, node, peer, msg + po, pl, nullptr, 0, &need, &cnt);
+    if (st == GS_OK) {
+        *out_count = cnt;
+        *out_len = need;
+        return GS_OK;
     }
+    if (st != GS_ERR_SERIALISATION) return st;
+    if (!out || cap < signed_size(need, cnt)) {
+        *out_len = signed_size(need, cnt);
+        return GS_ERR_SERIALISATION;
+    }
+    std::vector<uint8_t> frames(need);
+    uint32_t got = 0;
+    st = gs_handle_received(e, node, peer, msg + po, pl, frames.data(), need, &got, &cnt);
     if (st != GS_OK) return st;
-    frames.resize(need);
+    frames.resize(got);
     *out_count = cnt;
     return sign_frames(gs_device(e), node_seed, frames, out, cap, out_len);
 }

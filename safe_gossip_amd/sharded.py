@@ -69,19 +69,21 @@ class _Shard:
         (self.lo, self.m, self.capP, self.idrows, self.wa, self.world, self.rank, self.chunk,
          self.parts, self.mP, self.rowsA, self.rowsB) = list(info)
         dev = torch.device("cuda", device)
-        i64 = torch.int64
+        # rows of wa u32 words: the 2-plane class code (4W words), or one u32
+        # push / pull code at R_pad <= 16 (code rows)
+        i32 = torch.int32
         # exchange A: two buffer sets (round parity); B: one
-        self.sendA = [torch.zeros(self.rowsA * self.wa, dtype=i64, device=dev) for _ in range(2)]
-        self.recvA = [torch.zeros(self.rowsA * self.wa, dtype=i64, device=dev) for _ in range(2)]
-        self.sendB = torch.zeros(self.rowsB * self.wa, dtype=i64, device=dev)
-        self.recvB = torch.zeros(self.rowsB * self.wa, dtype=i64, device=dev)
+        self.sendA = [torch.zeros(self.rowsA * self.wa, dtype=i32, device=dev) for _ in range(2)]
+        self.recvA = [torch.zeros(self.rowsA * self.wa, dtype=i32, device=dev) for _ in range(2)]
+        self.sendB = torch.zeros(self.rowsB * self.wa, dtype=i32, device=dev)
+        self.recvB = torch.zeros(self.rowsB * self.wa, dtype=i32, device=dev)
         _check(lib.gs_shard_bind(h, self.sendA[0].data_ptr(), self.sendA[1].data_ptr(),
                                  self.recvA[0].data_ptr(), self.recvA[1].data_ptr(),
                                  self.sendB.data_ptr(), self.recvB.data_ptr()))
         self.stream = torch.cuda.ExternalStream(lib.gs_stream(h), device=dev)
 
     def region(self, which: str, h: int):
-        """Part h of an exchange buffer: (first u64 word, u64 words per rank
+        """Part h of an exchange buffer: (first u32 word, u32 words per rank
         sub-block); the part's world sub-blocks are contiguous."""
         # (info[2] "capP" here = rows per sub-block: row slots + flag rows)
         rows = self.capP + (self.idrows if which == "A" and h == self.parts - 1 else 0)
@@ -144,7 +146,7 @@ class ShardedNetwork:
             self.parts = (1 if self.host_staged else 4) if parts is None else parts
             self.shards = [_Shard(self.lib, cfg, self.rank, world, self.parts, torch, device)]
             s = self.shards[0]
-            biggest = max(world * s.region(which, h)[1] * 8 for which in "AB" for h in range(s.parts))
+            biggest = max(world * s.region(which, h)[1] * 4 for which in "AB" for h in range(s.parts))
             if not self.host_staged and world > 1 and biggest > self.max_collective_bytes:
                 for sh in self.shards:
                     sh.close()
@@ -218,7 +220,7 @@ class ShardedNetwork:
         torch, dist = self.torch, self.dist
         if self.host_staged:  # gloo: rows through host memory, synchronously
             _check(self.lib.gs_sync(s.h))
-            hout = torch.empty(self.world * w, dtype=torch.int64)
+            hout = torch.empty(self.world * w, dtype=torch.int32)
             dist.all_to_all_single(hout, send[span].cpu(), group=self.group)
             recv[span].copy_(hout.to(recv.device))
             torch.cuda.synchronize(self.device)
@@ -232,11 +234,11 @@ class ShardedNetwork:
         # span is its own single block, cut anywhere); with several ranks the
         # parts keep every exchange far below it (constructor check).
         limit = self.max_collective_bytes
-        if self.world * w * 8 <= limit:
+        if self.world * w * 4 <= limit:
             with torch.cuda.stream(s.stream):
                 return dist.all_to_all_single(recv[span], send[span], group=self.group, async_op=True)
         assert self.world == 1, "multi-rank exchange above the RCCL size limit (constructor check)"
-        step = max(1, limit // 8)
+        step = max(1, limit // 4)
         works = []
         with torch.cuda.stream(s.stream):
             for a in range(off, off + w, step):
@@ -393,6 +395,15 @@ class ShardedNetwork:
             return np.concatenate([rec.astype(np.uint32), ps[:, None]], axis=1)
         both = self._gather_rows(self._per_shard(f))
         return both[:, :-1].astype(np.uint16), both[:, -1].astype(np.uint32)
+
+    def state_digest(self) -> np.ndarray:
+        """Per-node digest (gs_state_digest) of the whole network, in node order."""
+        def f(s):
+            out = np.zeros(s.m, dtype=np.uint64)
+            if s.m:
+                _check(self.lib.gs_state_digest(s.h, out.ctypes.data_as(_U64P)))
+            return out[:, None]
+        return self._gather_rows(self._per_shard(f))[:, 0]
 
     def known_counts(self, min_known: Optional[int] = None):
         mk = self.R if min_known is None else min_known

@@ -24,6 +24,12 @@ parts of mP nodes and each part's rows move in an all-to-all of their own
 part, index) order, which is ascending source order, and B answers part by
 part in the same sub-blocks.
 
+Code rows (R_pad <= 16, the engine's ShardPlan::codes): a push row carries
+the pusher's push code and a pull row the pull batch's code, one u32 each
+(b0 | b1 << 16: 01 counter 1, 10 counter 2, 11 counter 255), and parts are
+whole 1024-node blocks; the receiver decodes a code into the class planes the
+algebra reads (a C entry as C{round 0}, "none" as A).
+
 Delivery and transition then use Model's bit-sliced algebra on the received
 rows only, so a rank never reads another rank's state directly.  Faults follow
 Model (flags of every edge derived locally from the Philox stream, like the
@@ -40,17 +46,37 @@ def shard_range(n, G, g):
     return lo, min(lo + chunk, n) - lo, chunk
 
 
-def part_nodes(n, G, parts):
-    """Nodes per pipeline part (shard_plan: whole 256-node plan blocks)."""
+def part_nodes(n, G, parts, codes=False):
+    """Nodes per pipeline part (shard_plan: whole 256-node plan blocks; code
+    rows: whole 1024-node blocks)."""
     chunk = shard_range(n, G, 0)[2]
-    return -(-(-(-chunk // parts)) // 256) * 256
+    align = 1024 if codes else 256
+    return -(-(-(-chunk // parts)) // align) * align
 
 
-def shard_cap(n, G, W=1, parts=1):
+def uses_codes(R):
+    """Code rows at R_pad <= 16 (2P)."""
+    return R <= 16
+
+
+def push_code(qc, q0, q1, M):
+    """Class planes -> the u32 push code (b0 | b1 << 16)."""
+    vC = qc & ~(q0 & q1) & M
+    vB = ~qc & (q0 | q1) & M
+    return ((vB & q0 & ~q1) | vC) | (((vB & q1 & ~q0) | vC) << 16)
+
+
+def decode_code(code):
+    """u32 code -> class planes (gs_kernels.hip decode16)."""
+    b0, b1 = code & 0xFFFF, code >> 16
+    return b0 & b1, b0 & ~b1, b1 & ~b0
+
+
+def shard_cap(n, G, W=1, parts=1, codes=False):
     """Row slots per (source rank, destination rank, part) sub-block (shard_plan)."""
     import math
     chunk = shard_range(n, G, 0)[2]
-    mp = part_nodes(n, G, parts)
+    mp = part_nodes(n, G, parts, codes)
     mean = mp * chunk / max(1.0, n - 1.0)
     cap = min(float(mp), mean + 16.0 * math.sqrt(mean + 1.0) + 64.0)
     q = max(64, 4 * W)
@@ -64,8 +90,9 @@ class ShardModel(Model):
         self.rank, self.world, self.a2a = rank, world, a2a
         self.lo, self.m, self.chunk = shard_range(n, world, rank)
         self.parts = parts
-        self.mP = part_nodes(n, world, parts)
-        self.cap = shard_cap(n, world, parts=parts)
+        self.codes = uses_codes(R)
+        self.mP = part_nodes(n, world, parts, self.codes)
+        self.cap = shard_cap(n, world, parts=parts, codes=self.codes)
         self.tg, self.fl = {}, {}
         self.P = {x: [0] * 8 for x in self.owned()}
         self.stats = {x: [0] * 5 for x in self.owned()}
@@ -91,12 +118,16 @@ class ShardModel(Model):
             sa = [[] for _ in range(G)]
             for x in self.part(h):
                 if not self.fl[x] & DEAD:
-                    sa[self.owner(self.tg[x])].append([x] + list(self.cls(x)))
+                    row = [push_code(*self.cls(x), self.M)] if self.codes else list(self.cls(x))
+                    sa[self.owner(self.tg[x])].append([x] + row)
+            width = 2 if self.codes else 4
             for blk in sa:
                 assert len(blk) <= cap, "block capacity exceeded (the engine flags a device limit)"
-                blk.extend([[-1, 0, 0, 0]] * (cap - len(blk)))
+                blk.extend([[-1] + [0] * (width - 1)] * (cap - len(blk)))
             sendA.append(sa)
-            recvA.append(self.a2a(sa, 4))
+            recvA.append(self.a2a(sa, width))
+            if self.codes:  # the receiver decodes each code into class planes
+                recvA[-1] = [[[r[0]] + list(decode_code(r[1])) for r in blk] for blk in recvA[-1]]
         # pushers in (source rank, part, index) order = ascending source order
         rows = [r for s in range(G) for h in range(P) for r in recvA[h][s] if r[0] >= 0]
         srcs = [r[0] for r in rows]
@@ -112,12 +143,14 @@ class ShardModel(Model):
         for h in range(P):  # B_h answers A_h's rows in the same sub-blocks
             sendB = [[[r[0]] + list(self.pull_row(tgt[r[0]], r[0], ins[tgt[r[0]]]))
                       if r[0] >= 0 else [-1, 0, 0] for r in blk] for blk in recvA[h]]
-            recvB = self.a2a(sendB, 3)
+            if self.codes:  # one u32 code per pull row
+                sendB = [[[r[0], r[1] | (r[2] << 16)] for r in blk] for blk in sendB]
+            recvB = self.a2a(sendB, 2 if self.codes else 3)
             for d in range(G):
                 assert [r[0] for r in recvB[d]] == [r[0] for r in sendA[h][d]], "B order = A order"
-                for x, b0, b1 in recvB[d]:
-                    if x >= 0:
-                        pull[x] = (b0, b1)
+                for r in recvB[d]:
+                    if r[0] >= 0:
+                        pull[r[0]] = (r[1] & 0xFFFF, r[1] >> 16) if self.codes else (r[1], r[2])
         self.ins, self.pull = ins, pull
         self.exchanged = True
 

@@ -77,6 +77,10 @@ _SIGS = {
     "dn_send_new": (None, [_P, ctypes.c_uint32, ctypes.c_uint32]),
     "dn_next_round": (ctypes.c_int, [_P, _U32P]),
     "dn_dump_state": (None, [_P, _U16P, _U64P]),
+    "dn_dump_records": (None, [_P, _U16P, _U32P]),
+    "dn_set_faults": (None, [_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
+    "dn_digest": (None, [_P, _U64P]),
+    "dn_next_round_digest": (ctypes.c_int, [_P, _U32P, _U64P]),
     "dn_threads": (ctypes.c_int, []),
     "or_ms_step": (None, [_U8P, _U32P, _U8P, ctypes.c_uint32, _U32P, ctypes.c_uint32,
                           ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_int]),
@@ -247,13 +251,16 @@ class OracleNet:
 
 
 class DenseNet:
-    """The dense bit-sliced OpenMP CPU program (oracle/gs_dense.c), 2P only."""
+    """The dense bit-sliced OpenMP CPU program (oracle/gs_dense.c), 2P only;
+    faults = (churn, drop_push, drop_pull) thresholds over 2^32."""
 
-    def __init__(self, n, R, seed=0x5AFE6055, epoch=0):
+    def __init__(self, n, R, seed=0x5AFE6055, epoch=0, faults=None):
         self._l = lib()
         self.h = self._l.dn_create(n, R, seed, epoch)
         assert self.h
         self.n, self.R = n, R
+        if faults:
+            self._l.dn_set_faults(self.h, *faults)
 
     def close(self):
         if self.h:
@@ -269,13 +276,60 @@ class DenseNet:
     def send_new(self, node, rumor):
         self._l.dn_send_new(self.h, node, rumor)
 
-    def next_round(self):
+    def next_round(self, digest=False):
+        """One round; with digest=True returns (live, the digest of the state
+        before it), computed in the same pass."""
         live = ctypes.c_uint32()
-        self._l.dn_next_round(self.h, ctypes.byref(live))
-        return bool(live.value)
+        if not digest:
+            self._l.dn_next_round(self.h, ctypes.byref(live))
+            return bool(live.value)
+        out = np.zeros(self.n, dtype=np.uint64)
+        self._l.dn_next_round_digest(self.h, ctypes.byref(live), out.ctypes.data_as(_U64P))
+        return bool(live.value), out
 
     def dump(self):
         codes = np.zeros((self.n, self.R), dtype=np.uint16)
         st = np.zeros((self.n, 5), dtype=np.uint64)
         self._l.dn_dump_state(self.h, codes.ctypes.data_as(_U16P), st.ctypes.data_as(_U64P))
         return codes, st
+
+    def dump_records(self):
+        rec = np.zeros((self.n, self.R), dtype=np.uint16)
+        ps = np.zeros(self.n, dtype=np.uint32)
+        self._l.dn_dump_records(self.h, rec.ctypes.data_as(_U16P), ps.ctypes.data_as(_U32P))
+        return rec, ps
+
+    def digest(self):
+        out = np.zeros(self.n, dtype=np.uint64)
+        self._l.dn_digest(self.h, out.ctypes.data_as(_U64P))
+        return out
+
+
+def digest_of(codes, recs, psize, stats):
+    """The per-node digest (gs_common.h digest_*, oracle/gs_dense.c dn_digest)
+    of parity dumps, in numpy: pins both implementations to one definition."""
+    def mix(z):
+        z = np.asarray(z, dtype=np.uint64)
+        with np.errstate(over="ignore"):
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+    n, R = codes.shape
+    W = (R + 63) // 64
+    # the 20 planes: code bits 14, 15, 7, 8, 0..4, record bits 15, 0..4, 7..11
+    bits = [(codes, 14), (codes, 15), (codes, 7), (codes, 8)] + [(codes, b) for b in range(5)] + \
+        [(recs, 15)] + [(recs, b) for b in range(5)] + [(recs, b) for b in range(7, 12)]
+    weights = np.uint64(1) << np.arange(64, dtype=np.uint64)
+    h = np.zeros(n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        for p, (arr, b) in enumerate(bits):
+            v = ((arr.astype(np.uint64) >> np.uint64(b)) & np.uint64(1))
+            v = np.concatenate([v, np.zeros((n, W * 64 - R), dtype=np.uint64)], axis=1).reshape(n, W, 64)
+            words = (v * weights).sum(axis=2, dtype=np.uint64)  # distinct bits: the sum is the OR
+            for j in range(W):
+                salt = mix(np.uint64(((j << 8) | p) + 0x632BE59BD9B4E019))
+                h = h + mix(words[:, j] ^ salt)
+        h = h + mix(np.uint64(1 << 63) | psize.astype(np.uint64))
+        for i in range(5):
+            h = h + mix(stats[:, i].astype(np.uint64) ^ np.uint64((0x9E3779B97F4A7C15 * (i + 1)) % (1 << 64)))
+    return h

@@ -1,0 +1,130 @@
+"""Full-size configurations bit-exact against a CPU program that is itself
+checked against the oracle: oracle/gs_dense.c (the dense bit-sliced OpenMP
+2P round; tests/test_dense_cpu.py holds it equal to the reference-faithful
+oracle round by round, faults included) runs beside the engine, and every
+round the two are compared node by node through the per-node state digest
+(gs_state_digest: every state code, record summary, |peers_in_this_round| and
+Statistics counter of the node; dn_digest computes the same function), plus
+the any-live flag and the Statistics sums.  Semantics: src/gossip.rs:79-166,
+src/message_state.rs:86-171.
+
+The small cases also pin the GPU digest to its definition (tests/oracle_lib.py
+digest_of over the engine's own dumps)."""
+import numpy as np
+import pytest
+
+import oracle_lib
+from oracle_lib import DenseNet, digest_of
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5AFE6055
+
+
+def _first_bad(a, b):
+    bad = np.flatnonzero(a != b)
+    return None if bad.size == 0 else (int(bad[0]), bad.size)
+
+
+def _run(engine, net, n, R, faults, max_rounds, every=1, epoch=0, dumps=False):
+    """Inject every rumor at its Philox origin, then run both programs round
+    by round; returns the rounds run.  The engine's digest after round t is
+    compared with the one dense's round t+1 computes on the way (the same
+    deliveries, before its transition)."""
+    thr = [engine.fault_threshold(p) for p in faults] if faults else None
+    dn = DenseNet(n, R, seed=SEED, epoch=epoch, faults=thr)
+
+    def check(g, c, rnd):
+        bad = _first_bad(g, c)
+        assert bad is None, f"round {rnd}: {bad[1]} nodes differ, first {bad[0]}"
+    try:
+        for r in range(R):
+            x = engine.origin_of(SEED, epoch, r, n)
+            net.send_new(x, r)
+            dn.send_new(x, r)
+        prev = None
+        for rnd in range(1, max_rounds + 1):
+            rep = net.next_round()
+            if prev is not None:
+                live, before = dn.next_round(digest=True)
+                check(prev, before, rnd - 1)
+            else:
+                live = dn.next_round()
+            assert rep.any_live == live, f"round {rnd}: any_live"
+            prev = None
+            if rnd % every == 0 or not live or rnd == max_rounds:
+                prev = net.state_digest()
+                if dumps:  # the GPU digest is the digest of its own dumps
+                    codes, st = net.dump_state(), net.statistics_all()
+                    rec, ps = net.dump_records()
+                    np.testing.assert_array_equal(prev, digest_of(codes, rec, ps, st))
+            if not live or rnd == max_rounds:
+                check(prev, dn.digest(), rnd)
+                return rnd
+        return max_rounds
+    finally:
+        dn.close()
+
+
+@pytest.mark.parametrize("n,R,faults", [
+    (20000, 256, None),                    # the gather path, W = 4
+    (5000, 16, (0.05, 0.05, 0.05)),        # DLV records, faults
+    (3000, 64, (0.1, 0.1, 0.1)),           # R_pad 64
+    (4000, 5, None),                       # four nodes per DLV lane
+    (777, 20, (0.05, 0.05, 0.05)),         # 32-bit lanes
+])
+def test_digest_small(engine, n, R, faults):
+    net = engine.Network(n, R, seed=SEED, **_fk(faults))
+    try:
+        _run(engine, net, n, R, faults, 60, dumps=True)
+    finally:
+        net.close()
+
+
+def _fk(faults):
+    return dict(churn=faults[0], drop_push=faults[1], drop_pull=faults[2]) if faults else {}
+
+
+def test_config3_to_termination(engine):
+    # config 3: 2^20 x 64, every round until no live push
+    n, R = 1 << 20, 64
+    net = engine.Network(n, R, seed=SEED)
+    try:
+        assert _run(engine, net, n, R, None, 60) < 60
+    finally:
+        net.close()
+
+
+def test_config4_to_termination(engine):
+    # config 4 (the bench line): 2^24 x 256, every round until no live push
+    n, R = 1 << 24, 256
+    net = engine.Network(n, R, seed=SEED)
+    try:
+        assert _run(engine, net, n, R, None, 60) < 60
+    finally:
+        net.close()
+
+
+def test_config5_faults_rounds(engine):
+    # config 5: 10^8 x 16 with 1 % churn / push drop / pull drop, 10 rounds
+    # (the DLV build and the packed round kernel)
+    n, R = 100_000_000, 16
+    faults = (0.01, 0.01, 0.01)
+    net = engine.Network(n, R, seed=SEED, **_fk(faults))
+    try:
+        _run(engine, net, n, R, faults, 10)
+    finally:
+        net.close()
+
+
+def test_config5_code_row_shards(engine):
+    # config 5 over 4 code-row shards on one GPU (device-copy exchanges, 2
+    # pipeline parts each): the multi-GPU layout at full size, 8 rounds
+    from safe_gossip_amd.sharded import ShardedNetwork
+    n, R = 100_000_000, 16
+    faults = (0.01, 0.01, 0.01)
+    net = ShardedNetwork(n, R, 4, seed=SEED, transport="local", parts=2, **_fk(faults))
+    try:
+        _run(engine, net, n, R, faults, 8, every=2)
+    finally:
+        net.close()

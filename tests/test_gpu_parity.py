@@ -473,9 +473,12 @@ def test_parity_pipe(engine, monkeypatch, n, R, kind, faults, grid):
 
 @pytest.mark.parametrize("n,R,filt", [(3000, 256, "1"), (3000, 256, "0"), (2000, 128, "1")])
 def test_parity_round_kernel_wide(engine, monkeypatch, n, R, filt):
-    # the 64-bit lane round_kernel on the wide 2P path (SAFE_GOSSIP_AMD_W32=0;
-    # the default for R_pad 64..256 is round_kernel_w32, which every other
-    # filtered wide test runs), filtered and unfiltered
+    # the 64-bit lane round_kernel on the wide 2P path, filtered and
+    # unfiltered, with the 32-bit lane kernel explicitly off
+    # (SAFE_GOSSIP_AMD_W32=0).  round_kernel is the default at R_pad 64..256
+    # (every other wide 2P test runs it too); round_kernel_w32 is the default
+    # at R_pad 32 only, and runs at R_pad 64..256 where test_parity_w32
+    # forces it (SAFE_GOSSIP_AMD_W32=1)
     monkeypatch.setenv("SAFE_GOSSIP_AMD_PIPE", "0")
     monkeypatch.setenv("SAFE_GOSSIP_AMD_W32", "0")
     monkeypatch.setenv("SAFE_GOSSIP_AMD_FILTER", filt)

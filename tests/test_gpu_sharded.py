@@ -112,3 +112,35 @@ def test_sharded_parity_row_flags(engine, monkeypatch, n, R, kind, faults):
     # receivers and the pull kernel skip rows flagged empty
     monkeypatch.setenv("SAFE_GOSSIP_AMD_SHARD_FLAGS", "1")
     run_parity(engine, n, R, kind, make_net=_maker(3, 2), faults=faults)
+
+
+# Code rows (R_pad <= 16, 2P): one u32 push / pull code per
+# exchange row, the pull kernel writes delivery records, and the packed DLV
+# round kernel (gs_dlv4.hip) runs each part; every R <= 16 case above runs them.
+@pytest.mark.parametrize("world,parts,n,R,kind,faults", [
+    (2, 2, 5000, 16, "origins", None),                # parts of 2048 / 512 nodes
+    (3, 3, 20000, 16, "trickle", (0.05, 0.05, 0.05)),  # 3072 / 3072 / 768 nodes, faults
+    (2, 4, 9000, 5, "reinject", (0.1, 0.1, 0.1)),     # R_pad 8: four nodes per lane
+    (4, 2, 30000, 16, "origins", (0.01, 0.01, 0.01)),  # the config-5 shape
+])
+def test_sharded_code_rows_parts(engine, world, parts, n, R, kind, faults):
+    run_parity(engine, n, R, kind, make_net=_maker(world, parts), faults=faults, check_every=2)
+
+
+@pytest.mark.parametrize("pack", ["u64", "u32x1"])
+def test_sharded_code_rows_packings(engine, monkeypatch, pack):
+    # the other lane packings of the packed kernel on a code-row shard
+    monkeypatch.setenv("SAFE_GOSSIP_AMD_DLV_PACK", pack)
+    run_parity(engine, 5000, 16, "origins", make_net=_maker(3, 2), faults=(0.05, 0.05, 0.05))
+
+
+@pytest.mark.parametrize("n,R,kind,faults", [
+    (97, 16, "origins", None),
+    (1619, 4, "origins", None),
+    (600, 16, "origins", (0.05, 0.05, 0.05)),
+])
+def test_sharded_class_rows_small_r(engine, monkeypatch, n, R, kind, faults):
+    # SAFE_GOSSIP_AMD_NO_DLV=1: class rows and the per-node shard kernel at
+    # R_pad <= 16 (the layout before code rows)
+    monkeypatch.setenv("SAFE_GOSSIP_AMD_NO_DLV", "1")
+    run_parity(engine, n, R, kind, make_net=_maker(3, 2), faults=faults)

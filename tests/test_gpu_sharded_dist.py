@@ -53,7 +53,7 @@ def _worker(rank, world, port, cases, q, backend="gloo", parts=None, env=None):
 def test_sharded_dist_gloo_two_ranks(engine, parts):
     import torch.multiprocessing as mp
     world = 2
-    cases = [(600, 48, "origins"), (1000, 3, "trickle"), (700, 256, "reinject")]
+    cases = [(600, 48, "origins"), (1000, 3, "trickle"), (700, 256, "reinject"), (5000, 16, "origins")]
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
@@ -79,7 +79,7 @@ def test_sharded_dist_rccl_single_rank(engine, parts):
     # (parts 2: the exchanges of one part overlap the other part's round
     # kernel), no host synchronisation per round
     import torch.multiprocessing as mp
-    cases = [(600, 48, "origins"), (700, 256, "reinject"), (1000, 3, "trickle")]
+    cases = [(600, 48, "origins"), (700, 256, "reinject"), (1000, 3, "trickle"), (5000, 16, "origins")]
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     p = ctx.Process(target=_worker, args=(0, 1, _free_port(), cases, q, "nccl", parts))
@@ -98,7 +98,7 @@ def test_sharded_dist_rccl_chunked_exchange(engine):
     # (exp/r3/rccl_size.py): one rank's larger exchange moves in pieces.  The
     # piece limit is lowered to 4 KiB so the chunked path runs at oracle sizes.
     import torch.multiprocessing as mp
-    cases = [(700, 256, "reinject"), (1000, 3, "trickle")]
+    cases = [(700, 256, "reinject"), (1000, 3, "trickle"), (3000, 16, "origins")]
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     p = ctx.Process(target=_worker, args=(0, 1, _free_port(), cases, q, "nccl", 1,

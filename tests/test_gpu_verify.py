@@ -105,3 +105,41 @@ def test_signed_wire_round_trip(engine):
     finally:
         a.close()
         b.close()
+
+
+def test_signed_responses_larger_than_first_buffer(engine):
+    # a node with 128 live rumors answers a first Push with 128 signed Pulls
+    # (~14 KB, more than the wrapper's first 4 KB buffer, while the unsigned
+    # frames, ~3.7 KB, fit it): the RPC must be applied exactly once (the
+    # signed size is checked before anything is applied), so responses,
+    # states and Statistics equal an unsigned twin's
+    rnd = random.Random(14)
+    peer_seed, node_seed = bytes(rnd.randrange(256) for _ in range(32)), bytes(rnd.randrange(256) for _ in range(32))
+    peer_key, node_key = E.public_key(peer_seed), E.public_key(node_seed)
+    nets = [engine.Network(64, 128, seed=SEED) for _ in range(2)]
+    a, b = nets
+    try:
+        for net in nets:
+            for r in range(128):
+                net.send_new(5, r)
+            net.next_round()
+        rpc = engine.rpc_encode(False, a.rumor_key(3), 1)
+        frame = engine.message_wrap(rpc, E.sign(peer_seed, rpc))
+        resp = a.handle_received_signed(5, 300, peer_key, frame, node_seed)
+        want = b.handle_received(5, 300, rpc)
+        assert len(want) == 128 and sum(4 + len(w) for w in want) < 4096
+        assert len(resp) == len(want)
+        for f, w in zip(resp, want):
+            payload, sig = engine.message_unwrap(f)
+            assert payload == w and E.verify(node_key, payload, sig)
+        # a second copy from the same peer: no responses, applied once more on both
+        assert a.handle_received_signed(5, 300, peer_key, frame, node_seed) == b.handle_received(5, 300, rpc) == []
+        np.testing.assert_array_equal(a.statistics_all(), b.statistics_all())
+        a.next_round()
+        b.next_round()
+        np.testing.assert_array_equal(a.dump_state(), b.dump_state())
+        np.testing.assert_array_equal(a.statistics_all(), b.statistics_all())
+        np.testing.assert_array_equal(a.dump_records()[0], b.dump_records()[0])
+    finally:
+        a.close()
+        b.close()

@@ -1,4 +1,5 @@
-"""Sharded protocol on CPU over torch.distributed (gloo, world 2 and 3).
+"""Sharded protocol on CPU over torch.distributed (gloo, world 2 and 3), with
+code rows (R <= 16: one u32 push / pull code per row) and class rows.
 
 Each process is one rank of tests/model_sharded.py: it owns a node range, moves
 push rows to the owners of their targets and pull rows back with
@@ -108,8 +109,11 @@ def _worker(rank, world, port, n, R, params, kind, q, faults=None, parts=1):
     (3, 600, 12, None, "origins", None, 1),      # 256 / 256 / 88
     (2, 600, 16, None, "origins", (0.1, 0.1, 0.1), 1),    # config 5 faults
     (3, 600, 8, None, "reinject", (0.3, 0.2, 0.2), 1),
-    (2, 1100, 16, None, "origins", None, 2),     # pipeline parts of 256 nodes
-    (3, 1600, 8, None, "reinject", (0.1, 0.1, 0.1), 3),
+    (2, 5000, 16, None, "origins", None, 2),     # code rows: pipeline parts of 2048 / 512 nodes
+    (3, 1600, 8, None, "reinject", (0.1, 0.1, 0.1), 3),  # parts of 1024 / 0 nodes
+    (2, 600, 40, None, "origins", None, 1),      # class rows (R_pad 64)
+    (2, 1100, 33, None, "origins", None, 2),     # class rows: pipeline parts of 256 nodes
+    (3, 1600, 20, None, "reinject", (0.1, 0.1, 0.1), 3),
 ])
 def test_sharded_protocol_gloo(oracle, world, n, R, params, kind, faults, parts):
     ctx = mp.get_context("spawn")
