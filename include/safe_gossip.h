@@ -147,10 +147,9 @@ gs_status   gs_dump_state(gs_engine *e, uint16_t *out);
 gs_status   gs_dump_records(gs_engine *e, uint16_t *rec, uint32_t *psize);
 /* A 64-bit digest per node of everything the parity dumps and gs_statistics_all
  * report (n u64, 8 B per node instead of 4R + 44): the sum mod 2^64 of one
- * SplitMix64-finaliser term per (64-rumor word, bit-plane) of the 20 bit
- * planes of the state codes and record summaries, one for psize and one per
- * Statistics counter (exact definition: safe_gossip_amd/csrc/gs_common.h
- * digest_*).  For checking large networks against a CPU program that computes
+ * SplitMix64-finaliser term per 64-rumor word over the 20 bit-planes of its
+ * state codes and record summaries, one for psize and one per Statistics
+ * counter (exact definition: safe_gossip_amd/csrc/gs_common.h digest_*).  For checking large networks against a CPU program that computes
  * the same function (oracle/gs_dense.c dn_digest).  GS_ERR_INVALID_ARGUMENT
  * while send_new calls are queued (call it before injecting). */
 gs_status   gs_state_digest(gs_engine *e, uint64_t *out);
@@ -198,8 +197,15 @@ gs_status   gs_round_traffic(gs_engine *e, double *bytes_per_launch, uint32_t *l
  *           ids of round t+1 for the in-lists, built one round ahead) -- push
  *           rows of round t of the sources in part h;
  *   B_h(t): part h of sendB -> part h of recvB, world sub-blocks of blk rows.
- * A row is `row words` u64.  Sequence per round t >= 1, after round t exists:
- *   [t == 1: A_{P-1}(0) on set 0] -> all A_h(t) -> gs_shard_pull -> B_h(t) ->
+ * A row holds `row words` u32 (info[4] for A, info[12] for B): the 2-plane
+ * class code of the rows' rumors (2W u64 both ways), or at R_pad <= 16 in
+ * the 2P schedule "code rows" (info[13] = 1): an A row is the push code (b0 |
+ * b1 << 16: 01 counter 1, 10 counter 2, 11 counter 255) and the pusher's
+ * target local to the receiving rank, bit 31 set when the pusher is that
+ * target's own target; a B row is the pull code.  Code rows carry no id rows
+ * (idrows = 0): the receiver sorts the arrived rows into delivery records
+ * and runs the packed kernels.  Sequence per round t >= 1, after round t exists:
+ *   [t == 1, class rows: A_{P-1}(0) on set 0] -> all A_h(t) -> gs_shard_pull -> B_h(t) ->
  *   for h < P-1: gs_shard_round_part(h) (needs B_h(t); its rows are A_h(t+1))
  *   -> gs_next_round (the remaining parts: round t+1 exists) -> A_{P-1}(t+1).
  * So A_h(t+1) and B_{h+1}(t) run while the round kernel of another part does.
@@ -212,13 +218,21 @@ gs_status   gs_shard_create(const gs_config *cfg, uint32_t rank, uint32_t world,
 gs_status   gs_shard_create_parts(const gs_config *cfg, uint32_t rank, uint32_t world, uint32_t parts,
                                   gs_engine **out);
 /* info = {lo, m, blk (rows per rank sub-block of a part: row slots + flag
- *         rows), idrows (id rows per sub-block of A's last part), row words,
+ *         rows), idrows (id rows per sub-block of A's last part), A row words
+ *         (u32 words per row: 4W for the class-code rows, 2 for code rows),
  *         world, rank, nodes per rank, parts P, nodes per part mP, rows of an
  *         A buffer (world * (P*blk + idrows)), rows of a B buffer (world * P *
- *         blk)}.  Every rank must see the same SAFE_GOSSIP_AMD_SHARD_FLAGS. */
-gs_status   gs_shard_info(const gs_engine *e, uint32_t info[12]);
-/* Device buffers: sendA[2], recvA[2] (info[10] rows each), sendB, recvB
- * (info[11] rows each). */
+ *         blk), B row words (4W, or 1 for code rows), 1 for code rows}.  Every
+ *         rank must see the same SAFE_GOSSIP_AMD_SHARD_FLAGS and
+ *         SAFE_GOSSIP_AMD_NO_DLV. */
+gs_status   gs_shard_info(const gs_engine *e, uint32_t info[14]);
+/* The same layout without creating an engine (host only, no device needed):
+ * what gs_shard_create_parts(cfg, rank, world, parts) would report, so a
+ * caller can size its exchange buffers and collectives beforehand. */
+gs_status   gs_shard_plan_info(const gs_config *cfg, uint32_t rank, uint32_t world, uint32_t parts,
+                               uint32_t info[14]);
+/* Device buffers: sendA[2], recvA[2] (info[10] rows of info[4] u32 each),
+ * sendB, recvB (info[11] rows of info[12] u32 each). */
 gs_status   gs_shard_bind(gs_engine *e, void *sendA0, void *sendA1, void *recvA0, void *recvA1,
                           void *sendB, void *recvB);
 /* Round kernel of pipeline part `part` of the pending round (parts in order,

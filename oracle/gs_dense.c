@@ -27,9 +27,11 @@
  * (safe_gossip_amd/csrc/gs_common.h digest_*), so networks too large for the
  * oracle are checked node by node against this program.
  */
+#define _DEFAULT_SOURCE
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include "gs_oracle.h"
 
@@ -95,8 +97,8 @@ static u64 dg_word(uint32_t j, u64 m, u64 B, u64 C, u64 D, u64 crB, u64 crC, u64
         pl[15 + i] = E & c2[i];
     }
     u64 h = 0;
-    for (uint32_t p = 0; p < 20; ++p) h += dg_mix((pl[p] & m) ^ dg_mix((((u64)j << 8) | p) + 0x632BE59BD9B4E019ull));
-    return h;
+    for (uint32_t p = 0; p < 20; ++p) h += (pl[p] & m) * (0x9E3779B97F4A7C15ull * (2ull * p + 1ull));
+    return dg_mix(h ^ dg_mix((u64)j + 0x632BE59BD9B4E019ull));
 }
 
 static u64 dg_node(uint32_t psize, const u64 st5[5])
@@ -135,6 +137,22 @@ static u64 ge_k(const u64 *x, int nb, uint32_t K)
     return gt | eq;
 }
 
+/* Zeroed memory for the plane buffers, on transparent huge pages where the
+ * kernel offers them: the round gathers random records across gigabytes, and
+ * with 4 KiB pages nearly every gather is a TLB miss too. */
+static void *big_zeroed(size_t bytes)
+{
+    const size_t align = (size_t)2 << 20;
+    void *p = NULL;
+    bytes = (bytes + align - 1) / align * align;
+    if (posix_memalign(&p, align, bytes) != 0) return NULL;
+#ifdef MADV_HUGEPAGE
+    (void)madvise(p, bytes, MADV_HUGEPAGE);
+#endif
+    memset(p, 0, bytes);
+    return p;
+}
+
 void *dn_create(uint32_t n, uint32_t R, uint64_t seed, uint32_t epoch)
 {
     dn_net *d = (dn_net *)calloc(1, sizeof(dn_net));
@@ -144,8 +162,8 @@ void *dn_create(uint32_t n, uint32_t R, uint64_t seed, uint32_t epoch)
     or_derive_params(n, p);
     d->cmax = p[0]; d->maxc = p[1]; d->maxr = p[2];
     const size_t sw = (size_t)n * PLANES * d->W;
-    d->S[0] = (u64 *)calloc(sw, 8);
-    d->S[1] = (u64 *)calloc(sw, 8);
+    d->S[0] = (u64 *)big_zeroed(sw * 8);
+    d->S[1] = (u64 *)big_zeroed(sw * 8);
     d->st = (u64 *)calloc((size_t)n * 4, 8);
     d->tg = (uint32_t *)calloc(n, 4);
     d->off = (uint32_t *)calloc((size_t)n + 1, 4);
@@ -213,15 +231,37 @@ static void build_lists(dn_net *d)
     }
     memset(d->off, 0, ((size_t)n + 1) * 4);
     memset(d->rank, 0, (size_t)n * 4);
+    /* parallel counting sort: in-degrees, one serial prefix sum, a scatter by
+     * atomic cursors (rank[] doubles as the cursor), then each list sorted
+     * (pushers ascending: the order Gossip::receive sees them) */
+    #pragma omp parallel for schedule(static)
     for (uint32_t x = 0; x < n; ++x)
-        if (!(d->fl[x] & DN_DEAD)) d->off[d->tg[x] + 1]++;
+        if (!(d->fl[x] & DN_DEAD)) {
+            #pragma omp atomic
+            d->off[d->tg[x] + 1]++;
+        }
     for (uint32_t y = 0; y < n; ++y) d->off[y + 1] += d->off[y];
+    #pragma omp parallel for schedule(static)
     for (uint32_t x = 0; x < n; ++x) {
         if (d->fl[x] & DN_DEAD) continue;
         const uint32_t y = d->tg[x];
-        const uint32_t pos = d->off[y] + d->rank[y];  /* rank[] doubles as a cursor */
-        d->src[pos] = x;
-        d->rank[y]++;
+        uint32_t c;
+        #pragma omp atomic capture
+        c = d->rank[y]++;
+        d->src[d->off[y] + c] = x;
+    }
+    #pragma omp parallel for schedule(static)
+    for (uint32_t y = 0; y < n; ++y) {
+        const uint32_t a = d->off[y], e = d->off[y + 1];
+        for (uint32_t i = a + 1; i < e; ++i) {
+            const uint32_t v = d->src[i];
+            uint32_t j = i;
+            while (j > a && d->src[j - 1] > v) {
+                d->src[j] = d->src[j - 1];
+                --j;
+            }
+            d->src[j] = v;
+        }
     }
     #pragma omp parallel for schedule(static)
     for (uint32_t y = 0; y < n; ++y)

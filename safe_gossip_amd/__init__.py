@@ -155,6 +155,7 @@ SYMBOLS = {
                                              ctypes.c_uint32, ctypes.POINTER(_P)]),
     "gs_shard_round_part": (ctypes.c_int, [_P, ctypes.c_uint32]),
     "gs_shard_info": (ctypes.c_int, [_P, _U32P]),
+    "gs_shard_plan_info": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _U32P]),
     "gs_shard_bind": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P]),
     "gs_shard_pull": (ctypes.c_int, [_P]),
     "gs_stream": (ctypes.c_uint64, [_P]),

@@ -212,10 +212,11 @@ static_assert(sizeof(DlvRec) == 16, "one delivery record is 16 bytes");
 
 // State digest (gs_state_digest; oracle/gs_dense.c and tests/oracle_lib.py
 // digest_of compute the same): per node, the sum mod 2^64 of
-//   * per 64-rumor word j < ceil(R/64), one term per bit-plane p of the 20
-//     bit-planes of what gs_dump_state and gs_dump_records report for those
-//     rumors (state code bits 14, 15, 7, 8, 0..4, then record bits 15,
-//     0..4, 7..11; bit b of plane p = that bit of rumor 64j + b);
+//   * per 64-rumor word j < ceil(R/64), one term mixing the 20 bit-planes
+//     of what gs_dump_state and gs_dump_records report for those rumors
+//     (state code bits 14, 15, 7, 8, 0..4, then record bits 15, 0..4,
+//     7..11; bit b of plane p = that bit of rumor 64j + b): mix(sum_p
+//     plane_p * K_p ^ mix(j + C));
 //   * one term for |peers_in_this_round| and one per Statistics counter.
 // Order-free, so the lanes holding the words of a node add their terms.
 __host__ __device__ inline u64 digest_mix(u64 z) {
@@ -223,9 +224,8 @@ __host__ __device__ inline u64 digest_mix(u64 z) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
-__host__ __device__ inline u64 digest_plane(uint32_t j, uint32_t p, u64 w) {
-    return digest_mix(w ^ digest_mix((((u64)j << 8) | p) + 0x632BE59BD9B4E019ull));
-}
+// odd multipliers of the 20 planes (SplitMix64's golden-ratio increments)
+__host__ __device__ inline u64 digest_plane_k(uint32_t p) { return 0x9E3779B97F4A7C15ull * (2ull * p + 1ull); }
 // The 20 observation planes of word j (m: its valid rumor bits) from the
 // post-delivery bit-sliced state: entries in A/B/C/D before the deliveries
 // (B, C, D; a0, a1 and the five b planes bp), the entries the deliveries
@@ -246,8 +246,8 @@ __host__ __device__ inline u64 digest_word(uint32_t j, u64 m, u64 B, u64 C, u64 
         pl[15 + i] = E & c2[i];   // record bits 7..11
     }
     u64 h = 0;
-    for (uint32_t p = 0; p < 20; ++p) h += digest_plane(j, p, pl[p] & m);
-    return h;
+    for (uint32_t p = 0; p < 20; ++p) h += (pl[p] & m) * digest_plane_k(p);
+    return digest_mix(h ^ digest_mix((u64)j + 0x632BE59BD9B4E019ull));
 }
 __host__ __device__ inline u64 digest_node(uint32_t psize, const u64 *st5) {
     u64 h = digest_mix((1ull << 63) | psize);

@@ -47,8 +47,9 @@ GS_DEV T ge_seg(const T (&x)[NB], const T (&km)[NB]) {
 // FUSE: the launch also runs the next build's first partition (a.cp_e set).
 // SH: a code-row shard engine (gs_shard.hip, ShardPlan::codes): the pull code
 // x received is read from exchange B at x's slot (spos_cur) instead of
-// PULL[x], and its next push code goes to its exchange-A slot (spos_next)
-// instead of PC[x]; blocks [blk_off, blk_off + grid) (a pipeline part).
+// PULL[x], and its next push code goes with its target into its exchange-A
+// row (spos_next) instead of PC[x]; blocks [blk_off, blk_off + grid) (a
+// pipeline part).
 template <int MODE, typename T, uint32_t kNpl, bool FUSE, bool SH = false>
 __global__ __launch_bounds__(kDlv4Threads, (kNpl == 2 && sizeof(T) == 4 && !FUSE) ? GS_DLV4_MINW_R16 : GS_DLV4_MINW)
 void round_kernel_dlv4(RoundArgs a) {
@@ -155,7 +156,7 @@ void round_kernel_dlv4(RoundArgs a) {
     __syncthreads();
     // class planes now; the five b planes only for the transition (still in
     // LDS then: fewer registers live across the deliveries)
-    const uint32_t ul = (lane >> lpw_log) - blockIdx.x * units_blk;  // the lane's word within the block
+    const uint32_t ul = (lane >> lpw_log) - bid * units_blk;  // the lane's word within the block
     T P[kPlanes];
 #pragma unroll
     for (int p = 0; p < 3; ++p) P[p] = nv ? (T)(stage[ul * kPlanes + p] >> shL) & mV : (T)0;
@@ -399,12 +400,19 @@ void round_kernel_dlv4(RoundArgs a) {
             // (not stored)
         } else if (SH) {
             // exchange A of round t+1: to owner(t_{t+1}(x)) (no slot: an
-            // undelivered edge, or a capacity overflow, flagged by the plan)
-            uint32_t *sA = reinterpret_cast<uint32_t *>(a.sendA);
+            // undelivered edge, or a capacity overflow, flagged by the plan),
+            // the row (push code, target local to that rank | kRowMutual when
+            // t_{t+1}(t_{t+1}(x)) = x: x is its target's own target, whose
+            // push copy the pull copy supersedes, src/message_state.rs:79)
+            uint2 *sA = reinterpret_cast<uint2 *>(a.sendA);
 #pragma unroll
             for (uint32_t q = 0; q < kNpl; ++q) {
                 const uint32_t sp = q < nv ? a.spos_next[x0 + q] : 0xFFFFFFFFu;
-                if (sp != 0xFFFFFFFFu) sA[sp] = pc[q];
+                if (sp == 0xFFFFFFFFu) continue;
+                const uint32_t t = a.tg_next[x0 + q] & kTgMask;
+                const uint32_t tl = t - (t / a.sp.chunk) * a.sp.chunk;
+                const bool mutual = peer_of(a.seed, a.epoch, a.round_new, t, a.sp.n) == a.node_lo + x0 + q;
+                sA[sp] = make_uint2(pc[q], tl | (mutual ? kRowMutual : 0u));
             }
         } else if (kNpl == 4 && nv == kNpl) {
             *reinterpret_cast<uint4 *>(a.pc_out + x0) =
@@ -563,7 +571,8 @@ static hipError_t launch_dlv4_t(const RoundArgs &a, int mode, hipStream_t s) {
         return hipErrorInvalidValue;
     const dim3 gd((uint32_t)grid), bd(kDlv4Threads);
     if (a.recvA) {  // code-row shard
-        if (!a.sp.codes || !a.recvB || !a.sendA || !a.spos_cur || !a.spos_next) return hipErrorInvalidValue;
+        if (!a.sp.codes || !a.recvB || !a.sendA || !a.spos_cur || !a.spos_next || !a.tg_next || !a.sp.chunk)
+            return hipErrorInvalidValue;
         if (mode == 0) hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL, false, true>), gd, bd, 0, s, a);
         else hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, false, true>), gd, bd, 0, s, a);
     } else if (a.cp_e) {

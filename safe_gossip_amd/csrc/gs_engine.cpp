@@ -128,11 +128,8 @@ struct gs_engine {
     hipEvent_t ev_main = nullptr;                          // engine stream position (cstream waits)
     u64 *sendA[2] = {nullptr, nullptr}, *recvA[2] = {nullptr, nullptr};
     u64 *sendB = nullptr, *recvB = nullptr;
-    // code-row shards (dlv && shard: R_pad <= 16, 2P): round t's delivery
-    // records and tail codes, written by the pull kernel after exchange A
-    // (gs_shard.hip pull_codes), read by the packed round kernel
-    gs::DlvRec *sDR = nullptr;
-    uint32_t *sdtail = nullptr;
+    // (code-row shards, dlv && shard: round t's delivery records are built
+    // into csr[0] from the rows exchange A delivered, gs_shard_pull)
     uint32_t pulled_round = 0;  // round whose gs_shard_pull ran (its plan of t+2 is launched)
     // Pipeline parts of the round in progress (gs_shard_round_part): parts
     // [0, parts_done) are launched with the arguments `ra` (mode ra_mode).
@@ -260,7 +257,7 @@ void release(gs_engine *e) {
     for (int i = 0; i < 2; ++i)
         if (e->ev_dens[i]) (void)hipEventDestroy(e->ev_dens[i]);
     if (e->dens_host) (void)hipHostFree(e->dens_host);
-    void *bufs[] = {e->lvm, e->cpm, e->rows_dev, e->zb[0], e->zb[1], e->lb[0], e->lb[1], e->ab[0], e->ab[1], e->acct, e->dens, e->pc, e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->sDR, e->sdtail, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
+    void *bufs[] = {e->lvm, e->cpm, e->rows_dev, e->zb[0], e->zb[1], e->lb[0], e->lb[1], e->ab[0], e->ab[1], e->acct, e->dens, e->pc, e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
                     e->partials, e->obs_state, e->obs_rec, e->obs_psize, e->obs_digest, e->obs_pend, e->ext_dev,
                     e->node_state};
     for (void *b : bufs)
@@ -371,11 +368,11 @@ gs::RoundArgs base_args(gs_engine *e) {
         a.recvA = e->recvA[t % 2];
         a.recvB = e->recvB;
         a.sendA = e->sendA[(t + 1) % 2];
-        a.sp = gs::ShardRows{e->sp.G,    e->sp.P,      e->sp.W,  e->sp.capP,  e->sp.flagrows,
-                             e->sp.blk,  e->sp.idrows, e->sp.rw, e->sp.codes};
-        if (e->dlv) {  // code rows: delivery records of the pull kernel
-            a.DR = e->sDR;
-            a.dtail = e->sdtail;
+        a.sp = gs::ShardRows{e->sp.G,   e->sp.P,    e->sp.W,     e->sp.capP,  e->sp.flagrows, e->sp.blk,
+                             e->sp.idrows, e->sp.rw, e->sp.rwb, e->sp.codes, e->sp.chunk,    e->sp.n};
+        if (e->dlv) {  // code rows: the delivery records built from exchange A (gs_shard_pull)
+            a.DR = e->csr[0].DR;
+            a.dtail = e->csr[0].src;
         }
     } else {
         const auto &cs = e->csr[e->round & 1u];  // round-t lists (t = e->round)
@@ -547,7 +544,7 @@ gs_status observe(gs_engine *e, bool dumps, bool digest = false) {
     if (digest) a.obs_digest = e->obs_digest;
     if (e->slice) a.emin = e->eb[3];  // pending empty pulls of this slice
     if (e->deliver_pending) {
-        if (e->shard) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_edges[e->round % 2], 0));
+        if (e->shard && !e->dlv) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_edges[e->round % 2], 0));
         else if (built_elsewhere(e)) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
         st = seq_prepare(e);
         if (st != GS_OK) return st;
@@ -648,6 +645,44 @@ uint32_t gs_fault(uint64_t seed, uint32_t epoch, uint32_t round, uint32_t node, 
 
 namespace {
 
+// The exchange layout of rank `rank` of `world` (gs_shard.hip shard_plan).
+gs::ShardPlan plan_of(const gs_config *cfg, uint32_t rank, uint32_t world, uint32_t parts) {
+    const uint32_t R = cfg->n_rumors;
+    // row flags (receivers skip empty rows; A/B, measured slower: DESIGN.md
+    // section 7): SAFE_GOSSIP_AMD_SHARD_FLAGS=1; every rank must agree (it
+    // changes the layout)
+    const char *v = std::getenv("SAFE_GOSSIP_AMD_SHARD_FLAGS");
+    const bool flags = v && *v == '1';
+    // code rows (one u32 push / pull code per row, delivery records and the
+    // packed DLV round kernel) at R_pad <= 16 in the 2P schedule;
+    // SAFE_GOSSIP_AMD_NO_DLV=1 keeps class rows (every rank must agree)
+    const char *nd = std::getenv("SAFE_GOSSIP_AMD_NO_DLV");
+    const bool codes = !(nd && *nd && *nd != '0') && next_pow2(R) <= 16 && cfg->schedule == GS_SCHED_2P;
+    return gs::shard_plan(cfg->n_nodes, world, rank, R >= 64 ? (next_pow2(R) / 64) : 1u, parts, flags, codes);
+}
+
+// Slot keys of exchange A (sources of a code-row shard's DLV build).
+uint32_t shard_keys(const gs::ShardPlan &sp) { return sp.G * sp.P * sp.capP; }
+
+void fill_shard_info(const gs::ShardPlan &sp, uint32_t info[14]) {
+    info[0] = sp.lo;
+    info[1] = sp.m;
+    info[2] = sp.blk;  // rows per rank sub-block of a part: capP row slots + flag rows
+    info[3] = sp.idrows;
+    // u32 words per exchange-A row: the 2-plane class code (2W u64 = 4W u32),
+    // or (code rows, R_pad <= 16) the push code and the target word
+    info[4] = sp.rw;
+    info[5] = sp.G;
+    info[6] = sp.g;
+    info[7] = sp.chunk;
+    info[8] = sp.P;
+    info[9] = sp.mP;
+    info[10] = gs::shard_slotsA(sp);  // rows of an exchange-A buffer
+    info[11] = gs::shard_slotsB(sp);  // rows of an exchange-B buffer
+    info[12] = sp.rwb;                // u32 words per exchange-B row
+    info[13] = sp.codes;              // 1: code rows
+}
+
 // Common constructor: a whole network (world == 0) or the node range of rank
 // `rank` of a network sharded over `world` ranks.
 gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uint32_t parts, gs_engine **out) {
@@ -661,19 +696,7 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
     if (nglob > gs::kTgMask + 1u) return GS_ERR_UNSUPPORTED;
     gs::ShardPlan sp{};
     if (world && (parts == 0 || parts > gs::kMaxParts)) return GS_ERR_INVALID_ARGUMENT;
-    if (world) {
-        // row flags (receivers skip empty rows; A/B, measured slower: DESIGN.md
-        // section 7): SAFE_GOSSIP_AMD_SHARD_FLAGS=1; every rank must agree (it
-        // changes the layout)
-        const char *v = std::getenv("SAFE_GOSSIP_AMD_SHARD_FLAGS");
-        const bool flags = v && *v == '1';
-        // code rows (one u32 push / pull code per row, delivery records and
-        // the packed DLV round kernel) at R_pad <= 16 in the 2P schedule;
-        // SAFE_GOSSIP_AMD_NO_DLV=1 keeps class rows (every rank must agree)
-        const char *nd = std::getenv("SAFE_GOSSIP_AMD_NO_DLV");
-        const bool codes = !(nd && *nd && *nd != '0') && next_pow2(R) <= 16 && cfg->schedule == GS_SCHED_2P;
-        sp = gs::shard_plan(nglob, world, rank, R >= 64 ? (next_pow2(R) / 64) : 1u, parts, flags, codes);
-    }
+    if (world) sp = plan_of(cfg, rank, world, parts);
     const uint32_t n = world ? sp.m : nglob;  // nodes owned by this engine
     uint8_t p[3];
     gs_derive_params(nglob, p);
@@ -743,7 +766,13 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         const std::string m = v ? v : "";
         e->dlv_pack = m == "0" ? 0u : (m == "u64" ? 2u : (m == "u32x1" ? 3u : 1u));
     }
-    e->plan = e->dlv ? gs::dlv_plan(n) : gs::csr_plan(n);
+    // (code-row shards: the DLV build's sources are the slot keys of
+    // exchange A, its targets the owned nodes)
+    e->plan = e->dlv ? gs::dlv_plan(e->shard ? std::max(n, shard_keys(e->sp)) : n) : gs::csr_plan(n);
+    if (e->dlv && !e->plan.binned) {  // (n <= 2^27: every shard of a network the state layout holds)
+        delete e;
+        return GS_ERR_UNSUPPORTED;
+    }
     {
         // Sparse records on the wide 2P path (W <= 8, so a wave's node bits
         // are whole bytes).  SAFE_GOSSIP_AMD_SPARSE = off (default) | dense
@@ -818,14 +847,18 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         ok = hipEventCreateWithFlags(&e->ev_plan[i], hipEventDisableTiming) == hipSuccess &&
              dalloc(&e->planw[i], words) == hipSuccess;
     }
-    for (int i = 0; i < 2 && ok && e->shard; ++i) {
+    for (int i = 0; i < 2 && ok && e->shard && !e->dlv; ++i) {  // (code rows need no in-lists ahead)
         const size_t words = gs::shard_edge_words(e->sp, &e->sel);
         ok = hipEventCreateWithFlags(&e->ev_edges[i], hipEventDisableTiming) == hipSuccess &&
              dalloc(&e->edgew[i], words) == hipSuccess;
     }
     if (ok && e->shard) ok = hipEventCreateWithFlags(&e->ev_main, hipEventDisableTiming) == hipSuccess;
-    if (ok && e->shard && e->dlv)
-        ok = dalloc(&e->sDR, n) == hipSuccess && dalloc(&e->sdtail, gs::shard_slotsA(e->sp)) == hipSuccess;
+    if (ok && e->shard && e->dlv) {  // one build set: built and read on the engine stream, in order
+        const gs::InListSizes dz = gs::inlist_sizes(e->plan);
+        auto &c = e->csr[0];
+        ok = dalloc(&c.src, dz.src_words) == hipSuccess && dalloc(&c.region, dz.region_words) == hipSuccess &&
+             dalloc(&c.scratch, dz.scratch_words) == hipSuccess && dalloc(&c.DR, e->plan.n) == hipSuccess;
+    }
     const gs::InListSizes isz = gs::inlist_sizes(e->plan);
     // per-node arrays the pipelined round kernel reads by whole 64-node tiles
     const size_t npad = gs::pipe_padded(n);
@@ -887,10 +920,12 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
 }
 
 // Plan of round r on the side stream: owned targets and send slots (set
-// r % 3), and the ids exchange A of round r-1 carries (buffer set (r-1) % 2).
+// r % 3), and the ids exchange A of round r-1 carries (buffer set (r-1) % 2);
+// code rows carry no ids: the plan marks the empty row slots of round r's own
+// buffer set (r % 2) instead.
 gs_status launch_plan(gs_engine *e, uint32_t r) {
-    GS_HIP(gs::launch_shard_plan(e->sp, e->spl, e->planw[r % 3], e->sendA[(r + 1) % 2], e->seed, e->epoch, r,
-                                 e->faults, e->flags, e->cstream));
+    GS_HIP(gs::launch_shard_plan(e->sp, e->spl, e->planw[r % 3], e->sendA[(e->dlv ? r : r + 1) % 2], e->seed,
+                                 e->epoch, r, e->faults, e->flags, e->cstream));
     GS_HIP(hipEventRecord(e->ev_plan[r % 3], e->cstream));
     return GS_OK;
 }
@@ -902,6 +937,44 @@ gs_status launch_edges(gs_engine *e, uint32_t r) {
                                   e->planw[r % 3] + e->spl.tg, e->seed, e->epoch, r, e->faults, e->flags,
                                   e->cstream));
     GS_HIP(hipEventRecord(e->ev_edges[r % 2], e->cstream));
+    return GS_OK;
+}
+
+// Code-row shard, after exchange A of round t: the plan of round t+2 on the
+// side stream (its ids are not exchanged: code rows carry their targets),
+// then on the engine stream the delivery-record build of round t over the
+// arrived rows (gs_inlist.hip, sources = slot keys): every owned node's
+// record and each pusher's pull code into sendB at its exchange-B slot.
+gs_status shard_build(gs_engine *e) {
+    const uint32_t t = e->round;
+    GS_HIP(hipEventRecord(e->ev_main, e->stream));
+    GS_HIP(hipStreamWaitEvent(e->cstream, e->ev_main, 0));
+    gs_status st = launch_plan(e, t + 2);
+    if (st != GS_OK) return st;
+    e->pulled_round = t;
+    auto &c = e->csr[0];
+    gs::InListArgs la{};
+    la.p = e->plan;
+    la.dlv = 1;
+    la.S = e->S[e->cur];
+    la.g = e->g;
+    la.DR = c.DR;
+    la.dtail = c.src;
+    la.src = c.src;
+    la.region = c.region;
+    la.scratch = c.scratch;
+    la.flags = e->flags;
+    la.seed = e->seed;
+    la.epoch = e->epoch;
+    la.round = t;
+    la.f = e->faults;
+    la.rowsA = reinterpret_cast<const uint32_t *>(e->recvA[t % 2]);
+    la.pullB = reinterpret_cast<uint32_t *>(e->sendB);
+    la.sr = gs::ShardRows{e->sp.G,      e->sp.P,  e->sp.W,   e->sp.capP,  e->sp.flagrows, e->sp.blk,
+                          e->sp.idrows, e->sp.rw, e->sp.rwb, e->sp.codes, e->sp.chunk,    e->sp.n};
+    la.nkeys = shard_keys(e->sp);
+    la.ntargets = e->g.n;
+    GS_HIP(gs::launch_build_inlists(la, e->stream));
     return GS_OK;
 }
 
@@ -922,23 +995,17 @@ gs_status gs_shard_create_parts(const gs_config *cfg, uint32_t rank, uint32_t wo
     return create_engine(cfg, rank, world, parts, out);
 }
 
-gs_status gs_shard_info(const gs_engine *e, uint32_t info[12]) {
+gs_status gs_shard_info(const gs_engine *e, uint32_t info[14]) {
     if (!e || !info || !e->shard) return GS_ERR_INVALID_ARGUMENT;
-    // u32 words per row: the 2-plane class code (2W u64 = 4W u32), or one u32
-    // push / pull code (code rows, R_pad <= 16)
-    const uint32_t wa = e->sp.rw;
-    info[0] = e->sp.lo;
-    info[1] = e->sp.m;
-    info[2] = e->sp.blk;  // rows per rank sub-block of a part: capP row slots + flag rows
-    info[3] = e->sp.idrows;
-    info[4] = wa;
-    info[5] = e->sp.G;
-    info[6] = e->sp.g;
-    info[7] = e->sp.chunk;
-    info[8] = e->sp.P;
-    info[9] = e->sp.mP;
-    info[10] = gs::shard_slotsA(e->sp);  // rows of an exchange-A buffer
-    info[11] = gs::shard_slotsB(e->sp);  // rows of an exchange-B buffer
+    fill_shard_info(e->sp, info);
+    return GS_OK;
+}
+
+gs_status gs_shard_plan_info(const gs_config *cfg, uint32_t rank, uint32_t world, uint32_t parts, uint32_t info[14]) {
+    if (!cfg || !info || world == 0 || rank >= world || world > gs::kMaxShards || parts == 0 ||
+        parts > gs::kMaxParts || cfg->n_nodes == 0 || cfg->n_rumors == 0 || cfg->n_rumors > 4096)
+        return GS_ERR_INVALID_ARGUMENT;
+    fill_shard_info(plan_of(cfg, rank, world, parts), info);
     return GS_OK;
 }
 
@@ -960,6 +1027,7 @@ gs_status gs_shard_pull(gs_engine *e) {
     gs_status st = set_device(e);
     if (st != GS_OK) return st;
     const uint32_t t = e->round;
+    if (e->dlv) return shard_build(e);
     // Exchange A of round t (and, in round 1, the ids-only exchange A of
     // round 0) is complete on the engine stream: build the in-lists of round
     // t+1 (and of round 1) on the side stream, behind this round's work.
@@ -989,8 +1057,6 @@ gs_status gs_shard_pull(gs_engine *e) {
     a.sendB = e->sendB;
     a.P = e->sp;
     a.g = e->g;
-    a.DR = e->sDR;
-    a.dtail = e->sdtail;
     GS_HIP(gs::launch_pull(a, e->stream));
     return GS_OK;
 }
@@ -1163,7 +1229,7 @@ gs_status round_begin(gs_engine *e) {
     const uint32_t rs = R0 & 1u;  // set holding round t = e->round
     if (e->shard) {
         GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[(R0 + 1) % 3], 0));
-        if (e->deliver_pending) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_edges[R0 % 2], 0));
+        if (e->deliver_pending && !e->dlv) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_edges[R0 % 2], 0));
     } else if (e->deliver_pending) {
         if (built_elsewhere(e))  // (built on the engine stream: in order already)
             GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[rs], 0));

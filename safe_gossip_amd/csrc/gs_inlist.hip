@@ -64,6 +64,33 @@ GS_DEV uint32_t target_of(const InListArgs &a, uint32_t x) {
     return target_word(a.seed, a.epoch, a.round, x, a.p.n, a.f);
 }
 
+// A source of the DLV build: its target word, push code and source field.
+// On the single engine source x is node x (Philox target, written to tg for
+// the round kernel; push code from the transition launch).  On a code-row
+// shard it is slot key x of exchange A, read from its row (empty slot: no
+// edge); its source field carries kRowMutual when the pusher is its target's
+// own target (the receiver's t(y), src/message_state.rs:79).
+GS_DEV void dlv_source(const InListArgs &a, uint32_t x, uint32_t &t, uint32_t &code, uint32_t &src) {
+    if (a.rowsA) {
+        t = kTgDead;
+        code = 0u;
+        src = x;
+        if (x < a.nkeys) {
+            const uint2 r = reinterpret_cast<const uint2 *>(a.rowsA)[shard_key_slot(a.sr, x)];
+            if (r.y != 0xFFFFFFFFu) {
+                t = r.y & ~kRowMutual;
+                code = r.x;
+                src = x | (r.y & kRowMutual);
+            }
+        }
+        return;
+    }
+    t = target_of(a, x);
+    a.tg[x] = t;
+    code = a.PC[x];
+    src = x;
+}
+
 // Per-target record emission, shared by both paths.  `lst` holds y's k
 // sources ascending (LDS or global); `first` is where lst[kInline..k) are
 // (already) stored in a.src.  Live-filtered gathers (a.lvm, binned path
@@ -535,18 +562,16 @@ __global__ __launch_bounds__(NT) void dl_coarse(InListArgs a) {
     for (uint32_t i = threadIdx.x; i < nc; i += NT) cnt[i] = 0u;
     __syncthreads();
     const uint32_t lo = blockIdx.x * kPartChunk;
-    uint32_t tv[kPer], cv[kPer];
+    uint32_t tv[kPer], cv[kPer], xs[kPer];
 #pragma unroll
     for (uint32_t q = 0; q < kPer; ++q) {
         const uint32_t x = lo + threadIdx.x + q * NT;
         tv[q] = kTgDead;
         cv[q] = 0u;
+        xs[q] = x;
         if (x < p.n) {
-            const uint32_t t = target_of(a, x);
-            a.tg[x] = t;
-            tv[q] = t;
-            cv[q] = a.PC[x];
-            if (!(t & kTgDead)) atomicAdd(&cnt[(t & kTgMask) >> kCoarseLog], 1u);
+            dlv_source(a, x, tv[q], cv[q], xs[q]);
+            if (!(tv[q] & kTgDead)) atomicAdd(&cnt[(tv[q] & kTgMask) >> kCoarseLog], 1u);
         }
     }
     __syncthreads();
@@ -573,7 +598,7 @@ __global__ __launch_bounds__(NT) void dl_coarse(InListArgs a) {
         if (tv[q] & kTgDead) continue;
         const uint32_t t = tv[q] & kTgMask;
         const uint32_t pos = atomicAdd(&cnt[t >> kCoarseLog], 1u);
-        sx[pos] = lo + threadIdx.x + q * NT;
+        sx[pos] = xs[q];
         st[pos] = t;
         sc[pos] = cv[q];
     }
@@ -695,18 +720,16 @@ __global__ __launch_bounds__(kInlThreads) void dl_direct(InListArgs a) {
     for (uint32_t i = threadIdx.x; i < np; i += kInlThreads) cnt[i] = 0u;
     __syncthreads();
     const uint32_t lo = blockIdx.x * kPartChunk;
-    uint32_t tv[kPartPer], cv[kPartPer];
+    uint32_t tv[kPartPer], cv[kPartPer], xs[kPartPer];
 #pragma unroll
     for (uint32_t q = 0; q < kPartPer; ++q) {
         const uint32_t x = lo + threadIdx.x + q * kInlThreads;
         tv[q] = kTgDead;
         cv[q] = 0u;
+        xs[q] = x;
         if (x < p.n) {
-            const uint32_t t = target_of(a, x);
-            a.tg[x] = t;
-            tv[q] = t;
-            cv[q] = a.PC[x];
-            if (!(t & kTgDead)) atomicAdd(&cnt[(t & kTgMask) >> plog], 1u);
+            dlv_source(a, x, tv[q], cv[q], xs[q]);
+            if (!(tv[q] & kTgDead)) atomicAdd(&cnt[(tv[q] & kTgMask) >> plog], 1u);
         }
     }
     __syncthreads();
@@ -732,7 +755,7 @@ __global__ __launch_bounds__(kInlThreads) void dl_direct(InListArgs a) {
         if (tv[q] & kTgDead) continue;
         const uint32_t t = tv[q] & kTgMask, b = t >> plog;
         const uint32_t pos = atomicAdd(&cnt[b], 1u);
-        sx[pos] = lo + threadIdx.x + q * kInlThreads;
+        sx[pos] = xs[q];
         sc[pos] = cv[q];
         slt[pos] = (uint16_t)(t & (kBin - 1u));  // (relative to the bin)
         sb[pos] = (uint16_t)b;
@@ -842,16 +865,19 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
     uint32_t tgv[kHalfPer];
     uint32_t w0[kHalfPer], w1[kHalfPer], w2[kHalfPer];
     const uint32_t *S32 = reinterpret_cast<const uint32_t *>(a.S);
+    // (code-row shard: targets are the ntargets local nodes, p.n may be
+    // larger -- the slot keys -- and t(y)'s pusher is flagged in its row)
+    const uint32_t ny = a.rowsA ? a.ntargets : p.n;
     auto load_targets = [&](uint32_t wp) {
         const uint32_t t0p = wp << kHalfLog;
-        const uint32_t np = t0p < p.n ? min(kHalf, p.n - t0p) : 0u;
+        const uint32_t np = t0p < ny ? min(kHalf, ny - t0p) : 0u;
 #pragma unroll
         for (uint32_t q = 0; q < kHalfPer; ++q) {
             const uint32_t lt = threadIdx.x + q * kInlThreads;
             const uint32_t y = np ? t0p + (lt < np ? lt : 0u) : 0u;  // (a part past the last node: node 0)
             const uint32_t ysh = (y & ((1u << a.g.lognpu) - 1u)) << a.g.logr;
             const u64 rb = (u64)(y >> a.g.lognpu) * kPlanes * 2u + (ysh >> 5);
-            tgv[q] = a.tg[y];
+            tgv[q] = a.rowsA ? 0u : a.tg[y];
             w0[q] = S32[rb];
             w1[q] = S32[rb + 2];
             w2[q] = S32[rb + 4];
@@ -929,7 +955,7 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
         for (uint32_t j = s + 1; j < e; ++j) {  // insertion sort of (id, code) by id
             const uint32_t v = sid[j], vc = scd[j];
             uint32_t r = j;
-            while (r > s && sid[r - 1] > v) {
+            while (r > s && (sid[r - 1] & kIdMask) > (v & kIdMask)) {  // (bit 31: kRowMutual)
                 sid[r] = sid[r - 1];
                 scd[r] = scd[r - 1];
                 --r;
@@ -946,7 +972,7 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
         const uint32_t first = (mt && cur != kNone) ? cur : 0u;
         uint32_t zi = kDlvNoZ;
         for (uint32_t j = 0; j < k; ++j) {
-            if (sid[s + j] == tz) zi = j;
+            if (a.rowsA ? (sid[s + j] & kRowMutual) != 0u : sid[s + j] == tz) zi = j;
             if (j >= kDlvInline && cur != kNone) a.dtail[first + j - kDlvInline] = scd[s + j];
         }
         if (mt && cur != kNone) cur += mt;
@@ -975,13 +1001,19 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
             pC |= nw & vC;
             pnot &= ~sl;
             // an empty pull batch is not passed back: PULL[] reads 0 for it
-            if (!direct && scd[j]) atomicAdd(&pcnt[sid[j] >> kCoarseLog], 1u);
+            if (!direct && scd[j]) atomicAdd(&pcnt[(sid[j] & kIdMask) >> kCoarseLog], 1u);
         }
     }
     __syncthreads();
     if (direct) {  // one coarse bucket: every pull straight into PULL (cache-resident)
         const uint32_t placed = min(total, kHalfCap);
-        for (uint32_t j = threadIdx.x; j < placed; j += kInlThreads) a.pull[sid[j]] = scd[j];
+        if (a.rowsA) {  // a code-row shard: to the pusher's exchange-B slot
+            uint32_t *pb = a.pullB;
+            for (uint32_t j = threadIdx.x; j < placed; j += kInlThreads)
+                pb[shard_key_bslot(a.sr, sid[j] & kIdMask)] = scd[j];
+        } else {
+            for (uint32_t j = threadIdx.x; j < placed; j += kInlThreads) a.pull[sid[j]] = scd[j];
+        }
         return;
     }
     // the (pusher, pull) pairs into the pushers' coarse source buckets
@@ -994,7 +1026,7 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
     const uint32_t placed = min(total, kHalfCap);
     for (uint32_t j = threadIdx.x; j < placed; j += kInlThreads) {
         if (!scd[j]) continue;  // empty pull (pb_place zero-fills)
-        const uint32_t x = sid[j], cb = x >> kCoarseLog;
+        const uint32_t x = sid[j] & kIdMask, cb = x >> kCoarseLog;
         const uint32_t slot = pres[cb] + atomicAdd(&pcnt[cb], 1u);  // < 2^kCoarseLog: one per source
         const u64 o = ((u64)cb << kCoarseLog) + slot;
         pa.x[o] = x;
@@ -1085,6 +1117,11 @@ __global__ __launch_bounds__(kInlThreads) void pb_place(InListArgs a) {
     }
     __syncthreads();
     const uint32_t x0 = b << kBinLog;
+    if (a.rowsA) {  // a code-row shard: sources are slot keys, pulls go to their exchange-B slots
+        const uint32_t keys = x0 < a.nkeys ? min(kBin, a.nkeys - x0) : 0u;
+        for (uint32_t i = threadIdx.x; i < keys; i += kInlThreads) a.pullB[shard_key_bslot(a.sr, x0 + i)] = img[i];
+        return;
+    }
     const uint32_t nodes = min(kBin, p.n - x0);
     for (uint32_t i = threadIdx.x; i < nodes; i += kInlThreads) a.pull[x0 + i] = img[i];
 }

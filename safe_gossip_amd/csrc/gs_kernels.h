@@ -7,7 +7,7 @@ namespace gs {
 // The exchange layout a round kernel needs (ShardPlan's fields of the same
 // names; the slot helpers below take either).
 struct ShardRows {
-    uint32_t G, P, W, capP, flagrows, blk, idrows, rw, codes;
+    uint32_t G, P, W, capP, flagrows, blk, idrows, rw, rwb, codes, chunk, n;
 };
 
 struct RoundArgs {
@@ -225,6 +225,16 @@ struct InListArgs {
     const u64 *lvm, *cpm;
     u64 *zl;
     u64 *rows;          // + node class rows the flags leave to gather (zeroed by the caller)
+    // Code-row shard engine (DLV build over received rows; null otherwise):
+    // the sources are the slot keys [0, nkeys) of exchange A (ascending key =
+    // ascending source id, gs_shard.hip), their (target, push code) come from
+    // the rows rowsA, the targets are the ntargets local nodes (p.n =
+    // max(nkeys, ntargets)), and the pull batches go to pullB at each key's
+    // exchange-B slot; t(y)'s pusher is the one whose row has kRowMutual.
+    const uint32_t *rowsA;
+    uint32_t *pullB;
+    ShardRows sr;
+    uint32_t nkeys, ntargets;
 };
 // Peer choices of `round` (into tg) and their in-lists (IN8, SIB8 tagged with
 // `serial`).  Depends on nothing but the Philox stream, so it runs on its own
@@ -294,13 +304,19 @@ struct ShardPlan {
     // slower); flagrows = 0 when off or W > 8.  blk = capP + flagrows.
     uint32_t flagrows, blk;
     uint32_t idrows;    // rows of u32 ids per block of the last part of A (P*capP ids)
-    // Row format: u32 words per row.  Class rows (R_pad >= 32, or the gather
-    // shards): the 2-plane class code as 2W u64 words, rw = 4W.  Code rows
-    // (codes = 1: delivery-record shards, R_pad <= 16, 2P): the push / pull
-    // code itself, one u32 (b0 | b1 << 16, gs_common.h DlvRec), rw = 1.
-    uint32_t rw, codes;
+    // Row format: u32 words per row of exchange A (rw) and B (rwb).  Class
+    // rows (R_pad >= 32, or forced): the 2-plane class code as 2W u64 words,
+    // rw = rwb = 4W, and the id rows of next round's sources.  Code rows
+    // (codes = 1: delivery-record shards, R_pad <= 16, 2P): an A row is the
+    // push code (b0 | b1 << 16, gs_common.h DlvRec) and the pusher's target
+    // local to the receiving rank with bit 31 set when the pusher is its
+    // target's own target (kRowMutual; an empty slot's target word is
+    // 0xFFFFFFFF), rw = 2; a B row is the pull code, rwb = 1; no id rows (the
+    // receiver needs no in-lists ahead: its build sorts the arrived rows).
+    uint32_t rw, rwb, codes;
     CsrPlan edges;      // counting sort of the A receive slots over the m targets
 };
+constexpr uint32_t kRowMutual = 1u << 31;
 // Row slot of (rank block s, part h, index i) in an exchange-A / -B buffer.
 template <class SP>
 __host__ __device__ inline uint32_t shard_blockA(const SP &P, uint32_t h) {
@@ -343,6 +359,12 @@ __host__ __device__ inline uint32_t shard_key_slot(const SP &P, uint32_t key) {
     const uint32_t s = key / per, r = key - s * per, h = r / P.capP;
     return shard_a_slot(P, s, h, r - h * P.capP);
 }
+template <class SP>
+__host__ __device__ inline uint32_t shard_key_bslot(const SP &P, uint32_t key) {
+    const uint32_t per = P.P * P.capP;
+    const uint32_t s = key / per, r = key - s * per, h = r / P.capP;
+    return shard_b_slot(P, s, h, r - h * P.capP);
+}
 // The flag byte of row slot e of an exchange buffer (A: sub-blocks of
 // shard_blockA rows, B: of blk rows): byte i of the flag rows after the
 // capP row slots of e's sub-block.
@@ -382,11 +404,6 @@ hipError_t launch_shard_edges(const ShardPlan &P, const ShardEdgeLayout &L, uint
 
 struct PullArgs {
     const u64 *S;          // round-t planes of the owned nodes
-    // code rows (P.codes): the delivery records of round t for the packed
-    // DLV round kernel (DR[z] with the pushers' codes; pushers >= 2 at
-    // dtail[DR[z].first + i - 2])
-    DlvRec *DR;
-    uint32_t *dtail;
     const uint4 *IN;       // round-t in-lists of receive slots
     const uint32_t *IN2;   // their third pushers
     const uint32_t *EP;

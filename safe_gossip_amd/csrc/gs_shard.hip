@@ -162,18 +162,22 @@ __global__ __launch_bounds__(kPlanBlock) void plan_emit(ShardPlan P, const uint3
         if (i < P.capP) {  // an overflow is flagged by plan_scan
             sa = shard_a_slot(P, d, h, i);
             sb = shard_b_slot(P, d, h, i);
-            id_slots(P, bufA, d)[h * P.capP + i] = P.lo + xl;
+            if (P.idrows) id_slots(P, bufA, d)[h * P.capP + i] = P.lo + xl;
         }
     }
     SPOSA[xl] = sa;
     SPOSB[xl] = sb;
 }
 
-// Empty id slots of every sub-block (d, h) (past cnt[d * P + h]).
+// Empty slots of every sub-block (d, h) (past cnt[d * P + h]): class rows
+// mark their id slot, code rows their row's target word (its receiver's
+// build skips the slot).
 __global__ __launch_bounds__(256) void plan_idle(ShardPlan P, const uint32_t *__restrict__ cnt, u64 *bufA) {
     const uint32_t d = blockIdx.y / P.P, h = blockIdx.y - d * P.P;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < P.capP && i >= cnt[blockIdx.y]) id_slots(P, bufA, d)[h * P.capP + i] = kNoId;
+    if (i >= P.capP || i < cnt[blockIdx.y]) return;
+    if (P.codes) reinterpret_cast<uint32_t *>(bufA)[(u64)shard_a_slot(P, d, h, i) * 2u + 1u] = kNoId;
+    else id_slots(P, bufA, d)[h * P.capP + i] = kNoId;
 }
 
 // ------------------------------------------------ in-lists of receive slots
@@ -335,7 +339,8 @@ ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t pa
                      bool codes) {
     ShardPlan P{};
     P.codes = codes ? 1u : 0u;
-    P.rw = codes ? 1u : 4u * W;
+    P.rw = codes ? 2u : 4u * W;   // A: (push code, target word) / class code
+    P.rwb = codes ? 1u : 4u * W;  // B: pull code / class code
     P.n = n;
     P.G = G;
     P.g = g;
@@ -361,7 +366,7 @@ ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t pa
     double capd = std::min<double>((double)mp, mean + 16.0 * std::sqrt(mean + 1.0) + 64.0);
     const u64 q = std::max<u64>(64, P.rw);  // P*capP u32 ids fill whole rows of rw u32 words
     P.capP = (uint32_t)(((u64)std::ceil(capd) + q - 1) / q * q);
-    P.idrows = P.P * P.capP / P.rw;
+    P.idrows = codes ? 0u : P.P * P.capP / P.rw;  // (code rows carry their targets: no ids)
     // a flag byte per row slot (bit j: row word j), capP bytes in rows of 16W
     P.flagrows = (row_flags && !codes && W <= 8u) ? (P.capP + 16u * W - 1u) / (16u * W) : 0u;
     P.blk = P.capP + P.flagrows;
@@ -511,59 +516,8 @@ __global__ __launch_bounds__(256) void pull_kernel(PullArgs a) {
 }
 
 // ------------------------------------------------ code rows (R_pad <= 16)
-// The same response half at z over one-u32 rows (ShardPlan::codes): a push
-// row is the pusher's push code, a pull row the code of the batch z returns
-// (b0 | b1 << 16: 01 counter 1, 10 counter 2, 11 counter 255).  On the way z's
-// delivery record of round t is written for the packed round kernel
-// (gs_dlv4.hip), the input the single-GPU DLV build produces
-// (gs_inlist.hip inl_sort_dlv): the pushers' codes in ascending source order
-// (the receive slots' order), and t(z)'s index among them
-// (src/message_state.rs:79: its pull copy supersedes its push copy).
-__global__ __launch_bounds__(256) void pull_codes(PullArgs a) {
-    const uint32_t z = blockIdx.x * 256u + threadIdx.x;
-    if (z >= a.g.n) return;
-    const uint32_t *__restrict__ rA = reinterpret_cast<const uint32_t *>(a.recvA);
-    uint32_t *sB = reinterpret_cast<uint32_t *>(a.sendB);
-    const uint4 in = a.IN[z];
-    const uint32_t e2 = a.IN2[z];
-    const uint32_t k = in.y & 0xFFFFu, zi = in.y >> 16;
-    // z's class planes: its R_pad-bit segment lies in one 32-bit half of its
-    // unit word (R_pad <= 16), planes 0..2 at words 0, 2, 4 of the unit
-    const uint32_t sh = (z & ((1u << a.g.lognpu) - 1u)) << a.g.logr;
-    const u64 wb = (u64)(z >> a.g.lognpu) * kPlanes * 2u + (sh >> 5);
-    const uint32_t *S32 = reinterpret_cast<const uint32_t *>(a.S);
-    const uint32_t w0 = S32[wb], w1 = S32[wb + 2], w2 = S32[wb + 4];
-    uint32_t c[3];
-    c[0] = k > 0 ? rA[in.z] : 0u;
-    c[1] = k > 1 ? rA[in.w] : 0u;
-    c[2] = k > 2 ? rA[e2] : 0u;
-    const uint32_t m = (uint32_t)((1ull << a.g.rpad) - 1ull), s5 = sh & 31u;
-    const uint32_t cz = (w0 >> s5) & m, a0 = (w1 >> s5) & m, a1 = (w2 >> s5) & m;
-    const uint32_t zB = ~cz & (a0 | a1), zC = cz & ~(a0 & a1);
-    const uint32_t zB1 = zB & a0 & ~a1, zB2 = zB & a1 & ~a0;
-    uint32_t pnot = ~cz & ~a0 & ~a1 & m, pB = 0u, pC = 0u;
-    for (uint32_t i = 0; i < k; ++i) {
-        const uint32_t e = i == 0 ? in.z : (i == 1 ? in.w : (i == 2 ? e2 : a.EP[in.x + i]));
-        const uint32_t code = i < 3u ? c[i] : rA[e];
-        if (i >= kDlvInline) a.dtail[in.x + i - kDlvInline] = code;
-        const uint32_t pcl = zC | pC;
-        const SlotPos q = shard_a_decode(a.P, e);
-        sB[shard_b_slot(a.P, q.s, q.h, q.i)] = ((zB1 | pB | pcl) & 0xFFFFu) | ((zB2 | pcl) << 16);
-        const uint32_t b0 = code & 0xFFFFu, b1 = code >> 16;
-        const uint32_t vC = b0 & b1, sl = b0 | b1;  // the pusher's batch; C carries 255
-        const uint32_t nw = pnot & sl;
-        pB |= nw & ~vC;
-        pC |= nw & vC;
-        pnot &= ~sl;
-    }
-    DlvRec r;
-    r.meta = k | ((zi == 0xFFFFu ? kDlvNoZ : zi) << 5);
-    r.first = in.x;  // pusher i >= 2 at dtail[in.x + i - 2]
-    r.c[0] = c[0];
-    r.c[1] = c[1];
-    a.DR[z] = r;
-}
-
+// Observers of a code-row shard: the pull code each node received, in node
+// order (its exchange-B slot; none without a delivered push).
 __global__ __launch_bounds__(256) void pull_unpack(const uint32_t *__restrict__ spos, const uint32_t *__restrict__ recvB,
                                                    uint32_t *pull, uint32_t m) {
     const uint32_t x = blockIdx.x * 256u + threadIdx.x;
@@ -582,11 +536,7 @@ hipError_t launch_shard_pull_unpack(const uint32_t *spos, const uint32_t *recvB,
 hipError_t launch_pull(const PullArgs &a, hipStream_t s) {
     const u64 grid = (a.g.nseg + 255) / 256;
     if (grid == 0) return hipSuccess;
-    if (a.P.codes) {
-        if (!a.g.small || a.g.rpad > 16 || !a.DR || !a.dtail) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(pull_codes, dim3((uint32_t)grid), dim3(256), 0, s, a);
-        return hipGetLastError();
-    }
+    if (a.P.codes) return hipErrorInvalidValue;  // code rows: the delivery-record build (gs_inlist.hip)
     if (a.g.small) hipLaunchKernelGGL(pull_kernel<true>, dim3((uint32_t)grid), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(pull_kernel<false>, dim3((uint32_t)grid), dim3(256), 0, s, a);
     return hipGetLastError();

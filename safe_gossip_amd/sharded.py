@@ -56,6 +56,27 @@ def _lib():
     return load_library()
 
 
+def plan_info(n_nodes: int, n_rumors: int, world: int, rank: int = 0, parts: int = 4,
+              schedule: int = 0) -> dict:
+    """The exchange layout of one rank without creating an engine
+    (``gs_shard_plan_info``, host only): node range, rows per sub-block, row
+    size, buffer rows, and the largest single collective of a round (one
+    part's all-to-all, bytes per rank)."""
+    cfg = _Config()
+    cfg.n_nodes, cfg.n_rumors, cfg.schedule = n_nodes, n_rumors, schedule
+    info = (ctypes.c_uint32 * 14)()
+    _check(_lib().gs_shard_plan_info(ctypes.byref(cfg), rank, world, parts, info))
+    keys = ("lo", "m", "blk", "idrows", "row_words", "world", "rank", "chunk", "parts", "mP", "rowsA", "rowsB",
+            "row_words_b", "codes")
+    d = dict(zip(keys, list(info)))
+    ra, rb = d["row_words"] * 4, d["row_words_b"] * 4
+    d["row_bytes"], d["row_bytes_b"] = ra, rb
+    # part h of A: world sub-blocks of blk rows (+ idrows for the last part); B: blk rows
+    d["max_collective_bytes"] = max(world * (d["blk"] + d["idrows"]) * ra, world * d["blk"] * rb)
+    d["bytes_per_round"] = d["rowsA"] * ra + d["rowsB"] * rb  # A + B sent per rank (self block included)
+    return d
+
+
 class _Shard:
     """One rank's engine plus its exchange buffers (torch device tensors)."""
 
@@ -64,19 +85,20 @@ class _Shard:
         h = _P()
         _check(lib.gs_shard_create_parts(ctypes.byref(cfg), rank, world, parts, ctypes.byref(h)))
         self.h = h
-        info = (ctypes.c_uint32 * 12)()
+        info = (ctypes.c_uint32 * 14)()
         _check(lib.gs_shard_info(h, info))
         (self.lo, self.m, self.capP, self.idrows, self.wa, self.world, self.rank, self.chunk,
-         self.parts, self.mP, self.rowsA, self.rowsB) = list(info)
+         self.parts, self.mP, self.rowsA, self.rowsB, self.wb, self.codes) = list(info)
         dev = torch.device("cuda", device)
-        # rows of wa u32 words: the 2-plane class code (4W words), or one u32
-        # push / pull code at R_pad <= 16 (code rows)
+        # rows of wa (A) / wb (B) u32 words: the 2-plane class code (4W
+        # words), or at R_pad <= 16 code rows (A: push code + target word, B:
+        # pull code)
         i32 = torch.int32
         # exchange A: two buffer sets (round parity); B: one
         self.sendA = [torch.zeros(self.rowsA * self.wa, dtype=i32, device=dev) for _ in range(2)]
         self.recvA = [torch.zeros(self.rowsA * self.wa, dtype=i32, device=dev) for _ in range(2)]
-        self.sendB = torch.zeros(self.rowsB * self.wa, dtype=i32, device=dev)
-        self.recvB = torch.zeros(self.rowsB * self.wa, dtype=i32, device=dev)
+        self.sendB = torch.zeros(self.rowsB * self.wb, dtype=i32, device=dev)
+        self.recvB = torch.zeros(self.rowsB * self.wb, dtype=i32, device=dev)
         _check(lib.gs_shard_bind(h, self.sendA[0].data_ptr(), self.sendA[1].data_ptr(),
                                  self.recvA[0].data_ptr(), self.recvA[1].data_ptr(),
                                  self.sendB.data_ptr(), self.recvB.data_ptr()))
@@ -87,7 +109,8 @@ class _Shard:
         sub-block); the part's world sub-blocks are contiguous."""
         # (info[2] "capP" here = rows per sub-block: row slots + flag rows)
         rows = self.capP + (self.idrows if which == "A" and h == self.parts - 1 else 0)
-        return h * self.world * self.capP * self.wa, rows * self.wa
+        w = self.wa if which == "A" else self.wb
+        return h * self.world * self.capP * w, rows * w
 
     def close(self):
         if self.h:
@@ -269,7 +292,7 @@ class ShardedNetwork:
         if self._delivered or self.round == 0:
             return
         t = self.round
-        if t == 1:
+        if t == 1 and not self.shards[0].codes:  # (code rows carry no ids)
             self._pendA.append(self._exchange("A", self.parts - 1, 0))
         for w in self._pendA:
             self._wait(w)

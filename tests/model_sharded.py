@@ -112,22 +112,20 @@ class ShardModel(Model):
         """Exchanges A and B of the current round (needs self.tg of round t)."""
         if self.exchanged or not self.deliver_pending:
             return
+        if self.codes:
+            return self.exchange_codes()
         G, cap, P = self.world, self.cap, self.parts
         sendA, recvA = [], []  # [part][rank] sub-blocks
         for h in range(P):
             sa = [[] for _ in range(G)]
             for x in self.part(h):
                 if not self.fl[x] & DEAD:
-                    row = [push_code(*self.cls(x), self.M)] if self.codes else list(self.cls(x))
-                    sa[self.owner(self.tg[x])].append([x] + row)
-            width = 2 if self.codes else 4
+                    sa[self.owner(self.tg[x])].append([x] + list(self.cls(x)))
             for blk in sa:
                 assert len(blk) <= cap, "block capacity exceeded (the engine flags a device limit)"
-                blk.extend([[-1] + [0] * (width - 1)] * (cap - len(blk)))
+                blk.extend([[-1, 0, 0, 0]] * (cap - len(blk)))
             sendA.append(sa)
-            recvA.append(self.a2a(sa, width))
-            if self.codes:  # the receiver decodes each code into class planes
-                recvA[-1] = [[[r[0]] + list(decode_code(r[1])) for r in blk] for blk in recvA[-1]]
+            recvA.append(self.a2a(sa, 4))
         # pushers in (source rank, part, index) order = ascending source order
         rows = [r for s in range(G) for h in range(P) for r in recvA[h][s] if r[0] >= 0]
         srcs = [r[0] for r in rows]
@@ -143,16 +141,78 @@ class ShardModel(Model):
         for h in range(P):  # B_h answers A_h's rows in the same sub-blocks
             sendB = [[[r[0]] + list(self.pull_row(tgt[r[0]], r[0], ins[tgt[r[0]]]))
                       if r[0] >= 0 else [-1, 0, 0] for r in blk] for blk in recvA[h]]
-            if self.codes:  # one u32 code per pull row
-                sendB = [[[r[0], r[1] | (r[2] << 16)] for r in blk] for blk in sendB]
-            recvB = self.a2a(sendB, 2 if self.codes else 3)
+            recvB = self.a2a(sendB, 3)
             for d in range(G):
                 assert [r[0] for r in recvB[d]] == [r[0] for r in sendA[h][d]], "B order = A order"
-                for r in recvB[d]:
-                    if r[0] >= 0:
-                        pull[r[0]] = (r[1] & 0xFFFF, r[1] >> 16) if self.codes else (r[1], r[2])
+                for x, b0, b1 in recvB[d]:
+                    if x >= 0:
+                        pull[x] = (b0, b1)
         self.ins, self.pull = ins, pull
         self.exchanged = True
+
+    def exchange_codes(self):
+        """Code rows: an A row is (push code, target local to the receiving
+        rank | mutual << 31) -- no source id: the receiver orders a target's
+        pushers by slot key (source rank, part, index), which is ascending
+        source order, and knows t(z)'s pusher by the mutual bit the sender set
+        (t(t(x)) == x); a B row is the pull code, in the same slot."""
+        G, cap, P = self.world, self.cap, self.parts
+        EMPTY = 0xFFFFFFFF
+        sent = []  # [part][rank] -> the sources of the rows, in slot order (the plan's SPOSB)
+        recvA = []
+        for h in range(P):
+            sa = [[] for _ in range(G)]
+            xs = [[] for _ in range(G)]
+            for x in self.part(h):
+                if not self.fl[x] & DEAD:
+                    t = self.tg[x]
+                    d = self.owner(t)
+                    mutual = self.peer_fn(self.seed, self.epoch, self.round, t, self.n) == x
+                    sa[d].append([push_code(*self.cls(x), self.M), (t - d * self.chunk) | (mutual << 31)])
+                    xs[d].append(x)
+            for blk in sa:
+                assert len(blk) <= cap, "block capacity exceeded (the engine flags a device limit)"
+                blk.extend([[0, EMPTY]] * (cap - len(blk)))
+            sent.append(xs)
+            recvA.append(self.a2a([[[c, w - (1 << 32) if w >= 1 << 31 else w] for c, w in blk] for blk in sa], 2))
+        ins = {z: [] for z in self.owned()}
+        tz = {}  # the receiver's t(z), known only through the mutual bit
+        for s in range(G):
+            for h in range(P):
+                for i, (code, w) in enumerate(recvA[h][s]):
+                    w &= 0xFFFFFFFF
+                    if w == EMPTY:
+                        continue
+                    z = self.lo + (w & 0x7FFFFFFF)
+                    assert self.lo <= z < self.lo + self.m, "row sent to a rank that does not own its target"
+                    key = (s * P + h) * cap + i
+                    ins[z].append((key, w >> 31, decode_code(code & 0xFFFFFFFF)))
+        pull = {}
+        for h in range(P):  # B_h answers A_h's rows in the same sub-blocks
+            sendB = []
+            for s in range(G):
+                blk = []
+                for i, (code, w) in enumerate(recvA[h][s]):
+                    w &= 0xFFFFFFFF
+                    if w == EMPTY:
+                        blk.append([0, 0])
+                        continue
+                    z, key = self.lo + (w & 0x7FFFFFFF), (s * P + h) * cap + i
+                    b0, b1 = self.pull_row(z, key, [(k, c) for k, _, c in ins[z]])
+                    blk.append([0, b0 | (b1 << 16)])
+                sendB.append(blk)
+            recvB = self.a2a(sendB, 2)
+            for d in range(G):
+                for x, r in zip(sent[h][d], recvB[d]):
+                    pull[x] = (r[1] & 0xFFFF, r[1] >> 16)
+        # deliveries see pushers by slot key; t(z)'s pusher carries z's own
+        # target as its identity (the engine's zi from the mutual bit)
+        self.ins = {z: [(self.tg_of(z) if m else -1 - k, c) for k, m, c in lst] for z, lst in ins.items()}
+        self.pull = pull
+        self.exchanged = True
+
+    def tg_of(self, z):
+        return self.tg[z]
 
     def deliver(self, x):
         pulled = not self.fl[x] & NOPULL

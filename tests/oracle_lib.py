@@ -321,14 +321,15 @@ def digest_of(codes, recs, psize, stats):
         [(recs, 15)] + [(recs, b) for b in range(5)] + [(recs, b) for b in range(7, 12)]
     weights = np.uint64(1) << np.arange(64, dtype=np.uint64)
     h = np.zeros(n, dtype=np.uint64)
+    acc = np.zeros((n, W), dtype=np.uint64)
     with np.errstate(over="ignore"):
         for p, (arr, b) in enumerate(bits):
             v = ((arr.astype(np.uint64) >> np.uint64(b)) & np.uint64(1))
             v = np.concatenate([v, np.zeros((n, W * 64 - R), dtype=np.uint64)], axis=1).reshape(n, W, 64)
             words = (v * weights).sum(axis=2, dtype=np.uint64)  # distinct bits: the sum is the OR
-            for j in range(W):
-                salt = mix(np.uint64(((j << 8) | p) + 0x632BE59BD9B4E019))
-                h = h + mix(words[:, j] ^ salt)
+            acc = acc + words * np.uint64((0x9E3779B97F4A7C15 * (2 * p + 1)) % (1 << 64))
+        for j in range(W):
+            h = h + mix(acc[:, j] ^ mix(np.uint64(j + 0x632BE59BD9B4E019)))
         h = h + mix(np.uint64(1 << 63) | psize.astype(np.uint64))
         for i in range(5):
             h = h + mix(stats[:, i].astype(np.uint64) ^ np.uint64((0x9E3779B97F4A7C15 * (i + 1)) % (1 << 64)))

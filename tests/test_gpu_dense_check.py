@@ -26,40 +26,57 @@ def _first_bad(a, b):
     return None if bad.size == 0 else (int(bad[0]), bad.size)
 
 
-def _run(engine, net, n, R, faults, max_rounds, every=1, epoch=0, dumps=False):
-    """Inject every rumor at its Philox origin, then run both programs round
-    by round; returns the rounds run.  The engine's digest after round t is
+# rounds to termination and first round of full spread at seed 0x5AFE6055,
+# epoch 1, every rumor injected in round 1 at its Philox origin: the spread
+# record bench.py prints for configs 3 and 4 (it times and spreads epoch 1)
+SPREAD = {(1 << 20, 64): (22, 16), (1 << 24, 256): (34, 18)}
+
+
+def _run(engine, nets, n, R, faults, max_rounds, every=1, epoch=0, dumps=False, spread=None):
+    """Inject every rumor at its Philox origin into every engine of `nets`
+    (one network each) and into the dense program, then run them round by
+    round; returns the rounds run.  An engine's digest after round t is
     compared with the one dense's round t+1 computes on the way (the same
     deliveries, before its transition)."""
     thr = [engine.fault_threshold(p) for p in faults] if faults else None
     dn = DenseNet(n, R, seed=SEED, epoch=epoch, faults=thr)
 
-    def check(g, c, rnd):
-        bad = _first_bad(g, c)
-        assert bad is None, f"round {rnd}: {bad[1]} nodes differ, first {bad[0]}"
+    def check(gs, c, rnd):
+        for i, g in enumerate(gs):
+            bad = _first_bad(g, c)
+            assert bad is None, f"net {i}, round {rnd}: {bad[1]} nodes differ, first {bad[0]}"
     try:
         for r in range(R):
             x = engine.origin_of(SEED, epoch, r, n)
-            net.send_new(x, r)
+            for net in nets:
+                net.send_new(x, r)
             dn.send_new(x, r)
         prev = None
+        r_full = 0
         for rnd in range(1, max_rounds + 1):
-            rep = net.next_round()
+            reps = [net.next_round() for net in nets]
+            if spread is not None and not r_full and nets[0].known_counts()[1] == n:
+                r_full = rnd
             if prev is not None:
                 live, before = dn.next_round(digest=True)
                 check(prev, before, rnd - 1)
             else:
                 live = dn.next_round()
-            assert rep.any_live == live, f"round {rnd}: any_live"
+            for i, rep in enumerate(reps):
+                assert rep.any_live == live, f"net {i}, round {rnd}: any_live"
             prev = None
             if rnd % every == 0 or not live or rnd == max_rounds:
-                prev = net.state_digest()
+                prev = [net.state_digest() for net in nets]
                 if dumps:  # the GPU digest is the digest of its own dumps
-                    codes, st = net.dump_state(), net.statistics_all()
-                    rec, ps = net.dump_records()
-                    np.testing.assert_array_equal(prev, digest_of(codes, rec, ps, st))
+                    for net, g in zip(nets, prev):
+                        codes, st = net.dump_state(), net.statistics_all()
+                        rec, ps = net.dump_records()
+                        np.testing.assert_array_equal(g, digest_of(codes, rec, ps, st))
             if not live or rnd == max_rounds:
                 check(prev, dn.digest(), rnd)
+                if spread is not None:
+                    assert nets[0].known_counts() == (n * R, n), "full dissemination at termination"
+                    assert (rnd, r_full) == spread, f"spread record {(rnd, r_full)}"
                 return rnd
         return max_rounds
     finally:
@@ -76,7 +93,7 @@ def _run(engine, net, n, R, faults, max_rounds, every=1, epoch=0, dumps=False):
 def test_digest_small(engine, n, R, faults):
     net = engine.Network(n, R, seed=SEED, **_fk(faults))
     try:
-        _run(engine, net, n, R, faults, 60, dumps=True)
+        _run(engine, [net], n, R, faults, 60, dumps=True)
     finally:
         net.close()
 
@@ -85,46 +102,30 @@ def _fk(faults):
     return dict(churn=faults[0], drop_push=faults[1], drop_pull=faults[2]) if faults else {}
 
 
-def test_config3_to_termination(engine):
-    # config 3: 2^20 x 64, every round until no live push
-    n, R = 1 << 20, 64
-    net = engine.Network(n, R, seed=SEED)
+@pytest.mark.parametrize("n,R", [(1 << 20, 64), (1 << 24, 256)])
+def test_to_termination(engine, n, R):
+    # configs 3 and 4 (the bench line) at the bench's epoch, every round until
+    # no live push (the harness's termination, src/gossiper.rs:209-212); the
+    # spread record is the one the bench prints
+    net = engine.Network(n, R, seed=SEED, epoch=1)
     try:
-        assert _run(engine, net, n, R, None, 60) < 60
-    finally:
-        net.close()
-
-
-def test_config4_to_termination(engine):
-    # config 4 (the bench line): 2^24 x 256, every round until no live push
-    n, R = 1 << 24, 256
-    net = engine.Network(n, R, seed=SEED)
-    try:
-        assert _run(engine, net, n, R, None, 60) < 60
+        assert _run(engine, [net], n, R, None, 60, epoch=1, spread=SPREAD[(n, R)]) < 60
     finally:
         net.close()
 
 
 def test_config5_faults_rounds(engine):
-    # config 5: 10^8 x 16 with 1 % churn / push drop / pull drop, 10 rounds
-    # (the DLV build and the packed round kernel)
-    n, R = 100_000_000, 16
-    faults = (0.01, 0.01, 0.01)
-    net = engine.Network(n, R, seed=SEED, **_fk(faults))
-    try:
-        _run(engine, net, n, R, faults, 10)
-    finally:
-        net.close()
-
-
-def test_config5_code_row_shards(engine):
-    # config 5 over 4 code-row shards on one GPU (device-copy exchanges, 2
-    # pipeline parts each): the multi-GPU layout at full size, 8 rounds
+    # config 5: 10^8 x 16 with 1 % churn / push drop / pull drop, 8 rounds, on
+    # the single engine (the DLV build and the packed round kernel) and on 4
+    # code-row node shards of the same network (one GPU, device-copy
+    # exchanges, 2 pipeline parts each: the multi-GPU layout at full size)
     from safe_gossip_amd.sharded import ShardedNetwork
     n, R = 100_000_000, 16
     faults = (0.01, 0.01, 0.01)
-    net = ShardedNetwork(n, R, 4, seed=SEED, transport="local", parts=2, **_fk(faults))
+    single = engine.Network(n, R, seed=SEED, **_fk(faults))
+    shards = ShardedNetwork(n, R, 4, seed=SEED, transport="local", parts=2, **_fk(faults))
     try:
-        _run(engine, net, n, R, faults, 8, every=2)
+        _run(engine, [single, shards], n, R, faults, 8, every=2)
     finally:
-        net.close()
+        shards.close()
+        single.close()

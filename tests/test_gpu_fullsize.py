@@ -2,14 +2,14 @@
 kernel against the one-node-per-lane one at a config-5-shaped size.
 
 Configs 3 and 4 (2^20 x 64, 2^24 x 256: the bench workload) are too large for
-the oracle; they are run to termination and checked every round by the
-accounting laws of the reference that a lost, duplicated or misrouted copy
-breaks (src/gossip.rs:80,103,139,155): Statistics.rounds = rounds x n, every
-full copy sent is received, at most one empty pull per push, known sets only
-grow, the processed flag (src/gossiper.rs:209-212) agrees with the empty-push
-count, and no device limit is hit; at termination every node knows every
-rumor, the spread follows Karp et al.'s bound, and the spread record equals
-the one the bench prints.
+the oracle; here their first rounds are checked by the accounting laws of the
+reference that a lost, duplicated or misrouted copy breaks
+(src/gossip.rs:80,103,139,155): Statistics.rounds = rounds x n, every full copy
+sent is received, known sets only grow, the processed flag
+(src/gossiper.rs:209-212) agrees with the empty-push count, and no device limit
+is hit.  Bit-exact checks of configs 3, 4 and 5 at full size, to termination,
+are in test_gpu_dense_check.py (against oracle/gs_dense.c, which
+test_dense_cpu.py holds equal to the oracle).
 
 The packed DLV kernel (gs_dlv4.hip) is checked bit-exactly against the per-node
 kernel of gs_kernels.hip -- itself bit-exact against the oracle at oracle sizes
@@ -45,64 +45,6 @@ def test_full_size_accounting(engine, n, R, rounds):
             prev_known, prev = known, st
         t, _ = net.known_counts()
         assert t > R * 3 ** (rounds - 2)
-        net.sync()  # no device limit hit
-    finally:
-        net.close()
-
-
-# rounds to termination and first round of full spread at seed 0x5AFE6055 with
-# every rumor injected in round 1 at its Philox origin (the bench's spread
-# record for config 4; config 3 pinned from its first GPU run)
-SPREAD = {(1 << 20, 64): (21, 16), (1 << 24, 256): (34, 18)}
-
-
-@pytest.mark.parametrize("n,R", [(1 << 20, 64), (1 << 24, 256)])
-def test_full_size_to_termination(engine, n, R):
-    # configs 3 and 4 run until no node pushes a live rumor (the harness's
-    # termination, src/gossiper.rs:209-212), every round checked by the
-    # accounting laws (device reductions; per-node known counts, and the
-    # whole known sets every 8th round), then the spread record
-    import math
-    net = engine.Network(n, R, seed=SEED)
-    try:
-        for r in range(R):
-            net.send_new(engine.origin_of(SEED, 0, r, n), r)
-        prev_cnt = net.known_popcounts()
-        prev_known = net.known_all()
-        prev = net.statistics_reduce("sum")
-        r_full = 0
-        rnd = 0
-        while True:
-            rep = net.next_round()
-            rnd += 1
-            assert rep.round == rnd and rnd <= 200
-            st = net.statistics_reduce("sum")
-            assert st.rounds == rnd * n, f"round {rnd}: Statistics.rounds"
-            assert st.full_message_received == st.full_message_sent, f"round {rnd}: copies lost"
-            d_empty_push = st.empty_push_sent - prev.empty_push_sent
-            assert rep.any_live == (d_empty_push < n), f"round {rnd}: processed flag"
-            assert st.empty_pull_sent - prev.empty_pull_sent <= n, f"round {rnd}: one pull batch per push"
-            cnt = net.known_popcounts()
-            assert np.all(cnt >= prev_cnt), f"round {rnd}: a node's known set shrank"
-            if rnd % 8 == 0 or not rep.any_live:
-                known = net.known_all()
-                assert not np.any(prev_known & ~known), f"round {rnd}: a known rumor was lost"
-                prev_known = known
-            tot, complete = net.known_counts()
-            assert tot == int(cnt.sum(dtype=np.uint64))
-            if not r_full and complete == n:
-                r_full = rnd
-            prev_cnt, prev = cnt, st
-            if not rep.any_live:
-                break
-        assert net.known_counts() == (n * R, n), "full dissemination at termination"
-        cmax, maxc, maxr = net.params
-        # Karp et al.: log3(n) + O(ln ln n) rounds to full spread, and the
-        # median-counter rule stops within max_rounds of it
-        assert r_full <= math.log(n, 3) + 2 * math.log(math.log(n)) + 2
-        assert rnd <= r_full + maxr
-        print(f"spread n={n} R={R}: {rnd} rounds, full spread at round {r_full}")
-        assert (rnd, r_full) == SPREAD[(n, R)]
         net.sync()  # no device limit hit
     finally:
         net.close()
