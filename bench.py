@@ -338,7 +338,9 @@ def main():
 
     # PMC traffic of the same kernel from the committed rocprofv3 run of this
     # workload (profiles/summarize.py writes one file per (nodes, rumors))
-    traffic = None
+    # (rocprofv3 cannot profile the process it runs in: the counters come from
+    # a separate run of this same workload, named with its commit below)
+    traffic = traffic_src = None
     for name in (f"pmc_n{n}_r{R}.json", "pmc_latest.json"):
         pmc_path = os.path.join(REPO, "profiles", name)
         if traffic is None and os.path.exists(pmc_path) and world == 1 and best["mode"] == "single":
@@ -346,8 +348,11 @@ def main():
                 pmc = json.load(open(pmc_path))
                 if pmc.get("nodes") == n and pmc.get("rumors") == R:
                     traffic = pmc.get("hbm_bytes_per_launch")
+                    traffic_src = {"file": "profiles/" + name, "profile": pmc.get("tag"),
+                                   "commit": pmc.get("commit"),
+                                   "kernel_avg_ms_rocprof": pmc.get("kernel_avg_ms_rocprof")}
             except Exception:
-                traffic = None
+                traffic = traffic_src = None
 
     cpu = cpu_best_line = None
     if rank == 0 and world == 1 and dist is None and not args.no_cpu_baseline:
@@ -385,7 +390,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                 "step_frac": step_frac,
                 "kernel": best["name"] + " (deliver round t + transition to t+1)",
                 "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": best["bytes_per"],

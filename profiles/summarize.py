@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--rumors", type=int, default=256)
     ap.add_argument("--dominant", default=DOMINANT, help="substring of the dominant kernel's name")
     ap.add_argument("--no-latest", action="store_true", help="do not update profiles/pmc_latest.json")
+    ap.add_argument("--commit", default=None,
+                    help="commit of the profiled tree (default: this repository's HEAD, for a run "
+                         "of a committed tree)")
     ap.add_argument("--skip-first", type=int, default=2,
                     help="dominant-kernel launches before the timed window (the bench's warmup "
                          "rounds that deliver: warmup 3 -> 2), left out of the PMC means")
@@ -60,7 +63,12 @@ def main():
         f = pmc[dom]["FETCH_SIZE_KiB_mean"] * 1024
         w = pmc[dom]["WRITE_SIZE_KiB_mean"] * 1024
         dom_ms = next(k["avg_ms"] for k in kernels if a.dominant in k["name"])
-        latest = dict(tag=a.tag, kernel=dom, nodes=a.nodes, rumors=a.rumors,
+        commit = a.commit
+        if commit is None:
+            import subprocess
+            commit = subprocess.run(["git", "-C", HERE, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                                    text=True).stdout.strip() or None
+        latest = dict(tag=a.tag, commit=commit, kernel=dom, nodes=a.nodes, rumors=a.rumors,
                       fetch_bytes_raw=f, write_bytes=w, hbm_bytes_per_launch=2 * f + w,
                       kernel_avg_ms_rocprof=dom_ms,
                       hbm_gbs=(2 * f + w) / (dom_ms * 1e-3) / 1e9,
