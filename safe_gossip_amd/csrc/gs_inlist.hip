@@ -70,8 +70,9 @@ GS_DEV uint32_t target_of(const InListArgs &a, uint32_t x) {
 // shard it is slot key x of exchange A, read from its row (empty slot: no
 // edge); its source field carries kRowMutual when the pusher is its target's
 // own target (the receiver's t(y), src/message_state.rs:79).
+template <bool SH>
 GS_DEV void dlv_source(const InListArgs &a, uint32_t x, uint32_t &t, uint32_t &code, uint32_t &src) {
-    if (a.rowsA) {
+    if constexpr (SH) {
         t = kTgDead;
         code = 0u;
         src = x;
@@ -83,12 +84,12 @@ GS_DEV void dlv_source(const InListArgs &a, uint32_t x, uint32_t &t, uint32_t &c
                 src = x | (r.y & kRowMutual);
             }
         }
-        return;
+    } else {
+        t = target_of(a, x);
+        a.tg[x] = t;
+        code = a.PC[x];
+        src = x;
     }
-    t = target_of(a, x);
-    a.tg[x] = t;
-    code = a.PC[x];
-    src = x;
 }
 
 // Per-target record emission, shared by both paths.  `lst` holds y's k
@@ -546,8 +547,9 @@ __host__ __device__ inline PullArrays pull_arrays(uint32_t *region, uint32_t nb)
                       base + 2 * pc + (size_t)nb * kBin / 2};
 }
 
-// NT threads per block (GS_COARSE_THREADS): 512 lets three blocks share a CU
-template <uint32_t NT>
+// NT threads per block (GS_COARSE_THREADS): 512 lets three blocks share a CU;
+// SH: a code-row shard's build (sources = slot keys, dlv_source)
+template <uint32_t NT, bool SH = false>
 __global__ __launch_bounds__(NT) void dl_coarse(InListArgs a) {
     constexpr uint32_t kPer = kPartChunk / NT;
     static_assert(kPartChunk % NT == 0 && kMaxCoarse <= NT, "dl_coarse: whole sources, a scan slot per bucket");
@@ -570,7 +572,7 @@ __global__ __launch_bounds__(NT) void dl_coarse(InListArgs a) {
         cv[q] = 0u;
         xs[q] = x;
         if (x < p.n) {
-            dlv_source(a, x, tv[q], cv[q], xs[q]);
+            dlv_source<SH>(a, x, tv[q], cv[q], xs[q]);
             if (!(tv[q] & kTgDead)) atomicAdd(&cnt[(tv[q] & kTgMask) >> kCoarseLog], 1u);
         }
     }
@@ -598,7 +600,7 @@ __global__ __launch_bounds__(NT) void dl_coarse(InListArgs a) {
         if (tv[q] & kTgDead) continue;
         const uint32_t t = tv[q] & kTgMask;
         const uint32_t pos = atomicAdd(&cnt[t >> kCoarseLog], 1u);
-        sx[pos] = xs[q];
+        sx[pos] = SH ? xs[q] : lo + threadIdx.x + q * NT;
         st[pos] = t;
         sc[pos] = cv[q];
     }
@@ -707,6 +709,7 @@ __global__ __launch_bounds__(NT) void dl_fine(InListArgs a) {
 // the 2^sub parts of every bin that inl_sort_dlv sorts (dl_coarse + dl_fine in
 // one pass; the regions stay in cache at this size).
 constexpr uint32_t kDirectParts = kInlThreads;  // nb << sub <= 1024 (one scan slot per part)
+template <bool SH = false>
 __global__ __launch_bounds__(kInlThreads) void dl_direct(InListArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
     uint32_t *sx = sh, *sc = sh + kPartChunk;
@@ -728,7 +731,7 @@ __global__ __launch_bounds__(kInlThreads) void dl_direct(InListArgs a) {
         cv[q] = 0u;
         xs[q] = x;
         if (x < p.n) {
-            dlv_source(a, x, tv[q], cv[q], xs[q]);
+            dlv_source<SH>(a, x, tv[q], cv[q], xs[q]);
             if (!(tv[q] & kTgDead)) atomicAdd(&cnt[(tv[q] & kTgMask) >> plog], 1u);
         }
     }
@@ -755,7 +758,7 @@ __global__ __launch_bounds__(kInlThreads) void dl_direct(InListArgs a) {
         if (tv[q] & kTgDead) continue;
         const uint32_t t = tv[q] & kTgMask, b = t >> plog;
         const uint32_t pos = atomicAdd(&cnt[b], 1u);
-        sx[pos] = xs[q];
+        sx[pos] = SH ? xs[q] : lo + threadIdx.x + q * kInlThreads;
         sc[pos] = cv[q];
         slt[pos] = (uint16_t)(t & (kBin - 1u));  // (relative to the bin)
         sb[pos] = (uint16_t)b;
@@ -811,7 +814,7 @@ inline uint32_t dlv_split_log(uint32_t nb) {
 // while the current one's records and pulls are computed (one block per CU
 // holds the LDS of a half bin, so without this a CU's loads and its LDS work
 // take turns).
-template <uint32_t SL, bool OWN, bool PP = false>
+template <uint32_t SL, bool OWN, bool PP = false, bool SH = false>
 // (own quarter-bin regions: two blocks per CU, 48 KiB of LDS and
 // <= 64 VGPRs each; the second bound is waves per SIMD)
 __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sort_dlv(InListArgs a) {
@@ -867,7 +870,7 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
     const uint32_t *S32 = reinterpret_cast<const uint32_t *>(a.S);
     // (code-row shard: targets are the ntargets local nodes, p.n may be
     // larger -- the slot keys -- and t(y)'s pusher is flagged in its row)
-    const uint32_t ny = a.rowsA ? a.ntargets : p.n;
+    const uint32_t ny = SH ? a.ntargets : p.n;
     auto load_targets = [&](uint32_t wp) {
         const uint32_t t0p = wp << kHalfLog;
         const uint32_t np = t0p < ny ? min(kHalf, ny - t0p) : 0u;
@@ -877,7 +880,7 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
             const uint32_t y = np ? t0p + (lt < np ? lt : 0u) : 0u;  // (a part past the last node: node 0)
             const uint32_t ysh = (y & ((1u << a.g.lognpu) - 1u)) << a.g.logr;
             const u64 rb = (u64)(y >> a.g.lognpu) * kPlanes * 2u + (ysh >> 5);
-            tgv[q] = a.rowsA ? 0u : a.tg[y];
+            tgv[q] = SH ? 0u : a.tg[y];
             w0[q] = S32[rb];
             w1[q] = S32[rb + 2];
             w2[q] = S32[rb + 4];
@@ -955,7 +958,7 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
         for (uint32_t j = s + 1; j < e; ++j) {  // insertion sort of (id, code) by id
             const uint32_t v = sid[j], vc = scd[j];
             uint32_t r = j;
-            while (r > s && (sid[r - 1] & kIdMask) > (v & kIdMask)) {  // (bit 31: kRowMutual)
+            while (r > s && (SH ? (sid[r - 1] & kIdMask) > (v & kIdMask) : sid[r - 1] > v)) {  // (SH: bit 31 kRowMutual)
                 sid[r] = sid[r - 1];
                 scd[r] = scd[r - 1];
                 --r;
@@ -972,7 +975,7 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
         const uint32_t first = (mt && cur != kNone) ? cur : 0u;
         uint32_t zi = kDlvNoZ;
         for (uint32_t j = 0; j < k; ++j) {
-            if (a.rowsA ? (sid[s + j] & kRowMutual) != 0u : sid[s + j] == tz) zi = j;
+            if (SH ? (sid[s + j] & kRowMutual) != 0u : sid[s + j] == tz) zi = j;
             if (j >= kDlvInline && cur != kNone) a.dtail[first + j - kDlvInline] = scd[s + j];
         }
         if (mt && cur != kNone) cur += mt;
@@ -1001,13 +1004,13 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
             pC |= nw & vC;
             pnot &= ~sl;
             // an empty pull batch is not passed back: PULL[] reads 0 for it
-            if (!direct && scd[j]) atomicAdd(&pcnt[(sid[j] & kIdMask) >> kCoarseLog], 1u);
+            if (!direct && scd[j]) atomicAdd(&pcnt[(SH ? sid[j] & kIdMask : sid[j]) >> kCoarseLog], 1u);
         }
     }
     __syncthreads();
     if (direct) {  // one coarse bucket: every pull straight into PULL (cache-resident)
         const uint32_t placed = min(total, kHalfCap);
-        if (a.rowsA) {  // a code-row shard: to the pusher's exchange-B slot
+        if constexpr (SH) {  // a code-row shard: to the pusher's exchange-B slot
             uint32_t *pb = a.pullB;
             for (uint32_t j = threadIdx.x; j < placed; j += kInlThreads)
                 pb[shard_key_bslot(a.sr, sid[j] & kIdMask)] = scd[j];
@@ -1026,7 +1029,7 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
     const uint32_t placed = min(total, kHalfCap);
     for (uint32_t j = threadIdx.x; j < placed; j += kInlThreads) {
         if (!scd[j]) continue;  // empty pull (pb_place zero-fills)
-        const uint32_t x = sid[j] & kIdMask, cb = x >> kCoarseLog;
+        const uint32_t x = SH ? sid[j] & kIdMask : sid[j], cb = x >> kCoarseLog;
         const uint32_t slot = pres[cb] + atomicAdd(&pcnt[cb], 1u);  // < 2^kCoarseLog: one per source
         const u64 o = ((u64)cb << kCoarseLog) + slot;
         pa.x[o] = x;
@@ -1103,6 +1106,7 @@ __global__ __launch_bounds__(kInlThreads) void pb_fine(InListArgs a) {
 // back (while a dissemination is young most pulls are empty): a slot nobody
 // wrote is an empty pull, or one not delivered this round, which the round
 // kernel ignores.
+template <bool SH = false>
 __global__ __launch_bounds__(kInlThreads) void pb_place(InListArgs a) {
     __shared__ uint32_t img[kBin];
     const CsrPlan &p = a.p;
@@ -1117,7 +1121,7 @@ __global__ __launch_bounds__(kInlThreads) void pb_place(InListArgs a) {
     }
     __syncthreads();
     const uint32_t x0 = b << kBinLog;
-    if (a.rowsA) {  // a code-row shard: sources are slot keys, pulls go to their exchange-B slots
+    if constexpr (SH) {  // a code-row shard: sources are slot keys, pulls go to their exchange-B slots
         const uint32_t keys = x0 < a.nkeys ? min(kBin, a.nkeys - x0) : 0u;
         for (uint32_t i = threadIdx.x; i < keys; i += kInlThreads) a.pullB[shard_key_bslot(a.sr, x0 + i)] = img[i];
         return;
@@ -1467,9 +1471,84 @@ hipError_t launch_build_sort(const InListArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// The DLV build (binned plan, p.dlv): partitions, the part sorts with the
+// records and pulls, the pull pass-back.  SH: a code-row shard's build.
+template <bool SH>
+hipError_t launch_dlv_build(const InListArgs &a, hipStream_t s) {
+    const CsrPlan &p = a.p;
+    const uint32_t dsl = dlv_split_log(p.nb);
+    const size_t lds_dlv = ((size_t)(kBin >> dsl) / 2 + 2 * (size_t)(kBinCap >> dsl)) * sizeof(uint32_t);
+    const bool own = p.sub != 0u;
+    const void *kd = dsl == kSplitLog
+                         ? (own ? (const void *)inl_sort_dlv<kSplitLog, true, false, SH>
+                                : (const void *)inl_sort_dlv<kSplitLog, false, false, SH>)
+                         : (own ? (const void *)inl_sort_dlv<kDlvSmallLog, true, false, SH>
+                                : (const void *)inl_sort_dlv<kDlvSmallLog, false, false, SH>);
+    hipError_t e = hipFuncSetAttribute(kd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dlv);
+    if (e != hipSuccess) return e;
+    if (a.lvm || a.zl) return hipErrorInvalidValue;  // DLV records gather nothing
+    if (SH && (!a.rowsA || !a.pullB || a.nkeys > p.n || a.ntargets > p.n)) return hipErrorInvalidValue;
+    InListArgs ab = a;
+    // fill counts (both half-bin blocks of a bin read them, so they are
+    // cleared here rather than by the sort), tail count, coarse fills
+    const uint32_t nc = (p.nb + kCoarseBins - 1) / kCoarseBins;
+    if (!a.prezeroed) e = hipMemsetAsync(a.scratch, 0, inlist_sizes(p).scratch_words * sizeof(uint32_t), s);
+    const size_t lds_c = 3 * (size_t)kPartChunk * sizeof(uint32_t);
+    const size_t lds_f = 3 * (size_t)kFineChunk * sizeof(uint32_t);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void *)dl_coarse<kCoarseThreads, SH>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds_c);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void *)dl_fine<kFineThreads>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds_f);
+    if (e != hipSuccess) return e;
+    const bool direct = nc == 1u;  // small n: one pass into the parts, pulls written directly
+    if ((p.sub && p.sub != dsl) || (direct && (!p.sub || (p.nb << p.sub) > kDirectParts)) ||
+        (!direct && p.sub > kMaxFineSub))
+        return hipErrorInvalidValue;
+    if (direct) {
+        const size_t lds_d = (2 * (size_t)kPartChunk + kPartChunk) * sizeof(uint32_t);
+        e = hipFuncSetAttribute((const void *)dl_direct<SH>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_d);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(dl_direct<SH>, dim3(p.ba), dim3(kInlThreads), lds_d, s, ab);
+    } else {
+        if (!a.coarse_done)  // (else the transition launch before partitioned the entries)
+            hipLaunchKernelGGL((dl_coarse<kCoarseThreads, SH>), dim3(p.ba), dim3(kCoarseThreads), lds_c, s, ab);
+        hipLaunchKernelGGL(dl_fine<kFineThreads>, dim3((kShardCap + kFineChunk - 1) / kFineChunk, nc * kCoarseShards),
+                           dim3(kFineThreads), lds_f, s, ab);
+    }
+    void *kargs[] = {&ab};
+    if (GS_DLV_PP && own && !direct && !SH) {  // persistent walk over the parts (A/B)
+        const void *kp = dsl == kSplitLog ? (const void *)inl_sort_dlv<kSplitLog, true, true>
+                                          : (const void *)inl_sort_dlv<kDlvSmallLog, true, true>;
+        e = hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dlv);
+        int dev = 0, cus = 0, per_cu = 0;
+        if (e == hipSuccess) e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, kInlThreads, lds_dlv);
+        if (e != hipSuccess) return e;
+        const u64 items = ((u64)p.n + (kBin >> dsl) - 1) >> (kBinLog - dsl);
+        const uint32_t grid = (uint32_t)std::min<u64>(items, (u64)std::max(1, per_cu) * std::max(1, cus));
+        e = hipLaunchKernel(kp, dim3(grid), dim3(kInlThreads), kargs, lds_dlv, s);
+    } else {
+        e = hipLaunchKernel(kd, dim3(p.nb, 1u << dsl), dim3(kInlThreads), kargs, lds_dlv, s);
+    }
+    if (e != hipSuccess) return e;
+    const size_t lds_pb = ((size_t)kPartChunk + kPartChunk / 2 + kPartChunk / 4) * sizeof(uint32_t);
+    e = hipFuncSetAttribute((const void *)pb_fine, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_pb);
+    if (e != hipSuccess) return e;
+    if (!direct) {
+        hipLaunchKernelGGL(pb_fine, dim3((1u << kCoarseLog) / kPartChunk, nc), dim3(kInlThreads), lds_pb, s, ab);
+        hipLaunchKernelGGL(pb_place<SH>, dim3(p.nb), dim3(kInlThreads), 0, s, ab);
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
     const CsrPlan &p = a.p;
     if (p.n == 0) return hipSuccess;
+    if (p.binned && p.dlv) return a.rowsA ? launch_dlv_build<true>(a, s) : launch_dlv_build<false>(a, s);
+    if (a.rowsA) return hipErrorInvalidValue;  // code-row shards build delivery records only
     if (p.binned) {
         const uint32_t np = p.nb << p.sub;
         const size_t lds_bin = ((size_t)p.chunk + p.chunk / 2 + (np + 1) / 2) * sizeof(uint32_t) +
@@ -1477,99 +1556,28 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s) {
         const void *kb = p.chunk == kChunk ? (const void *)inl_bin<kChunk> : (const void *)inl_bin<kChunkSmall>;
         const uint32_t sl = sort_split_log(p.nb);
         const size_t lds_sort = ((size_t)(kBin >> sl) / 2 + (kBinCap >> sl)) * sizeof(uint32_t);
-        const uint32_t dsl = dlv_split_log(p.nb);
-        const size_t lds_dlv = ((size_t)(kBin >> dsl) / 2 + 2 * (size_t)(kBinCap >> dsl)) * sizeof(uint32_t);
-        const bool own = p.sub != 0u;
-        const void *kd = dsl == kSplitLog
-                             ? (own ? (const void *)inl_sort_dlv<kSplitLog, true> : (const void *)inl_sort_dlv<kSplitLog, false>)
-                             : (own ? (const void *)inl_sort_dlv<kDlvSmallLog, true>
-                                    : (const void *)inl_sort_dlv<kDlvSmallLog, false>);
-        const void *ks = p.dlv ? kd
-                               : (sl == 0   ? (const void *)inl_sort<0, kSortThreads>
-                                  : sl == 1 ? (const void *)inl_sort<1, kSortThreads>
-                                  : sl == 2 ? (const void *)inl_sort<2, kSortThreads>
-                                            : (const void *)inl_sort<3, kSortThreads>);
-        // (inl_bin is the gather path's partition: its LDS, sized by the parts,
-        // is not set for a DLV plan, whose part count it may not fit)
-        hipError_t e = p.dlv ? hipSuccess : hipFuncSetAttribute(kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bin);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute(ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(p.dlv ? lds_dlv : lds_sort));
+        const void *ks = sl == 0   ? (const void *)inl_sort<0, kSortThreads>
+                         : sl == 1 ? (const void *)inl_sort<1, kSortThreads>
+                         : sl == 2 ? (const void *)inl_sort<2, kSortThreads>
+                                   : (const void *)inl_sort<3, kSortThreads>;
+        hipError_t e = hipFuncSetAttribute(kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bin);
+        if (e == hipSuccess) e = hipFuncSetAttribute(ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sort);
         if (e != hipSuccess) return e;
-        if (p.dlv && (a.lvm || a.zl)) return hipErrorInvalidValue;  // DLV records gather nothing
         if ((a.lvm == nullptr) != (a.zl == nullptr) || (a.lvm && !a.cpm)) return hipErrorInvalidValue;
         InListArgs ab = a;
-            if (p.dlv) {
-            // fill counts (both half-bin blocks of a bin read them, so they are
-            // cleared here rather than by the sort), tail count, coarse fills
-            const uint32_t nc = (p.nb + kCoarseBins - 1) / kCoarseBins;
-            if (!a.prezeroed) e = hipMemsetAsync(a.scratch, 0, inlist_sizes(p).scratch_words * sizeof(uint32_t), s);
-            const size_t lds_c = 3 * (size_t)kPartChunk * sizeof(uint32_t);
-            const size_t lds_f = 3 * (size_t)kFineChunk * sizeof(uint32_t);
-            if (e == hipSuccess)
-                e = hipFuncSetAttribute((const void *)dl_coarse<kCoarseThreads>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_c);
-            if (e == hipSuccess)
-                e = hipFuncSetAttribute((const void *)dl_fine<kFineThreads>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f);
+        if (sl > 0) {  // the split sort cannot clear the fill counts itself
+            if (p.sub != sl) return hipErrorInvalidValue;
+            if (!a.prezeroed)
+                e = hipMemsetAsync(a.scratch + p.fill_off, 0, ((size_t)p.nb << p.sub) * sizeof(uint32_t), s);
             if (e != hipSuccess) return e;
-            const bool direct = nc == 1u;  // small n: one pass into the parts, pulls written directly
-            if ((p.sub && p.sub != dsl) || (direct && (!p.sub || (p.nb << p.sub) > kDirectParts)) ||
-                (!direct && p.sub > kMaxFineSub))
-                return hipErrorInvalidValue;
-            if (direct) {
-                const size_t lds_d = (2 * (size_t)kPartChunk + kPartChunk) * sizeof(uint32_t);
-                e = hipFuncSetAttribute((const void *)dl_direct, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)lds_d);
-                if (e != hipSuccess) return e;
-                hipLaunchKernelGGL(dl_direct, dim3(p.ba), dim3(kInlThreads), lds_d, s, ab);
-            } else {
-                if (!a.coarse_done)  // (else the transition launch before partitioned the entries)
-                    hipLaunchKernelGGL(dl_coarse<kCoarseThreads>, dim3(p.ba), dim3(kCoarseThreads), lds_c, s, ab);
-                hipLaunchKernelGGL(dl_fine<kFineThreads>,
-                                   dim3((kShardCap + kFineChunk - 1) / kFineChunk, nc * kCoarseShards),
-                                   dim3(kFineThreads), lds_f, s, ab);
-            }
-            void *kargs[] = {&ab};
-            if (GS_DLV_PP && own && !direct) {  // persistent walk over the parts (A/B)
-                const void *kp = dsl == kSplitLog ? (const void *)inl_sort_dlv<kSplitLog, true, true>
-                                                  : (const void *)inl_sort_dlv<kDlvSmallLog, true, true>;
-                e = hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dlv);
-                int dev = 0, cus = 0, per_cu = 0;
-                if (e == hipSuccess) e = hipGetDevice(&dev);
-                if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-                if (e == hipSuccess)
-                    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, kInlThreads, lds_dlv);
-                if (e != hipSuccess) return e;
-                const u64 items = ((u64)p.n + (kBin >> dsl) - 1) >> (kBinLog - dsl);
-                const uint32_t grid = (uint32_t)std::min<u64>(items, (u64)std::max(1, per_cu) * std::max(1, cus));
-                e = hipLaunchKernel(kp, dim3(grid), dim3(kInlThreads), kargs, lds_dlv, s);
-            } else {
-                e = hipLaunchKernel(kd, dim3(p.nb, 1u << dsl), dim3(kInlThreads), kargs, lds_dlv, s);
-            }
-            if (e != hipSuccess) return e;
-            const size_t lds_pb = ((size_t)kPartChunk + kPartChunk / 2 + kPartChunk / 4) * sizeof(uint32_t);
-            e = hipFuncSetAttribute((const void *)pb_fine, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_pb);
-            if (e != hipSuccess) return e;
-            if (!direct) {
-                hipLaunchKernelGGL(pb_fine, dim3((1u << kCoarseLog) / kPartChunk, nc), dim3(kInlThreads), lds_pb, s,
-                                   ab);
-                hipLaunchKernelGGL(pb_place, dim3(p.nb), dim3(kInlThreads), 0, s, ab);
-            }
-        } else {
-            if (sl > 0) {  // the split sort cannot clear the fill counts itself
-                if (p.sub != sl) return hipErrorInvalidValue;
-                if (!a.prezeroed)
-                    e = hipMemsetAsync(a.scratch + p.fill_off, 0, ((size_t)p.nb << p.sub) * sizeof(uint32_t), s);
-                if (e != hipSuccess) return e;
-            }
-            if (p.chunk == kChunk) hipLaunchKernelGGL(inl_bin<kChunk>, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
-            else hipLaunchKernelGGL(inl_bin<kChunkSmall>, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
-            const dim3 gs(p.nb, 1u << sl);
-            if (sl == 0) hipLaunchKernelGGL((inl_sort<0, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
-            else if (sl == 1) hipLaunchKernelGGL((inl_sort<1, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
-            else if (sl == 2) hipLaunchKernelGGL((inl_sort<2, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
-            else hipLaunchKernelGGL((inl_sort<3, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
         }
+        if (p.chunk == kChunk) hipLaunchKernelGGL(inl_bin<kChunk>, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
+        else hipLaunchKernelGGL(inl_bin<kChunkSmall>, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
+        const dim3 gs(p.nb, 1u << sl);
+        if (sl == 0) hipLaunchKernelGGL((inl_sort<0, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
+        else if (sl == 1) hipLaunchKernelGGL((inl_sort<1, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
+        else if (sl == 2) hipLaunchKernelGGL((inl_sort<2, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
+        else hipLaunchKernelGGL((inl_sort<3, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
         return hipGetLastError();
     }
     // the generic path writes no skip flags (live-filtered gathers are binned only)
