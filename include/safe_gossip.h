@@ -323,6 +323,17 @@ gs_status   gs_push_batch(gs_engine *e, uint32_t node, uint8_t *out, uint32_t ca
 gs_status   gs_handle_received(gs_engine *e, uint32_t node, uint32_t peer, const uint8_t *msg,
                                uint32_t msg_len, uint8_t *out, uint32_t cap, uint32_t *out_len,
                                uint32_t *out_count);
+/* A batch of external RPCs in one call, exactly as `count` gs_handle_received
+ * calls in this order (message i = msgs[off[i] .. off[i] + len[i]) from
+ * peers[i] >= n to nodes[i]), with ONE observation launch for every node a
+ * first Push makes answer (instead of one per call): the responses of RPC i
+ * are out[resp_off[i] .. resp_off[i+1]) (frames "u32 LE length + RPC"; n+1
+ * offsets).  All or nothing: a malformed message, an unknown rumor or an
+ * `out` smaller than the responses (GS_ERR_SERIALISATION, *out_len = bytes
+ * needed) applies none of them. */
+gs_status   gs_handle_received_batch(gs_engine *e, uint32_t count, const uint32_t *nodes, const uint32_t *peers,
+                                     const uint8_t *msgs, const uint32_t *off, const uint32_t *len, uint8_t *out,
+                                     uint32_t cap, uint32_t *out_len, uint32_t *resp_off);
 
 /* ---- Signatures (src/messages.rs:28-44): ed25519 over SHA3-512 ----------
  * As ed25519-dalek ~0.6.1 with sha3 ~0.7.2 (not vendored in the reference;

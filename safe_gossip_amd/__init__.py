@@ -118,6 +118,8 @@ SYMBOLS = {
     "gs_push_batch": (ctypes.c_int, [_P, ctypes.c_uint32, _U8P, ctypes.c_uint32, _U32P, _U32P]),
     "gs_handle_received": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_uint32, _U8P, ctypes.c_uint32,
                                           _U8P, ctypes.c_uint32, _U32P, _U32P]),
+    "gs_handle_received_batch": (ctypes.c_int, [_P, ctypes.c_uint32, _U32P, _U32P, _U8P, _U32P, _U32P, _U8P,
+                                                ctypes.c_uint32, _U32P, _U32P]),
     "gs_device": (ctypes.c_int, [_P]),
     "gs_sha3_512": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, _U8P, _U32P, _U32P, _U8P]),
     "gs_ed25519_verify": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, _U8P, _U8P, _U8P, _U32P, _U32P, _U8P]),
@@ -566,6 +568,35 @@ class Network:
                 continue
             _check(st)
             return split_frames(bytes(out)[:n.value])
+
+    def handle_received_batch(self, rpcs) -> List[List[bytes]]:
+        """``handle_received`` for many (node, peer, message bytes) at once, in
+        order (``gs_handle_received_batch``: one observation launch for all
+        first Pushes); returns each RPC's Pull responses."""
+        rpcs = list(rpcs)
+        m = len(rpcs)
+        nodes = np.array([r[0] for r in rpcs], dtype=np.uint32)
+        peers = np.array([r[1] for r in rpcs], dtype=np.uint32)
+        lens = np.array([len(r[2]) for r in rpcs], dtype=np.uint32)
+        offs = np.zeros(m, dtype=np.uint32)
+        if m:
+            offs[1:] = np.cumsum(lens)[:-1]
+        msgs = _buf(b"".join(r[2] for r in rpcs))
+        resp = np.zeros(m + 1, dtype=np.uint32)
+        cap = 4096
+        while True:
+            out = (ctypes.c_uint8 * cap)()
+            n = ctypes.c_uint32()
+            st = self._lib.gs_handle_received_batch(
+                self._h, m, nodes.ctypes.data_as(_U32P), peers.ctypes.data_as(_U32P), msgs,
+                offs.ctypes.data_as(_U32P), lens.ctypes.data_as(_U32P), out, cap, ctypes.byref(n),
+                resp.ctypes.data_as(_U32P))
+            if st == 5 and n.value > cap:  # responses larger than the buffer: nothing was applied
+                cap = n.value
+                continue
+            _check(st)
+            data = bytes(out)[:n.value]
+            return [split_frames(data[resp[i]:resp[i + 1]]) for i in range(m)]
 
     def handle_received_signed(self, node: int, peer: int, peer_key: bytes, message: bytes,
                                node_seed: Optional[bytes] = None) -> List[bytes]:

@@ -1759,9 +1759,185 @@ gs_status observe_node(gs_engine *e, uint32_t node, std::vector<uint16_t> &codes
     return GS_OK;
 }
 
+// Post-delivery state codes of several nodes at once (sorted, distinct): one
+// observation launch over the blocks holding them, codes of nodes[j] at
+// codes[j*R ..], external RPCs queued so far included.
+gs_status observe_nodes(gs_engine *e, const std::vector<uint32_t> &nodes, std::vector<uint16_t> &codes) {
+    const uint32_t m = (uint32_t)nodes.size();
+    codes.assign((size_t)m * e->g.R, 0);
+    if (!m) return GS_OK;
+    gs_status st = upload_ext(e);
+    if (st != GS_OK) return st;
+    std::vector<uint32_t> blocks;
+    for (uint32_t x : nodes) {
+        const uint32_t b = (uint32_t)((e->g.small ? (u64)x : (u64)x * e->g.W) / 256);
+        if (blocks.empty() || blocks.back() != b) blocks.push_back(b);
+    }
+    uint32_t *dev = nullptr;  // [blocks | nodes]
+    uint16_t *dcodes = nullptr;
+    GS_HIP(dalloc(&dev, blocks.size() + m));
+    if (dalloc(&dcodes, (size_t)m * e->g.R) != hipSuccess) {
+        (void)hipFree(dev);
+        return GS_ERR_HIP;
+    }
+    gs::RoundArgs a = base_args(e);
+    a.obs_state = dcodes;
+    a.blk_list = dev;
+    a.blk_count = (uint32_t)blocks.size();
+    a.obs_list = dev + blocks.size();
+    a.n_obs = m;
+    hipError_t he = hipMemcpyAsync(dev, blocks.data(), blocks.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                   e->stream);
+    if (he == hipSuccess)
+        he = hipMemcpyAsync(dev + blocks.size(), nodes.data(), m * sizeof(uint32_t), hipMemcpyHostToDevice,
+                            e->stream);
+    if (he == hipSuccess && e->deliver_pending) {
+        if (built_elsewhere(e)) he = hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0);
+        if (he == hipSuccess && seq_prepare(e) != GS_OK) he = hipErrorUnknown;  // SEQ: the round's pull batches
+    }
+    if (he == hipSuccess) he = gs::launch_round(a, e->deliver_pending ? 2 : 3, e->stream);
+    if (he == hipSuccess)
+        he = hipMemcpyAsync(codes.data(), dcodes, codes.size() * sizeof(uint16_t), hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    (void)hipFree(dev);
+    (void)hipFree(dcodes);
+    return he == hipSuccess ? GS_OK : GS_ERR_HIP;
+}
+
 }  // namespace
 
 extern "C" {
+
+gs_status gs_handle_received_batch(gs_engine *e, uint32_t count, const uint32_t *nodes, const uint32_t *peers,
+                                   const uint8_t *msgs, const uint32_t *off, const uint32_t *len, uint8_t *out,
+                                   uint32_t cap, uint32_t *out_len, uint32_t *resp_off) {
+    if (!e || !out_len || (count && (!nodes || !peers || !msgs || !off || !len || !resp_off)))
+        return GS_ERR_INVALID_ARGUMENT;
+    *out_len = 0;
+    if (e->shard || e->slice) return GS_ERR_UNSUPPORTED;
+    if (e->round == 0 || !e->deliver_pending) return GS_ERR_INVALID_ARGUMENT;  // after a next_round
+    // Decode and check every RPC first: the batch is applied whole or not at all.
+    struct Item {
+        uint32_t node, peer, rumor;
+        uint8_t counter;
+        bool pull, empty, offline, is_new;
+    };
+    std::vector<Item> it(count);
+    std::set<std::pair<uint32_t, uint32_t>> peers_seen(e->ext_peers);
+    std::vector<uint32_t> obs;
+    for (uint32_t i = 0; i < count; ++i) {
+        Item &v = it[i];
+        v.node = nodes[i];
+        v.peer = peers[i];
+        if (v.node >= e->g.n || v.peer < e->g.n) return GS_ERR_INVALID_ARGUMENT;
+        int pull = 0;
+        uint32_t mo = 0, ml = 0;
+        gs_status st = gs_rpc_decode(msgs + off[i], len[i], &pull, &mo, &ml, &v.counter);
+        if (st != GS_OK) return st;  // Message::deserialise failure (src/gossiper.rs:89-94)
+        v.pull = pull != 0;
+        v.empty = ml == 0 && v.counter == 0;  // src/gossip.rs:153-154
+        v.rumor = 0;
+        if (!v.empty) {
+            auto k = e->key_rumor.find(std::string(reinterpret_cast<const char *>(msgs + off[i] + mo), ml));
+            if (k == e->key_rumor.end()) return GS_ERR_INVALID_ARGUMENT;  // no rumor slot for this message
+            v.rumor = k->second;
+        }
+        // churn: a node the harness took offline this round drops it
+        v.offline = e->faults.churn && gs::offline_of(e->seed, e->epoch, e->round, v.node, e->faults.churn);
+        v.is_new = !v.offline && peers_seen.insert({v.node, v.peer}).second;  // src/gossip.rs:125
+        if (v.is_new && !v.pull) obs.push_back(v.node);
+    }
+    std::sort(obs.begin(), obs.end());
+    obs.erase(std::unique(obs.begin(), obs.end()), obs.end());
+    gs_status st = set_device(e);
+    if (st != GS_OK) return st;
+    // the answering nodes' state with every RPC queued before this batch (one
+    // launch), then this batch's copies applied in call order on the host:
+    // a copy only ever creates an absent entry (B{0,1}, or C when its counter
+    // >= counter_max: src/message_state.rs:62-74) -- records never change
+    // which entries are live, so the Pull responses follow from the codes
+    std::vector<uint16_t> codes;
+    st = observe_nodes(e, obs, codes);
+    if (st != GS_OK) return st;
+    auto codes_of = [&](uint32_t x) {
+        const size_t j = (size_t)(std::lower_bound(obs.begin(), obs.end(), x) - obs.begin());
+        return codes.data() + j * e->g.R;
+    };
+    uint32_t need = 0;
+    auto frames = [&](bool write) {  // responses in call order; returns false when out is too small
+        need = 0;
+        // per answering node, the entries this batch's earlier copies created
+        std::map<uint32_t, std::vector<std::pair<uint32_t, uint16_t>>> over;
+        for (uint32_t i = 0; i < count; ++i) {
+            const Item &v = it[i];
+            if (write) resp_off[i] = need;
+            if (v.offline) continue;
+            if (v.is_new && !v.pull) {  // Pull responses: the node's live entries now (src/gossip.rs:126-148)
+                const uint16_t *c = codes_of(v.node);
+                auto &ov = over[v.node];
+                auto code_at = [&](uint32_t r) {
+                    for (auto &o : ov)
+                        if (o.first == r) return o.second;
+                    return c[r];
+                };
+                uint32_t cnt = 0;
+                for (uint32_t r : e->key_order) {
+                    const uint16_t cr = code_at(r);
+                    const uint32_t tag = cr >> 14;
+                    if (tag == 1 || tag == 2) {
+                        const uint8_t ctr = tag == 1 ? (uint8_t)((cr >> 7) & 0x7Fu) : 255;
+                        if (append_frame(1, e->keys[r], ctr, write ? out : nullptr, write ? cap : 0, &need) != GS_OK &&
+                            write)
+                            return false;
+                        ++cnt;
+                    }
+                }
+                if (cnt == 0 &&
+                    append_frame(1, std::string(), 0, write ? out : nullptr, write ? cap : 0, &need) != GS_OK && write)
+                    return false;
+            }
+            if (!v.empty && std::binary_search(obs.begin(), obs.end(), v.node)) {
+                // the copy creates an absent entry at once (Gossip::receive,
+                // src/gossip.rs:153-163): later responses of this node show it
+                auto &ov = over[v.node];
+                uint16_t cur = codes_of(v.node)[v.rumor];
+                for (auto &o : ov)
+                    if (o.first == v.rumor) cur = o.second;
+                if ((cur >> 14) == 0)  // A: absent -> B{0,1}, or C{0,0} for a counter >= counter_max
+                    ov.emplace_back(v.rumor, v.counter >= e->cmax ? (uint16_t)(2u << 14)
+                                                                   : (uint16_t)((1u << 14) | (1u << 7)));
+            }
+        }
+        if (write) resp_off[count] = need;
+        return true;
+    };
+    frames(false);
+    *out_len = need;
+    if (!out || need > cap) return GS_ERR_SERIALISATION;  // nothing applied; *out_len holds the size needed
+    frames(true);
+    // queue every RPC as gs_handle_received does, in call order
+    for (uint32_t i = 0; i < count; ++i) {
+        const Item &v = it[i];
+        if (v.offline) continue;
+        e->ext_peers.insert({v.node, v.peer});
+        uint32_t info = (v.pull ? 0u : gs::kExtPush) | (v.is_new ? gs::kExtNew : 0u);
+        if (v.empty) {
+            info |= gs::kExtEmpty;
+        } else {
+            e->started = true;
+            info |= v.rumor | ((uint32_t)v.counter << 12) | gs::kExtRec;
+            for (auto &x : e->ext)  // only the last copy from a peer is kept in peer_counters
+                if (x.node == v.node && x.peer == v.peer && !(x.info & gs::kExtEmpty) && (x.info & 0xFFFu) == v.rumor)
+                    x.info &= ~gs::kExtRec;
+        }
+        e->ext.push_back({v.node, (uint32_t)e->ext.size(), info, v.peer});
+    }
+    if (count) {
+        e->ext_uploaded = (uint32_t)-1;  // re-upload
+        e->obs_valid = false;
+    }
+    return GS_OK;
+}
 
 gs_status gs_push_batch(gs_engine *e, uint32_t node, uint8_t *out, uint32_t cap, uint32_t *len,
                         uint32_t *count) {

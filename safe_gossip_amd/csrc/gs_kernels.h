@@ -68,8 +68,13 @@ struct RoundArgs {
     const u64 *ext;
     uint32_t n_ext;
     // launch only blocks [blk_off, blk_off + blk_count) (0: all), and with
-    // obs_only != ~0 observe only that node (its codes at obs_state[0..R))
+    // obs_only != ~0 observe only that node (its codes at obs_state[0..R));
+    // observation launches may instead run the blocks blk_list[0..blk_count)
+    // and observe the n_obs nodes of the sorted obs_list (node obs_list[j]'s
+    // codes at obs_state[j*R .. (j+1)*R))
     uint32_t blk_off, blk_count, obs_only;
+    const uint32_t *blk_list, *obs_list;
+    uint32_t n_obs;
     // Sparse records (wide 2P engine, W <= 8; null otherwise), exact for the
     // plane buffer they describe: zb = a bit per segment "all 8 planes zero"
     // (a word of unknown rumors), lb = a bit per node "some B or C entry"

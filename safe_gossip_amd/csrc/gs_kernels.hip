@@ -95,7 +95,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     const Geometry &g = a.g;
     if (a.zero_buf || a.zero_rows) zero_for_build(a.zero_buf, a.zero_words, a.zero_rows);
     if (a.zero_buf2) zero_for_build(a.zero_buf2, a.zero_words2, nullptr);
-    const uint32_t bid = blockIdx.x + a.blk_off;
+    const uint32_t bid = (!TRANSITION && a.blk_list) ? a.blk_list[blockIdx.x] : blockIdx.x + a.blk_off;
     const u64 seg = (u64)bid * blockDim.x + threadIdx.x;
     const bool valid = seg < g.nseg;
     Lane<SMALL> L;
@@ -679,8 +679,20 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         // ---------------- observation (post phase 2 of round t) -------------
         if (kLateB) load_planes(3, kPlanes);
         if (!valid) return;
-        if (a.obs_only != 0xFFFFFFFFu) {  // one node's state codes only (obs_state[0..R))
-            if (x != a.obs_only) return;
+        if (a.obs_only != 0xFFFFFFFFu || a.obs_list) {  // listed nodes' state codes only
+            uint32_t slot = 0;
+            if (a.obs_list) {  // (sorted: a binary search)
+                uint32_t lo = 0, hi = a.n_obs;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (a.obs_list[mid] < x) lo = mid + 1; else hi = mid;
+                }
+                if (lo >= a.n_obs || a.obs_list[lo] != x) return;
+                slot = lo;
+            } else if (x != a.obs_only) {
+                return;
+            }
+            uint16_t *os = a.obs_state + (u64)slot * g.R;
             const uint32_t nb = SMALL ? g.rpad : 64u;
             for (uint32_t b = 0; b < nb; ++b) {
                 const uint32_t rr = SMALL ? b : L.j * 64u + b;
@@ -696,7 +708,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                 else if (B & bit) code = (uint16_t)((1u << 14) | (af << 7) | bf);
                 else if (C & bit) code = (uint16_t)((2u << 14) | (af << 7) | bf);
                 else if (D & bit) code = (uint16_t)(3u << 14);
-                a.obs_state[rr] = code;
+                os[rr] = code;
             }
             return;
         }
@@ -997,6 +1009,7 @@ static hipError_t launch_mode(const RoundArgs &a, int mode, hipStream_t s) {
     const uint32_t block = 256;
     const u64 grid = a.blk_count ? a.blk_count : (a.g.nseg + block - 1) / block;
     if (grid == 0) return hipSuccess;
+    if (a.blk_list && (mode == 0 || mode == 1)) return hipErrorInvalidValue;  // (observation launches only)
     if constexpr (!SMALL && !SHARD && !SEQ && !DLV) {
         if (a.zb_nxt && (mode == 0 || mode == 1)) {  // sparse records
             if (mode == 0)

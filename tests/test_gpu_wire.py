@@ -175,3 +175,76 @@ def test_handle_received_errors(engine):
             net.set_rumor_key(2, net.rumor_key(3))  # keys are distinct
     finally:
         net.close()
+
+
+@pytest.mark.parametrize("n,R,faults,schedule", [
+    (2000, 16, None, "2P"),                  # delivery-record path
+    (1500, 64, (0.05, 0.05, 0.05), "2P"),    # gather path, faults
+    (800, 200, None, "2P"),                  # several words
+    (1000, 64, None, "SEQ"),
+])
+def test_handle_received_batch_matches_oracle(engine, n, R, faults, schedule):
+    # gs_handle_received_batch: 1000 external RPCs in one call (one
+    # observation launch) = the same RPCs one by one through the oracle's
+    # Gossip::receive (src/gossiper.rs:82-99 -> src/gossip.rs:118-166): every
+    # response, then state, records, |P|, Statistics and known sets, and the
+    # rounds after -- with repeated peers, repeated nodes (responses that show
+    # the batch's earlier creations), empty RPCs and pulls
+    from oracle_lib import fault_threshold
+    fk = dict(churn=faults[0], drop_push=faults[1], drop_pull=faults[2]) if faults else {}
+    if schedule != "2P":
+        fk["schedule"] = schedule
+    osched = SCHED_SEQ if schedule == "SEQ" else SCHED_2P
+    net = engine.Network(n, R, seed=SEED, **fk)
+    orc = OracleNet(n, R, seed=SEED, faults=[fault_threshold(p) for p in faults] if faults else None)
+    rng = np.random.default_rng(11 * n + R)
+    params = net.params
+    try:
+        for r in range(0, R, 2):
+            x = engine.origin_of(SEED, 0, r, n)
+            net.send_new(x, r)
+            orc.send_new(x, r)
+        for rnd in range(1, 8):
+            net.next_round()
+            orc.next_round(osched)
+            off = orc.offline(rnd) if faults else np.zeros(n, dtype=bool)
+            if rnd in (2, 4):
+                hot = rng.integers(n, size=40)  # nodes hit many times
+                rpcs, exp = [], []
+                for _ in range(1000):
+                    y = int(hot[rng.integers(40)] if rng.random() < 0.5 else rng.integers(n))
+                    peer = n + 1 + int(rng.integers(30))
+                    push = bool(rng.random() < 0.6)
+                    if rng.random() < 0.1:
+                        rumor, ctr = -1, 0
+                    else:
+                        rumor = int(rng.integers(R))
+                        ctr = int(rng.choice([0, 1, 2, 3, 255, params[0] - 1 if params[0] > 1 else 1]))
+                    msg = b"" if rumor < 0 else net.rumor_key(rumor)
+                    rpcs.append((y, peer, engine.rpc_encode(not push, msg, ctr)))
+                    exp.append([] if off[y] else orc.receive(y, peer, push, rumor, ctr))
+                got = net.handle_received_batch(rpcs)
+                assert len(got) == len(rpcs)
+                for i, (g, e_) in enumerate(zip(got, exp)):
+                    assert _decode_batch(engine, net, g, pull=True) == _key_sorted(net, e_), f"round {rnd} rpc {i}"
+                _compare(net, orc, off)
+            if rnd % 2 == 1:
+                _compare(net, orc, off)
+    finally:
+        net.close()
+        orc.close()
+
+
+def test_handle_received_batch_all_or_nothing(engine):
+    net = engine.Network(60, 8, seed=SEED)
+    try:
+        net.next_round()
+        ok = engine.rpc_encode(False, net.rumor_key(3), 1)
+        with pytest.raises(engine.GossipError, match="status 5"):  # one undecodable message: nothing applied
+            net.handle_received_batch([(0, 70, ok), (1, 71, b"\x07\x00")])
+        assert 3 not in net.gossiper(0).messages()
+        # applied once it is well formed: node 0 answers its first Push (knows nothing yet)
+        assert net.handle_received_batch([(0, 70, ok), (1, 71, ok)]) == [[engine.rpc_encode(True, b"", 0)]] * 2
+        assert net.handle_received_batch([]) == []
+    finally:
+        net.close()
