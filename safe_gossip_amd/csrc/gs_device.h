@@ -207,6 +207,24 @@ GS_DEV uint32_t group_min(uint32_t v, uint32_t W) {
 
 constexpr uint32_t kNone = 0xffffffffu;
 
+// Statistics deltas of node x between folds (RoundArgs::st32): [n][4] u32,
+// or with st16 [n][4] u16 -- the delivery-record engines (R_pad <= 16), whose
+// per-round deltas of internal deliveries are below 32 R_pad + 32 and fold
+// into the u64 totals well before 16 bits wrap (8 B read + 8 written per node
+// and round instead of 16 + 16).  Order: empty_pull, empty_push, full_sent,
+// full_received.
+GS_DEV uint4 load_stats(const uint32_t *st, uint32_t st16, u64 x) {
+    if (st16) {
+        const uint2 h = reinterpret_cast<const uint2 *>(st)[x];
+        return make_uint4(h.x & 0xFFFFu, h.x >> 16, h.y & 0xFFFFu, h.y >> 16);
+    }
+    return reinterpret_cast<const uint4 *>(st)[x];
+}
+GS_DEV void store_stats(uint32_t *st, uint32_t st16, u64 x, uint4 v) {
+    if (st16) reinterpret_cast<uint2 *>(st)[x] = make_uint2((v.x & 0xFFFFu) | (v.y << 16), (v.z & 0xFFFFu) | (v.w << 16));
+    else reinterpret_cast<uint4 *>(st)[x] = v;
+}
+
 // First-carrier class of the entries z created from its pushers ahead of x
 // (the pull row is built before x's push is absorbed, src/gossip.rs:124-151).
 GS_DEV void sibling(const Cls &q, u64 &pnot, u64 &pB, u64 &pC) {

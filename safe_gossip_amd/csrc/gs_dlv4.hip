@@ -377,10 +377,9 @@ void round_kernel_dlv4(RoundArgs a) {
 
     // the Statistics counters this round updates (read now: the stores below
     // cover the load's latency)
-    uint4 *st = reinterpret_cast<uint4 *>(a.st32) + x0;
     uint4 stv[kNpl];
 #pragma unroll
-    for (uint32_t q = 0; q < kNpl; ++q) stv[q] = q < nv ? st[q] : make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t q = 0; q < kNpl; ++q) stv[q] = q < nv ? load_stats(a.st32, a.st16, x0 + q) : make_uint4(0u, 0u, 0u, 0u);
     // rumor slice: an earlier round's network empty counts (pull | push << 8)
     uint32_t eav[kNpl];
 #pragma unroll
@@ -483,7 +482,7 @@ void round_kernel_dlv4(RoundArgs a) {
         }
         v.z += live[q] + d_full[q];                   // full_message_sent
         v.w += recv[q];                               // full_message_received
-        st[q] = v;
+        store_stats(a.st32, a.st16, x0 + q, v);
         if (!on) a.offc[x0 + q] += 1u;
     }
 

@@ -144,7 +144,8 @@ struct gs_engine {
     // chunks, config 5 4.62 -> 6.03 ms per step)
     bool fuse_coarse = false;
     bool ra_fused = false;  // this round's launch did
-    uint32_t *st32 = nullptr;  // [n][4] u32 deltas
+    uint32_t *st32 = nullptr;  // [n][4] u32 deltas (u16 with st16)
+    bool st16 = false;         // delivery-record engines: u16 deltas (gs_device.h load_stats)
     u64 *st64 = nullptr;       // [n][4] folded totals
     uint32_t fold_every = 1, since_fold = 0;
     u64 *inj_key = nullptr, *inj_mask = nullptr;
@@ -392,6 +393,7 @@ gs::RoundArgs base_args(gs_engine *e) {
         }
     }
     a.st32 = e->st32;
+    a.st16 = e->st16 ? 1u : 0u;
     a.st64 = e->st64;
     a.f = e->faults;
     a.pend = e->pend;
@@ -526,7 +528,7 @@ gs_status observe(gs_engine *e, bool dumps, bool digest = false) {
     if (e->obs_valid && !dumps && !digest) return GS_OK;
     if (e->slice && !e->eb[3]) return GS_ERR_INVALID_ARGUMENT;  // gs_slice_bind first
     if (e->slice && e->eb_defer >= 0) {  // a deferred reduced buffer: add it now
-        GS_HIP(gs::launch_slice_apply(e->st32, e->eb[e->eb_defer], e->g.n, e->stream));
+        GS_HIP(gs::launch_slice_apply(e->st32, e->eb[e->eb_defer], e->g.n, e->st16 ? 1u : 0u, e->stream));
         e->eb_defer = -1;
     }
     gs_status st = ensure_obs(e, dumps);
@@ -824,9 +826,16 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         const char *v = std::getenv("SAFE_GOSSIP_AMD_SPLIT_BUILD");
         e->split_build = v && *v && *v != '0' && e->filt;
     }
-    // Per round a node's u32 Statistics deltas grow by at most 32*R_pad + 32
-    // (in-degree <= 30 is enforced); fold them into u64 well before a wrap.
-    e->fold_every = (uint32_t)std::max<uint64_t>(1, 0xFFFFFFFFull / (32ull * g.rpad + 32) / 2);
+    // Per round a node's Statistics deltas of internal deliveries grow by at
+    // most 32*R_pad + 32 (in-degree <= 30 is enforced); fold them into u64
+    // well before a wrap.  The delivery-record engines (R_pad <= 16) keep them
+    // in 16 bits (8 B per node and round less to read and write; external
+    // RPCs' counts go straight to the totals): a fold every >= 60 rounds.
+    {
+        const char *v = std::getenv("SAFE_GOSSIP_AMD_STATS32");  // A/B: u32 deltas everywhere
+        e->st16 = e->dlv && !(v && *v == '1');
+    }
+    e->fold_every = (uint32_t)std::max<uint64_t>(1, (e->st16 ? 0xFFFFull : 0xFFFFFFFFull) / (32ull * g.rpad + 32) / 2);
     bool ok;
     if (e->shard) {
         // Shard engines share the device with the process group's collective
@@ -1352,7 +1361,7 @@ gs_status round_end(gs_engine *e, gs_round_report *report) {
     e->ext_uploaded = 0;
     e->obs_valid = false;
     if (++e->since_fold >= e->fold_every) {
-        GS_HIP(gs::launch_stats_fold(e->st32, e->st64, e->g.n, e->stream));
+        GS_HIP(gs::launch_stats_fold(e->st32, e->st64, e->g.n, e->st16 ? 1u : 0u, e->stream));
         e->since_fold = 0;
     }
     if (e->shard) {
@@ -1457,7 +1466,7 @@ gs_status gs_slice_defer(gs_engine *e, uint32_t which) {
     gs_status st = set_device(e);
     if (st != GS_OK) return st;
     if (e->eb_defer >= 0)  // one deferred buffer at a time: add the older one now
-        GS_HIP(gs::launch_slice_apply(e->st32, e->eb[e->eb_defer], e->g.n, e->stream));
+        GS_HIP(gs::launch_slice_apply(e->st32, e->eb[e->eb_defer], e->g.n, e->st16 ? 1u : 0u, e->stream));
     e->eb_defer = (int)which;
     e->obs_valid = false;
     return GS_OK;
@@ -1469,7 +1478,7 @@ gs_status gs_slice_apply(gs_engine *e, uint32_t which) {
     if (st != GS_OK) return st;
     if (!e->eb[which]) return GS_ERR_INVALID_ARGUMENT;
     if (e->eb_defer == (int)which) e->eb_defer = -1;  // deferred: added now instead, once
-    GS_HIP(gs::launch_slice_apply(e->st32, e->eb[which], e->g.n, e->stream));
+    GS_HIP(gs::launch_slice_apply(e->st32, e->eb[which], e->g.n, e->st16 ? 1u : 0u, e->stream));
     e->obs_valid = false;
     return GS_OK;
 }
@@ -2061,13 +2070,15 @@ double gs_round_kernel_bytes(const gs_engine *e) {
     if (!e) return 0.0;
     const double n = e->g.n, rp = e->g.rpad;
     // DLV path: per slot 1 B planes read + 1 B written; per node its delivery
-    // record 16 + its pull batch 4 + target word 4 + Statistics deltas 16 r +
-    // 16 w + the next round's push code 4.
+    // record 16 + its pull batch 4 + target word 4 + u16 Statistics deltas 8 r
+    // + 8 w + the next round's push code 4: 44 B.
     // Code-row shards: the same, with the pull code read at x's exchange-B
-    // slot (slot 4 + code 4 B) and the push code written to its exchange-A
-    // slot (slot 4 + code 4): 68 B per node.
-    if (e->dlv && e->shard) return n * (2.0 * rp + 68.0);
-    if (e->dlv) return n * (2.0 * rp + 60.0);
+    // slot (slot 4 + code 4 B) and the 8-B row written at its exchange-A
+    // slot (slot 4 + next target word 4 + row 8): 60 B per node.
+    // (with u32 Statistics deltas, SAFE_GOSSIP_AMD_STATS32=1: 16 B more)
+    const double st = e->st16 ? 0.0 : 16.0;
+    if (e->dlv && e->shard) return n * (2.0 * rp + 60.0 + st);
+    if (e->dlv) return n * (2.0 * rp + 44.0 + st);
     return n * (2.75 * rp + 68.0);
 }
 

@@ -31,7 +31,9 @@ struct RoundArgs {
     const uint32_t *tg_next;  // shard engine: round t+1 target words of the owned nodes
     uint32_t serial;          // build serial of the round-t lists (SIB validity)
     uint32_t *st32;           // [n][4] u32 Statistics deltas (empty_pull, empty_push,
-                              //   full_sent, full_received)
+                              //   full_sent, full_received); u16 with st16
+    uint32_t st16;            // 1: u16 deltas (gs_device.h load_stats); external RPCs'
+                              //   counts then go straight to st64
     const u64 *st64;          // [n][4] folded u64 totals (observation only)
     u64 obs_rounds;           // Statistics.rounds of every node (observation)
     const u64 *inj_key;       // sorted segment keys with injections (round t+1)
@@ -250,9 +252,9 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s);
 // round kernel; phase B (the zl map from lvm, then inl_sort) runs after it.
 hipError_t launch_build_bins(const InListArgs &a, hipStream_t s);
 hipError_t launch_build_sort(const InListArgs &a, hipStream_t s);
-hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, hipStream_t s);
+hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, uint32_t st16, hipStream_t s);
 // Rumor slices: st32 empty_pull / empty_push += emin[2x] / emin[2x + 1].
-hipError_t launch_slice_apply(uint32_t *st32, const uint8_t *emin, uint32_t n, hipStream_t s);
+hipError_t launch_slice_apply(uint32_t *st32, const uint8_t *emin, uint32_t n, uint32_t st16, hipStream_t s);
 
 // ---------------------------------------------------------------- SEQ
 // The literal harness order (gs_seq.hip): per round, seq_levels classifies

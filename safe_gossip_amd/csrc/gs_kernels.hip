@@ -160,7 +160,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     // (GS_STATS_LATE: loaded after the transition, as before).
 #ifndef GS_STATS_LATE
     uint4 stv = {0u, 0u, 0u, 0u};
-    if (TRANSITION && valid && (SMALL || L.j == 0)) stv = reinterpret_cast<const uint4 *>(a.st32)[x];
+    if (TRANSITION && valid && (SMALL || L.j == 0)) stv = load_stats(a.st32, a.st16, x);
 #endif
     // rumor slice: an earlier round's network empty counts (pull | push << 8)
     uint32_t eadd = 0;
@@ -717,7 +717,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         if (a.obs_known && (SMALL || L.j < KW)) a.obs_known[(u64)x * KW + L.j] = known;
         if (leader) {
             if (a.obs_stats || a.obs_digest) {
-                const uint4 d32 = reinterpret_cast<const uint4 *>(a.st32)[x];
+                const uint4 d32 = load_stats(a.st32, a.st16, x);
                 const u64 *b64 = a.st64 + (u64)x * 4;
                 u64 o[5];
                 o[0] = a.obs_rounds - (a.offc ? a.offc[x] : 0u);  // next_round calls
@@ -981,12 +981,22 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
 #ifndef GS_EXP_NO_STATS
         // rounds is the engine's round count (every node runs every round);
         // the other four are u32 deltas folded into u64 before they can wrap.
-        uint4 *st = reinterpret_cast<uint4 *>(a.st32) + x;
 #ifdef GS_STATS_LATE
-        uint4 v = *st;
+        uint4 v = load_stats(a.st32, a.st16, x);
 #else
         uint4 v = stv;
 #endif
+        if (a.st16 && (ext_full | ext_empty | ext_recv)) {
+            // u16 deltas hold internal deliveries only (bounded per round):
+            // external RPCs, as many as the caller sends, go to the totals
+            u64 *s64 = const_cast<u64 *>(a.st64) + (u64)x * 4u;
+            s64[0] += ext_empty;
+            s64[2] += ext_full;
+            s64[3] += ext_recv;
+            d_empty_pull -= ext_empty;
+            d_full_sent -= ext_full;
+            d_recv -= ext_recv;
+        }
         const uint32_t d_empty_push = (on_next && live_new == 0u) ? 1u : 0u;
         if (a.emin) {  // rumor slice: empty only if empty in every slice (MIN per byte, caller)
             reinterpret_cast<uint16_t *>(a.emin)[x] = (uint16_t)(min(d_empty_pull, 255u) | (d_empty_push << 8));
@@ -998,7 +1008,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         }
         v.z += live_new + d_full_sent;             // full_message_sent
         v.w += d_recv;                             // full_message_received
-        *st = v;
+        store_stats(a.st32, a.st16, x, v);
         if (!on_next) a.offc[x] += 1u;
 #endif
     }
@@ -1051,35 +1061,41 @@ hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s) {
 
 // Rumor slices: add a round's empty-RPC counts, reduced with MIN over the
 // slices by the caller (gs_slice_apply), to the u32 Statistics deltas.
-__global__ __launch_bounds__(256) void slice_apply(uint32_t *st32, const uint8_t *__restrict__ emin, uint32_t n) {
+__global__ __launch_bounds__(256) void slice_apply(uint32_t *st32, const uint8_t *__restrict__ emin, uint32_t n,
+                                                   uint32_t st16) {
     const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= n) return;
-    uint2 *p = reinterpret_cast<uint2 *>(st32 + 4u * (u64)x);
-    uint2 v = *p;
+    uint4 v = load_stats(st32, st16, x);
     v.x += emin[2u * (u64)x];       // empty_pull_sent
     v.y += emin[2u * (u64)x + 1u];  // empty_push_sent
-    *p = v;
+    store_stats(st32, st16, x, v);
 }
 
-hipError_t launch_slice_apply(uint32_t *st32, const uint8_t *emin, uint32_t n, hipStream_t s) {
+hipError_t launch_slice_apply(uint32_t *st32, const uint8_t *emin, uint32_t n, uint32_t st16, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(slice_apply, dim3((n + 255u) / 256u), dim3(256), 0, s, st32, emin, n);
+    hipLaunchKernelGGL(slice_apply, dim3((n + 255u) / 256u), dim3(256), 0, s, st32, emin, n, st16);
     return hipGetLastError();
 }
 
-// Fold the u32 statistics deltas into the u64 totals (before they can wrap).
-__global__ __launch_bounds__(256) void stats_fold(uint32_t *st32, u64 *st64, u64 words) {
+// Fold the u32 (u16: st16) statistics deltas into the u64 totals (before they can wrap).
+__global__ __launch_bounds__(256) void stats_fold(uint32_t *st32, u64 *st64, u64 words, uint32_t st16) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= words) return;
-    st64[i] += st32[i];
-    st32[i] = 0u;
+    if (st16) {
+        uint16_t *s16 = reinterpret_cast<uint16_t *>(st32);
+        st64[i] += s16[i];
+        s16[i] = 0;
+    } else {
+        st64[i] += st32[i];
+        st32[i] = 0u;
+    }
 }
 
-hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, hipStream_t s) {
+hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, uint32_t st16, hipStream_t s) {
     const u64 words = (u64)n * 4;
     if (words == 0) return hipSuccess;
     hipLaunchKernelGGL(stats_fold, dim3((uint32_t)((words + 255) / 256)), dim3(256), 0, s, st32, st64,
-                       words);
+                       words, st16);
     return hipGetLastError();
 }
 

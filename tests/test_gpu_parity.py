@@ -43,6 +43,10 @@ def _injections(kind, n, R, seed, epoch, rnd, eng):
         if rnd in (1, 2, 4, 5):
             rng = np.random.default_rng(rnd * 7919 + n)
             out = [(int(rng.integers(n)), int(rng.integers(R))) for _ in range(max(1, R // 2))]
+    elif kind == "steady":         # rumors re-sent every 6 rounds: a dissemination that never ends
+        if rnd % 6 == 1:
+            rng = np.random.default_rng(rnd * 7919 + n)
+            out = [(int(rng.integers(n)), int(rng.integers(R))) for _ in range(max(1, R // 2))]
     return out
 
 
@@ -499,3 +503,12 @@ def test_parity_w32(engine, monkeypatch, n, R, kind, faults):
     monkeypatch.setenv("SAFE_GOSSIP_AMD_PIPE", "0")
     monkeypatch.setenv("SAFE_GOSSIP_AMD_W32", "1")
     run_parity(engine, n, R, kind, faults=faults, check_every=1 if n < 5000 else 3)
+
+
+@pytest.mark.parametrize("n,R,faults", [(400, 16, None), (300, 12, (0.05, 0.05, 0.05))])
+def test_parity_long_run_stats_folds(engine, n, R, faults):
+    # 200 rounds of a dissemination kept alive by re-sending: the delivery-
+    # record engines keep Statistics deltas in 16 bits and fold them into the
+    # u64 totals every 60 rounds (R_pad 16), so several folds happen here and
+    # every counter must still equal the oracle's
+    run_parity(engine, n, R, "steady", max_rounds=200, check_every=7, faults=faults)
