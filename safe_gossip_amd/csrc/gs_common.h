@@ -199,12 +199,16 @@ constexpr uint32_t kSibRankMask = 0x1Fu;
 // path fetches three random 128-B lines per node: pushers, t(x), t(x)'s
 // earlier pushers).
 //   DlvRec[y] = {meta = k | zi << 5 (index of t(y) among y's pushers, 31 =
-//               none), first, c[0], c[1]}: the push codes (b0 | b1 << 16: 01
+//               none) | flags << 10, first, c[0], c[1]}: the push codes (b0 | b1 << 16: 01
 //               counter 1, 10 counter 2, 11 counter 255) of y's pushers in
 //               ascending order, pushers i >= kDlvInline at dtail[first + i - 2]
 //   PULL[x]   = the pull batch t(x) returned to x, the same 2-plane code
 constexpr uint32_t kDlvInline = 2;
 constexpr uint32_t kDlvNoZ = 31u;
+// single-engine records also carry y's own delivery flags (kTgNoPull, kTgOff)
+// in meta bits 10 and 11, so the packed round kernel reads no target words
+constexpr uint32_t kDlvMetaNoPull = 10u, kDlvMetaOff = 11u;
+static_assert(kTgNoPull == 1u << 30 && kTgOff == 1u << 29, "meta flag bits mirror the target-word flags");
 struct alignas(16) DlvRec {
     uint32_t meta, first, c[kDlvInline];
 };

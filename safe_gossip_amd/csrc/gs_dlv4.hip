@@ -122,24 +122,17 @@ void round_kernel_dlv4(RoundArgs a) {
         }
 #pragma unroll
         for (uint32_t q = 0; q < kNpl; ++q) dp[q] = sp[q] != 0xFFFFFFFFu ? rB[sp[q]] : 0u;
-    } else if (DELIVER) {
+    } else if (DELIVER) {  // (the delivery flags come with the records below)
         if (kNpl == 4 && nv == kNpl) {
-            const uint4 t4 = *reinterpret_cast<const uint4 *>(a.tg + x0);
             const uint4 p4 = *reinterpret_cast<const uint4 *>(a.pull + x0);
-            tgw[0] = t4.x; tgw[1] = t4.y; tgw[kNpl > 2 ? 2 : 0] = t4.z; tgw[kNpl > 3 ? 3 : 0] = t4.w;
             dp[0] = p4.x; dp[1] = p4.y; dp[kNpl > 2 ? 2 : 0] = p4.z; dp[kNpl > 3 ? 3 : 0] = p4.w;
         } else if (kNpl == 2 && nv == kNpl) {
-            const uint2 t2 = *reinterpret_cast<const uint2 *>(a.tg + x0);
             const uint2 p2 = *reinterpret_cast<const uint2 *>(a.pull + x0);
-            tgw[0] = t2.x; tgw[1] = t2.y;
             dp[0] = p2.x; dp[1] = p2.y;
         } else {
 #pragma unroll
             for (uint32_t q = 0; q < kNpl; ++q)
-                if (q < nv) {
-                    tgw[q] = a.tg[x0 + q];
-                    dp[q] = a.pull[x0 + q];
-                }
+                if (q < nv) dp[q] = a.pull[x0 + q];
         }
     }
     if (DELIVER) {
@@ -151,6 +144,8 @@ void round_kernel_dlv4(RoundArgs a) {
             dfirst[q] = r.first;
             c0[q] = r.c[0];
             c1[q] = r.c[1];
+            if (!SH)  // the build put y's own delivery flags in meta (gs_common.h kDlvMeta*)
+                tgw[q] = (((r.meta >> kDlvMetaNoPull) & 1u) ? kTgNoPull : 0u) | (((r.meta >> kDlvMetaOff) & 1u) ? kTgOff : 0u);
         }
     }
     __syncthreads();

@@ -2070,15 +2070,17 @@ double gs_round_kernel_bytes(const gs_engine *e) {
     if (!e) return 0.0;
     const double n = e->g.n, rp = e->g.rpad;
     // DLV path: per slot 1 B planes read + 1 B written; per node its delivery
-    // record 16 + its pull batch 4 + target word 4 + u16 Statistics deltas 8 r
-    // + 8 w + the next round's push code 4: 44 B.
+    // record 16 (carrying the node's own delivery flags) + its pull batch 4 +
+    // u16 Statistics deltas 8 r + 8 w + the next round's push code 4: 40 B
+    // (the one-node-per-lane kernel, SAFE_GOSSIP_AMD_DLV_PACK=0, also reads
+    // the 4-B target word).
     // Code-row shards: the same, with the pull code read at x's exchange-B
     // slot (slot 4 + code 4 B) and the 8-B row written at its exchange-A
     // slot (slot 4 + next target word 4 + row 8): 60 B per node.
     // (with u32 Statistics deltas, SAFE_GOSSIP_AMD_STATS32=1: 16 B more)
     const double st = e->st16 ? 0.0 : 16.0;
     if (e->dlv && e->shard) return n * (2.0 * rp + 60.0 + st);
-    if (e->dlv) return n * (2.0 * rp + 44.0 + st);
+    if (e->dlv) return n * (2.0 * rp + (e->dlv_pack ? 40.0 : 44.0) + st);
     return n * (2.75 * rp + 68.0);
 }
 

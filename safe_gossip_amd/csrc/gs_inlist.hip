@@ -980,7 +980,9 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
         }
         if (mt && cur != kNone) cur += mt;
         DlvRec r;
-        r.meta = k | (zi << 5);
+        // (+ y's own delivery flags for the packed round kernel, which then
+        // reads no target word: bit 10 no pull reaches y, bit 11 y offline)
+        r.meta = k | (zi << 5) | (((tgv[q] >> 30) & 1u) << kDlvMetaNoPull) | (((tgv[q] >> 29) & 1u) << kDlvMetaOff);
         r.first = first;
         r.c[0] = k > 0 ? scd[s] : 0u;
         r.c[1] = k > 1 ? scd[s + 1] : 0u;
