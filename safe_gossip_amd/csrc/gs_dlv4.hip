@@ -478,7 +478,9 @@ void round_kernel_dlv4(RoundArgs a) {
         v.z += live[q] + d_full[q];                   // full_message_sent
         v.w += recv[q];                               // full_message_received
         store_stats(a.st32, a.st16, x0 + q, v);
-        if (!on) a.offc[x0 + q] += 1u;
+        // (a non-returning atomic: a load + store here left ~3/4 of the waves
+        // waiting a memory round trip at their end at 1 % churn)
+        if (!on) atomicAdd(&a.offc[x0 + q], 1u);
     }
 
     // ---- fused first partition of round t+1's build (dl_coarse's work,

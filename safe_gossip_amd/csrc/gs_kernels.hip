@@ -1009,7 +1009,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         v.z += live_new + d_full_sent;             // full_message_sent
         v.w += d_recv;                             // full_message_received
         store_stats(a.st32, a.st16, x, v);
-        if (!on_next) a.offc[x] += 1u;
+        if (!on_next) atomicAdd(&a.offc[x], 1u);  // (no return: nothing waits for it)
 #endif
     }
 }

@@ -439,7 +439,7 @@ __global__ __launch_bounds__(PipeTile<W>::kThreads) void round_pipe(RoundArgs a,
             v.z += live_new + d_full_sent;  // full_message_sent
             v.w += d_recv;                  // full_message_received
             reinterpret_cast<uint4 *>(a.st32)[x] = v;
-            if (!on_next) a.offc[x] += 1u;
+            if (!on_next) atomicAdd(&a.offc[x], 1u);  // (no return: nothing waits for it)
         }
     }
     __syncthreads();
