@@ -390,8 +390,29 @@ void round_kernel_dlv4(RoundArgs a) {
 #pragma unroll
         for (uint32_t q = 0; q < kNpl; ++q)
             pc[q] = (uint32_t)((b0 >> (q * rp)) & m1) | ((uint32_t)((b1 >> (q * rp)) & m1) << 16);
-        if (FUSE) {
-            // (not stored)
+        if (!SH) {
+            // the known masks (state != A): with its push code, all a target's
+            // planes tell the build about the pull batch it returns (4 + 2 B
+            // per node there instead of whole 128-B lines of plane records)
+            const T kn = N[0] | N[1] | N[2];
+            uint32_t k16[kNpl];
+#pragma unroll
+            for (uint32_t q = 0; q < kNpl; ++q) k16[q] = (uint32_t)((kn >> (q * rp)) & m1);
+            if (kNpl == 4 && nv == kNpl) {
+                *reinterpret_cast<uint2 *>(a.kn_out + x0) =
+                    make_uint2(k16[0] | (k16[kNpl > 1 ? 1 : 0] << 16), k16[kNpl > 2 ? 2 : 0] | (k16[kNpl > 3 ? 3 : 0] << 16));
+            } else if (kNpl == 2 && nv == kNpl) {
+                *reinterpret_cast<uint32_t *>(a.kn_out + x0) = k16[0] | (k16[kNpl > 1 ? 1 : 0] << 16);
+            } else {
+#pragma unroll
+                for (uint32_t q = 0; q < kNpl; ++q)
+                    if (q < nv) a.kn_out[x0 + q] = (uint16_t)k16[q];
+            }
+        }
+        if (FUSE) {  // (the partition below carries the push codes; the build's sort reads them too)
+#pragma unroll
+            for (uint32_t q = 0; q < kNpl; ++q)
+                if (q < nv) a.pc_out[x0 + q] = pc[q];
         } else if (SH) {
             // exchange A of round t+1: to owner(t_{t+1}(x)) (no slot: an
             // undelivered edge, or a capacity overflow, flagged by the plan),

@@ -96,6 +96,7 @@ struct gs_engine {
     hipEvent_t ev_dens[2] = {nullptr, nullptr};
     uint32_t dens_round[2] = {0, 0};  // round whose density each slot holds (0: none)
     uint32_t *pc = nullptr;  // DLV: push codes of the current round [n]
+    uint16_t *kn = nullptr;  // single-engine DLV: known masks of the current round [n]
     hipStream_t cstream = nullptr;
     hipEvent_t ev_built[2] = {nullptr, nullptr};  // set i complete
     hipEvent_t ev_read[2] = {nullptr, nullptr};   // last reader of set i done
@@ -258,7 +259,7 @@ void release(gs_engine *e) {
     for (int i = 0; i < 2; ++i)
         if (e->ev_dens[i]) (void)hipEventDestroy(e->ev_dens[i]);
     if (e->dens_host) (void)hipHostFree(e->dens_host);
-    void *bufs[] = {e->lvm, e->cpm, e->rows_dev, e->zb[0], e->zb[1], e->lb[0], e->lb[1], e->ab[0], e->ab[1], e->acct, e->dens, e->pc, e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
+    void *bufs[] = {e->lvm, e->cpm, e->rows_dev, e->zb[0], e->zb[1], e->lb[0], e->lb[1], e->ab[0], e->ab[1], e->acct, e->dens, e->pc, e->kn, e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
                     e->partials, e->obs_state, e->obs_rec, e->obs_psize, e->obs_digest, e->obs_pend, e->ext_dev,
                     e->node_state};
     for (void *b : bufs)
@@ -383,6 +384,7 @@ gs::RoundArgs base_args(gs_engine *e) {
         a.dtail = e->dlv ? cs.src : nullptr;
         a.pull = cs.pull;
         a.pc_out = e->pc;
+        a.kn_out = e->kn;
         a.src = cs.src;
         a.tg = cs.tg;
         a.serial = cs.serial;
@@ -892,7 +894,7 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
     ok = ok && dalloc(&e->S[0], sw_pad) == hipSuccess && dalloc(&e->S[1], sw_pad) == hipSuccess &&
          dalloc(&e->flags, 4) == hipSuccess && dalloc(&e->st32, (size_t)4 * npad) == hipSuccess &&
          dalloc(&e->st64, (size_t)4 * n) == hipSuccess;
-    if (ok && e->dlv) ok = dalloc(&e->pc, n) == hipSuccess;
+    if (ok && e->dlv) ok = dalloc(&e->pc, n) == hipSuccess && (e->shard || dalloc(&e->kn, n) == hipSuccess);
     if (ok && e->filt)
         ok = dalloc(&e->lvm, gs::node_map_words(n)) == hipSuccess &&
              dalloc(&e->cpm, gs::node_map_words(n)) == hipSuccess &&
@@ -1169,6 +1171,7 @@ gs::InListArgs inlist_args(gs_engine *e, gs_engine::CsrSet &c, uint32_t round) {
         la.dlv = 1;
         la.S = e->S[e->cur];
         la.PC = e->pc;
+        la.KN = e->kn;
         la.g = e->g;
         la.DR = c.DR;
         la.dtail = c.src;
@@ -2071,16 +2074,16 @@ double gs_round_kernel_bytes(const gs_engine *e) {
     const double n = e->g.n, rp = e->g.rpad;
     // DLV path: per slot 1 B planes read + 1 B written; per node its delivery
     // record 16 (carrying the node's own delivery flags) + its pull batch 4 +
-    // u16 Statistics deltas 8 r + 8 w + the next round's push code 4: 40 B
-    // (the one-node-per-lane kernel, SAFE_GOSSIP_AMD_DLV_PACK=0, also reads
-    // the 4-B target word).
+    // u16 Statistics deltas 8 r + 8 w + the next round's push code 4 and
+    // known mask 2: 42 B (the one-node-per-lane kernel,
+    // SAFE_GOSSIP_AMD_DLV_PACK=0, also reads the 4-B target word).
     // Code-row shards: the same, with the pull code read at x's exchange-B
     // slot (slot 4 + code 4 B) and the 8-B row written at its exchange-A
     // slot (slot 4 + next target word 4 + row 8): 60 B per node.
     // (with u32 Statistics deltas, SAFE_GOSSIP_AMD_STATS32=1: 16 B more)
     const double st = e->st16 ? 0.0 : 16.0;
     if (e->dlv && e->shard) return n * (2.0 * rp + 60.0 + st);
-    if (e->dlv) return n * (2.0 * rp + (e->dlv_pack ? 40.0 : 44.0) + st);
+    if (e->dlv) return n * (2.0 * rp + (e->dlv_pack ? 42.0 : 46.0) + st);
     return n * (2.75 * rp + 68.0);
 }
 

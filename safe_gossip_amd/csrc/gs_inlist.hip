@@ -862,11 +862,13 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
             el[q] = (ok && (lt >> kHalfLog) == hp) ? (lt & (kHalf - 1u)) : kNone;
         }
     };
-    // the targets' own target words and class planes (R_pad <= 16: a node's
-    // segment lies in one 32-bit half of its plane word); they depend on the
-    // part index only, so they are issued with the part's region loads
+    // the targets' own target words and what their planes say about the
+    // pull batches they return: on the single engine the push code and the
+    // known mask the round kernel wrote (PC, KN: 6 B per target), on a
+    // code-row shard the class planes (R_pad <= 16: a node's segment lies in
+    // one 32-bit half of its plane word; whole 128-B record lines)
     uint32_t tgv[kHalfPer];
-    uint32_t w0[kHalfPer], w1[kHalfPer], w2[kHalfPer];
+    uint32_t w0[kHalfPer], w1[kHalfPer], w2[kHalfPer];  // SH: planes 0-2; else w0 = PC, w1 = KN
     const uint32_t *S32 = reinterpret_cast<const uint32_t *>(a.S);
     // (code-row shard: targets are the ntargets local nodes, p.n may be
     // larger -- the slot keys -- and t(y)'s pusher is flagged in its row)
@@ -880,10 +882,18 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
             const uint32_t y = np ? t0p + (lt < np ? lt : 0u) : 0u;  // (a part past the last node: node 0)
             const uint32_t ysh = (y & ((1u << a.g.lognpu) - 1u)) << a.g.logr;
             const u64 rb = (u64)(y >> a.g.lognpu) * kPlanes * 2u + (ysh >> 5);
-            tgv[q] = SH ? 0u : a.tg[y];
-            w0[q] = S32[rb];
-            w1[q] = S32[rb + 2];
-            w2[q] = S32[rb + 4];
+            if constexpr (SH) {
+                tgv[q] = 0u;
+                w0[q] = S32[rb];
+                w1[q] = S32[rb + 2];
+                w2[q] = S32[rb + 4];
+            } else {
+                tgv[q] = a.tg[y];
+                w0[q] = a.PC[y];
+                w1[q] = a.KN[y];
+                w2[q] = 0u;
+                (void)rb;
+            }
         }
     };
     // (small parts only: at SL = 2 the registers they hold across the LDS
@@ -990,15 +1000,26 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
         // the pull batch of each pusher, in place of its push code: y's live
         // set (B with our_counter, C as 255) plus the entries y created from
         // the pushers ahead of it (first carrier B -> counter 1, C -> 255)
-        const uint32_t ysh = (((t0 + lt) & ((1u << a.g.lognpu) - 1u)) << a.g.logr) & 31u;
-        const uint32_t c = (w0[q] >> ysh) & m, a0 = (w1[q] >> ysh) & m, a1 = (w2[q] >> ysh) & m;
-        const uint32_t zB = ~c & (a0 | a1), zC = c & ~(a0 & a1);
-        const uint32_t zB1 = zB & a0 & ~a1, zB2 = zB & a1 & ~a0;
-        uint32_t pnot = ~c & ~a0 & ~a1 & m, pB = 0, pC = 0;
+        // y's own pull base: the push code of its planes (B counter 1 -> 01,
+        // counter 2 -> 10, C -> 11; the same as the round kernel's PC[y]) and
+        // the rumors it does not know (state A)
+        uint32_t y0, y1, pnot;
+        if constexpr (SH) {
+            const uint32_t ysh = (((t0 + lt) & ((1u << a.g.lognpu) - 1u)) << a.g.logr) & 31u;
+            const uint32_t c = (w0[q] >> ysh) & m, a0 = (w1[q] >> ysh) & m, a1 = (w2[q] >> ysh) & m;
+            const uint32_t zB = ~c & (a0 | a1), zC = c & ~(a0 & a1);
+            y0 = (zB & a0 & ~a1) | zC;
+            y1 = (zB & a1 & ~a0) | zC;
+            pnot = ~c & ~a0 & ~a1 & m;
+        } else {
+            y0 = w0[q] & 0xFFFFu;
+            y1 = w0[q] >> 16;
+            pnot = ~w1[q] & m;
+        }
+        uint32_t pB = 0, pC = 0;
         for (uint32_t j = s; j < e; ++j) {  // (entries past kMaxIn keep the clamped pulls)
             const uint32_t code = scd[j];
-            const uint32_t pcl = zC | pC;
-            scd[j] = ((zB1 | pB | pcl) & 0xFFFFu) | ((zB2 | pcl) << 16);
+            scd[j] = ((y0 | pB | pC) & 0xFFFFu) | ((y1 | pC) << 16);
             const uint32_t b0 = code & 0xFFFFu, b1 = code >> 16;
             const uint32_t vC = b0 & b1, sl = b0 | b1;  // the pusher's batch; C carries 255
             const uint32_t nw = pnot & sl;

@@ -19,6 +19,7 @@ struct RoundArgs {
     const uint32_t *dtail;    //   push codes of pushers >= kDlvInline
     const uint32_t *pull;     //   PULL[x]: the pull batch t(x) returned to x
     uint32_t *pc_out;         // DLV: push code of every node's round-(t+1) push batch
+    uint16_t *kn_out;         // single-engine DLV: every node's round-(t+1) known mask (state != A)
     // counters of the in-list build that follows this kernel on its stream,
     // cleared here (grid-stride) instead of by a memset launch (null: none)
     uint32_t *zero_buf;
@@ -210,6 +211,9 @@ struct InListArgs {
     uint32_t dlv;
     const u64 *S;
     const uint32_t *PC;     // push codes of the round (written by the round kernel)
+    // known masks of the round (state != A, R_pad bits; single engine): with
+    // PC[y] they are all a target's planes say about its pull batch
+    const uint16_t *KN;
     uint32_t prezeroed;     // 1: the round kernel before cleared the counters (RoundArgs::zero_*)
     uint32_t coarse_done;   // 1: the round kernel before wrote tg and the coarse partition
     Geometry g;

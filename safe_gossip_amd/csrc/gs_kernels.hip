@@ -811,6 +811,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         const u64 vC = N[0] & ~(N[1] & N[2]), vB = ~N[0] & (N[1] | N[2]);
         const u64 b0 = ((vB & N[1] & ~N[2]) | vC) & L.m, b1 = ((vB & N[2] & ~N[1]) | vC) & L.m;
         a.pc_out[x] = (uint32_t)b0 | ((uint32_t)b1 << 16);
+        if (a.kn_out) a.kn_out[x] = (uint16_t)((N[0] | N[1] | N[2]) & L.m);
     }
 
     // ---- live-filtered gathers: node maps of the round-(t+1) planes, "live"
