@@ -611,6 +611,7 @@ hipError_t launch_round_dlv4(const RoundArgs &a, int mode, hipStream_t s) {
         if (a.dlv_pack == 3) return launch_dlv4_t<uint32_t, 1>(a, mode, s);
         return launch_dlv4_t<uint32_t, 2>(a, mode, s);
     }
+    if (a.dlv_pack == 3) return launch_dlv4_t<uint32_t, 1>(a, mode, s);
     return launch_dlv4_t<uint32_t, 4>(a, mode, s);
 }
 

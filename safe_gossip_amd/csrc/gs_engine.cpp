@@ -1308,8 +1308,9 @@ gs_status round_begin(gs_engine *e) {
 
 // Nodes per lane of the packed DLV round kernel (gs_dlv4.hip launch_round_dlv4).
 uint32_t dlv_nodes_per_lane(const gs_engine *e) {
+    if (e->dlv_pack == 3) return 1u;
     if (e->g.rpad < 16) return 4u;
-    return e->dlv_pack == 2 ? 4u : (e->dlv_pack == 3 ? 1u : 2u);
+    return e->dlv_pack == 2 ? 4u : 2u;
 }
 
 gs_status launch_part(gs_engine *e, uint32_t h) {
