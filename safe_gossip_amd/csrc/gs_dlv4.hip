@@ -419,15 +419,23 @@ void round_kernel_dlv4(RoundArgs a) {
             // the row (push code, target local to that rank | kRowMutual when
             // t_{t+1}(t_{t+1}(x)) = x: x is its target's own target, whose
             // push copy the pull copy supersedes, src/message_state.rs:79)
+            // (a row to this rank's own nodes goes straight into the receive
+            // buffer's own block, same slot: one rank exchanges nothing; with
+            // several the all-to-all still copies the send buffer's own block
+            // over it, so the row goes there too)
             uint2 *sA = reinterpret_cast<uint2 *>(a.sendA);
+            uint2 *rA = reinterpret_cast<uint2 *>(a.recvA_next);
+            const uint32_t me = a.node_lo / a.sp.chunk;
 #pragma unroll
             for (uint32_t q = 0; q < kNpl; ++q) {
                 const uint32_t sp = q < nv ? a.spos_next[x0 + q] : 0xFFFFFFFFu;
                 if (sp == 0xFFFFFFFFu) continue;
                 const uint32_t t = a.tg_next[x0 + q] & kTgMask;
-                const uint32_t tl = t - (t / a.sp.chunk) * a.sp.chunk;
+                const uint32_t td = t / a.sp.chunk, tl = t - td * a.sp.chunk;
                 const bool mutual = peer_of(a.seed, a.epoch, a.round_new, t, a.sp.n) == a.node_lo + x0 + q;
-                sA[sp] = make_uint2(pc[q], tl | (mutual ? kRowMutual : 0u));
+                const uint2 row = make_uint2(pc[q], tl | (mutual ? kRowMutual : 0u));
+                if (td == me) rA[sp] = row;
+                if (td != me || a.sp.G > 1) sA[sp] = row;
             }
         } else if (kNpl == 4 && nv == kNpl) {
             *reinterpret_cast<uint4 *>(a.pc_out + x0) =
@@ -588,7 +596,8 @@ static hipError_t launch_dlv4_t(const RoundArgs &a, int mode, hipStream_t s) {
         return hipErrorInvalidValue;
     const dim3 gd((uint32_t)grid), bd(kDlv4Threads);
     if (a.recvA) {  // code-row shard
-        if (!a.sp.codes || !a.recvB || !a.sendA || !a.spos_cur || !a.spos_next || !a.tg_next || !a.sp.chunk)
+        if (!a.sp.codes || !a.recvB || !a.sendA || !a.recvA_next || !a.spos_cur || !a.spos_next || !a.tg_next ||
+            !a.sp.chunk)
             return hipErrorInvalidValue;
         if (mode == 0) hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL, false, true>), gd, bd, 0, s, a);
         else hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, false, true>), gd, bd, 0, s, a);

@@ -375,6 +375,7 @@ gs::RoundArgs base_args(gs_engine *e) {
         if (e->dlv) {  // code rows: the delivery records built from exchange A (gs_shard_pull)
             a.DR = e->csr[0].DR;
             a.dtail = e->csr[0].src;
+            a.recvA_next = e->recvA[(t + 1) % 2];  // (rows to this rank's own nodes)
         }
     } else {
         const auto &cs = e->csr[e->round & 1u];  // round-t lists (t = e->round)
@@ -985,6 +986,11 @@ gs_status shard_build(gs_engine *e) {
                           e->sp.idrows, e->sp.rw, e->sp.rwb, e->sp.codes, e->sp.chunk,    e->sp.n};
     la.nkeys = shard_keys(e->sp);
     la.ntargets = e->g.n;
+    // this rank's own block: written in place by the round kernel, counted by
+    // round t's plan, answered in place in exchange B's receive buffer
+    la.self_rank = e->sp.g;
+    la.self_cnt = e->planw[t % 3] + e->spl.cnt + (size_t)e->sp.g * e->sp.P;
+    la.pullB_self = reinterpret_cast<uint32_t *>(e->recvB);
     GS_HIP(gs::launch_build_inlists(la, e->stream));
     return GS_OK;
 }

@@ -76,7 +76,9 @@ GS_DEV void dlv_source(const InListArgs &a, uint32_t x, uint32_t &t, uint32_t &c
         t = kTgDead;
         code = 0u;
         src = x;
-        if (x < a.nkeys) {
+        // (this rank's own block: slots past the plan's count are empty)
+        const uint32_t per = a.sr.P * a.sr.capP, ks = x / per, kr = x - ks * per, kh = kr / a.sr.capP;
+        if (x < a.nkeys && (ks != a.self_rank || kr - kh * a.sr.capP < a.self_cnt[kh])) {
             const uint2 r = reinterpret_cast<const uint2 *>(a.rowsA)[shard_key_slot(a.sr, x)];
             if (r.y != 0xFFFFFFFFu) {
                 t = r.y & ~kRowMutual;
@@ -90,6 +92,17 @@ GS_DEV void dlv_source(const InListArgs &a, uint32_t x, uint32_t &t, uint32_t &c
         code = a.PC[x];
         src = x;
     }
+}
+
+// A code-row shard's pull for slot key `key` into exchange B: the send
+// buffer, and for this rank's own block also the receive buffer (one rank
+// exchanges nothing; with several the all-to-all copies the send buffer's own
+// block over the same slots).
+GS_DEV void shard_pull_store(const InListArgs &a, uint32_t key, uint32_t v) {
+    const uint32_t b = shard_key_bslot(a.sr, key);
+    const bool own = key / (a.sr.P * a.sr.capP) == a.self_rank;
+    if (own) a.pullB_self[b] = v;
+    if (!own || a.sr.G > 1) a.pullB[b] = v;
 }
 
 // Per-target record emission, shared by both paths.  `lst` holds y's k
@@ -1034,9 +1047,9 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
     if (direct) {  // one coarse bucket: every pull straight into PULL (cache-resident)
         const uint32_t placed = min(total, kHalfCap);
         if constexpr (SH) {  // a code-row shard: to the pusher's exchange-B slot
-            uint32_t *pb = a.pullB;
-            for (uint32_t j = threadIdx.x; j < placed; j += kInlThreads)
-                pb[shard_key_bslot(a.sr, sid[j] & kIdMask)] = scd[j];
+            for (uint32_t j = threadIdx.x; j < placed; j += kInlThreads) {
+                shard_pull_store(a, sid[j] & kIdMask, scd[j]);
+            }
         } else {
             for (uint32_t j = threadIdx.x; j < placed; j += kInlThreads) a.pull[sid[j]] = scd[j];
         }
@@ -1146,7 +1159,8 @@ __global__ __launch_bounds__(kInlThreads) void pb_place(InListArgs a) {
     const uint32_t x0 = b << kBinLog;
     if constexpr (SH) {  // a code-row shard: sources are slot keys, pulls go to their exchange-B slots
         const uint32_t keys = x0 < a.nkeys ? min(kBin, a.nkeys - x0) : 0u;
-        for (uint32_t i = threadIdx.x; i < keys; i += kInlThreads) a.pullB[shard_key_bslot(a.sr, x0 + i)] = img[i];
+        for (uint32_t i = threadIdx.x; i < keys; i += kInlThreads)
+            shard_pull_store(a, x0 + i, img[i]);
         return;
     }
     const uint32_t nodes = min(kBin, p.n - x0);
@@ -1510,7 +1524,8 @@ hipError_t launch_dlv_build(const InListArgs &a, hipStream_t s) {
     hipError_t e = hipFuncSetAttribute(kd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dlv);
     if (e != hipSuccess) return e;
     if (a.lvm || a.zl) return hipErrorInvalidValue;  // DLV records gather nothing
-    if (SH && (!a.rowsA || !a.pullB || a.nkeys > p.n || a.ntargets > p.n)) return hipErrorInvalidValue;
+    if (SH && (!a.rowsA || !a.pullB || !a.pullB_self || !a.self_cnt || a.nkeys > p.n || a.ntargets > p.n))
+        return hipErrorInvalidValue;
     InListArgs ab = a;
     // fill counts (both half-bin blocks of a bin read them, so they are
     // cleared here rather than by the sort), tail count, coarse fills

@@ -53,6 +53,9 @@ struct RoundArgs {
     const u64 *recvA;         // round-t push rows of this shard's pushers [slot][2][W]
     const u64 *recvB;         // round-t pull rows for this shard's nodes [slot][2][W]
     u64 *sendA;               // round-(t+1) push rows of this shard's nodes [slot][2][W]
+    // code rows: round-(t+1) receive buffer of exchange A, where rows to this
+    // rank's own nodes go directly (its own block is not exchanged)
+    u64 *recvA_next;
     const uint32_t *spos_cur; // slot of x in recvB (exchange B of round t)
     const uint32_t *spos_next;// slot of x in sendA (exchange A of round t+1)
     ShardRows sp;             // its layout (row flags when sp.flagrows != 0)
@@ -246,6 +249,14 @@ struct InListArgs {
     uint32_t *pullB;
     ShardRows sr;
     uint32_t nkeys, ntargets;
+    // This rank's own block is not exchanged (the self block of a send
+    // buffer and of a receive buffer have the same slots): its rows were
+    // written straight into rowsA by the round kernel, their count per part
+    // is self_cnt[h] (the plan's, no empty-slot marks), and the pulls answering
+    // them go straight to pullB_self (the exchange-B receive buffer).
+    uint32_t self_rank;
+    const uint32_t *self_cnt;
+    uint32_t *pullB_self;
 };
 // Peer choices of `round` (into tg) and their in-lists (IN8, SIB8 tagged with
 // `serial`).  Depends on nothing but the Philox stream, so it runs on its own

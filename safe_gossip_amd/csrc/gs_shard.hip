@@ -176,6 +176,8 @@ __global__ __launch_bounds__(256) void plan_idle(ShardPlan P, const uint32_t *__
     const uint32_t d = blockIdx.y / P.P, h = blockIdx.y - d * P.P;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.capP || i < cnt[blockIdx.y]) return;
+    // (code rows: the receiver of this rank's own block reads its count
+    // instead, InListArgs::self_cnt)
     if (P.codes) reinterpret_cast<uint32_t *>(bufA)[(u64)shard_a_slot(P, d, h, i) * 2u + 1u] = kNoId;
     else id_slots(P, bufA, d)[h * P.capP + i] = kNoId;
 }

@@ -223,11 +223,17 @@ class ShardedNetwork:
     def _exchange(self, which, h, k=0):
         """Part h of exchange A (buffer set k) or B: sub-block d of every
         rank's send region -> sub-block (its rank) of rank d's receive region.
+        Code rows: the engine also writes the rows of a rank's own sub-block
+        (and the pulls answering them) straight into its receive buffer, so
+        one rank exchanges nothing (no RCCL self-copy of the whole network).
         Returns an async work (RCCL) or None (done)."""
+        own = self.shards[0].codes and self.world == 1  # own sub-blocks are not exchanged
         if self.transport == "local":
             self._sync_all()
             for d, dst in enumerate(self.shards):
                 for r, src in enumerate(self.shards):
+                    if own and r == d:
+                        continue
                     off, w = src.region(which, h)
                     if which == "A":
                         sb, rb = src.sendA[k], dst.recvA[k]
@@ -245,8 +251,16 @@ class ShardedNetwork:
             _check(self.lib.gs_sync(s.h))
             hout = torch.empty(self.world * w, dtype=torch.int32)
             dist.all_to_all_single(hout, send[span].cpu(), group=self.group)
-            recv[span].copy_(hout.to(recv.device))
+            if own:  # (every sub-block but this rank's own)
+                hdev = hout.to(recv.device)
+                for r in range(self.world):
+                    if r != self.rank:
+                        recv[off + r * w:off + (r + 1) * w].copy_(hdev[r * w:(r + 1) * w])
+            else:
+                recv[span].copy_(hout.to(recv.device))
             torch.cuda.synchronize(self.device)
+            return None
+        if own:  # one rank, code rows: nothing moves
             return None
         # RCCL: the collective waits for the engine stream's work so far and
         # runs on the process group's stream; the engine stream waits for it
