@@ -198,10 +198,13 @@ constexpr uint32_t kSibRankMask = 0x1Fu;
 // reads only coalesced per-node data -- no class-plane gathers (the gather
 // path fetches three random 128-B lines per node: pushers, t(x), t(x)'s
 // earlier pushers).
-//   DlvRec[y] = {meta = k | zi << 5 (index of t(y) among y's pushers, 31 =
-//               none) | flags << 10, first, c[0], c[1]}: the push codes (b0 | b1 << 16: 01
-//               counter 1, 10 counter 2, 11 counter 255) of y's pushers in
-//               ascending order, pushers i >= kDlvInline at dtail[first + i - 2]
+//   DlvRec[y] = {mf = k | zi << 5 (index of t(y) among y's pushers, 31 =
+//               none) | flags << 10 | f << 12, c[0], c[1]} (12 B): the push
+//               codes (b0 | b1 << 16: 01 counter 1, 10 counter 2, 11 counter
+//               255) of y's pushers in ascending order, pushers i >= kDlvInline
+//               at dtail[first + i - 2], first = (y >> tlog) * tper + f: the
+//               tails of y's sort part (2^tlog targets) own a fixed region of
+//               tper slots (RoundArgs::dlv_tlog / dlv_tper, dlv_tail_parts)
 //   PULL[x]   = the pull batch t(x) returned to x, the same 2-plane code
 constexpr uint32_t kDlvInline = 2;
 constexpr uint32_t kDlvNoZ = 31u;
@@ -209,10 +212,11 @@ constexpr uint32_t kDlvNoZ = 31u;
 // in meta bits 10 and 11, so the packed round kernel reads no target words
 constexpr uint32_t kDlvMetaNoPull = 10u, kDlvMetaOff = 11u;
 static_assert(kTgNoPull == 1u << 30 && kTgOff == 1u << 29, "meta flag bits mirror the target-word flags");
-struct alignas(16) DlvRec {
-    uint32_t meta, first, c[kDlvInline];
+constexpr uint32_t kDlvFirstShift = 12u;  // mf bits 12..31: the tail offset within y's part
+struct alignas(4) DlvRec {
+    uint32_t mf, c[kDlvInline];
 };
-static_assert(sizeof(DlvRec) == 16, "one delivery record is 16 bytes");
+static_assert(sizeof(DlvRec) == 12, "one delivery record is 12 bytes");
 
 // State digest (gs_state_digest; oracle/gs_dense.c and tests/oracle_lib.py
 // digest_of compute the same): per node, the sum mod 2^64 of

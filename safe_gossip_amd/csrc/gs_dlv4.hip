@@ -139,13 +139,13 @@ void round_kernel_dlv4(RoundArgs a) {
 #pragma unroll
         for (uint32_t q = 0; q < kNpl; ++q) {
             const DlvRec r = a.DR[q < nv ? x0 + q : 0u];  // node 0: a harmless valid address
-            kk[q] = q < nv ? (r.meta & 31u) : 0u;
-            dzi[q] = (r.meta >> 5) & 31u;
-            dfirst[q] = r.first;
+            kk[q] = q < nv ? (r.mf & 31u) : 0u;
+            dzi[q] = (r.mf >> 5) & 31u;
+            dfirst[q] = ((x0 + q) >> a.dlv_tlog) * a.dlv_tper + (r.mf >> kDlvFirstShift);
             c0[q] = r.c[0];
             c1[q] = r.c[1];
-            if (!SH)  // the build put y's own delivery flags in meta (gs_common.h kDlvMeta*)
-                tgw[q] = (((r.meta >> kDlvMetaNoPull) & 1u) ? kTgNoPull : 0u) | (((r.meta >> kDlvMetaOff) & 1u) ? kTgOff : 0u);
+            if (!SH)  // the build put y's own delivery flags in mf (gs_common.h kDlvMeta*)
+                tgw[q] = (((r.mf >> kDlvMetaNoPull) & 1u) ? kTgNoPull : 0u) | (((r.mf >> kDlvMetaOff) & 1u) ? kTgOff : 0u);
         }
     }
     __syncthreads();

@@ -356,6 +356,7 @@ gs::RoundArgs base_args(gs_engine *e) {
     gs::RoundArgs a{};
     a.Scur = e->S[e->cur];
     a.Snext = e->S[e->cur ^ 1];
+    if (e->dlv) gs::dlv_tail_parts(e->plan, &a.dlv_tlog, &a.dlv_tper);  // (DlvRec tail offsets)
     if (e->shard) {
         const uint32_t t = e->round;
         uint32_t *cur = e->planw[t % 3], *nxt = e->planw[(t + 1) % 3], *ed = e->edgew[t % 2];
@@ -2080,17 +2081,17 @@ double gs_round_kernel_bytes(const gs_engine *e) {
     if (!e) return 0.0;
     const double n = e->g.n, rp = e->g.rpad;
     // DLV path: per slot 1 B planes read + 1 B written; per node its delivery
-    // record 16 (carrying the node's own delivery flags) + its pull batch 4 +
+    // record 12 (carrying the node's own delivery flags) + its pull batch 4 +
     // u16 Statistics deltas 8 r + 8 w + the next round's push code 4 and
-    // known mask 2: 42 B (the one-node-per-lane kernel,
+    // known mask 2: 38 B (the one-node-per-lane kernel,
     // SAFE_GOSSIP_AMD_DLV_PACK=0, also reads the 4-B target word).
-    // Code-row shards: the same, with the pull code read at x's exchange-B
-    // slot (slot 4 + code 4 B) and the 8-B row written at its exchange-A
-    // slot (slot 4 + next target word 4 + row 8): 60 B per node.
+    // Code-row shards: record 12 + target word 4 + deltas 16, the pull code
+    // read at x's exchange-B slot (slot 4 + code 4 B) and the 8-B row written
+    // at its exchange-A slot (slot 4 + next target word 4 + row 8): 56 B.
     // (with u32 Statistics deltas, SAFE_GOSSIP_AMD_STATS32=1: 16 B more)
     const double st = e->st16 ? 0.0 : 16.0;
-    if (e->dlv && e->shard) return n * (2.0 * rp + 60.0 + st);
-    if (e->dlv) return n * (2.0 * rp + (e->dlv_pack ? 42.0 : 46.0) + st);
+    if (e->dlv && e->shard) return n * (2.0 * rp + 56.0 + st);
+    if (e->dlv) return n * (2.0 * rp + (e->dlv_pack ? 38.0 : 42.0) + st);
     return n * (2.75 * rp + 68.0);
 }
 

@@ -847,6 +847,8 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
     __shared__ uint32_t lds_scan[kInlThreads / 64];
     __shared__ uint32_t pcnt[kMaxCoarse], pres[kMaxCoarse];
     const uint32_t nc = n_coarse(p.nb);
+    // tail slots each part owns (dlv_part_tails; DlvRec::mf holds the offset)
+    constexpr uint32_t kPartTails = (kBin >> SL) / 4u + (kBin >> SL) / 16u;
     // p.sub == SL: dl_fine / dl_direct wrote this half's own region; small
     // networks (one coarse bucket) write every pull straight to PULL (no
     // pass-back partition)
@@ -959,7 +961,6 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
     if (own && GS_DLV_OWN_TAILS) {  // the part's own tail region (dlv_part_tails): a block scan, no atomic
         uint32_t tot;
         const uint32_t offs = block_exclusive_scan_t<kInlThreads>(mine, lds_scan, tot);
-        constexpr uint32_t kPartTails = (kBin >> SL) / 4u + (kBin >> SL) / 16u;
         if (tot > kPartTails && threadIdx.x == 0) atomicOr(&a.flags[2], kFlagLimit);
         cur = tot > kPartTails ? kNone : w * kPartTails + offs;
     } else {
@@ -1004,9 +1005,10 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
         if (mt && cur != kNone) cur += mt;
         DlvRec r;
         // (+ y's own delivery flags for the packed round kernel, which then
-        // reads no target word: bit 10 no pull reaches y, bit 11 y offline)
-        r.meta = k | (zi << 5) | (((tgv[q] >> 30) & 1u) << kDlvMetaNoPull) | (((tgv[q] >> 29) & 1u) << kDlvMetaOff);
-        r.first = first;
+        // reads no target word: bit 10 no pull reaches y, bit 11 y offline;
+        // and the tail offset within the part's own region, kDlvFirstShift)
+        r.mf = k | (zi << 5) | (((tgv[q] >> 30) & 1u) << kDlvMetaNoPull) | (((tgv[q] >> 29) & 1u) << kDlvMetaOff) |
+               ((first - (first ? w * kPartTails : 0u)) << kDlvFirstShift);
         r.c[0] = k > 0 ? scd[s] : 0u;
         r.c[1] = k > 1 ? scd[s + 1] : 0u;
         a.DR[t0 + lt] = r;
@@ -1318,6 +1320,11 @@ inline uint32_t dlv_part_tails(uint32_t sub) {
     return half / 4u + half / 16u;
 }
 
+void dlv_tail_parts(const CsrPlan &p, uint32_t *log, uint32_t *per) {
+    *log = kBinLog - p.sub;
+    *per = dlv_part_tails(p.sub);
+}
+
 CsrPlan dlv_plan(uint32_t n) {
     CsrPlan p{};
     p.n = n;
@@ -1516,6 +1523,10 @@ hipError_t launch_dlv_build(const InListArgs &a, hipStream_t s) {
     const uint32_t dsl = dlv_split_log(p.nb);
     const size_t lds_dlv = ((size_t)(kBin >> dsl) / 2 + 2 * (size_t)(kBinCap >> dsl)) * sizeof(uint32_t);
     const bool own = p.sub != 0u;
+    // the records index their tails within their part's own region
+    // (DlvRec::mf): whole-bin regions and a shared tail counter (A/B
+    // variants) would need global tail indices
+    if (!own || !GS_DLV_OWN_TAILS) return hipErrorInvalidValue;
     const void *kd = dsl == kSplitLog
                          ? (own ? (const void *)inl_sort_dlv<kSplitLog, true, false, SH>
                                 : (const void *)inl_sort_dlv<kSplitLog, false, false, SH>)

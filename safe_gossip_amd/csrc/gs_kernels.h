@@ -20,6 +20,7 @@ struct RoundArgs {
     const uint32_t *pull;     //   PULL[x]: the pull batch t(x) returned to x
     uint32_t *pc_out;         // DLV: push code of every node's round-(t+1) push batch
     uint16_t *kn_out;         // single-engine DLV: every node's round-(t+1) known mask (state != A)
+    uint32_t dlv_tlog, dlv_tper;  // DLV: tail regions of the records' sort parts (gs_common.h DlvRec)
     // counters of the in-list build that follows this kernel on its stream,
     // cleared here (grid-stride) instead of by a memset launch (null: none)
     uint32_t *zero_buf;
@@ -262,6 +263,9 @@ struct InListArgs {
 // `serial`).  Depends on nothing but the Philox stream, so it runs on its own
 // stream concurrently with the round kernel of the round before.
 hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s);
+// A DLV plan's sort parts hold 2^*log targets and own *per tail slots each
+// (the decoding of DlvRec::mf, RoundArgs::dlv_tlog / dlv_tper).
+void dlv_tail_parts(const CsrPlan &p, uint32_t *log, uint32_t *per);
 // The filtered binned build in two phases (2P gather path): phase A (inl_bin:
 // targets and the bin partition, no node maps) can run beside the previous
 // round kernel; phase B (the zl map from lvm, then inl_sort) runs after it.

@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             tgw = a.tg[x];
             dpull = a.pull[x];
             z = tgw & kTgMask;
-            k = valid ? (dr.meta & 31u) : 0u;
+            k = valid ? (dr.mf & 31u) : 0u;
         } else if (SHARD) {
             if (valid) {
                 in = a.IN[x];
@@ -425,10 +425,11 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         u64 pv2, pvB, pCl;
         if (DLV) {
             static_assert(kDlvInline == 2, "inline pushers are read by hand");
-            const uint32_t dzi = (dr.meta >> 5) & 31u;  // t(x)'s index among x's pushers
+            const uint32_t dzi = (dr.mf >> 5) & 31u;  // t(x)'s index among x's pushers
+            const uint32_t dfirst = (x >> a.dlv_tlog) * a.dlv_tper + (dr.mf >> kDlvFirstShift);
             zin = dzi != kDlvNoZ;
             for (uint32_t i = 0; i < k; ++i) {
-                const uint32_t code = i == 0 ? dr.c[0] : (i == 1 ? dr.c[1] : a.dtail[dr.first + i - kDlvInline]);
+                const uint32_t code = i == 0 ? dr.c[0] : (i == 1 ? dr.c[1] : a.dtail[dfirst + i - kDlvInline]);
                 rv.push(decode16(code), i, k, !(pulled && i == dzi));
             }
             // the pull batch z returned (built by the in-list build): code
