@@ -27,6 +27,10 @@ constexpr uint32_t kDlv4Threads = 256;
 #ifndef GS_DLV4_MINW
 #define GS_DLV4_MINW 4
 #endif
+#ifndef GS_DLV4_TAIL_PRE
+#define GS_DLV4_TAIL_PRE 2  // tail codes per node loaded with the metadata (0..2), two nodes per lane or fewer
+#endif
+static_assert(GS_DLV4_TAIL_PRE <= 2, "tail prefetch depth");
 #ifndef GS_DLV4_MINW_R16
 #define GS_DLV4_MINW_R16 GS_DLV4_MINW  // the config-5 kernel (R_pad 16, two nodes per u32 lane)
 #endif
@@ -148,6 +152,18 @@ void round_kernel_dlv4(RoundArgs a) {
                 tgw[q] = (((r.mf >> kDlvMetaNoPull) & 1u) ? kTgNoPull : 0u) | (((r.mf >> kDlvMetaOff) & 1u) ? kTgOff : 0u);
         }
     }
+    // the first kDlvPre tail codes of every node, loaded now rather than in
+    // the delivery loop, where each pusher index with a tail was one
+    // dependent memory round trip for nearly every wave (its 128 nodes hold
+    // a pusher #3 with probability ~1 and a pusher #4 with ~0.9 at in-degree
+    // 1): config 5's kernel 1.689 -> 1.62 ms (two codes; one: no change).
+    // Four nodes per lane (R_pad < 16) measured slower with them.
+    constexpr uint32_t kDlvPre = kNpl <= 2 ? GS_DLV4_TAIL_PRE : 0u;
+    uint32_t tpre[kDlvPre > 0 ? kDlvPre : 1][kNpl];
+#pragma unroll
+    for (uint32_t j = 0; j < kDlvPre; ++j)
+#pragma unroll
+        for (uint32_t q = 0; q < kNpl; ++q) tpre[j][q] = (DELIVER && kk[q] > kDlvInline + j) ? a.dtail[dfirst[q] + j] : 0u;
     __syncthreads();
     // class planes now; the five b planes only for the transition (still in
     // LDS then: fewer registers live across the deliveries)
@@ -190,7 +206,12 @@ void round_kernel_dlv4(RoundArgs a) {
 #pragma unroll
             for (uint32_t q = 0; q < kNpl; ++q) {
                 if (i < kk[q]) {
-                    const uint32_t code = i == 0 ? c0[q] : (i == 1 ? c1[q] : a.dtail[dfirst[q] + i - kDlvInline]);
+                    uint32_t code;
+                    if (i == 0) code = c0[q];
+                    else if (i == 1) code = c1[q];
+                    else if (kDlvPre > 0 && i == kDlvInline) code = tpre[0][q];
+                    else if (kDlvPre > 1 && i == kDlvInline + 1) code = tpre[kDlvPre > 1 ? 1 : 0][q];
+                    else code = a.dtail[dfirst[q] + i - kDlvInline];
                     b0 |= ((T)code & m1) << (q * rp);
                     b1 |= ((T)(code >> 16) & m1) << (q * rp);
                     if ((pulledM & M[q]) && i == dzi[q]) recm &= ~M[q];
