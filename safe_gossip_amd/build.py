@@ -15,7 +15,7 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libsafe_gossip_amd.so")
 SOURCES = [os.path.join(CSRC, "gs_kernels.hip"), os.path.join(CSRC, "gs_inlist.hip"),
-           os.path.join(CSRC, "gs_shard.hip"), os.path.join(CSRC, "gs_seq.hip"), os.path.join(CSRC, "gs_dlv4.hip"), os.path.join(CSRC, "gs_pipe.hip"), os.path.join(CSRC, "gs_w32.hip"), os.path.join(CSRC, "gs_verify.hip"),
+           os.path.join(CSRC, "gs_shard.hip"), os.path.join(CSRC, "gs_seq.hip"), os.path.join(CSRC, "gs_dlv4.hip"), os.path.join(CSRC, "gs_w32.hip"), os.path.join(CSRC, "gs_verify.hip"),
            os.path.join(CSRC, "gs_engine.cpp"), os.path.join(CSRC, "gs_wire.cpp"),
            os.path.join(CSRC, "gs_sign.cpp")]
 HEADERS = [os.path.join(CSRC, f) for f in ("gs_common.h", "gs_kernels.h", "gs_device.h", "gs_recv.h")] + [

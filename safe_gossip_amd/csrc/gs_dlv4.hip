@@ -48,16 +48,14 @@ GS_DEV T ge_seg(const T (&x)[NB], const T (&km)[NB]) {
     return ~b;
 }
 
-// FUSE: the launch also runs the next build's first partition (a.cp_e set).
 // SH: a code-row shard engine (gs_shard.hip, ShardPlan::codes): the pull code
 // x received is read from exchange B at x's slot (spos_cur) instead of
 // PULL[x], and its next push code goes with its target into its exchange-A
 // row (spos_next) instead of PC[x]; blocks [blk_off, blk_off + grid) (a
 // pipeline part).
-template <int MODE, typename T, uint32_t kNpl, bool FUSE, bool SH = false>
-__global__ __launch_bounds__(kDlv4Threads, (kNpl == 2 && sizeof(T) == 4 && !FUSE) ? GS_DLV4_MINW_R16 : GS_DLV4_MINW)
+template <int MODE, typename T, uint32_t kNpl, bool SH = false>
+__global__ __launch_bounds__(kDlv4Threads, (kNpl == 2 && sizeof(T) == 4) ? GS_DLV4_MINW_R16 : GS_DLV4_MINW)
 void round_kernel_dlv4(RoundArgs a) {
-    static_assert(!(FUSE && SH), "shards build their in-lists from the exchanged ids");
     constexpr bool DELIVER = MODE == 1;
     const Geometry &g = a.g;
     if (a.zero_buf || a.zero_rows) zero_for_build(a.zero_buf, a.zero_words, a.zero_rows);
@@ -402,8 +400,7 @@ void round_kernel_dlv4(RoundArgs a) {
     for (uint32_t q = 0; q < kNpl; ++q)
         eav[q] = (a.eadd && q < nv) ? reinterpret_cast<const uint16_t *>(a.eadd)[x0 + q] : 0u;
 
-    // ---- push codes of round t+1 for the in-list build (4 B per node; the
-    // fused partition below carries them itself)
+    // ---- push codes of round t+1 for the in-list build (4 B per node)
     uint32_t pc[kNpl];
     {
         const T vC = N[0] & ~(N[1] & N[2]), vB = ~N[0] & (N[1] | N[2]);
@@ -430,11 +427,7 @@ void round_kernel_dlv4(RoundArgs a) {
                     if (q < nv) a.kn_out[x0 + q] = (uint16_t)k16[q];
             }
         }
-        if (FUSE) {  // (the partition below carries the push codes; the build's sort reads them too)
-#pragma unroll
-            for (uint32_t q = 0; q < kNpl; ++q)
-                if (q < nv) a.pc_out[x0 + q] = pc[q];
-        } else if (SH) {
+        if (SH) {
             // exchange A of round t+1: to owner(t_{t+1}(x)) (no slot: an
             // undelivered edge, or a capacity overflow, flagged by the plan),
             // the row (push code, target local to that rank | kRowMutual when
@@ -532,78 +525,6 @@ void round_kernel_dlv4(RoundArgs a) {
         // waiting a memory round trip at their end at 1 % churn)
         if (!on) atomicAdd(&a.offc[x0 + q], 1u);
     }
-
-    // ---- fused first partition of round t+1's build (dl_coarse's work,
-    // gs_inlist.hip): every node's round-(t+1) target word (peer choice and
-    // harness faults, src/gossiper.rs:71) and its (source, target, push code)
-    // entry into the coarse bucket of its target, one reservation per bucket
-    // in shard blockIdx.x % S of the next set's coarse regions
-    if constexpr (FUSE) {
-        constexpr uint32_t kMaxCp = 64;  // coarse buckets (the host fuses only nc <= 64)
-        constexpr uint32_t kBlkNodes = kDlv4Threads * kNpl;
-        __shared__ uint32_t ccnt[kMaxCp], coff[kMaxCp], cres[kMaxCp];
-        __shared__ uint32_t cx[kBlkNodes], ct[kBlkNodes], cc[kBlkNodes];
-        __shared__ uint32_t lds_scan[kDlv4Threads / 64];
-        const uint32_t nc = a.cp_nc, shard = blockIdx.x % a.cp_shards, cap = a.cp_shard_cap;
-        if (threadIdx.x < nc) ccnt[threadIdx.x] = 0u;
-        uint32_t tq[kNpl];
-#pragma unroll
-        for (uint32_t q = 0; q < kNpl; ++q)
-            tq[q] = q < nv ? target_word(a.seed, a.epoch, a.round_new, x0 + q, n_nodes, a.f) : kTgDead;
-        if (kNpl == 4 && nv == kNpl) {
-            *reinterpret_cast<uint4 *>(a.tg_out + x0) =
-                make_uint4(tq[0], tq[1], tq[kNpl > 2 ? 2 : 0], tq[kNpl > 3 ? 3 : 0]);
-        } else if (kNpl == 2 && nv == kNpl) {
-            *reinterpret_cast<uint2 *>(a.tg_out + x0) = make_uint2(tq[0], tq[1]);
-        } else {
-#pragma unroll
-            for (uint32_t q = 0; q < kNpl; ++q)
-                if (q < nv) a.tg_out[x0 + q] = tq[q];
-        }
-        __syncthreads();
-#pragma unroll
-        for (uint32_t q = 0; q < kNpl; ++q)
-            if (!(tq[q] & kTgDead)) atomicAdd(&ccnt[(tq[q] & kTgMask) >> a.cp_log], 1u);
-        __syncthreads();
-        {  // exclusive scan of the bucket counts; one reservation per bucket
-            const uint32_t c = threadIdx.x < nc ? ccnt[threadIdx.x] : 0u;
-            uint32_t total;
-            const uint32_t ex = block_exclusive_scan(c, lds_scan, total);
-            if (threadIdx.x < nc) {
-                coff[threadIdx.x] = ex;
-                uint32_t r0 = c ? atomicAdd(&a.cp_fill[threadIdx.x * a.cp_shards + shard], c) : 0u;
-                if (r0 + c > cap) {
-                    atomicOr(&a.flags[2], 2u);  // a device limit (coarse region full)
-                    r0 = cap;
-                }
-                cres[threadIdx.x] = r0;
-                ccnt[threadIdx.x] = ex;  // cursor
-            }
-        }
-        __syncthreads();
-        uint32_t total = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < kNpl; ++q) {
-            if (tq[q] & kTgDead) continue;
-            const uint32_t t = tq[q] & kTgMask;
-            const uint32_t pos = atomicAdd(&ccnt[t >> a.cp_log], 1u);
-            cx[pos] = x0 + q;
-            ct[pos] = t;
-            cc[pos] = pc[q];
-        }
-        __syncthreads();
-        total = ccnt[nc - 1u];  // the last bucket's cursor ends the block's entries
-        for (uint32_t i = threadIdx.x; i < total; i += kDlv4Threads) {
-            const uint32_t b = ct[i] >> a.cp_log;
-            const uint32_t slot = cres[b] + (i - coff[b]);
-            if (slot < cap) {
-                const u64 o = ((u64)(b * a.cp_shards + shard) * cap + slot) * 3u;
-                a.cp_e[o] = cx[i];
-                a.cp_e[o + 1] = ct[i];
-                a.cp_e[o + 2] = cc[i];
-            }
-        }
-    }
 }
 
 template <typename T, uint32_t NPL>
@@ -613,21 +534,16 @@ static hipError_t launch_dlv4_t(const RoundArgs &a, int mode, hipStream_t s) {
     const u64 grid = a.blk_count ? a.blk_count : nblk;
     if (grid == 0) return hipSuccess;
     if (a.blk_off + grid > nblk) return hipErrorInvalidValue;
-    if (a.cp_e && (a.cp_nc == 0 || a.cp_nc > 64 || a.cp_shards == 0 || !a.tg_out || a.recvA))
-        return hipErrorInvalidValue;
     const dim3 gd((uint32_t)grid), bd(kDlv4Threads);
     if (a.recvA) {  // code-row shard
         if (!a.sp.codes || !a.recvB || !a.sendA || !a.recvA_next || !a.spos_cur || !a.spos_next || !a.tg_next ||
             !a.sp.chunk)
             return hipErrorInvalidValue;
-        if (mode == 0) hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL, false, true>), gd, bd, 0, s, a);
-        else hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, false, true>), gd, bd, 0, s, a);
-    } else if (a.cp_e) {
         if (mode == 0) hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL, true>), gd, bd, 0, s, a);
         else hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, true>), gd, bd, 0, s, a);
     } else {
-        if (mode == 0) hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL, false>), gd, bd, 0, s, a);
-        else hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, false>), gd, bd, 0, s, a);
+        if (mode == 0) hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL>), gd, bd, 0, s, a);
+        else hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL>), gd, bd, 0, s, a);
     }
     return hipGetLastError();
 }

@@ -71,11 +71,7 @@ struct gs_engine {
     // SAFE_GOSSIP_AMD_DLV_PACK = 0 one node per lane, u64 four 16-bit nodes
     // per 64-bit lane word, otherwise (default) a 32-bit lane word
     uint32_t dlv_pack = 1;
-    // SAFE_GOSSIP_AMD_PIPE=1: the wide 2P gather path runs the pipelined
-    // round kernel (gs_pipe.hip) instead of round_kernel
-    bool no_pipe = false;
     bool w32 = false;  // 2P gather path: the 32-bit lane round kernel on eligible launches (gs_w32.hip)
-    uint32_t pipe_grid = 0;  // SAFE_GOSSIP_AMD_PIPE_GRID: fewer blocks (tests: many tiles per block)
     // Sparse records (wide 2P engine, W <= 8; gs_kernels.h RoundArgs): maps of
     // plane buffer i, the accounting words and MODE-1 launches counted in them
     // The sparse variant runs while the input planes are at least a quarter
@@ -139,12 +135,6 @@ struct gs_engine {
     int ra_mode = 0;
     bool ra_sparse = false;
     bool ra_prezeroed = false;  // the round kernel clears the next build's counters
-    // DLV: the transition launch runs the next build's first partition
-    // (opt-in SAFE_GOSSIP_AMD_FUSE_COARSE=1; measured slower: its 512-node
-    // blocks make 8x the coarse reservations of dl_coarse's 4 K-source
-    // chunks, config 5 4.62 -> 6.03 ms per step)
-    bool fuse_coarse = false;
-    bool ra_fused = false;  // this round's launch did
     uint32_t *st32 = nullptr;  // [n][4] u32 deltas (u16 with st16)
     bool st16 = false;         // delivery-record engines: u16 deltas (gs_device.h load_stats)
     u64 *st64 = nullptr;       // [n][4] folded totals
@@ -414,9 +404,7 @@ gs::RoundArgs base_args(gs_engine *e) {
     }
     a.obs_only = 0xFFFFFFFFu;
     a.dlv_pack = e->dlv_pack;
-    a.no_pipe = e->no_pipe ? 1u : 0u;
     a.w32 = e->w32 ? 1u : 0u;
-    a.pipe_grid = e->pipe_grid;
     a.g = e->g;
     a.seed = e->seed;
     a.epoch = e->epoch;
@@ -802,19 +790,13 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         e->key_order[r] = r;
     }
     {
-        const char *v = std::getenv("SAFE_GOSSIP_AMD_PIPE");
-        e->no_pipe = !(v && *v == '1');  // opt-in: measured slower than round_kernel
         // The 32-bit lane round kernel (gs_w32.hip) by default where a lane
         // holds one node (R_pad 32: 2^24 x 32, 1.24 -> 1.10 ms/step); at R_pad
         // 64..256 its duplicated per-node work costs more than its occupancy
         // gains (config 4: 2.61 -> 3.03 ms per launch).
         // SAFE_GOSSIP_AMD_W32=0/1 forces the 64-bit / 32-bit lane kernel.
-        const char *fc = std::getenv("SAFE_GOSSIP_AMD_FUSE_COARSE");
-        e->fuse_coarse = fc && *fc == '1';
         const char *w = std::getenv("SAFE_GOSSIP_AMD_W32");
         e->w32 = (w && *w) ? *w != '0' : (e->g.small && e->g.rpad == 32u);
-        const char *gv = std::getenv("SAFE_GOSSIP_AMD_PIPE_GRID");
-        e->pipe_grid = gv ? (uint32_t)std::strtoul(gv, nullptr, 10) : 0u;
     }
     {
         const char *v = std::getenv("SAFE_GOSSIP_AMD_CONCURRENT_INLISTS");
@@ -874,8 +856,8 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
     }
     const gs::InListSizes isz = gs::inlist_sizes(e->plan);
     // per-node arrays the pipelined round kernel reads by whole 64-node tiles
-    const size_t npad = gs::pipe_padded(n);
-    const size_t sw_pad = (size_t)gs::pipe_padded(g.units) * gs::kPlanes * g.W;
+    const size_t npad = gs::tile_padded(n);
+    const size_t sw_pad = (size_t)gs::tile_padded(g.units) * gs::kPlanes * g.W;
     for (int i = 0; i < 2 && ok && !e->shard; ++i) {
         auto &c = e->csr[i];
         ok = hipEventCreateWithFlags(&e->ev_built[i], hipEventDisableTiming) == hipSuccess &&
@@ -1270,7 +1252,6 @@ gs_status round_begin(gs_engine *e) {
     // the build of round t+1 runs right behind this kernel on its stream: the
     // kernel clears that build's counters (no memset launch)
     e->ra_prezeroed = !e->shard && !e->split_build && !(e->concurrent_inlists && !e->dlv);
-    e->ra_fused = false;
     if (e->ra_prezeroed) {
         auto &c = e->csr[(R0 + 1u) & 1u];
         size_t first = 0, words = 0;
@@ -1288,18 +1269,6 @@ gs_status round_begin(gs_engine *e) {
         if (words) {
             a.zero_buf2 = e->csr[R0 & 1u].scratch + first;
             a.zero_words2 = (uint32_t)words;
-        }
-        gs::CoarseTarget ct{};
-        if (e->dlv && e->fuse_coarse && e->dlv_pack && a.n_ext == 0 &&
-            gs::dlv_coarse_target(e->plan, c.region, c.scratch, &ct) && ct.nc <= 64) {
-            a.cp_e = ct.e;
-            a.cp_fill = ct.fill;
-            a.cp_nc = ct.nc;
-            a.cp_shards = ct.shards;
-            a.cp_shard_cap = ct.shard_cap;
-            a.cp_log = ct.log;
-            a.tg_out = c.tg;
-            e->ra_fused = true;
         }
     }
     e->ra = a;
@@ -1408,7 +1377,6 @@ gs_status round_end(gs_engine *e, gs_round_report *report) {
             if (st != GS_OK) return st;
             gs::InListArgs la = inlist_args(e, c, e->round);
             la.prezeroed = e->ra_prezeroed ? 1u : 0u;
-            la.coarse_done = e->ra_fused ? 1u : 0u;
             if (e->filt && !e->ra_prezeroed) GS_HIP(hipMemsetAsync(la.rows, 0, sizeof(u64), bs));
             GS_HIP(gs::launch_build_inlists(la, bs));
         }

@@ -1405,16 +1405,6 @@ void inlist_cfill_range(const CsrPlan &p, size_t *first, size_t *words) {
     *words = p.dlv && p.binned ? (size_t)n_coarse(p.nb) * kCoarseShards : 0u;
 }
 
-bool dlv_coarse_target(const CsrPlan &p, uint32_t *region, uint32_t *scratch, CoarseTarget *out) {
-    if (!p.binned || !p.dlv || n_coarse(p.nb) < 2u) return false;  // (one coarse bucket: dl_direct)
-    out->e = reinterpret_cast<uint32_t *>(coarse_entries(region, p.nb));
-    out->fill = scratch + cfill_off(p);
-    out->nc = n_coarse(p.nb);
-    out->shards = kCoarseShards;
-    out->shard_cap = kShardCap;
-    out->log = kCoarseLog;
-    return true;
-}
 
 InListSizes inlist_sizes(const CsrPlan &p) {
     InListSizes z{};
@@ -1561,8 +1551,7 @@ hipError_t launch_dlv_build(const InListArgs &a, hipStream_t s) {
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(dl_direct<SH>, dim3(p.ba), dim3(kInlThreads), lds_d, s, ab);
     } else {
-        if (!a.coarse_done)  // (else the transition launch before partitioned the entries)
-            hipLaunchKernelGGL((dl_coarse<kCoarseThreads, SH>), dim3(p.ba), dim3(kCoarseThreads), lds_c, s, ab);
+        hipLaunchKernelGGL((dl_coarse<kCoarseThreads, SH>), dim3(p.ba), dim3(kCoarseThreads), lds_c, s, ab);
         hipLaunchKernelGGL(dl_fine<kFineThreads>, dim3((kShardCap + kFineChunk - 1) / kFineChunk, nc * kCoarseShards),
                            dim3(kFineThreads), lds_f, s, ab);
     }

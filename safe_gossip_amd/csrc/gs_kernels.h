@@ -117,15 +117,7 @@ struct RoundArgs {
     // transition launch (gs_slice_defer: no separate apply pass).
     uint8_t *emin;
     const uint8_t *eadd;
-    uint32_t no_pipe;         // 1: the wide 2P path runs round_kernel instead of round_pipe
-    uint32_t pipe_grid;       // round_pipe's block count (0: every resident block)
     uint32_t w32;             // 1: eligible launches run round_kernel_w32 (gs_w32.hip)
-    // DLV transition launches (gs_dlv4.hip) may run the first partition of
-    // the next round's build in their epilogue, in place of dl_coarse: the
-    // round-(t+1) target words (tg_out) and the (source, target, push code)
-    // entries into the coarse shards of the next set (cp_e null: not fused)
-    uint32_t *cp_e, *cp_fill, *tg_out;  // cp_e: 12-byte (source, target, code) entries
-    uint32_t cp_nc, cp_shards, cp_shard_cap, cp_log;
     // a second range cleared at the start (the coarse fills of the set the
     // previous round's build consumed)
     uint32_t *zero_buf2;
@@ -155,15 +147,11 @@ hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s);
 // DLV transition launches (modes 0 and 1, no external RPCs) with four nodes
 // per lane (gs_dlv4.hip).
 hipError_t launch_round_dlv4(const RoundArgs &a, int mode, hipStream_t s);
-// The pipelined round kernel of the wide 2P gather path (gs_pipe.hip): modes
-// 0 and 1, W = 2 / 4 / 8, the whole grid, no sparse records.
-bool pipe_eligible(const RoundArgs &a, int mode);
-// Its tiles are 64 nodes; every per-node array it reads (planes, InRec,
-// SibRec, target words, Statistics deltas) is allocated for n rounded up to
-// whole tiles, since the last tile's DMA reads past n.
-constexpr uint32_t kPipeTileNodes = 64;
-inline uint64_t pipe_padded(uint64_t n) { return (n + kPipeTileNodes - 1) / kPipeTileNodes * kPipeTileNodes; }
-hipError_t launch_round_pipe(const RoundArgs &a, int mode, hipStream_t s);
+// Per-node arrays (planes, InRec, SibRec, target words, Statistics deltas)
+// are allocated for n rounded up to whole 64-node tiles (round 3's pipelined
+// round kernel read whole tiles; kept as headroom).
+constexpr uint32_t kTileNodes = 64;
+inline uint64_t tile_padded(uint64_t n) { return (n + kTileNodes - 1) / kTileNodes * kTileNodes; }
 // The 2P gather path with a 32-bit lane word (gs_w32.hip): modes 0 and 1,
 // R_pad 32 (a lane per node; the engine's default there) or 64..256 (half a
 // 64-rumor word per lane; only when SAFE_GOSSIP_AMD_W32=1 forces it),
@@ -200,12 +188,6 @@ InListSizes inlist_sizes(const CsrPlan &p);
 void inlist_zero_range(const CsrPlan &p, size_t *first, size_t *words);
 // DLV: the coarse shard fills (cleared one round later than the other counters).
 void inlist_cfill_range(const CsrPlan &p, size_t *first, size_t *words);
-// DLV with several coarse buckets: where a fused partition writes (false: none).
-struct CoarseTarget {
-    uint32_t *e, *fill;  // e: the 12-byte coarse entries
-    uint32_t nc, shards, shard_cap, log;
-};
-bool dlv_coarse_target(const CsrPlan &p, uint32_t *region, uint32_t *scratch, CoarseTarget *out);
 
 struct InListArgs {
     CsrPlan p;
@@ -219,7 +201,6 @@ struct InListArgs {
     // PC[y] they are all a target's planes say about its pull batch
     const uint16_t *KN;
     uint32_t prezeroed;     // 1: the round kernel before cleared the counters (RoundArgs::zero_*)
-    uint32_t coarse_done;   // 1: the round kernel before wrote tg and the coarse partition
     Geometry g;
     DlvRec *DR;         // [n]
     uint32_t *dtail;    // [tailcap] push codes of pushers >= kDlvInline

@@ -1056,7 +1056,6 @@ hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s) {
         if (a.dlv_pack && (mode == 0 || mode == 1) && a.n_ext == 0) return launch_round_dlv4(a, mode, s);
         return launch_mode<true, false, false, true>(a, mode, s);
     }
-    if (!a.no_pipe && pipe_eligible(a, mode)) return launch_round_pipe(a, mode, s);  // gs_pipe.hip (opt-in)
     if (w32_eligible(a, mode)) return launch_round_w32(a, mode, s);                   // gs_w32.hip
     return a.g.small ? launch_mode<true, false, false>(a, mode, s) : launch_mode<false, false, false>(a, mode, s);
 }

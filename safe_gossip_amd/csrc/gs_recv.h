@@ -1,6 +1,6 @@
 // gs_recv.h -- receiver-side bit-sliced state of phases 1-2 of a round at
 // one node (Gossip::receive, src/gossip.rs:118-163), shared by the round
-// kernels (gs_kernels.hip, gs_pipe.hip).
+// kernels (gs_kernels.hip, gs_w32.hip).
 #pragma once
 #include "gs_device.h"
 #include "gs_kernels.h"

@@ -76,18 +76,16 @@ def test_packed_dlv_matches_node_per_lane(engine, monkeypatch):
         b.close()
 
 
-@pytest.mark.parametrize("n,fuse", [((1 << 22) + 54321, "0"), ((1 << 23) + 4321, "0"), ((1 << 23) + 4321, "1")])
-def test_dlv_partition_build_matches_gather_path(engine, monkeypatch, n, fuse):
+@pytest.mark.parametrize("n", [(1 << 22) + 54321, (1 << 23) + 4321])
+def test_dlv_partition_build_matches_gather_path(engine, monkeypatch, n):
     # The DLV build of networks with more than one coarse bucket (n > 2^21:
     # dl_coarse -> dl_fine -> inl_sort_dlv -> pb_fine -> pb_place) against the
     # class-plane gather path (SAFE_GOSSIP_AMD_NO_DLV=1: inl_bin / inl_sort and
     # the gathers of gs_kernels.hip), an independent build of the same round:
     # every state code, Statistics row and known set, every round, with faults.
     # 260 / 513 bins: quarter-bin sort parts over 3 / 5 coarse buckets, the
-    # config-5 shape; fuse "1": the first partition in the transition launch's
-    # epilogue (SAFE_GOSSIP_AMD_FUSE_COARSE, opt-in) instead of dl_coarse.
+    # config-5 shape.
     R = 16
-    monkeypatch.setenv("SAFE_GOSSIP_AMD_FUSE_COARSE", fuse)
     faults = dict(churn=0.01, drop_push=0.01, drop_pull=0.01)
     a = engine.Network(n, R, seed=SEED, **faults)
     monkeypatch.setenv("SAFE_GOSSIP_AMD_NO_DLV", "1")

@@ -457,24 +457,6 @@ def test_parity_filtered_larger(engine):
     run_parity(engine, 20000, 256, "origins", check_every=3, faults=(0.02, 0.05, 0.05))
 
 
-@pytest.mark.parametrize("n,R,kind,faults,grid", [
-    (20000, 256, "origins", None, 7),             # 313 tiles over 7 blocks: the DMA pipeline
-    (20000, 256, "trickle", (0.02, 0.05, 0.05), 3),
-    (5000, 128, "reinject", None, 5),             # W = 2
-    (3000, 512, "origins", (0.05, 0.05, 0.05), 2),  # W = 8
-    (1000, 200, "origins", None, 1),              # one block walks every tile; R padded to 256
-    (4097, 256, "origins", None, 0),              # the resident grid; last tile of one node
-    (63, 256, "origins", None, 0),                # a single partial tile
-])
-def test_parity_pipe(engine, monkeypatch, n, R, kind, faults, grid):
-    # the pipelined round kernel (gs_pipe.hip) of the wide 2P gather path,
-    # with few blocks so each walks many tiles (prefetch into the other LDS
-    # buffer, partial last tile)
-    monkeypatch.setenv("SAFE_GOSSIP_AMD_PIPE", "1")
-    monkeypatch.setenv("SAFE_GOSSIP_AMD_PIPE_GRID", str(grid))
-    run_parity(engine, n, R, kind, faults=faults, check_every=2)
-
-
 @pytest.mark.parametrize("n,R,filt", [(3000, 256, "1"), (3000, 256, "0"), (2000, 128, "1")])
 def test_parity_round_kernel_wide(engine, monkeypatch, n, R, filt):
     # the 64-bit lane round_kernel on the wide 2P path, filtered and
@@ -483,7 +465,6 @@ def test_parity_round_kernel_wide(engine, monkeypatch, n, R, filt):
     # (every other wide 2P test runs it too); round_kernel_w32 is the default
     # at R_pad 32 only, and runs at R_pad 64..256 where test_parity_w32
     # forces it (SAFE_GOSSIP_AMD_W32=1)
-    monkeypatch.setenv("SAFE_GOSSIP_AMD_PIPE", "0")
     monkeypatch.setenv("SAFE_GOSSIP_AMD_W32", "0")
     monkeypatch.setenv("SAFE_GOSSIP_AMD_FILTER", filt)
     run_parity(engine, n, R, "origins", check_every=2)
@@ -500,7 +481,6 @@ def test_parity_round_kernel_wide(engine, monkeypatch, n, R, filt):
 ])
 def test_parity_w32(engine, monkeypatch, n, R, kind, faults):
     # the 32-bit lane round kernel (gs_w32.hip), forced on explicitly
-    monkeypatch.setenv("SAFE_GOSSIP_AMD_PIPE", "0")
     monkeypatch.setenv("SAFE_GOSSIP_AMD_W32", "1")
     run_parity(engine, n, R, kind, faults=faults, check_every=1 if n < 5000 else 3)
 
