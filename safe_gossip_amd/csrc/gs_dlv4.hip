@@ -497,12 +497,7 @@ void round_kernel_dlv4(RoundArgs a) {
     }
 
     // ---- any-live flag of round t+1, Statistics (src/gossip.rs:80,103-111)
-    if (bid == 0 && threadIdx.x == 0)  // slot of round t, read by the host already
-        __hip_atomic_store(&a.flags[(a.round_new + 1u) & 1u], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (threadIdx.x == 0 && blk_any) {
-        uint32_t *f = &a.flags[a.round_new & 1u];
-        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) atomicOr(f, 1u);
-    }
+    mark_any_live(a.live, a.round_new, bid, blk_any != 0u);
 #pragma unroll
     for (uint32_t q = 0; q < kNpl; ++q) {
         if (q >= nv) break;

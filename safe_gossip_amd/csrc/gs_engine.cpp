@@ -138,6 +138,7 @@ struct gs_engine {
     uint32_t *st32 = nullptr;  // [n][4] u32 deltas (u16 with st16)
     bool st16 = false;         // delivery-record engines: u16 deltas (gs_device.h load_stats)
     u64 *st64 = nullptr;       // [n][4] folded totals
+    uint32_t *live = nullptr;  // any-live words (gs_kernels.h RoundArgs::live)
     uint32_t fold_every = 1, since_fold = 0;
     u64 *inj_key = nullptr, *inj_mask = nullptr;
     u64 *inj_host = nullptr;  // pinned staging [2*cap]
@@ -249,7 +250,7 @@ void release(gs_engine *e) {
     for (int i = 0; i < 2; ++i)
         if (e->ev_dens[i]) (void)hipEventDestroy(e->ev_dens[i]);
     if (e->dens_host) (void)hipHostFree(e->dens_host);
-    void *bufs[] = {e->lvm, e->cpm, e->rows_dev, e->zb[0], e->zb[1], e->lb[0], e->lb[1], e->ab[0], e->ab[1], e->acct, e->dens, e->pc, e->kn, e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
+    void *bufs[] = {e->lvm, e->cpm, e->rows_dev, e->zb[0], e->zb[1], e->lb[0], e->lb[1], e->ab[0], e->ab[1], e->acct, e->dens, e->pc, e->kn, e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->live, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
                     e->partials, e->obs_state, e->obs_rec, e->obs_psize, e->obs_digest, e->obs_pend, e->ext_dev,
                     e->node_state};
     for (void *b : bufs)
@@ -271,6 +272,7 @@ gs_status reset_state(gs_engine *e) {
     if (e->offc) GS_HIP(hipMemsetAsync(e->offc, 0, (size_t)g.n * sizeof(uint32_t), e->stream));
     e->since_fold = 0;
     GS_HIP(hipMemsetAsync(e->flags, 0, 4 * sizeof(uint32_t), e->stream));
+    GS_HIP(hipMemsetAsync(e->live, 0, (size_t)2 * gs::kLiveSlots * gs::kLiveStride * sizeof(uint32_t), e->stream));
     if (e->spr) {  // both plane buffers are zero: every word zero, no node live
         for (int i = 0; i < 2; ++i) {
             GS_HIP(hipMemsetAsync(e->zb[i], 0xFF, gs::spr_zb_words(g) * sizeof(u64), e->stream));
@@ -398,6 +400,7 @@ gs::RoundArgs base_args(gs_engine *e) {
     }
     a.obs_rounds = e->round;
     a.flags = e->flags;
+    a.live = e->live;
     if (e->deliver_pending && !e->ext.empty()) {  // uploaded by the caller (upload_ext)
         a.ext = e->ext_dev;
         a.n_ext = e->ext_uploaded;
@@ -876,7 +879,7 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         }
     }
     ok = ok && dalloc(&e->S[0], sw_pad) == hipSuccess && dalloc(&e->S[1], sw_pad) == hipSuccess &&
-         dalloc(&e->flags, 4) == hipSuccess && dalloc(&e->st32, (size_t)4 * npad) == hipSuccess &&
+         dalloc(&e->flags, 4) == hipSuccess && dalloc(&e->live, (size_t)2 * gs::kLiveSlots * gs::kLiveStride) == hipSuccess && dalloc(&e->st32, (size_t)4 * npad) == hipSuccess &&
          dalloc(&e->st64, (size_t)4 * n) == hipSuccess;
     if (ok && e->dlv) ok = dalloc(&e->pc, n) == hipSuccess && (e->shard || dalloc(&e->kn, n) == hipSuccess);
     if (ok && e->filt)
@@ -1384,10 +1387,15 @@ gs_status round_end(gs_engine *e, gs_round_report *report) {
     }
     if (report) {
         uint32_t fl[4];
+        static thread_local uint32_t lw[gs::kLiveSlots * gs::kLiveStride];
         GS_HIP(hipMemcpyAsync(fl, e->flags, sizeof(fl), hipMemcpyDeviceToHost, e->stream));
+        GS_HIP(hipMemcpyAsync(lw, e->live + (size_t)(e->round & 1u) * gs::kLiveSlots * gs::kLiveStride, sizeof(lw),
+                              hipMemcpyDeviceToHost, e->stream));
         GS_HIP(hipStreamSynchronize(e->stream));
         report->round = e->round;
-        report->any_live = fl[e->round & 1u];
+        uint32_t any = 0;
+        for (uint32_t i = 0; i < gs::kLiveSlots; ++i) any |= lw[i * gs::kLiveStride];
+        report->any_live = any;
         if (fl[2]) return GS_ERR_DEVICE_LIMIT;
     }
     return GS_OK;

@@ -41,8 +41,13 @@ struct RoundArgs {
     const u64 *inj_key;       // sorted segment keys with injections (round t+1)
     const u64 *inj_mask;      //   rumor masks in segment coordinates
     uint32_t n_inj;
-    uint32_t *flags;          // [0..1] any_live per round parity (the kernel of round
-                              // t+1 clears round t's slot), [2] device limit
+    uint32_t *flags;          // [2] device limit
+    // any_live of round t+1: kLiveSlots words per round parity, kLiveStride
+    // apart (separate 128-B lines); a block with a live node stores 1 into
+    // word bid % kLiveSlots (a plain store: no read at the block's end, no
+    // returning atomic), the host ORs them; block 0 of the kernel of round
+    // t+1 clears round t's words
+    uint32_t *live;
     // observation outputs (mode OBSERVE); any may be null
     u64 *obs_known;           // [n][KW]
     u64 *obs_stats;           // [n][5]
@@ -147,6 +152,17 @@ hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s);
 // DLV transition launches (modes 0 and 1, no external RPCs) with four nodes
 // per lane (gs_dlv4.hip).
 hipError_t launch_round_dlv4(const RoundArgs &a, int mode, hipStream_t s);
+constexpr uint32_t kLiveSlots = 64, kLiveStride = 32;
+// The any-live words of round t+1 (RoundArgs::live) at the end of a
+// transition launch's block.
+__device__ __forceinline__ void mark_any_live(uint32_t *live, uint32_t round_new, uint32_t bid, bool blk_live) {
+    if (bid == 0 && threadIdx.x < kLiveSlots)  // round t's words, read by the host already
+        __hip_atomic_store(&live[(((round_new + 1u) & 1u) * kLiveSlots + threadIdx.x) * kLiveStride], 0u,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0 && blk_live)
+        __hip_atomic_store(&live[((round_new & 1u) * kLiveSlots + (bid & (kLiveSlots - 1u))) * kLiveStride], 1u,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // Per-node arrays (planes, InRec, SibRec, target words, Statistics deltas)
 // are allocated for n rounded up to whole 64-node tiles (round 3's pipelined
 // round kernel read whole tiles; kept as headroom).

@@ -971,14 +971,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     }
 
     // ---- push list + Statistics (src/gossip.rs:80,103-111)
-    if (bid == 0 && threadIdx.x == 0)  // slot of round t, read by the host already
-        __hip_atomic_store(&a.flags[(a.round_new + 1u) & 1u], 0u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    if (threadIdx.x == 0 && blk_live) {
-        uint32_t *f = &a.flags[a.round_new & 1u];
-        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-            atomicOr(f, 1u);
-    }
+    mark_any_live(a.live, a.round_new, bid, blk_live);
     if (leader) {
 #ifndef GS_EXP_NO_STATS
         // rounds is the engine's round count (every node runs every round);

@@ -317,12 +317,7 @@ __global__ __launch_bounds__(kW32Threads, GS_W32_MINW) void round_kernel_w32(Rou
     }
 
     // ---- push list + Statistics (src/gossip.rs:80,103-111)
-    if (bid == 0 && threadIdx.x == 0)  // slot of round t, read by the host already
-        __hip_atomic_store(&a.flags[(a.round_new + 1u) & 1u], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (threadIdx.x == 0 && blk_live) {
-        uint32_t *f = &a.flags[a.round_new & 1u];
-        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) atomicOr(f, 1u);
-    }
+    mark_any_live(a.live, a.round_new, bid, blk_live);
     if (leader) {
         // rounds is the engine's round count (every node runs every round);
         // the other four are u32 deltas folded into u64 before they can wrap.
