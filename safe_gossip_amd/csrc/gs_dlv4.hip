@@ -28,11 +28,13 @@ constexpr uint32_t kDlv4Threads = 256;
 #define GS_DLV4_MINW 4
 #endif
 #ifndef GS_DLV4_TAIL_PRE
-#define GS_DLV4_TAIL_PRE 2  // tail codes per node loaded with the metadata (0..2), two nodes per lane or fewer
+#define GS_DLV4_TAIL_PRE 3  // tail codes per node loaded with the metadata (0..3), two nodes per lane or fewer
 #endif
-static_assert(GS_DLV4_TAIL_PRE <= 2, "tail prefetch depth");
+static_assert(GS_DLV4_TAIL_PRE <= 3, "tail prefetch depth");
+// the config-5 kernel (R_pad 16, two nodes per u32 lane): 7 waves per SIMD
+// (72 VGPRs, no spill with three prefetched tail codes; 8 spilled, round 3)
 #ifndef GS_DLV4_MINW_R16
-#define GS_DLV4_MINW_R16 GS_DLV4_MINW  // the config-5 kernel (R_pad 16, two nodes per u32 lane)
+#define GS_DLV4_MINW_R16 7
 #endif
 
 // The lane word T holds the lane's nodes side by side (u32: two 16-bit or
@@ -154,7 +156,8 @@ void round_kernel_dlv4(RoundArgs a) {
     // the delivery loop, where each pusher index with a tail was one
     // dependent memory round trip for nearly every wave (its 128 nodes hold
     // a pusher #3 with probability ~1 and a pusher #4 with ~0.9 at in-degree
-    // 1): config 5's kernel 1.689 -> 1.62 ms (two codes; one: no change).
+    // 1): config 5's kernel 1.689 -> 1.62 ms with two codes (one: no
+    // change), 1.62 -> 1.59 with three at 7 waves per SIMD.
     // Four nodes per lane (R_pad < 16) measured slower with them.
     constexpr uint32_t kDlvPre = kNpl <= 2 ? GS_DLV4_TAIL_PRE : 0u;
     uint32_t tpre[kDlvPre > 0 ? kDlvPre : 1][kNpl];
@@ -209,6 +212,7 @@ void round_kernel_dlv4(RoundArgs a) {
                     else if (i == 1) code = c1[q];
                     else if (kDlvPre > 0 && i == kDlvInline) code = tpre[0][q];
                     else if (kDlvPre > 1 && i == kDlvInline + 1) code = tpre[kDlvPre > 1 ? 1 : 0][q];
+                    else if (kDlvPre > 2 && i == kDlvInline + 2) code = tpre[kDlvPre > 2 ? 2 : 0][q];
                     else code = a.dtail[dfirst[q] + i - kDlvInline];
                     b0 |= ((T)code & m1) << (q * rp);
                     b1 |= ((T)(code >> 16) & m1) << (q * rp);
