@@ -243,6 +243,10 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     // load is conditional.  Rarer deeper in-lists are walked afterwards.
     Cls q[kBatchK], e[kBatchE], qz = {0, 0, 0}, wz = {0, 0, 0};
     uint32_t ngath = 0;  // class rows gathered (pushers, t(x)): accounting
+    // 2P gather path: the id of pusher #kInline (the first tail entry) read
+    // with the batch, so the walk below waits for its row only (a wave's 16
+    // nodes at config 4 hold such a pusher with probability ~0.26)
+    uint32_t tail0 = 0;
 #pragma unroll
     for (uint32_t i = 0; i < kBatchK; ++i) q[i] = {0, 0, 0};
 #pragma unroll
@@ -308,6 +312,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             for (uint32_t i = 0; i < kBatchE; ++i)
                 if (ge[i]) e[i] = L.load_cls(S, sb8.e[i]);
         } else if (filt) {
+            if (!SEQ && k > kInline) tail0 = a.src[in8.first()];
             // live-filtered: a row that cannot change any result (a pusher with
             // nothing live, a t(x) with nothing live and no live sibling ahead
             // of x to create from, a sibling that is not live or whose target
@@ -330,6 +335,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                 ngath += ge[i] ? 1u : 0u;
             }
         } else {
+            if (!SEQ && k > kInline) tail0 = a.src[in8.first()];
 #pragma unroll
             for (uint32_t i = 0; i < kBatchK; ++i) q[i] = L.load_cls(S, i < k ? in8.s[i] : x);
             ngath += min(k, kBatchK) + (valid ? 1u : 0u);
@@ -554,7 +560,8 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                 }
             }
             for (uint32_t i = kBatchK; i < k; ++i) {  // in-degree > kBatchK (1.9% of nodes)
-                const uint32_t s = i < kInline ? pick_inline(in8.s, i) : a.src[in8.first() + (i - kInline)];
+                const uint32_t s = i < kInline ? pick_inline(in8.s, i)
+                                               : ((i == kInline && !gchk) ? tail0 : a.src[in8.first() + (i - kInline)]);
                 zin |= s == z;
                 const bool gs_ = !gchk || map_bit(a.lb_cur, s);
                 ngath += gs_ ? 1u : 0u;
