@@ -359,6 +359,10 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             }
         }
     }
+    // ... and that pusher's row, issued as soon as the id is in (the batch's
+    // rows, issued after it, stay in flight)
+    Cls t0 = {0, 0, 0};
+    if (DELIVER && !SEQ && !DLV && !SHARD && !gchk && k > kInline) t0 = L.load_cls(S, tail0);
     {
         uint4 *dst4 = reinterpret_cast<uint4 *>(stage);
         dst4[threadIdx.x] = st0;
@@ -565,7 +569,10 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                 zin |= s == z;
                 const bool gs_ = !gchk || map_bit(a.lb_cur, s);
                 ngath += gs_ ? 1u : 0u;
-                rv.push(gs_ ? L.load_cls(S, s) : Cls{0, 0, 0}, i, k, !(pulled && s == z));
+                Cls row = {0, 0, 0};
+                if (i == kInline && !gchk) row = t0;
+                else if (gs_) row = L.load_cls(S, s);
+                rv.push(row, i, k, !(pulled && s == z));
             }
             // Pull batch from z: z's live set plus what z created from pushers
             // ahead of x.
