@@ -363,6 +363,12 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     // rows, issued after it, stay in flight)
     Cls t0 = {0, 0, 0};
     if (DELIVER && !SEQ && !DLV && !SHARD && !gchk && k > kInline) t0 = L.load_cls(S, tail0);
+    // likewise the row of t(x)'s pusher #kBatchE ahead of x (its id is inline)
+    static_assert(kBatchE < kSibInline, "sibling #kBatchE is inline");
+    Cls s2 = {0, 0, 0};
+    if (DELIVER && !SEQ && !DLV && !SHARD && !gchk && r > kBatchE && !(tgw & kTgNoPull) &&
+        (!filt || zneed) && !((eskip >> kBatchE) & 1u))
+        s2 = L.load_cls(S, pick_sib(sb8.e, kBatchE));
     {
         uint4 *dst4 = reinterpret_cast<uint4 *>(stage);
         dst4[threadIdx.x] = st0;
@@ -590,8 +596,17 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                     ++ngath;
                     return L.load_cls(S, s);
                 };
-                for (uint32_t i = kBatchE; i < min(r, kSibInline); ++i)
-                    sibling(sib_row(pick_sib(sb8.e, i), ((eskip >> i) & 1u) != 0), pnot, pB, pC);
+                for (uint32_t i = kBatchE; i < min(r, kSibInline); ++i) {
+                    const bool sk = ((eskip >> i) & 1u) != 0;
+                    Cls row;
+                    if (i == kBatchE && !gchk) {
+                        row = s2;
+                        ngath += sk ? 0u : 1u;
+                    } else {
+                        row = sib_row(pick_sib(sb8.e, i), sk);
+                    }
+                    sibling(row, pnot, pB, pC);
+                }
                 if (r > kSibInline && pnot) {  // rank > 3: 0.2% of nodes
                     InRec zin8 = a.IN8[z];
                     if (filt) zin8.kf &= kInFlagMask;  // (skip flags above the tail start)
