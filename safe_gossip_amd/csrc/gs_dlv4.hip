@@ -165,6 +165,19 @@ void round_kernel_dlv4(RoundArgs a) {
     for (uint32_t j = 0; j < kDlvPre; ++j)
 #pragma unroll
         for (uint32_t q = 0; q < kNpl; ++q) tpre[j][q] = (DELIVER && kk[q] > kDlvInline + j) ? a.dtail[dfirst[q] + j] : 0u;
+    // likewise the votes a node back from offline kept (`pend`, the low words:
+    // R_pad <= 16 here), which the transition otherwise waited for mid-kernel
+    // (at 1 % churn most waves hold such a node; two nodes per lane only,
+    // like the tail codes)
+    constexpr bool kPendPre = kNpl <= 2;
+    uint32_t pv0[kNpl], pv1[kNpl];
+#pragma unroll
+    for (uint32_t q = 0; q < kNpl; ++q) {
+        const uint32_t *pe = reinterpret_cast<const uint32_t *>(a.pend + (u64)(x0 + q) * 2u);
+        const bool off = kPendPre && DELIVER && (tgw[q] & kTgOff);
+        pv0[q] = off ? pe[0] : 0u;
+        pv1[q] = off ? pe[2] : 0u;
+    }
     __syncthreads();
     // class planes now; the five b planes only for the transition (still in
     // LDS then: fewer registers live across the deliveries)
@@ -315,8 +328,9 @@ void round_kernel_dlv4(RoundArgs a) {
         for (uint32_t q = 0; q < kNpl; ++q)
             if (offM & M[q]) {
                 const u64 *pe = a.pend + (u64)(x0 + q) * 2u;
-                bump = (bump & ~M[q]) | (((T)pe[0] & m1) << (q * rp) & Bold);
-                anyCe = (anyCe & ~M[q]) | (((T)pe[1] & m1) << (q * rp) & ninj);
+                const T v0 = kPendPre ? (T)pv0[q] : (T)pe[0], v1 = kPendPre ? (T)pv1[q] : (T)pe[1];
+                bump = (bump & ~M[q]) | ((v0 & m1) << (q * rp) & Bold);
+                anyCe = (anyCe & ~M[q]) | ((v1 & m1) << (q * rp) & ninj);
             }
     }
 #pragma unroll
