@@ -12,6 +12,10 @@ roofline: algorithmic HBM bytes of the round kernel (DESIGN.md "Roofline") per
           launch / its average duration measured with HIP events on the
           engine's stream over the timed rounds; peak 8.0 TB/s.  step_frac:
           the same bytes over the whole step (round kernel + in-list build).
+traffic:  HBM bytes per launch of that kernel from PMC counters, measured in
+          this run by two child rocprofv3 --pmc passes of the same workload
+          (--pmc auto, N=1; else the committed profiles/pmc_n*_r*.json, marked
+          with whether its build id is the loaded library's).
 cpu_baseline: the CPU oracle (reference-faithful port: per-node ordered maps,
           one thread, same 2P schedule) on a bounded sample of the same
           workload (fewer nodes, same R and injection), rank 0 at N=1 only.
@@ -84,6 +88,10 @@ def parse():
     p.add_argument("--sharded", action="store_true",
                    help="run a multi-GPU mode even at N=1 (one RCCL rank: node-shard exchanges are "
                         "self-copies, the slice all-reduce a no-op; measures that path's overhead)")
+    p.add_argument("--pmc", default="auto", choices=["auto", "off"],
+                   help="auto (N=1, single engine): measure roofline.traffic live -- two child "
+                        "rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) of this same workload and "
+                        "library; off: take it from the committed profiles/pmc_n*_r*.json")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (RCCL, one GPU per rank) or gloo (host-staged rows; rehearsal of "
                         "the N>1 path with several ranks on one GPU)")
@@ -180,6 +188,72 @@ def cpu_best(R, seed, budget_s):
                 kind="port (dense bit-sliced, OpenMP)",
                 sample=f"oracle/gs_dense.c, n={n_cpu}, R={R}, all rumors injected round 1, "
                        f"{rounds} rounds in {el:.1f}s")
+
+
+def rocprof_pattern(kernel_name):
+    """The rocprofv3 (demangled) name prefix of an engine's deliver+transition
+    kernel, e.g. "round_kernel<false,1> (...)" -> "round_kernel<false, 1,",
+    "round_kernel_dlv4<1,u32,2>" -> "round_kernel_dlv4<1,",
+    "round_kernel_w32<1> (...)" -> "round_kernel_w32<1>"."""
+    base = kernel_name.split(" ")[0]
+    fn, _, targs = base.partition("<")
+    args = [a.strip() for a in targs.rstrip(">").split(",")]
+    if fn == "round_kernel":
+        return f"{fn}<{args[0]}, {args[1]},"
+    if fn == "round_kernel_w32":
+        return f"{fn}<{args[0]}>"
+    return f"{fn}<{args[0]},"
+
+
+def live_pmc(args, kernel_name, skip):
+    """HBM bytes per launch of the dominant kernel, measured now: one child
+    rocprofv3 run per counter group (FETCH_SIZE, then WRITE_SIZE -- they do
+    not fit one pass, MI355X_MICROARCH.md), each running this same workload
+    with this same library; bytes = 2 * FETCH_SIZE + WRITE_SIZE (FETCH_SIZE
+    counts 64 B per 128-B read request on gfx950).  The launches of the
+    child's timed window are averaged (its first `skip` deliver launches are
+    warmup).  Returns (bytes, source dict) or (None, reason)."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None, "rocprofv3 not found"
+    pat = rocprof_pattern(kernel_name)
+    child = [sys.executable, os.path.abspath(__file__), "--config", args.config, "--nodes", str(args.nodes),
+             "--rumors", str(args.rumors), "--steps", str(args.steps), "--warmup", str(args.warmup),
+             "--churn", str(args.faults[0]), "--drop-push", str(args.faults[1]), "--drop-pull",
+             str(args.faults[2]), "--schedule", args.schedule, "--seed", hex(args.seed),
+             "--no-cpu-baseline", "--no-spread", "--pmc", "off"]
+    vals = {}
+    tmp = tempfile.mkdtemp(prefix="gs_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, counter)
+            cmd = [prof, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--"] + child
+            env = dict(os.environ, SAFE_GOSSIP_AMD_UNDER_PROFILER="1")
+            try:
+                r = subprocess.run(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                                   timeout=300, cwd=tmp)
+            except subprocess.TimeoutExpired:
+                return None, f"rocprofv3 --pmc {counter} timed out"
+            path = os.path.join(d, "run_counter_collection.csv")
+            if r.returncode != 0 or not os.path.exists(path):
+                return None, f"rocprofv3 --pmc {counter} failed (rc {r.returncode}): {r.stderr[-300:]}"
+            rows = sorted((x for x in csv.DictReader(open(path)) if pat in x["Kernel_Name"]),
+                          key=lambda x: int(x["Dispatch_Id"]))
+            v = [float(x["Counter_Value"]) for x in rows][skip:]
+            if not v:
+                return None, f"no {pat} launches in the {counter} pass"
+            vals[counter] = (sum(v) / len(v) * 1024.0, len(v), rows[0]["Kernel_Name"])
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    f, w = vals["FETCH_SIZE"][0], vals["WRITE_SIZE"][0]
+    return 2.0 * f + w, {"kind": "live", "kernel": vals["FETCH_SIZE"][2], "launches": vals["FETCH_SIZE"][1],
+                         "fetch_bytes_raw": f, "write_bytes": w,
+                         "note": "child rocprofv3 --pmc passes of this workload: 2*FETCH_SIZE + WRITE_SIZE "
+                                 "per launch of the timed window"}
 
 
 def self_launch(args):
@@ -336,11 +410,18 @@ def main():
     # bytes against the time of the round kernel AND the in-list build
     step_frac = best["bytes_per"] / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS
 
-    # PMC traffic of the same kernel from the committed rocprofv3 run of this
-    # workload (profiles/summarize.py writes one file per (nodes, rumors))
-    # (rocprofv3 cannot profile the process it runs in: the counters come from
-    # a separate run of this same workload, named with its commit below)
+    # HBM traffic of the same kernel from PMC counters: measured live by child
+    # rocprofv3 runs of this workload (N=1, single engine; rocprofv3 cannot
+    # count the process it runs in), else from the committed rocprofv3 run of
+    # this workload (profiles/summarize.py writes one file per (nodes,
+    # rumors)), marked with whether it profiled this very library build
     traffic = traffic_src = None
+    build_id = sg.build_id()
+    if (rank == 0 and world == 1 and best["mode"] == "single" and args.pmc == "auto"
+            and not os.environ.get("SAFE_GOSSIP_AMD_UNDER_PROFILER")):
+        traffic, traffic_src = live_pmc(args, best["name"], skip=max(0, args.warmup - 1))
+        if traffic is None:
+            traffic_src = {"kind": "live", "failed": traffic_src}
     for name in (f"pmc_n{n}_r{R}.json", "pmc_latest.json"):
         pmc_path = os.path.join(REPO, "profiles", name)
         if traffic is None and os.path.exists(pmc_path) and world == 1 and best["mode"] == "single":
@@ -348,11 +429,13 @@ def main():
                 pmc = json.load(open(pmc_path))
                 if pmc.get("nodes") == n and pmc.get("rumors") == R:
                     traffic = pmc.get("hbm_bytes_per_launch")
-                    traffic_src = {"file": "profiles/" + name, "profile": pmc.get("tag"),
-                                   "commit": pmc.get("commit"),
-                                   "kernel_avg_ms_rocprof": pmc.get("kernel_avg_ms_rocprof")}
+                    traffic_src = {"kind": "committed", "file": "profiles/" + name, "profile": pmc.get("tag"),
+                                   "commit": pmc.get("commit"), "build_id": pmc.get("build_id"),
+                                   "build_id_match": pmc.get("build_id") == build_id,
+                                   "kernel_avg_ms_rocprof": pmc.get("kernel_avg_ms_rocprof"),
+                                   "live_failed": (traffic_src or {}).get("failed")}
             except Exception:
-                traffic = traffic_src = None
+                traffic = None
 
     cpu = cpu_best_line = None
     if rank == 0 and world == 1 and dist is None and not args.no_cpu_baseline:
@@ -405,6 +488,8 @@ def main():
             },
             "cpu_baseline": cpu,
             "cpu_best": cpu_best_line,
+            "build": {"id": build_id, "abi": sg.ABI_VERSION,
+                      "note": "gs_build_id: SHA-256 prefix of the library's sources (safe_gossip_amd/build.py)"},
             "spread": spread,
         }
         if len(runs) > 1:

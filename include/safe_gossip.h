@@ -107,6 +107,16 @@ typedef struct {
 
 typedef struct gs_engine gs_engine;
 
+/* Version of this C ABI (struct layouts and array lengths of the entry points
+ * below); a binding checks it before calling anything else.  2: gs_shard_info
+ * writes 14 entries, info[4] in u32 words. */
+#define GS_ABI_VERSION 2u
+uint32_t    gs_abi_version(void);
+/* Provenance of the loaded library: the first 16 hex digits of the SHA-256
+ * of its sources and headers (safe_gossip_amd/build.py source_hash computes
+ * the same over a tree), fixed at build time. */
+const char *gs_build_id(void);
+
 gs_status   gs_create(const gs_config *cfg, gs_engine **out);
 void        gs_destroy(gs_engine *e);
 gs_status   gs_get_params(const gs_engine *e, uint8_t out[3]);
@@ -153,6 +163,19 @@ gs_status   gs_dump_records(gs_engine *e, uint16_t *rec, uint32_t *psize);
  * the same function (oracle/gs_dense.c dn_digest).  GS_ERR_INVALID_ARGUMENT
  * while send_new calls are queued (call it before injecting). */
 gs_status   gs_state_digest(gs_engine *e, uint64_t *out);
+/* The same digest for a network whose rumors are sliced over several engines
+ * (gs_config.rumor_slice; this engine holds the network's rumors [rumor_lo,
+ * rumor_lo + R)): adds this engine's per-word sums (before the final mix,
+ * gs_common.h digest_sum) with device atomics into the caller's device buffer
+ * dpart[n][words] (words = ceil(R_network / 64); zeroed by the caller), then
+ * gs_digest_finish mixes the summed parts of every slice and adds each
+ * node's term of |peers_in_this_round| (equal on every slice) and its network
+ * Statistics (host, n*5: gs_statistics_all's rows after the slices' MIN /
+ * SUM combine) into out (host, n).  The result is what gs_state_digest of one
+ * engine holding all rumors would give. */
+gs_status   gs_state_digest_part(gs_engine *e, uint32_t rumor_lo, uint32_t words, uint64_t *dpart);
+gs_status   gs_digest_finish(gs_engine *e, const uint64_t *dpart, uint32_t words, const uint64_t *stats,
+                             uint64_t *out);
 
 /* Gossiper::clear for every node.  Returns GS_ERR_DEVICE_LIMIT (after
  * clearing) when a device limit was hit since the previous clear. */
@@ -177,10 +200,10 @@ double      gs_round_kernel_bytes(const gs_engine *e);
  * gs_round_kernel_bytes describes), e.g. "round_kernel_dlv4<1,u32,2>". */
 const char *gs_round_kernel_name(const gs_engine *e);
 /* Algorithmic HBM bytes per deliver+transition round kernel launched since
- * gs_set_timing(e, 1), as counted by the kernels: with sparse records (the
- * wide 2P engine) words known to be zero are neither read nor rewritten and
- * pushers with nothing live are not gathered, so the bytes depend on the
- * state; otherwise gs_round_kernel_bytes (and *launches = 0).  Synchronises. */
+ * gs_set_timing(e, 1), as counted by the kernels: with live-filtered gathers
+ * (the 2P gather path) only the class rows the in-list build leaves to
+ * gather count, so the bytes depend on the state; otherwise
+ * gs_round_kernel_bytes (and *launches = 0).  Synchronises. */
 gs_status   gs_round_traffic(gs_engine *e, double *bytes_per_launch, uint32_t *launches);
 
 /* ---- Sharded network (multi-GPU): one engine per rank owns the node range
@@ -188,15 +211,13 @@ gs_status   gs_round_traffic(gs_engine *e, double *bytes_per_launch, uint32_t *l
  * moves two sets of rows between ranks with FIXED-SIZE
  * all-to-all exchanges (equal splits: no row count ever reaches the host, a
  * round needs no host synchronisation).  Both buffers are part-major: part h's
- * region starts at row h*world*blk and holds one sub-block per rank, so the
- * exchange of one part is ONE equal-split all-to-all over a contiguous region
- * (blk = the row slots plus, with SAFE_GOSSIP_AMD_SHARD_FLAGS=1, flag rows:
- * one byte per slot telling the receiver which words of the row are nonzero):
- *   A_h(t): exchange-A buffer set t % 2, part h: world sub-blocks of blk rows
- *           (the last part: blk + idrows rows, the idrows carrying the source
+ * region starts at row h*world*capP and holds one sub-block per rank, so the
+ * exchange of one part is ONE equal-split all-to-all over a contiguous region:
+ *   A_h(t): exchange-A buffer set t % 2, part h: world sub-blocks of capP rows
+ *           (the last part: capP + idrows rows, the idrows carrying the source
  *           ids of round t+1 for the in-lists, built one round ahead) -- push
  *           rows of round t of the sources in part h;
- *   B_h(t): part h of sendB -> part h of recvB, world sub-blocks of blk rows.
+ *   B_h(t): part h of sendB -> part h of recvB, world sub-blocks of capP rows.
  * A row holds `row words` u32 (info[4] for A, info[12] for B): the 2-plane
  * class code of the rows' rumors (2W u64 both ways), or at R_pad <= 16 in
  * the 2P schedule "code rows" (info[13] = 1): an A row is the push code (b0 |
@@ -217,13 +238,14 @@ gs_status   gs_shard_create(const gs_config *cfg, uint32_t rank, uint32_t world,
 /* The same with `parts` (1..4) pipeline parts (gs_shard_create: 1). */
 gs_status   gs_shard_create_parts(const gs_config *cfg, uint32_t rank, uint32_t world, uint32_t parts,
                                   gs_engine **out);
-/* info = {lo, m, blk (rows per rank sub-block of a part: row slots + flag
- *         rows), idrows (id rows per sub-block of A's last part), A row words
- *         (u32 words per row: 4W for the class-code rows, 2 for code rows),
- *         world, rank, nodes per rank, parts P, nodes per part mP, rows of an
- *         A buffer (world * (P*blk + idrows)), rows of a B buffer (world * P *
- *         blk), B row words (4W, or 1 for code rows), 1 for code rows}.  Every
- *         rank must see the same SAFE_GOSSIP_AMD_SHARD_FLAGS and
+/* info = {lo, m, capP (row slots per rank sub-block of a part), idrows (id
+ *         rows per sub-block of A's last part), A row words (u32 words per
+ *         row: 4W for the class-code rows, 2 for code rows), world, rank,
+ *         nodes per rank, parts P, nodes per part mP, rows of an A buffer
+ *         (world * (P*capP + idrows)), rows of a B buffer (world * P * capP),
+ *         B row words (4W, or 1 for code rows), 1 for code rows}: 14 entries
+ *         since ABI version 2 (gs_abi_version; version 1 wrote 12 and counted
+ *         info[4] in u64 words).  Every rank must see the same
  *         SAFE_GOSSIP_AMD_NO_DLV. */
 gs_status   gs_shard_info(const gs_engine *e, uint32_t info[14]);
 /* The same layout without creating an engine (host only, no device needed):
@@ -327,8 +349,8 @@ gs_status   gs_handle_received(gs_engine *e, uint32_t node, uint32_t peer, const
  * calls in this order (message i = msgs[off[i] .. off[i] + len[i]) from
  * peers[i] >= n to nodes[i]), with ONE observation launch for every node a
  * first Push makes answer (instead of one per call): the responses of RPC i
- * are out[resp_off[i] .. resp_off[i+1]) (frames "u32 LE length + RPC"; n+1
- * offsets).  All or nothing: a malformed message, an unknown rumor or an
+ * are out[resp_off[i] .. resp_off[i+1]) (frames "u32 LE length + RPC";
+ * resp_off holds count+1 offsets).  All or nothing: a malformed message, an unknown rumor or an
  * `out` smaller than the responses (GS_ERR_SERIALISATION, *out_len = bytes
  * needed) applies none of them. */
 gs_status   gs_handle_received_batch(gs_engine *e, uint32_t count, const uint32_t *nodes, const uint32_t *peers,

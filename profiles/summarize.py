@@ -68,7 +68,10 @@ def main():
             import subprocess
             commit = subprocess.run(["git", "-C", HERE, "rev-parse", "--short=12", "HEAD"], capture_output=True,
                                     text=True).stdout.strip() or None
-        latest = dict(tag=a.tag, commit=commit, kernel=dom, nodes=a.nodes, rumors=a.rumors,
+        import sys
+        sys.path.insert(0, os.path.dirname(HERE))
+        from safe_gossip_amd.build import source_hash
+        latest = dict(tag=a.tag, commit=commit, build_id=source_hash(), kernel=dom, nodes=a.nodes, rumors=a.rumors,
                       fetch_bytes_raw=f, write_bytes=w, hbm_bytes_per_launch=2 * f + w,
                       kernel_avg_ms_rocprof=dom_ms,
                       hbm_gbs=(2 * f + w) / (dom_ms * 1e-3) / 1e9,

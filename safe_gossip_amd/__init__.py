@@ -130,6 +130,8 @@ SYMBOLS = {
     "gs_dump_state": (ctypes.c_int, [_P, _U16P]),
     "gs_dump_records": (ctypes.c_int, [_P, _U16P, _U32P]),
     "gs_state_digest": (ctypes.c_int, [_P, _U64P]),
+    "gs_state_digest_part": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]),
+    "gs_digest_finish": (ctypes.c_int, [_P, ctypes.c_void_p, ctypes.c_uint32, _U64P, _U64P]),
     "gs_clear": (ctypes.c_int, [_P, ctypes.c_uint32]),
     "gs_sync": (ctypes.c_int, [_P]),
     "gs_round": (ctypes.c_uint32, [_P]),
@@ -150,6 +152,8 @@ SYMBOLS = {
                                    ctypes.c_uint32]),
     "gs_derive_params": (None, [ctypes.c_uint32, _U8P]),
     "gs_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "gs_abi_version": (ctypes.c_uint32, []),
+    "gs_build_id": (ctypes.c_char_p, []),
     # sharded engines (safe_gossip_amd.sharded)
     "gs_shard_create": (ctypes.c_int, [ctypes.POINTER(_Config), ctypes.c_uint32, ctypes.c_uint32,
                                        ctypes.POINTER(_P)]),
@@ -191,8 +195,21 @@ def _share_torch_hip_runtime() -> None:
         ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)
 
 
+ABI_VERSION = 2  # include/safe_gossip.h GS_ABI_VERSION
+
+
+def build_id() -> str:
+    """The loaded library's provenance id (gs_build_id): the source hash of
+    the tree it was built from (safe_gossip_amd/build.py source_hash)."""
+    return load_library().gs_build_id().decode()
+
+
 def load_library(path: Optional[str] = None):
-    """Load ``libsafe_gossip_amd.so`` (built by ``__graft_entry__.build()``)."""
+    """Load ``libsafe_gossip_amd.so`` (built by ``__graft_entry__.build()``).
+
+    Fails loudly when the library was built from other sources than the tree
+    it is loaded from (its gs_build_id against build.source_hash()), or
+    speaks another ABI version: a stale binary never runs silently."""
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
@@ -205,6 +222,13 @@ def load_library(path: Optional[str] = None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.gs_abi_version() != ABI_VERSION:
+        raise DeviceError(f"{p}: C ABI version {lib.gs_abi_version()}, this binding speaks {ABI_VERSION}")
+    from .build import source_hash
+    have, want = lib.gs_build_id().decode(), source_hash()
+    if have.split("+")[0] != want:
+        raise DeviceError(f"{p} was built from other sources (build id {have}, tree {want}): "
+                          "run __graft_entry__.build()")
     if path is None:
         _LIB = lib
     return lib
@@ -686,7 +710,7 @@ class Network:
 
     def round_traffic(self):
         """(algorithmic bytes per deliver+transition launch since set_timing(True),
-        launches counted): the bytes sparse records let the kernels skip are
+        launches counted): the class rows the live filter leaves ungathered are
         not counted; launches = 0 means the static model (round_kernel_bytes)."""
         b, m = ctypes.c_double(), ctypes.c_uint32()
         _check(self._lib.gs_round_traffic(self._h, ctypes.byref(b), ctypes.byref(m)))

@@ -25,6 +25,21 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 
+def source_hash(root: str = REPO_DIR) -> str:
+    """Provenance id of a library built from the tree at `root`: the first 16
+    hex digits of the SHA-256 over (relative path, contents) of every source
+    and header, in path order.  Compiled into the library (gs_build_id) and
+    compared by load_library with the tree it runs from."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in sorted(os.path.relpath(f, REPO_DIR) for f in SOURCES + HEADERS):
+        h.update(p.encode() + b"\0")
+        with open(os.path.join(root, p), "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
 def _stale(target: str, deps: list[str]) -> bool:
     if not os.path.exists(target):
         return True
@@ -50,28 +65,44 @@ def build_engine(force: bool = False, verbose: bool = False, defines=(), out: st
     """
     from concurrent.futures import ThreadPoolExecutor
     target = out or LIB_PATH
-    if not force and not defines and not _stale(target, SOURCES + HEADERS):
+    tag = "product" if not defines else "_".join(sorted(defines)).replace("=", "-")
+    # the library's build id: the tree's source hash (+ the variant's defines)
+    bid = source_hash() + ("" if not defines else "+" + tag)
+    idfile = target + ".buildid"
+    if not force and not _stale(target, SOURCES + HEADERS) and os.path.exists(idfile) and \
+            open(idfile).read().strip() == bid:
         return target
     flags = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-Wall", "-Wextra", "-Werror"] + [
         f"-D{d}" for d in defines]
-    tag = "product" if not defines else "_".join(sorted(defines)).replace("=", "-")
     bdir = os.path.join(PKG_DIR, "build", tag)
     os.makedirs(bdir, exist_ok=True)
     objs, jobs = [], []
     for src in SOURCES:
         obj = os.path.join(bdir, os.path.basename(src) + ".o")
         objs.append(obj)
-        if force or _stale(obj, [src] + HEADERS):
-            jobs.append((src, obj))
+        extra = []
+        if src.endswith("gs_engine.cpp"):  # the build id lives here: rebuilt whenever it changes
+            extra = [f'-DGS_BUILD_ID="{bid}"']
+            stale_id = not os.path.exists(obj + ".buildid") or open(obj + ".buildid").read().strip() != bid
+        else:
+            stale_id = False
+        if force or stale_id or _stale(obj, [src] + HEADERS):
+            jobs.append((src, obj, extra))
     workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
     with ThreadPoolExecutor(max_workers=workers) as ex:
-        for f in [ex.submit(_compile, s_, o_, flags, verbose) for s_, o_ in jobs]:
+        for f in [ex.submit(_compile, s_, o_, flags + x_, verbose) for s_, o_, x_ in jobs]:
             f.result()
+    for s_, o_, x_ in jobs:
+        if x_:
+            with open(o_ + ".buildid", "w") as f:
+                f.write(bid)
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", target + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(target + ".tmp", target)
+    with open(idfile, "w") as f:
+        f.write(bid)
     return target
 
 

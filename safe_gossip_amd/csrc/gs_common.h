@@ -239,10 +239,9 @@ __host__ __device__ inline u64 digest_plane_k(uint32_t p) { return 0x9E3779B97F4
 // (B, C, D; a0, a1 and the five b planes bp), the entries the deliveries
 // created (crB: B{0,1}, crC: C{0,0}), and the record counters of B entries
 // (anyC; c1: #counters in [1, counter_max); c2: #counters == 2).
-__host__ __device__ inline u64 digest_word(uint32_t j, u64 m, u64 B, u64 C, u64 D, u64 crB, u64 crC, u64 a0,
-                                           u64 a1, const u64 *bp, u64 anyC, const u64 *c1, const u64 *c2) {
+__host__ __device__ inline void digest_planes(u64 m, u64 B, u64 C, u64 D, u64 crB, u64 crC, u64 a0, u64 a1,
+                                              const u64 *bp, u64 anyC, const u64 *c1, const u64 *c2, u64 pl[20]) {
     const u64 BC = B | C, E = B | crB;
-    u64 pl[20];
     pl[0] = crB | B | D;          // code bit 14 (tag 1 or 3)
     pl[1] = crC | C | D;          // code bit 15 (tag 2 or 3)
     pl[2] = crB | (BC & a0);      // code bit 7 (f2 bit 0; a created B has our_counter 1)
@@ -253,9 +252,22 @@ __host__ __device__ inline u64 digest_word(uint32_t j, u64 m, u64 B, u64 C, u64 
         pl[10 + i] = E & c1[i];   // record bits 0..4
         pl[15 + i] = E & c2[i];   // record bits 7..11
     }
+    for (int p = 0; p < 20; ++p) pl[p] &= m;
+}
+// The word's sum before the final mix, and the mix (word j of the network).
+// The sum is linear over disjoint rumor bits, so engines holding parts of one
+// word (rumor slices) add their parts' sums (gs_state_digest_part).
+__host__ __device__ inline u64 digest_sum(const u64 pl[20], uint32_t shl = 0) {
     u64 h = 0;
-    for (uint32_t p = 0; p < 20; ++p) h += (pl[p] & m) * digest_plane_k(p);
-    return digest_mix(h ^ digest_mix((u64)j + 0x632BE59BD9B4E019ull));
+    for (uint32_t p = 0; p < 20; ++p) h += (pl[p] << shl) * digest_plane_k(p);
+    return h;
+}
+__host__ __device__ inline u64 digest_fin(uint32_t j, u64 h) { return digest_mix(h ^ digest_mix((u64)j + 0x632BE59BD9B4E019ull)); }
+__host__ __device__ inline u64 digest_word(uint32_t j, u64 m, u64 B, u64 C, u64 D, u64 crB, u64 crC, u64 a0,
+                                           u64 a1, const u64 *bp, u64 anyC, const u64 *c1, const u64 *c2) {
+    u64 pl[20];
+    digest_planes(m, B, C, D, crB, crC, a0, a1, bp, anyC, c1, c2, pl);
+    return digest_fin(j, digest_sum(pl));
 }
 __host__ __device__ inline u64 digest_node(uint32_t psize, const u64 *st5) {
     u64 h = digest_mix((1ull << 63) | psize);

@@ -167,7 +167,6 @@ struct Lane {
         } else {
             const uint32_t lw = logr - 6u;
             u64 b = ((u64)s << (lw + 3u)) + j;
-#if !defined(GS_EXP_G1) && !defined(GS_EXP_G2)
             if (GS_CLS_VEC && lw == 0u) {
                 // one word per plane (64 rumors): planes 0-1 in one 16-byte
                 // load, two load requests per row instead of three
@@ -177,18 +176,9 @@ struct Lane {
                 r.a1 = S[b + 2];
                 return r;
             }
-#endif
             r.c = S[b];
-#if defined(GS_EXP_G1)
-            r.a0 = r.c >> 1;
-            r.a1 = r.c << 1;
-#elif defined(GS_EXP_G2)
-            r.a0 = S[b + W];
-            r.a1 = r.c ^ r.a0;
-#else
             r.a0 = S[b + W];
             r.a1 = S[b + 2 * (u64)W];
-#endif
         }
         return r;
     }

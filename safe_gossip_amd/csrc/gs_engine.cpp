@@ -40,8 +40,8 @@ struct gs_engine {
     u64 *S[2] = {nullptr, nullptr};
     int cur = 0;
     // In-edge lists, double-buffered: set (r & 1) holds round r's lists.  The
-    // set of round r+1 is built on cstream while the round kernel of round
-    // r+1 (which reads round r's set) runs on `stream`.
+    // set of round r+1 is built on the engine stream right after the round
+    // kernel of round r (beside it measured slower).
     struct CsrSet {
         uint32_t *src = nullptr, *tg = nullptr, *scratch = nullptr, *region = nullptr;
         gs::InRec *IN8 = nullptr;
@@ -53,11 +53,6 @@ struct gs_engine {
         uint32_t wraps = 0;        // serial wraps this set's SibRecs were cleared for
     } csr[2];
     uint32_t serial_wraps = 0;
-    // Two-phase build (SAFE_GOSSIP_AMD_SPLIT_BUILD=1, filtered 2P gather path):
-    // inl_bin of round t+1 on cstream beside round t's kernel, then the zl map
-    // and inl_sort on the round stream after it (ev_binned[set]: phase A done).
-    bool split_build = false;
-    hipEvent_t ev_binned[2] = {nullptr, nullptr};
     // Live-filtered gathers (gs_common.h kSkipBit): node maps "live" and
     // "complete" of the planes the last transition launch wrote, read by the
     // in-list build that follows it on the same stream.  On for the 2P gather
@@ -72,32 +67,11 @@ struct gs_engine {
     // per 64-bit lane word, otherwise (default) a 32-bit lane word
     uint32_t dlv_pack = 1;
     bool w32 = false;  // 2P gather path: the 32-bit lane round kernel on eligible launches (gs_w32.hip)
-    // Sparse records (wide 2P engine, W <= 8; gs_kernels.h RoundArgs): maps of
-    // plane buffer i, the accounting words and MODE-1 launches counted in them
-    // The sparse variant runs while the input planes are at least a quarter
-    // zero words (spr_active); zero words only decrease within a dissemination
-    // (A never returns), so once the dense variant takes over the maps are not
-    // kept again until the next reset.  The decision for round t+2 reads the
-    // density of round t's planes (copied to pinned memory, one round behind,
-    // so the host never waits on the running kernel).
-    bool spr = false;         // maps allocated (eligible engine, not disabled)
-    bool spr_always = false;  // SAFE_GOSSIP_AMD_SPARSE=on: never switch to dense
-    bool spr_active = false;
-    u64 *zb[2] = {nullptr, nullptr};
-    uint8_t *lb[2] = {nullptr, nullptr}, *ab[2] = {nullptr, nullptr};
-    u64 *acct = nullptr;
-    uint32_t acct_launches = 0, dense_launches = 0;  // mode-1 launches since set_timing(1)
-    u64 *dens = nullptr;       // [2][kDensSlots], by parity of the round written
-    u64 *dens_host = nullptr;  // pinned copy [2][kDensSlots]
-    hipEvent_t ev_dens[2] = {nullptr, nullptr};
-    uint32_t dens_round[2] = {0, 0};  // round whose density each slot holds (0: none)
+    u64 *acct = nullptr;       // filtered timed launches: class rows counted by the builds (acct[0])
     uint32_t *pc = nullptr;  // DLV: push codes of the current round [n]
     uint16_t *kn = nullptr;  // single-engine DLV: known masks of the current round [n]
-    hipStream_t cstream = nullptr;
-    hipEvent_t ev_built[2] = {nullptr, nullptr};  // set i complete
-    hipEvent_t ev_read[2] = {nullptr, nullptr};   // last reader of set i done
+    hipStream_t cstream = nullptr;  // shard engines: plan / in-list side stream
     uint32_t build_serial = 0;
-    bool concurrent_inlists = false;  // SAFE_GOSSIP_AMD_CONCURRENT_INLISTS=1: build on cstream
     uint32_t *flags = nullptr;
     gs::CsrPlan plan{};
     // Shard engine (gs_shard_create): this rank's node range of a network
@@ -133,7 +107,6 @@ struct gs_engine {
     uint32_t parts_done = 0;
     gs::RoundArgs ra{};
     int ra_mode = 0;
-    bool ra_sparse = false;
     bool ra_prezeroed = false;  // the round kernel clears the next build's counters
     uint32_t *st32 = nullptr;  // [n][4] u32 deltas (u16 with st16)
     bool st16 = false;         // delivery-record engines: u16 deltas (gs_device.h load_stats)
@@ -157,6 +130,11 @@ struct gs_engine {
     u64 *ext_dev = nullptr;
     uint32_t ext_cap = 0, ext_uploaded = 0;
     uint16_t *node_state = nullptr;         // one node's observed codes [R]
+    // gs_handle_received_batch scratch, grown only (a hipFree would
+    // synchronise the device at every batch): block + node lists, codes
+    uint32_t *batch_lists = nullptr;
+    uint16_t *batch_codes = nullptr;
+    size_t batch_lists_cap = 0, batch_codes_cap = 0;
     uint32_t round = 0;
     bool deliver_pending = false;
     // observation buffers (lazy)
@@ -232,11 +210,6 @@ void release(gs_engine *e) {
         for (void *b : cb)
             if (b) (void)hipFree(b);
     }
-    for (int i = 0; i < 2; ++i) {
-        if (e->ev_built[i]) (void)hipEventDestroy(e->ev_built[i]);
-        if (e->ev_read[i]) (void)hipEventDestroy(e->ev_read[i]);
-        if (e->ev_binned[i]) (void)hipEventDestroy(e->ev_binned[i]);
-    }
     for (int i = 0; i < 3; ++i) {
         if (e->planw[i]) (void)hipFree(e->planw[i]);
         if (e->ev_plan[i]) (void)hipEventDestroy(e->ev_plan[i]);
@@ -247,12 +220,9 @@ void release(gs_engine *e) {
     }
     if (e->ev_main) (void)hipEventDestroy(e->ev_main);
     if (e->cstream) (void)hipStreamDestroy(e->cstream);
-    for (int i = 0; i < 2; ++i)
-        if (e->ev_dens[i]) (void)hipEventDestroy(e->ev_dens[i]);
-    if (e->dens_host) (void)hipHostFree(e->dens_host);
-    void *bufs[] = {e->lvm, e->cpm, e->rows_dev, e->zb[0], e->zb[1], e->lb[0], e->lb[1], e->ab[0], e->ab[1], e->acct, e->dens, e->pc, e->kn, e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->live, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
+    void *bufs[] = {e->lvm, e->cpm, e->rows_dev, e->acct, e->pc, e->kn, e->Wb, e->sinfo, e->seqw, e->pend, e->offc, e->S[0], e->S[1], e->flags, e->live, e->st32, e->st64, e->inj_key, e->inj_mask, e->obs_known, e->obs_stats,
                     e->partials, e->obs_state, e->obs_rec, e->obs_psize, e->obs_digest, e->obs_pend, e->ext_dev,
-                    e->node_state};
+                    e->node_state, e->batch_lists, e->batch_codes};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (e->inj_host) (void)hipHostFree(e->inj_host);
@@ -273,15 +243,6 @@ gs_status reset_state(gs_engine *e) {
     e->since_fold = 0;
     GS_HIP(hipMemsetAsync(e->flags, 0, 4 * sizeof(uint32_t), e->stream));
     GS_HIP(hipMemsetAsync(e->live, 0, (size_t)2 * gs::kLiveSlots * gs::kLiveStride * sizeof(uint32_t), e->stream));
-    if (e->spr) {  // both plane buffers are zero: every word zero, no node live
-        for (int i = 0; i < 2; ++i) {
-            GS_HIP(hipMemsetAsync(e->zb[i], 0xFF, gs::spr_zb_words(g) * sizeof(u64), e->stream));
-            GS_HIP(hipMemsetAsync(e->lb[i], 0, gs::spr_node_bytes(g), e->stream));
-            GS_HIP(hipMemsetAsync(e->ab[i], 0xFF, gs::spr_node_bytes(g), e->stream));
-        }
-        e->spr_active = true;
-        e->dens_round[0] = e->dens_round[1] = 0;
-    }
     if (e->dlv) {  // both sets' coarse fills (the round kernels clear them a round late)
         size_t first = 0, words = 0;
         gs::inlist_cfill_range(e->plan, &first, &words);
@@ -339,11 +300,6 @@ gs_status device_limit(gs_engine *e) {
     return fl ? GS_ERR_DEVICE_LIMIT : GS_OK;
 }
 
-// The in-lists of the next round are built on the side stream (opt-in
-// SAFE_GOSSIP_AMD_CONCURRENT_INLISTS, gather path): only then do the engine
-// stream's readers wait for ev_built (else stream order suffices).
-bool built_elsewhere(const gs_engine *e) { return e->concurrent_inlists && !e->dlv; }
-
 gs::RoundArgs base_args(gs_engine *e) {
     gs::RoundArgs a{};
     a.Scur = e->S[e->cur];
@@ -363,8 +319,8 @@ gs::RoundArgs base_args(gs_engine *e) {
         a.recvA = e->recvA[t % 2];
         a.recvB = e->recvB;
         a.sendA = e->sendA[(t + 1) % 2];
-        a.sp = gs::ShardRows{e->sp.G,   e->sp.P,    e->sp.W,     e->sp.capP,  e->sp.flagrows, e->sp.blk,
-                             e->sp.idrows, e->sp.rw, e->sp.rwb, e->sp.codes, e->sp.chunk,    e->sp.n};
+        a.sp = gs::ShardRows{e->sp.G,  e->sp.P,   e->sp.W,     e->sp.capP,  e->sp.idrows,
+                             e->sp.rw, e->sp.rwb, e->sp.codes, e->sp.chunk, e->sp.n};
         if (e->dlv) {  // code rows: the delivery records built from exchange A (gs_shard_pull)
             a.DR = e->csr[0].DR;
             a.dtail = e->csr[0].src;
@@ -483,7 +439,6 @@ gs_status ensure_obs(gs_engine *e, bool dumps) {
 gs_status seq_prepare(gs_engine *e) {
     if (!e->seq || !e->deliver_pending || e->seq_round == e->round) return GS_OK;
     const auto &cs = e->csr[e->round & 1u];
-    if (built_elsewhere(e)) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
     gs::SeqArgs sa{};
     sa.S = e->S[e->cur];
     sa.IN8 = cs.IN8;
@@ -519,8 +474,9 @@ gs_status seq_prepare(gs_engine *e) {
 }
 
 // Fill the observation buffers with the state after the last delivery.
-gs_status observe(gs_engine *e, bool dumps, bool digest = false) {
-    if (e->obs_valid && !dumps && !digest) return GS_OK;
+gs_status observe(gs_engine *e, bool dumps, bool digest = false, u64 *dpart = nullptr, uint32_t dp_lo = 0,
+                  uint32_t dp_words = 0) {
+    if (e->obs_valid && !dumps && !digest && !dpart) return GS_OK;
     if (e->slice && !e->eb[3]) return GS_ERR_INVALID_ARGUMENT;  // gs_slice_bind first
     if (e->slice && e->eb_defer >= 0) {  // a deferred reduced buffer: add it now
         GS_HIP(gs::launch_slice_apply(e->st32, e->eb[e->eb_defer], e->g.n, e->st16 ? 1u : 0u, e->stream));
@@ -539,10 +495,12 @@ gs_status observe(gs_engine *e, bool dumps, bool digest = false) {
         a.obs_rec = e->obs_rec;
     }
     if (digest) a.obs_digest = e->obs_digest;
+    a.obs_dpart = dpart;
+    a.dp_lo = dp_lo;
+    a.dp_words = dp_words;
     if (e->slice) a.emin = e->eb[3];  // pending empty pulls of this slice
     if (e->deliver_pending) {
         if (e->shard && !e->dlv) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_edges[e->round % 2], 0));
-        else if (built_elsewhere(e)) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
         st = seq_prepare(e);
         if (st != GS_OK) return st;
     }
@@ -585,6 +543,12 @@ gs_status observe(gs_engine *e, bool dumps, bool digest = false) {
 }  // namespace
 
 extern "C" {
+
+#ifndef GS_BUILD_ID
+#define GS_BUILD_ID "unknown"
+#endif
+uint32_t gs_abi_version(void) { return GS_ABI_VERSION; }
+const char *gs_build_id(void) { return GS_BUILD_ID; }
 
 const char *gs_status_string(gs_status s) {
     switch (s) {
@@ -645,17 +609,12 @@ namespace {
 // The exchange layout of rank `rank` of `world` (gs_shard.hip shard_plan).
 gs::ShardPlan plan_of(const gs_config *cfg, uint32_t rank, uint32_t world, uint32_t parts) {
     const uint32_t R = cfg->n_rumors;
-    // row flags (receivers skip empty rows; A/B, measured slower: DESIGN.md
-    // section 7): SAFE_GOSSIP_AMD_SHARD_FLAGS=1; every rank must agree (it
-    // changes the layout)
-    const char *v = std::getenv("SAFE_GOSSIP_AMD_SHARD_FLAGS");
-    const bool flags = v && *v == '1';
     // code rows (one u32 push / pull code per row, delivery records and the
     // packed DLV round kernel) at R_pad <= 16 in the 2P schedule;
     // SAFE_GOSSIP_AMD_NO_DLV=1 keeps class rows (every rank must agree)
     const char *nd = std::getenv("SAFE_GOSSIP_AMD_NO_DLV");
     const bool codes = !(nd && *nd && *nd != '0') && next_pow2(R) <= 16 && cfg->schedule == GS_SCHED_2P;
-    return gs::shard_plan(cfg->n_nodes, world, rank, R >= 64 ? (next_pow2(R) / 64) : 1u, parts, flags, codes);
+    return gs::shard_plan(cfg->n_nodes, world, rank, R >= 64 ? (next_pow2(R) / 64) : 1u, parts, codes);
 }
 
 // Slot keys of exchange A (sources of a code-row shard's DLV build).
@@ -664,7 +623,7 @@ uint32_t shard_keys(const gs::ShardPlan &sp) { return sp.G * sp.P * sp.capP; }
 void fill_shard_info(const gs::ShardPlan &sp, uint32_t info[14]) {
     info[0] = sp.lo;
     info[1] = sp.m;
-    info[2] = sp.blk;  // rows per rank sub-block of a part: capP row slots + flag rows
+    info[2] = sp.capP;  // row slots per rank sub-block of a part
     info[3] = sp.idrows;
     // u32 words per exchange-A row: the 2-plane class code (2W u64 = 4W u32),
     // or (code rows, R_pad <= 16) the push code and the target word
@@ -680,33 +639,52 @@ void fill_shard_info(const gs::ShardPlan &sp, uint32_t info[14]) {
     info[13] = sp.codes;              // 1: code rows
 }
 
-// Common constructor: a whole network (world == 0) or the node range of rank
-// `rank` of a network sharded over `world` ranks.
-gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uint32_t parts, gs_engine **out) {
-    if (!cfg || !out) return GS_ERR_INVALID_ARGUMENT;
-    *out = nullptr;
+// The checks of a configuration (a whole network: world == 0, or rank `rank`
+// of `world` node shards with `parts` pipeline parts): the shard layout and
+// the protocol parameters.  gs_create / gs_shard_create_parts and
+// gs_shard_plan_info run the same checks, so a reported layout is one an
+// engine can be created with.
+gs_status check_config(const gs_config *cfg, uint32_t rank, uint32_t world, uint32_t parts, gs::ShardPlan *sp,
+                       uint8_t p[3]) {
     const uint32_t nglob = cfg->n_nodes, R = cfg->n_rumors;
     if (nglob == 0 || nglob == 0xffffffffu || R == 0 || R > 4096) return GS_ERR_INVALID_ARGUMENT;
     if (world && (rank >= world || world > gs::kMaxShards)) return GS_ERR_INVALID_ARGUMENT;
+    if (world && (parts == 0 || parts > gs::kMaxParts)) return GS_ERR_INVALID_ARGUMENT;
+    if (cfg->schedule > GS_SCHED_SEQ) return GS_ERR_INVALID_ARGUMENT;
     // Target words pack t(x) into 29 bits below the delivery flags
     // (gs_common.h kTgMask), whatever the parameters.
     if (nglob > gs::kTgMask + 1u) return GS_ERR_UNSUPPORTED;
-    gs::ShardPlan sp{};
-    if (world && (parts == 0 || parts > gs::kMaxParts)) return GS_ERR_INVALID_ARGUMENT;
-    if (world) sp = plan_of(cfg, rank, world, parts);
-    const uint32_t n = world ? sp.m : nglob;  // nodes owned by this engine
-    uint8_t p[3];
     gs_derive_params(nglob, p);
     if (cfg->counter_max) p[0] = cfg->counter_max;
     if (cfg->max_c_rounds) p[1] = cfg->max_c_rounds;
     if (cfg->max_rounds) p[2] = cfg->max_rounds;
     if (nglob >= 2 && (p[0] > 3 || p[1] > 3 || p[2] > 32 || !p[0] || !p[1] || !p[2]))
         return GS_ERR_UNSUPPORTED;
-    if (cfg->schedule > GS_SCHED_SEQ) return GS_ERR_INVALID_ARGUMENT;
     if (world && cfg->schedule == GS_SCHED_SEQ) return GS_ERR_UNSUPPORTED;  // chains cross ranks
     // rumor slices: the 2P single-engine path (SEQ's empty pulls are not a MIN
     // over slices of a per-slice count, and node shards slice nodes instead)
     if (cfg->rumor_slice && (world || cfg->schedule == GS_SCHED_SEQ)) return GS_ERR_UNSUPPORTED;
+    *sp = gs::ShardPlan{};
+    if (world) {
+        *sp = plan_of(cfg, rank, world, parts);
+        // code rows run the delivery-record build over max(owned nodes, slot
+        // keys) sources: only on its binned plan
+        if (sp->codes && !gs::dlv_plan(std::max(sp->m, shard_keys(*sp))).binned) return GS_ERR_UNSUPPORTED;
+    }
+    return GS_OK;
+}
+
+// Common constructor: a whole network (world == 0) or the node range of rank
+// `rank` of a network sharded over `world` ranks.
+gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uint32_t parts, gs_engine **out) {
+    if (!cfg || !out) return GS_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    gs::ShardPlan sp{};
+    uint8_t p[3];
+    const gs_status cst = check_config(cfg, rank, world, parts, &sp, p);
+    if (cst != GS_OK) return cst;
+    const uint32_t nglob = cfg->n_nodes, R = cfg->n_rumors;
+    const uint32_t n = world ? sp.m : nglob;  // nodes owned by this engine
 
     gs_engine *e = new gs_engine();
     e->shard = world != 0;
@@ -770,17 +748,6 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         delete e;
         return GS_ERR_UNSUPPORTED;
     }
-    {
-        // Sparse records on the wide 2P path (W <= 8, so a wave's node bits
-        // are whole bytes).  SAFE_GOSSIP_AMD_SPARSE = off (default) | dense
-        // (same) | auto (the sparse variant while a quarter of the words are
-        // unknown) | on (the sparse variant every round).  Opt-in: measured
-        // slower than the dense variant at config 4.
-        const char *v = std::getenv("SAFE_GOSSIP_AMD_SPARSE");
-        const std::string m = v ? v : "off";
-        e->spr = m != "off" && m != "dense" && !e->seq && !e->shard && !e->dlv && !g.small && g.W <= 8;
-        e->spr_always = m == "on";
-    }
     // Default message bytes of rumor slot r: bincode of a 4-byte Vec<u8>
     // holding r big-endian (u64 length 4, then the bytes), so key order is
     // slot order.  gs_set_rumor_key replaces them.
@@ -802,28 +769,17 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         e->w32 = (w && *w) ? *w != '0' : (e->g.small && e->g.rpad == 32u);
     }
     {
-        const char *v = std::getenv("SAFE_GOSSIP_AMD_CONCURRENT_INLISTS");
-        e->concurrent_inlists = v && *v && *v != '0';
-    }
-    {
+        // SAFE_GOSSIP_AMD_FILTER=0 keeps the unfiltered kernel (parity tests)
         const char *v = std::getenv("SAFE_GOSSIP_AMD_FILTER");
         const bool off = v && *v == '0';
-        e->filt = !off && !e->shard && !e->seq && !e->dlv && !e->spr && !e->concurrent_inlists &&
-                  e->plan.binned && (g.small || g.W <= 8);
-    }
-    {
-        const char *v = std::getenv("SAFE_GOSSIP_AMD_SPLIT_BUILD");
-        e->split_build = v && *v && *v != '0' && e->filt;
+        e->filt = !off && !e->shard && !e->seq && !e->dlv && e->plan.binned && (g.small || g.W <= 8);
     }
     // Per round a node's Statistics deltas of internal deliveries grow by at
     // most 32*R_pad + 32 (in-degree <= 30 is enforced); fold them into u64
     // well before a wrap.  The delivery-record engines (R_pad <= 16) keep them
     // in 16 bits (8 B per node and round less to read and write; external
     // RPCs' counts go straight to the totals): a fold every >= 60 rounds.
-    {
-        const char *v = std::getenv("SAFE_GOSSIP_AMD_STATS32");  // A/B: u32 deltas everywhere
-        e->st16 = e->dlv && !(v && *v == '1');
-    }
+    e->st16 = e->dlv;
     e->fold_every = (uint32_t)std::max<uint64_t>(1, (e->st16 ? 0xFFFFull : 0xFFFFFFFFull) / (32ull * g.rpad + 32) / 2);
     bool ok;
     if (e->shard) {
@@ -863,10 +819,7 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
     const size_t sw_pad = (size_t)gs::tile_padded(g.units) * gs::kPlanes * g.W;
     for (int i = 0; i < 2 && ok && !e->shard; ++i) {
         auto &c = e->csr[i];
-        ok = hipEventCreateWithFlags(&e->ev_built[i], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&e->ev_read[i], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&e->ev_binned[i], hipEventDisableTiming) == hipSuccess &&
-             dalloc(&c.src, isz.src_words) == hipSuccess && dalloc(&c.tg, npad) == hipSuccess &&
+        ok = dalloc(&c.src, isz.src_words) == hipSuccess && dalloc(&c.tg, npad) == hipSuccess &&
              dalloc(&c.region, isz.region_words) == hipSuccess &&
              dalloc(&c.scratch, isz.scratch_words) == hipSuccess &&
              hipMemset(c.scratch, 0, std::max<size_t>(isz.scratch_words, 1) * sizeof(uint32_t)) == hipSuccess;
@@ -886,19 +839,7 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         ok = dalloc(&e->lvm, gs::node_map_words(n)) == hipSuccess &&
              dalloc(&e->cpm, gs::node_map_words(n)) == hipSuccess &&
              dalloc(&e->rows_dev, 2) == hipSuccess &&
-             dalloc(&e->acct, gs::kAcctSlots) == hipSuccess &&
-             hipMemset(e->acct, 0, gs::kAcctSlots * sizeof(u64)) == hipSuccess;
-    for (int i = 0; i < 2 && ok && e->spr; ++i)
-        ok = dalloc(&e->zb[i], gs::spr_zb_words(g)) == hipSuccess &&
-             dalloc(&e->lb[i], gs::spr_node_bytes(g)) == hipSuccess &&
-             dalloc(&e->ab[i], gs::spr_node_bytes(g)) == hipSuccess;
-    if (ok && e->spr)
-        ok = dalloc(&e->dens, 2 * gs::kDensSlots) == hipSuccess &&
-             hipHostMalloc((void **)&e->dens_host, 2 * gs::kDensSlots * sizeof(u64), 0) == hipSuccess &&
-             hipEventCreateWithFlags(&e->ev_dens[0], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&e->ev_dens[1], hipEventDisableTiming) == hipSuccess &&
-             dalloc(&e->acct, gs::kAcctSlots) == hipSuccess &&
-             hipMemset(e->acct, 0, gs::kAcctSlots * sizeof(u64)) == hipSuccess;
+             dalloc(&e->acct, 1) == hipSuccess && hipMemset(e->acct, 0, sizeof(u64)) == hipSuccess;
     if (ok && e->seq)
         ok = dalloc(&e->Wb, (size_t)n * 2 * g.W) == hipSuccess && dalloc(&e->sinfo, n) == hipSuccess &&
              dalloc(&e->seqw, (size_t)gs::seq_blocks(n) * gs::kSeqLists + gs::kSeqLists + n) == hipSuccess;
@@ -968,8 +909,8 @@ gs_status shard_build(gs_engine *e) {
     la.f = e->faults;
     la.rowsA = reinterpret_cast<const uint32_t *>(e->recvA[t % 2]);
     la.pullB = reinterpret_cast<uint32_t *>(e->sendB);
-    la.sr = gs::ShardRows{e->sp.G,      e->sp.P,  e->sp.W,   e->sp.capP,  e->sp.flagrows, e->sp.blk,
-                          e->sp.idrows, e->sp.rw, e->sp.rwb, e->sp.codes, e->sp.chunk,    e->sp.n};
+    la.sr = gs::ShardRows{e->sp.G,  e->sp.P,   e->sp.W,     e->sp.capP,  e->sp.idrows,
+                          e->sp.rw, e->sp.rwb, e->sp.codes, e->sp.chunk, e->sp.n};
     la.nkeys = shard_keys(e->sp);
     la.ntargets = e->g.n;
     // this rank's own block: written in place by the round kernel, counted by
@@ -1005,10 +946,12 @@ gs_status gs_shard_info(const gs_engine *e, uint32_t info[14]) {
 }
 
 gs_status gs_shard_plan_info(const gs_config *cfg, uint32_t rank, uint32_t world, uint32_t parts, uint32_t info[14]) {
-    if (!cfg || !info || world == 0 || rank >= world || world > gs::kMaxShards || parts == 0 ||
-        parts > gs::kMaxParts || cfg->n_nodes == 0 || cfg->n_rumors == 0 || cfg->n_rumors > 4096)
-        return GS_ERR_INVALID_ARGUMENT;
-    fill_shard_info(plan_of(cfg, rank, world, parts), info);
+    if (!cfg || !info || world == 0) return GS_ERR_INVALID_ARGUMENT;
+    gs::ShardPlan sp{};
+    uint8_t p[3];
+    const gs_status st = check_config(cfg, rank, world, parts, &sp, p);  // (as gs_shard_create_parts)
+    if (st != GS_OK) return st;
+    fill_shard_info(sp, info);
     return GS_OK;
 }
 
@@ -1197,64 +1140,21 @@ gs_status round_begin(gs_engine *e) {
         if (e->eb_defer >= 0) a.eadd = e->eb[e->eb_defer];
         e->eb_defer = -1;
     }
-    if (e->spr_active && !e->spr_always && R0 >= 2) {
-        // density of round R0-1's planes (written by the launch of two calls
-        // ago): switch to the dense variant once under a quarter are zero words
-        const uint32_t par = (R0 - 1) & 1u;
-        if (e->dens_round[par] == R0 - 1) {
-            GS_HIP(hipEventSynchronize(e->ev_dens[par]));
-            u64 zw = 0;
-            for (uint32_t i = 0; i < gs::kDensSlots; ++i) zw += e->dens_host[par * gs::kDensSlots + i];
-            if (4 * zw < e->g.nseg) e->spr_active = false;
-        }
-    }
-    const bool sparse = e->spr_active;
-    if (sparse) {
-        a.zb_cur = e->zb[e->cur];
-        a.zb_nxt = e->zb[e->cur ^ 1];
-        a.lb_cur = e->lb[e->cur];
-        a.lb_nxt = e->lb[e->cur ^ 1];
-        a.ab_cur = e->ab[e->cur];
-        a.ab_nxt = e->ab[e->cur ^ 1];
-        a.dens = e->dens + ((R0 + 1) & 1u) * gs::kDensSlots;
-        GS_HIP(hipMemsetAsync(a.dens, 0, gs::kDensSlots * sizeof(u64), e->stream));
-        if (e->deliver_pending) {
-            a.acct = e->acct;
-            e->acct_launches++;
-        }
-    } else if (e->deliver_pending) {
-        e->dense_launches++;
-    }
     if (e->filt && e->deliver_pending && e->timing) {  // rows gathered, for gs_round_traffic
         a.acct = e->acct;
         a.rows_cnt = e->rows_dev + (R0 & 1u);  // counted by the build of round t's lists
         e->filt_launches++;
     }
-    const uint32_t rs = R0 & 1u;  // set holding round t = e->round
     if (e->shard) {
         GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[(R0 + 1) % 3], 0));
         if (e->deliver_pending && !e->dlv) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_edges[R0 % 2], 0));
     } else if (e->deliver_pending) {
-        if (built_elsewhere(e))  // (built on the engine stream: in order already)
-            GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[rs], 0));
         st = seq_prepare(e);  // SEQ: pull batches of round t (no-op for 2P)
         if (st != GS_OK) return st;
     }
-    if (e->split_build) {
-        // phase A of round t+1's in-lists (targets, bin partition) on the side
-        // stream beside this round's kernel; the set's last reader was the
-        // kernel of round t-1
-        const uint32_t ns = (R0 + 1u) & 1u;
-        auto &c = e->csr[ns];
-        GS_HIP(hipStreamWaitEvent(e->cstream, e->ev_read[ns], 0));
-        st = next_serial(e, c, e->cstream);
-        if (st != GS_OK) return st;
-        GS_HIP(gs::launch_build_bins(inlist_args(e, c, R0 + 1u), e->cstream));
-        GS_HIP(hipEventRecord(e->ev_binned[ns], e->cstream));
-    }
     // the build of round t+1 runs right behind this kernel on its stream: the
     // kernel clears that build's counters (no memset launch)
-    e->ra_prezeroed = !e->shard && !e->split_build && !(e->concurrent_inlists && !e->dlv);
+    e->ra_prezeroed = !e->shard;
     if (e->ra_prezeroed) {
         auto &c = e->csr[(R0 + 1u) & 1u];
         size_t first = 0, words = 0;
@@ -1276,7 +1176,6 @@ gs_status round_begin(gs_engine *e) {
     }
     e->ra = a;
     e->ra_mode = e->deliver_pending ? 1 : 0;
-    e->ra_sparse = sparse;
     e->tslot = ~0u;
     if (e->timing && e->tcount < kTimingSlots) {
         e->tslot = e->tcount++;
@@ -1322,19 +1221,6 @@ gs_status launch_part(gs_engine *e, uint32_t h) {
 gs_status round_end(gs_engine *e, gs_round_report *report) {
     gs_status st = GS_OK;
     const uint32_t R0 = e->round;
-    const bool sparse = e->ra_sparse;
-    const uint32_t rs = R0 & 1u;  // set holding round t = e->round
-    const gs::RoundArgs &a = e->ra;
-    if (sparse) {  // this round's density, for the call after next
-        const uint32_t par = (R0 + 1) & 1u;
-        GS_HIP(hipMemcpyAsync(e->dens_host + par * gs::kDensSlots, a.dens, gs::kDensSlots * sizeof(u64),
-                              hipMemcpyDeviceToHost, e->stream));
-        GS_HIP(hipEventRecord(e->ev_dens[par], e->stream));
-        e->dens_round[par] = R0 + 1;
-    }
-    // (read only by a build on the side stream; an event record costs the
-    // stream a few microseconds between kernels, ~8 us per round at config 2)
-    if (!e->shard && (e->split_build || built_elsewhere(e))) GS_HIP(hipEventRecord(e->ev_read[rs], e->stream));
     e->timed = e->timing;
     e->round += 1;
     e->cur ^= 1;
@@ -1358,32 +1244,18 @@ gs_status round_end(gs_engine *e, gs_round_report *report) {
         GS_HIP(hipStreamWaitEvent(e->stream, e->ev_plan[(R0 + 2) % 3], 0));
     } else {
         // Lists of the new round t+1 into the other set, whose last reader
-        // was the round kernel before this one; runs beside this round's kernel.
-        const uint32_t ns = e->round & 1u;
-        auto &c = e->csr[ns];
-        // Built on the round stream right after the round kernel by default:
-        // both are HBM-bound, and the in-list kernels hold whole CUs (1024
-        // threads, >100 KiB LDS), so running them beside the round kernel
-        // measured slower than in sequence.
-        // (DLV: the build reads the planes this round kernel writes: in sequence)
-        hipStream_t bs = built_elsewhere(e) ? e->cstream : e->stream;
-        if (e->split_build) {
-            // phase A (inl_bin) ran beside this round kernel (round_begin);
-            // phase B needs the node maps this kernel wrote
-            GS_HIP(hipStreamWaitEvent(e->stream, e->ev_binned[ns], 0));
-            gs::InListArgs la = inlist_args(e, c, e->round);
-            GS_HIP(hipMemsetAsync(la.rows, 0, sizeof(u64), e->stream));
-            GS_HIP(gs::launch_build_sort(la, e->stream));
-        } else {
-            if (bs != e->stream) GS_HIP(hipStreamWaitEvent(bs, e->ev_read[ns], 0));
-            st = next_serial(e, c, bs);
-            if (st != GS_OK) return st;
-            gs::InListArgs la = inlist_args(e, c, e->round);
-            la.prezeroed = e->ra_prezeroed ? 1u : 0u;
-            if (e->filt && !e->ra_prezeroed) GS_HIP(hipMemsetAsync(la.rows, 0, sizeof(u64), bs));
-            GS_HIP(gs::launch_build_inlists(la, bs));
-        }
-        if (bs != e->stream) GS_HIP(hipEventRecord(e->ev_built[ns], bs));  // (else: stream order)
+        // was the round kernel before this one.  Built on the round stream
+        // right after the round kernel: both are HBM-bound, and the in-list
+        // kernels hold whole CUs (1024 threads, >100 KiB LDS), so running them
+        // beside the round kernel measured slower than in sequence (DESIGN.md
+        // section 4); the DLV and filtered builds also read what this round
+        // kernel writes (push codes, node maps).
+        auto &c = e->csr[e->round & 1u];
+        st = next_serial(e, c, e->stream);
+        if (st != GS_OK) return st;
+        gs::InListArgs la = inlist_args(e, c, e->round);
+        la.prezeroed = e->ra_prezeroed ? 1u : 0u;
+        GS_HIP(gs::launch_build_inlists(la, e->stream));
     }
     if (report) {
         uint32_t fl[4];
@@ -1600,6 +1472,33 @@ gs_status gs_state_digest(gs_engine *e, uint64_t *out) {
     return GS_OK;
 }
 
+gs_status gs_state_digest_part(gs_engine *e, uint32_t rumor_lo, uint32_t words, uint64_t *dpart) {
+    if (!e || !dpart || words == 0 || (uint64_t)rumor_lo + e->g.R > 64ull * words) return GS_ERR_INVALID_ARGUMENT;
+    if (!e->pending.empty()) return GS_ERR_INVALID_ARGUMENT;  // queued send_new: observe before injecting
+    gs_status st = set_device(e);
+    if (st == GS_OK) st = observe(e, false, false, reinterpret_cast<u64 *>(dpart), rumor_lo, words);
+    if (st != GS_OK) return st;
+    GS_HIP(hipStreamSynchronize(e->stream));
+    return GS_OK;
+}
+
+gs_status gs_digest_finish(gs_engine *e, const uint64_t *dpart, uint32_t words, const uint64_t *stats,
+                           uint64_t *out) {
+    if (!e || !dpart || !stats || !out || words == 0) return GS_ERR_INVALID_ARGUMENT;
+    if (!e->obs_psize) return GS_ERR_INVALID_ARGUMENT;  // gs_state_digest_part first
+    gs_status st = set_device(e);
+    if (st != GS_OK) return st;
+    if (!e->obs_digest) GS_HIP(dalloc(&e->obs_digest, e->g.n));
+    // the Statistics rows go through obs_stats (rewritten by the next observation)
+    GS_HIP(hipMemcpyAsync(e->obs_stats, stats, (size_t)e->g.n * 5 * sizeof(u64), hipMemcpyHostToDevice, e->stream));
+    GS_HIP(gs::launch_digest_finish(reinterpret_cast<const u64 *>(dpart), e->g.n, words, e->obs_psize, e->obs_stats,
+                                    e->obs_digest, e->stream));
+    GS_HIP(hipMemcpyAsync(out, e->obs_digest, (size_t)e->g.n * sizeof(u64), hipMemcpyDeviceToHost, e->stream));
+    GS_HIP(hipStreamSynchronize(e->stream));
+    e->obs_valid = false;  // obs_stats overwritten
+    return GS_OK;
+}
+
 gs_status gs_dump_records(gs_engine *e, uint16_t *rec, uint32_t *psize) {
     if (!e || !rec) return GS_ERR_INVALID_ARGUMENT;
     gs_status st = set_device(e);
@@ -1651,13 +1550,9 @@ void gs_set_timing(gs_engine *e, int enable) {
             }
     }
     e->tcount = 0;
-    if (e->timing && (e->spr || e->filt)) {  // restart the traffic accounting with the ring
+    if (e->timing && e->filt) {  // restart the traffic accounting with the ring
         (void)hipSetDevice(e->device);
-        if (hipMemsetAsync(e->acct, 0, gs::kAcctSlots * sizeof(u64), e->stream) == hipSuccess) {
-            e->acct_launches = 0;
-            e->dense_launches = 0;
-            e->filt_launches = 0;
-        }
+        if (hipMemsetAsync(e->acct, 0, sizeof(u64), e->stream) == hipSuccess) e->filt_launches = 0;
     }
 }
 
@@ -1743,7 +1638,6 @@ gs_status observe_node(gs_engine *e, uint32_t node, std::vector<uint16_t> &codes
     a.blk_off = (uint32_t)(seg0 / 256);
     a.blk_count = 1;
     if (e->deliver_pending) {
-        if (built_elsewhere(e)) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0));
         st = seq_prepare(e);  // SEQ: the round's pull batches (no-op for 2P)
         if (st != GS_OK) return st;
     }
@@ -1769,13 +1663,26 @@ gs_status observe_nodes(gs_engine *e, const std::vector<uint32_t> &nodes, std::v
         const uint32_t b = (uint32_t)((e->g.small ? (u64)x : (u64)x * e->g.W) / 256);
         if (blocks.empty() || blocks.back() != b) blocks.push_back(b);
     }
-    uint32_t *dev = nullptr;  // [blocks | nodes]
-    uint16_t *dcodes = nullptr;
-    GS_HIP(dalloc(&dev, blocks.size() + m));
-    if (dalloc(&dcodes, (size_t)m * e->g.R) != hipSuccess) {
-        (void)hipFree(dev);
-        return GS_ERR_HIP;
+    // grow-only scratch on the engine (engine stream order protects its reuse)
+    const size_t lw = blocks.size() + m, cw = (size_t)m * e->g.R;
+    if (lw > e->batch_lists_cap) {
+        GS_HIP(hipStreamSynchronize(e->stream));
+        if (e->batch_lists) (void)hipFree(e->batch_lists);
+        e->batch_lists = nullptr;
+        e->batch_lists_cap = 0;
+        GS_HIP(dalloc(&e->batch_lists, 2 * lw));
+        e->batch_lists_cap = 2 * lw;
     }
+    if (cw > e->batch_codes_cap) {
+        GS_HIP(hipStreamSynchronize(e->stream));
+        if (e->batch_codes) (void)hipFree(e->batch_codes);
+        e->batch_codes = nullptr;
+        e->batch_codes_cap = 0;
+        GS_HIP(dalloc(&e->batch_codes, 2 * cw));
+        e->batch_codes_cap = 2 * cw;
+    }
+    uint32_t *dev = e->batch_lists;  // [blocks | nodes]
+    uint16_t *dcodes = e->batch_codes;
     gs::RoundArgs a = base_args(e);
     a.obs_state = dcodes;
     a.blk_list = dev;
@@ -1787,16 +1694,12 @@ gs_status observe_nodes(gs_engine *e, const std::vector<uint32_t> &nodes, std::v
     if (he == hipSuccess)
         he = hipMemcpyAsync(dev + blocks.size(), nodes.data(), m * sizeof(uint32_t), hipMemcpyHostToDevice,
                             e->stream);
-    if (he == hipSuccess && e->deliver_pending) {
-        if (built_elsewhere(e)) he = hipStreamWaitEvent(e->stream, e->ev_built[e->round & 1u], 0);
-        if (he == hipSuccess && seq_prepare(e) != GS_OK) he = hipErrorUnknown;  // SEQ: the round's pull batches
-    }
+    if (he == hipSuccess && e->deliver_pending && seq_prepare(e) != GS_OK)
+        he = hipErrorUnknown;  // SEQ: the round's pull batches
     if (he == hipSuccess) he = gs::launch_round(a, e->deliver_pending ? 2 : 3, e->stream);
     if (he == hipSuccess)
         he = hipMemcpyAsync(codes.data(), dcodes, codes.size() * sizeof(uint16_t), hipMemcpyDeviceToHost, e->stream);
-    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
-    (void)hipFree(dev);
-    (void)hipFree(dcodes);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);  // (codes, blocks and nodes are host temporaries)
     return he == hipSuccess ? GS_OK : GS_ERR_HIP;
 }
 
@@ -2064,10 +1967,8 @@ double gs_round_kernel_bytes(const gs_engine *e) {
     // Code-row shards: record 12 + target word 4 + deltas 16, the pull code
     // read at x's exchange-B slot (slot 4 + code 4 B) and the 8-B row written
     // at its exchange-A slot (slot 4 + next target word 4 + row 8): 56 B.
-    // (with u32 Statistics deltas, SAFE_GOSSIP_AMD_STATS32=1: 16 B more)
-    const double st = e->st16 ? 0.0 : 16.0;
-    if (e->dlv && e->shard) return n * (2.0 * rp + 56.0 + st);
-    if (e->dlv) return n * (2.0 * rp + (e->dlv_pack ? 38.0 : 42.0) + st);
+    if (e->dlv && e->shard) return n * (2.0 * rp + 56.0);
+    if (e->dlv) return n * (2.0 * rp + (e->dlv_pack ? 38.0 : 42.0));
     return n * (2.75 * rp + 68.0);
 }
 
@@ -2086,7 +1987,6 @@ const char *gs_round_kernel_name(const gs_engine *e) {
         return e->dlv_pack == 2 ? "round_kernel_dlv4<1,u64,4>"
                                 : (e->dlv_pack == 3 ? "round_kernel_dlv4<1,u32,1>" : "round_kernel_dlv4<1,u32,2>");
     }
-    if (e->spr) return "round_kernel<false,1,SPARSE>";
     if (e->filt && e->w32 && (e->g.small ? e->g.rpad == 32 : e->g.logr <= 8))
         return "round_kernel_w32<1> (32-bit lanes, live-filtered gathers)";
     if (e->filt) return e->g.small ? "round_kernel<true,1> (live-filtered gathers)"
@@ -2109,42 +2009,15 @@ gs_status gs_round_traffic(gs_engine *e, double *bytes_per_launch, uint32_t *lau
             *bytes_per_launch = dense;
             return GS_OK;
         }
-        std::vector<u64> v(gs::kAcctSlots);
+        u64 rows = 0;
         GS_HIP(hipStreamSynchronize(e->stream));
-        GS_HIP(hipMemcpy(v.data(), e->acct, v.size() * sizeof(u64), hipMemcpyDeviceToHost));
-        const double rows = (double)v[0], n = e->g.n, rp = e->g.rpad;
-        *bytes_per_launch = n * (68.0 + 3.0 / 8.0 + 2.0 * rp) + 3.0 * rp / 8.0 * rows / e->filt_launches;
+        GS_HIP(hipMemcpy(&rows, e->acct, sizeof(u64), hipMemcpyDeviceToHost));
+        const double n = e->g.n, rp = e->g.rpad;
+        *bytes_per_launch = n * (68.0 + 3.0 / 8.0 + 2.0 * rp) + 3.0 * rp / 8.0 * (double)rows / e->filt_launches;
         return GS_OK;
     }
-    if (!e->spr) {
-        *bytes_per_launch = dense;
-        *launches = 0;
-        return GS_OK;
-    }
-    gs_status st = set_device(e);
-    if (st != GS_OK) return st;
-    std::vector<u64> v(gs::kAcctSlots);
-    GS_HIP(hipStreamSynchronize(e->stream));
-    GS_HIP(hipMemcpy(v.data(), e->acct, v.size() * sizeof(u64), hipMemcpyDeviceToHost));
-    double segs = 0, rows = 0;
-    for (u64 w : v) {
-        segs += (double)(w & 0xFFFFFFFFull);
-        rows += (double)(w >> 32);
-    }
-    const uint32_t Ls = e->acct_launches, Ld = e->dense_launches;
-    *launches = Ls + Ld;
-    if (Ls + Ld == 0) {
-        *bytes_per_launch = dense;
-        return GS_OK;
-    }
-    // sparse launches: per node the 68 B of gs_round_kernel_bytes plus the maps
-    // (zero-word bits of both buffers read, one written; live / all-A bits
-    // written); per plane segment moved 64 B (8 planes x 8 B); per class row
-    // gathered 24 B (3 planes x 8 B, per 64-rumor word).  Dense launches: the
-    // static model.
-    const double n = e->g.n, W = e->g.W;
-    const double sparse_total = Ls * n * (68.0 + (3.0 * W + 2.0) / 8.0) + 64.0 * segs + 24.0 * rows;
-    *bytes_per_launch = (sparse_total + Ld * dense) / (Ls + Ld);
+    *bytes_per_launch = dense;
+    *launches = 0;
     return GS_OK;
 }
 

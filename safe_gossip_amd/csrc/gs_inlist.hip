@@ -136,9 +136,6 @@ GS_DEV uint32_t emit_target(const InListArgs &a, uint32_t y, const uint32_t *lst
     if (filt) r.kf |= (~lv & 7u) << kInSkipShift;  // skip flags of pushers 0..2
     a.IN8[y] = r;
     uint32_t rows = filt ? (uint32_t)__popc(lv) + (k > kInline ? k - kInline : 0u) : 0u;
-#ifdef GS_EXP_NO_SIB
-    k = 0;  // timing only: no SibRec writes
-#endif
     bool any_live = false;  // some pusher ahead of lst[j] is live
     for (uint32_t j = 1; j < k; ++j) {
         const uint32_t prev = j - 1u;
@@ -1428,81 +1425,6 @@ InListSizes inlist_sizes(const CsrPlan &p) {
         z.scratch_words = (size_t)p.ba * p.nb + 2 * (size_t)p.nb + 1;  // M, tot, base, tail count
     }
     return z;
-}
-
-// zl = "t(x) is live" (and the rows it leaves to gather) from the targets
-// inl_bin wrote and the live map of the planes the round kernel just wrote:
-// a wave's 64 lanes are 64 consecutive sources, i.e. one zl word.
-constexpr uint32_t kZlPer = 4;  // sources per thread (strided by the block)
-__global__ __launch_bounds__(kInlThreads) void inl_zl(InListArgs a) {
-    __shared__ uint32_t zrows;
-    if (threadIdx.x == 0) zrows = 0u;
-    __syncthreads();
-    uint32_t zr = 0;  // (wave-uniform)
-#pragma unroll
-    for (uint32_t q = 0; q < kZlPer; ++q) {
-        const uint32_t x = (blockIdx.x * kZlPer + q) * kInlThreads + threadIdx.x;
-        bool l = false, np = true;
-        if (x < a.p.n) {
-            const uint32_t t = a.tg[x];
-            l = !(t & kTgDead) && map_test(a.lvm, t & kTgMask);
-            np = (t & kTgNoPull) != 0u;
-        }
-        const u64 b = __ballot(l);
-        if ((threadIdx.x & 63u) == 0u && x < a.p.n) a.zl[x >> 6] = b;
-        if (a.rows) zr += (uint32_t)__popcll(__ballot(l && !np));
-    }
-    if (a.rows && (threadIdx.x & 63u) == 0u && zr) atomicAdd(&zrows, zr);
-    __syncthreads();
-    if (a.rows && threadIdx.x == 0 && zrows) atomicAdd(a.rows, (u64)zrows);
-}
-
-hipError_t launch_build_bins(const InListArgs &a, hipStream_t s) {
-    const CsrPlan &p = a.p;
-    if (p.n == 0) return hipSuccess;
-    if (!p.binned || p.dlv) return hipErrorInvalidValue;
-    const uint32_t np = p.nb << p.sub;
-    const size_t lds_bin = ((size_t)p.chunk + p.chunk / 2 + (np + 1) / 2) * sizeof(uint32_t) +
-                           ((size_t)2 * np + p.chunk) * sizeof(uint16_t);
-    const void *kb = p.chunk == kChunk ? (const void *)inl_bin<kChunk> : (const void *)inl_bin<kChunkSmall>;
-    hipError_t e = hipFuncSetAttribute(kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bin);
-    if (e != hipSuccess) return e;
-    const uint32_t sl = sort_split_log(p.nb);
-    if (sl > 0) {  // the split sort cannot clear the fill counts itself
-        if (p.sub != sl) return hipErrorInvalidValue;
-        e = hipMemsetAsync(a.scratch + p.fill_off, 0, ((size_t)p.nb << p.sub) * sizeof(uint32_t), s);
-        if (e != hipSuccess) return e;
-    }
-    InListArgs ab = a;
-    ab.lvm = ab.cpm = nullptr;  // no node maps in this phase (inl_zl writes zl)
-    ab.zl = nullptr;
-    ab.rows = nullptr;
-    if (p.chunk == kChunk) hipLaunchKernelGGL(inl_bin<kChunk>, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
-    else hipLaunchKernelGGL(inl_bin<kChunkSmall>, dim3(p.ba), dim3(kInlThreads), lds_bin, s, ab);
-    return hipGetLastError();
-}
-
-hipError_t launch_build_sort(const InListArgs &a, hipStream_t s) {
-    const CsrPlan &p = a.p;
-    if (p.n == 0) return hipSuccess;
-    if (!p.binned || p.dlv || !a.lvm || !a.cpm || !a.zl) return hipErrorInvalidValue;
-    const uint32_t sl = sort_split_log(p.nb);
-    const size_t lds_sort = ((size_t)(kBin >> sl) / 2 + (kBinCap >> sl)) * sizeof(uint32_t);
-    const void *ks = sl == 0   ? (const void *)inl_sort<0, kSortThreads>
-                     : sl == 1 ? (const void *)inl_sort<1, kSortThreads>
-                     : sl == 2 ? (const void *)inl_sort<2, kSortThreads>
-                               : (const void *)inl_sort<3, kSortThreads>;
-    hipError_t e = hipFuncSetAttribute(ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sort);
-    if (e != hipSuccess) return e;
-    InListArgs ab = a;
-    const uint32_t zb = (uint32_t)(((u64)p.n + kZlPer * kInlThreads - 1) / (kZlPer * kInlThreads));
-    hipLaunchKernelGGL(inl_zl, dim3(zb), dim3(kInlThreads), 0, s, ab);
-    const dim3 gs(p.nb, 1u << sl);
-    if (sl == 0) hipLaunchKernelGGL((inl_sort<0, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
-    else if (sl == 1) hipLaunchKernelGGL((inl_sort<1, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
-    else if (sl == 2) hipLaunchKernelGGL((inl_sort<2, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
-    else hipLaunchKernelGGL((inl_sort<3, kSortThreads>), gs, dim3(kSortThreads), lds_sort, s, ab);
-    return hipGetLastError();
 }
 
 // The DLV build (binned plan, p.dlv): partitions, the part sorts with the

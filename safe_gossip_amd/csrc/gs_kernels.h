@@ -7,7 +7,7 @@ namespace gs {
 // The exchange layout a round kernel needs (ShardPlan's fields of the same
 // names; the slot helpers below take either).
 struct ShardRows {
-    uint32_t G, P, W, capP, flagrows, blk, idrows, rw, rwb, codes, chunk, n;
+    uint32_t G, P, W, capP, idrows, rw, rwb, codes, chunk, n;
 };
 
 struct RoundArgs {
@@ -55,6 +55,11 @@ struct RoundArgs {
     uint16_t *obs_rec;        // [n][R]
     uint32_t *obs_psize;      // [n]
     u64 *obs_digest;          // [n] state digest (gs_common.h digest_*)
+    // Digest parts of a rumor slice (gs_state_digest_part): this engine's word
+    // sums before the final mix (digest_sum), added with atomics into
+    // obs_dpart[n][dp_words] at the network's words of rumors [dp_lo, dp_lo + R)
+    u64 *obs_dpart;
+    uint32_t dp_lo, dp_words;
     // shard engine only (null otherwise): exchange rows, see gs_shard.hip
     const u64 *recvA;         // round-t push rows of this shard's pushers [slot][2][W]
     const u64 *recvB;         // round-t pull rows for this shard's nodes [slot][2][W]
@@ -64,7 +69,7 @@ struct RoundArgs {
     u64 *recvA_next;
     const uint32_t *spos_cur; // slot of x in recvB (exchange B of round t)
     const uint32_t *spos_next;// slot of x in sendA (exchange A of round t+1)
-    ShardRows sp;             // its layout (row flags when sp.flagrows != 0)
+    ShardRows sp;             // its layout
     // harness-injected faults (gs_common.h); pend/offc exist iff f.churn != 0
     Faults f;
     u64 *pend;                // [n][2][W]: votes (bump, anyC) of nodes frozen offline
@@ -87,22 +92,7 @@ struct RoundArgs {
     uint32_t blk_off, blk_count, obs_only;
     const uint32_t *blk_list, *obs_list;
     uint32_t n_obs;
-    // Sparse records (wide 2P engine, W <= 8; null otherwise), exact for the
-    // plane buffer they describe: zb = a bit per segment "all 8 planes zero"
-    // (a word of unknown rumors), lb = a bit per node "some B or C entry"
-    // (its push is not empty), ab = a bit per node "no known entry".  A zero
-    // word is neither loaded nor rewritten over a zero word, and a pusher with
-    // nothing live is not gathered ("Sparse records").
-    // Written by the sparse-variant transition launches (modes 0 and 1), which
-    // the engine uses while a dissemination is young; null = dense variant.
-    const u64 *zb_cur;
-    u64 *zb_nxt;
-    const uint8_t *lb_cur, *ab_cur;
-    uint8_t *lb_nxt, *ab_nxt;
-    u64 *acct;                // mode 1: [kAcctSlots] packed (plane segments read +
-                              // written) | lane gathers << 32, one atomic per block
-    u64 *dens;                // [kDensSlots] zero words of the round-(t+1) planes
-                              // (spread atomics, cleared by the engine per launch)
+    u64 *acct;                // filtered timed launches: acct[0] += *rows_cnt (block 0)
     // Live-filtered gathers (gs_common.h kSkipBit; null: every row gathered):
     // zlm = a bit per source "t(x) is live" of round t (in-list build), and
     // the node maps of the round-(t+1) planes this launch writes (transition
@@ -136,11 +126,6 @@ struct RoundArgs {
     uint32_t cmax, maxc, maxr;
 };
 constexpr uint32_t kExtPush = 1u << 20, kExtNew = 1u << 21, kExtRec = 1u << 22, kExtEmpty = 1u << 23;
-constexpr uint32_t kAcctSlots = 4096;  // accounting atomics spread over this many words
-constexpr uint32_t kDensSlots = 16;    // density counts spread over this many words
-// Sparse-record map sizes: zb words per buffer, lb / ab bytes per buffer.
-inline u64 spr_zb_words(const Geometry &g) { return (g.nseg + 255u) / 256u * 4u + 4u; }
-inline u64 spr_node_bytes(const Geometry &g) { return ((u64)g.n + 63u) / 64u * 8u + 64u; }
 // Node bit maps of the live-filtered gathers: u64 words (+ one spare word).
 inline u64 node_map_words(uint32_t n) { return ((u64)n + 63u) / 64u + 1u; }
 __host__ __device__ inline bool map_test(const u64 *m, uint32_t i) { return ((m[i >> 6] >> (i & 63u)) & 1ull) != 0; }
@@ -263,11 +248,6 @@ hipError_t launch_build_inlists(const InListArgs &a, hipStream_t s);
 // A DLV plan's sort parts hold 2^*log targets and own *per tail slots each
 // (the decoding of DlvRec::mf, RoundArgs::dlv_tlog / dlv_tper).
 void dlv_tail_parts(const CsrPlan &p, uint32_t *log, uint32_t *per);
-// The filtered binned build in two phases (2P gather path): phase A (inl_bin:
-// targets and the bin partition, no node maps) can run beside the previous
-// round kernel; phase B (the zl map from lvm, then inl_sort) runs after it.
-hipError_t launch_build_bins(const InListArgs &a, hipStream_t s);
-hipError_t launch_build_sort(const InListArgs &a, hipStream_t s);
 hipError_t launch_stats_fold(uint32_t *st32, u64 *st64, uint32_t n, uint32_t st16, hipStream_t s);
 // Rumor slices: st32 empty_pull / empty_push += emin[2x] / emin[2x + 1].
 hipError_t launch_slice_apply(uint32_t *st32, const uint8_t *emin, uint32_t n, uint32_t st16, hipStream_t s);
@@ -320,12 +300,6 @@ struct ShardPlan {
     // is ONE equal-split all-to-all over a contiguous region.
     uint32_t P, mP, bP; // parts, nodes per part, plan blocks per part
     uint32_t capP;      // row slots per (source rank, destination rank, part)
-    // Row flags: after its capP row slots every sub-block carries flagrows
-    // rows of one byte per slot, bit j = word j of that slot's row is nonzero
-    // (written by the row's producer), so a receiver skips empty rows
-    // without reading them (opt-in, SAFE_GOSSIP_AMD_SHARD_FLAGS=1: measured
-    // slower); flagrows = 0 when off or W > 8.  blk = capP + flagrows.
-    uint32_t flagrows, blk;
     uint32_t idrows;    // rows of u32 ids per block of the last part of A (P*capP ids)
     // Row format: u32 words per row of exchange A (rw) and B (rwb).  Class
     // rows (R_pad >= 32, or forced): the 2-plane class code as 2W u64 words,
@@ -343,28 +317,28 @@ constexpr uint32_t kRowMutual = 1u << 31;
 // Row slot of (rank block s, part h, index i) in an exchange-A / -B buffer.
 template <class SP>
 __host__ __device__ inline uint32_t shard_blockA(const SP &P, uint32_t h) {
-    return P.blk + (h + 1u == P.P ? P.idrows : 0u);
+    return P.capP + (h + 1u == P.P ? P.idrows : 0u);
 }
 template <class SP>
 __host__ __device__ inline uint32_t shard_a_slot(const SP &P, uint32_t s, uint32_t h, uint32_t i) {
-    return h * P.G * P.blk + s * shard_blockA(P, h) + i;
+    return h * P.G * P.capP + s * shard_blockA(P, h) + i;
 }
 template <class SP>
 __host__ __device__ inline uint32_t shard_b_slot(const SP &P, uint32_t s, uint32_t h, uint32_t i) {
-    return (h * P.G + s) * P.blk + i;
+    return (h * P.G + s) * P.capP + i;
 }
 template <class SP>
 __host__ __device__ inline uint32_t shard_slotsA(const SP &P) {
-    return P.G * (P.P * P.blk + P.idrows);
+    return P.G * (P.P * P.capP + P.idrows);
 }
 template <class SP>
-__host__ __device__ inline uint32_t shard_slotsB(const SP &P) { return P.G * P.P * P.blk; }
+__host__ __device__ inline uint32_t shard_slotsB(const SP &P) { return P.G * P.P * P.capP; }
 struct SlotPos {
     uint32_t s, h, i;  // i >= capP: an id row
 };
 template <class SP>
 __host__ __device__ inline SlotPos shard_a_decode(const SP &P, uint32_t e) {
-    const uint32_t reg = P.G * P.blk;
+    const uint32_t reg = P.G * P.capP;
     uint32_t h = e / reg;
     if (h > P.P - 1u) h = P.P - 1u;
     const uint32_t r = e - h * reg, ba = shard_blockA(P, h);
@@ -388,19 +362,6 @@ __host__ __device__ inline uint32_t shard_key_bslot(const SP &P, uint32_t key) {
     const uint32_t s = key / per, r = key - s * per, h = r / P.capP;
     return shard_b_slot(P, s, h, r - h * P.capP);
 }
-// The flag byte of row slot e of an exchange buffer (A: sub-blocks of
-// shard_blockA rows, B: of blk rows): byte i of the flag rows after the
-// capP row slots of e's sub-block.
-template <class SP>
-__host__ __device__ inline u64 shard_flag_a(const SP &P, uint32_t e) {
-    const SlotPos q = shard_a_decode(P, e);
-    return (u64)(e - q.i + P.capP) * (16u * P.W) + q.i;
-}
-template <class SP>
-__host__ __device__ inline u64 shard_flag_b(const SP &P, uint32_t e) {
-    const uint32_t i = e % P.blk;
-    return (u64)(e - i + P.capP) * (16u * P.W) + i;
-}
 // u32-word offsets inside one plan set (round r: targets and send slots of
 // the owned sources) and one in-list set (round r: receive-slot in-lists).
 struct ShardPlanLayout {
@@ -411,8 +372,7 @@ struct ShardEdgeLayout {
 };
 // codes: one u32 code per row (delivery-record shards; no row flags), and
 // parts of whole 1024-node blocks (the packed DLV round kernel's blocks)
-ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t parts, bool row_flags = true,
-                     bool codes = false);
+ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t parts, bool codes = false);
 size_t shard_plan_words(const ShardPlan &P, ShardPlanLayout *L);
 size_t shard_edge_words(const ShardPlan &P, ShardEdgeLayout *L);
 // Plan of `round`: owned targets, send slots, and the ids of every block of
@@ -462,6 +422,10 @@ hipError_t launch_known_popc(const u64 *known, uint32_t n, uint32_t KW, uint32_t
 // B{0,1}, records dropped; state/rec may be null.
 hipError_t launch_obs_pending(const u64 *pairs, uint32_t m, uint32_t R, u64 *known, uint16_t *state,
                               uint16_t *rec, hipStream_t s);
+// The digests of a sliced network (gs_digest_finish): per node the mixed word
+// sums of dpart[n][words] plus the node term of psize and stats[n][5].
+hipError_t launch_digest_finish(const u64 *dpart, uint32_t n, uint32_t words, const uint32_t *psize,
+                                const u64 *stats, u64 *out, hipStream_t s);
 hipError_t launch_stats_reduce(const u64 *stats, uint32_t n, int op,
                                u64 *partials /* [5*blocks] */, uint32_t blocks,
                                hipStream_t s);

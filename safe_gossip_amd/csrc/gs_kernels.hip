@@ -36,9 +36,6 @@ constexpr uint32_t kStageIters = kBlockWords / 2u / 256u;  // uint4 loads per th
 #ifndef GS_RK_MINW
 #define GS_RK_MINW 1
 #endif
-#ifndef GS_RK_LATE_B
-#define GS_RK_LATE_B 0
-#endif
 
 // MODE: 0 transition only (first round), 1 deliver round t + transition to
 // t+1, 2 deliver round t + observe, 3 observe only.
@@ -57,38 +54,7 @@ GS_DEV Cls decode16(uint32_t code) {
 // DLV: delivery records (gs_common.h DlvRec) replace every class-plane
 // gather: a lane's pushers' push codes are in its own record and its pull
 // batch in PULL[x], both read coalesced.
-// Sparse records: the 256 bits of a block's segments, word i = wave i.
-struct Bits256 {
-    u64 w0, w1, w2, w3;
-    GS_DEV void load(const u64 *p) {
-        w0 = p[0];
-        w1 = p[1];
-        w2 = p[2];
-        w3 = p[3];
-    }
-    // word i for a wave-uniform i (scalar selects, no indexed access)
-    GS_DEV u64 word(uint32_t i) const {
-        return (w0 & (0ull - (u64)(i == 0u))) | (w1 & (0ull - (u64)(i == 1u))) | (w2 & (0ull - (u64)(i == 2u))) |
-               (w3 & (0ull - (u64)(i == 3u)));
-    }
-    GS_DEV uint32_t count() const { return popc(w0) + popc(w1) + popc(w2) + popc(w3); }
-};
-GS_DEV bool map_bit(const uint8_t *__restrict__ m, uint32_t i) { return ((m[i >> 3] >> (i & 7u)) & 1u) != 0; }
-// Staging chunk c = t + 256*i of a block (16 B = words 2c, 2c+1 of its
-// records [node][plane][W]) covers plane words of segments s0 and s0+1
-// (W >= 2) or s0 (W = 1), with s0 = chunk_seg(t) + 64*i: bit chunk_seg(t) of
-// word i.  True when they are all known zero.
-GS_DEV uint32_t chunk_seg(uint32_t t, uint32_t logw) {
-    const uint32_t w0 = 2u * t;
-    return (((w0 >> (logw + 3u)) << logw) | (w0 & ((1u << logw) - 1u))) & 63u;
-}
-GS_DEV bool chunk_zero(u64 word, uint32_t bit, uint32_t logw) {
-    const u64 m = logw ? 3ull : 1ull;
-    return ((word >> bit) & m) == m;
-}
-// SPRK: the sparse-records variant (wide 2P engine, transition modes), launched
-// while a dissemination is young (gs_engine.cpp picks it per round).
-template <bool SMALL, int MODE, bool SHARD, bool SEQ, bool DLV, bool SPRK = false>
+template <bool SMALL, int MODE, bool SHARD, bool SEQ, bool DLV>
 __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     constexpr bool DELIVER = (MODE == 1 || MODE == 2);
     constexpr bool TRANSITION = (MODE == 0 || MODE == 1);
@@ -103,34 +69,13 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     const uint32_t x = L.x;
     const u64 *__restrict__ S = a.Scur;
 
-    // ---- sparse records (wide 2P engine): the zero-word bits of the block's
-    // 256 segments in the round-t planes (zc) and in the planes the
-    // round-(t+1) output overwrites (zn)
-    constexpr bool spr = SPRK && !SMALL && !SHARD && !SEQ && !DLV && TRANSITION;
-    Bits256 zc = {}, zn = {};
-    bool skip_planes = false, gchk = false;
-    __shared__ u64 acc_blk;
-    __shared__ uint32_t zero_blk;  // zero words of the block in the round-(t+1) planes
     __shared__ uint32_t blk_any;  // some node pushes a live rumor in round t+1
     if (threadIdx.x == 0) blk_any = 0;
-    if (spr) {
-        zc.load(a.zb_cur + (u64)bid * 4u);
-        zn.load(a.zb_nxt + (u64)bid * 4u);
-        skip_planes = true;
-        // gathers check the live / all-A maps first (L2 hits): most pushes are
-        // empty while a dissemination is young
-        gchk = DELIVER;
-        if (threadIdx.x == 0) {
-            acc_blk = 0;
-            zero_blk = 0;
-        }
-    }
 
     // ---- own round-t planes: the block's records are one contiguous range
     // (W <= 256), loaded first with 16-byte coalesced loads (clamped, so every
     // load is unconditional) and transposed through LDS below, instead of
-    // eight strided 8-byte loads per lane.  Sparse records: a chunk whose two
-    // words are known zero is not loaded.
+    // eight strided 8-byte loads per lane.
     __shared__ __attribute__((aligned(16))) u64 stage[kBlockWords];
     const uint32_t npu_blk = SMALL ? (1u << g.lognpu) : 1u;
     const u64 blk_base = (u64)bid * (kBlockWords / npu_blk);
@@ -138,30 +83,16 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                                           g.units * kPlanes * (SMALL ? 1u : g.W) - blk_base) / 2u;
     static_assert(kStageIters == 4, "stage loads are unrolled by hand");
     const uint4 *src4 = reinterpret_cast<const uint4 *>(S + blk_base);
-    const uint32_t logw = SMALL ? 0u : g.logr - 6u;
-    const uint32_t cbit = chunk_seg(threadIdx.x, logw);
-    uint4 st0 = {0u, 0u, 0u, 0u}, st1 = {0u, 0u, 0u, 0u}, st2 = {0u, 0u, 0u, 0u}, st3 = {0u, 0u, 0u, 0u};
-    if (skip_planes) {
-        const uint32_t t = threadIdx.x;
-        if (t < blk_v4 && !chunk_zero(zc.w0, cbit, logw)) st0 = src4[t];
-        if (t + 256u < blk_v4 && !chunk_zero(zc.w1, cbit, logw)) st1 = src4[t + 256u];
-        if (t + 512u < blk_v4 && !chunk_zero(zc.w2, cbit, logw)) st2 = src4[t + 512u];
-        if (t + 768u < blk_v4 && !chunk_zero(zc.w3, cbit, logw)) st3 = src4[t + 768u];
-    } else {
-        st0 = src4[min(threadIdx.x, blk_v4 - 1u)];
-        st1 = src4[min(threadIdx.x + 256u, blk_v4 - 1u)];
-        st2 = src4[min(threadIdx.x + 512u, blk_v4 - 1u)];
-        st3 = src4[min(threadIdx.x + 768u, blk_v4 - 1u)];
-    }
+    const uint4 st0 = src4[min(threadIdx.x, blk_v4 - 1u)];
+    const uint4 st1 = src4[min(threadIdx.x + 256u, blk_v4 - 1u)];
+    const uint4 st2 = src4[min(threadIdx.x + 512u, blk_v4 - 1u)];
+    const uint4 st3 = src4[min(threadIdx.x + 768u, blk_v4 - 1u)];
 
     // ---- coalesced per-node metadata (level 1)
     // Statistics deltas of x, loaded with the other level-1 reads so the
     // read-modify-write at the end adds no dependent memory round trip
-    // (GS_STATS_LATE: loaded after the transition, as before).
-#ifndef GS_STATS_LATE
     uint4 stv = {0u, 0u, 0u, 0u};
     if (TRANSITION && valid && (SMALL || L.j == 0)) stv = load_stats(a.st32, a.st16, x);
-#endif
     // rumor slice: an earlier round's network empty counts (pull | push << 8)
     uint32_t eadd = 0;
     if (TRANSITION && a.eadd && valid && (SMALL || L.j == 0)) eadd = reinterpret_cast<const uint16_t *>(a.eadd)[x];
@@ -176,7 +107,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     DlvRec dr = {};     // DLV: x's record
     uint32_t dpull = 0;  // DLV: x's pull batch
     // live-filtered gathers (2P gather path; gs_common.h kSkipBit)
-    const bool filt = !SHARD && !SEQ && !DLV && !spr && a.zlm != nullptr;
+    const bool filt = !SHARD && !SEQ && !DLV && a.zlm != nullptr;
     u64 zlw = 0;            // the zl word of x: bit x & 63 = t(x) is live
     uint32_t qskip = 0;     // inline pushers that push nothing
     uint32_t eskip = 0;     // inline siblings that cannot pass anything on
@@ -224,17 +155,6 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                 if (!seq_inl) r = 0;
             }
         }
-#ifdef GS_EXP_NO_PUSHERS
-        k = 0;
-#endif
-#ifdef GS_EXP_NO_ZPUSHERS
-        r = 0;
-#endif
-#ifdef GS_EXP_NO_GATHER
-        k = 0;
-        r = 0;
-        z = x;
-#endif
     }
 
     // ---- the random gathers (level 2), issued together before the LDS
@@ -242,7 +162,6 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     // of t(x) ahead of x.  Slots past k / r load x's own row (an L2 hit) so no
     // load is conditional.  Rarer deeper in-lists are walked afterwards.
     Cls q[kBatchK], e[kBatchE], qz = {0, 0, 0}, wz = {0, 0, 0};
-    uint32_t ngath = 0;  // class rows gathered (pushers, t(x)): accounting
     // 2P gather path: the id of pusher #kInline (the first tail entry) read
     // with the batch, so the walk below waits for its row only (a wave's 16
     // nodes at config 4 hold such a pusher with probability ~0.26)
@@ -259,58 +178,18 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
                 static_assert(kBatchK == 3, "shard rows: three batched pushers");
                 const uint32_t e2 = a.IN2[x];
                 const uint32_t sp = a.spos_cur[x];  // the slot of x's pull row (z's answer)
-                const bool pl = !(tgw & kTgNoPull) && sp != 0xFFFFFFFFu;  // no slot: capacity overflow (flagged)
-                if (a.sp.flagrows) {
-                    // row flags (one byte per slot, bit j = word j nonzero):
-                    // rows that carry nothing for this lane's word are not read
-                    const uint8_t *fa = reinterpret_cast<const uint8_t *>(a.recvA);
-                    const uint8_t *fb = reinterpret_cast<const uint8_t *>(a.recvB);
-                    gq[0] = k > 0 && ((fa[shard_flag_a(a.sp, in.z)] >> L.j) & 1u);
-                    gq[1] = k > 1 && ((fa[shard_flag_a(a.sp, in.w)] >> L.j) & 1u);
-                    gq[2] = k > 2 && ((fa[shard_flag_a(a.sp, e2)] >> L.j) & 1u);
-                    gz = pl && ((fb[shard_flag_b(a.sp, sp)] >> L.j) & 1u);
-                    if (gq[0]) q[0] = L.load_push_row(a.recvA, in.z);
-                    if (gq[1]) q[1] = L.load_push_row(a.recvA, in.w);
-                    if (gq[2]) q[2] = L.load_push_row(a.recvA, e2);
-                    ngath += (gq[0] ? 1u : 0u) + (gq[1] ? 1u : 0u) + (gq[2] ? 1u : 0u);
-                } else {
-                    // the first three pushers' rows together (unconditional:
-                    // row 0 stands in for a missing pusher)
-                    q[0] = L.load_push_row(a.recvA, in.z);
-                    q[1] = L.load_push_row(a.recvA, in.w);
-                    q[2] = L.load_push_row(a.recvA, e2);
-                    ngath += min(k, kBatchK);
-                    gz = pl;
-                }
+                // the first three pushers' rows together (unconditional:
+                // row 0 stands in for a missing pusher)
+                q[0] = L.load_push_row(a.recvA, in.z);
+                q[1] = L.load_push_row(a.recvA, in.w);
+                q[2] = L.load_push_row(a.recvA, e2);
+                gz = !(tgw & kTgNoPull) && sp != 0xFFFFFFFFu;  // no slot: capacity overflow (flagged)
                 if (gz) {
                     qz.c = a.recvB[L.row_index(sp, 2, 0)];
                     qz.a0 = a.recvB[L.row_index(sp, 2, 1)];
                     qz.a1 = 0;
-                    ++ngath;
                 }
             }
-        } else if (gchk) {
-            // sparse: look the pushers and t(x)'s earlier pushers up in the
-            // live map and t(x) in the all-A map (2 MB at config 4: L2 hits),
-            // then gather only rows that carry something.  A row with nothing
-            // live pushes nothing, exactly as the zero row does; t(x)'s row
-            // also decides what t(x) lacks, so only an all-A t(x) is skipped.
-            bool gq[kBatchK], ge[kBatchE];
-#pragma unroll
-            for (uint32_t i = 0; i < kBatchK; ++i) gq[i] = i < k && map_bit(a.lb_cur, in8.s[i]);
-#pragma unroll
-            for (uint32_t i = 0; i < kBatchE; ++i) ge[i] = i < r && map_bit(a.lb_cur, sb8.e[i]);
-            const bool gz = valid && !map_bit(a.ab_cur, z);
-#pragma unroll
-            for (uint32_t i = 0; i < kBatchK; ++i) {
-                if (gq[i]) q[i] = L.load_cls(S, in8.s[i]);
-                ngath += gq[i] ? 1u : 0u;
-            }
-            if (gz) qz = L.load_cls(S, z);
-            ngath += gz ? 1u : 0u;
-#pragma unroll
-            for (uint32_t i = 0; i < kBatchE; ++i)
-                if (ge[i]) e[i] = L.load_cls(S, sb8.e[i]);
         } else if (filt) {
             if (!SEQ && k > kInline) tail0 = a.src[in8.first()];
             // live-filtered: a row that cannot change any result (a pusher with
@@ -323,22 +202,18 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             for (uint32_t i = 0; i < kBatchK; ++i) {
                 gq[i] = i < k && !((qskip >> i) & 1u);
                 if (gq[i]) q[i] = L.load_cls(S, in8.s[i]);
-                ngath += gq[i] ? 1u : 0u;
             }
             gz = valid && !(tgw & kTgNoPull) && (((zlw >> (x & 63u)) & 1ull) != 0 || zneed);
             if (gz) qz = L.load_cls(S, z);
-            ngath += gz ? 1u : 0u;
 #pragma unroll
             for (uint32_t i = 0; i < kBatchE; ++i) {
                 ge[i] = i < r && !((eskip >> i) & 1u);
                 if (ge[i]) e[i] = L.load_cls(S, sb8.e[i]);
-                ngath += ge[i] ? 1u : 0u;
             }
         } else {
             if (!SEQ && k > kInline) tail0 = a.src[in8.first()];
 #pragma unroll
             for (uint32_t i = 0; i < kBatchK; ++i) q[i] = L.load_cls(S, i < k ? in8.s[i] : x);
-            ngath += min(k, kBatchK) + (valid ? 1u : 0u);
             if (SEQ && !seq_inl) {  // W(x), coalesced (qz holds its code planes)
                 if (valid && (sinf & kSeqGot)) {
                     const u64 wi = ((u64)x * 2u) * g.W + L.j;
@@ -362,11 +237,11 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     // ... and that pusher's row, issued as soon as the id is in (the batch's
     // rows, issued after it, stay in flight)
     Cls t0 = {0, 0, 0};
-    if (DELIVER && !SEQ && !DLV && !SHARD && !gchk && k > kInline) t0 = L.load_cls(S, tail0);
+    if (DELIVER && !SEQ && !DLV && !SHARD && k > kInline) t0 = L.load_cls(S, tail0);
     // likewise the row of t(x)'s pusher #kBatchE ahead of x (its id is inline)
     static_assert(kBatchE < kSibInline, "sibling #kBatchE is inline");
     Cls s2 = {0, 0, 0};
-    if (DELIVER && !SEQ && !DLV && !SHARD && !gchk && r > kBatchE && !(tgw & kTgNoPull) &&
+    if (DELIVER && !SEQ && !DLV && !SHARD && r > kBatchE && !(tgw & kTgNoPull) &&
         (!filt || zneed) && !((eskip >> kBatchE) & 1u))
         s2 = L.load_cls(S, pick_sib(sb8.e, kBatchE));
     {
@@ -377,40 +252,13 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         dst4[threadIdx.x + 768u] = st3;
     }
     __syncthreads();
-    // GS_RK_LATE_B: the five b planes are read from the stage only for the
-    // transition (fewer registers live across the deliveries; A/B)
-    constexpr bool kLateB = GS_RK_LATE_B != 0;
     u64 P[kPlanes];
-    auto load_planes = [&](int p0, int p1) {
 #pragma unroll
-        for (int p = p0; p < p1; ++p) {
-            u64 v = valid ? stage[L.plane_index(p) - blk_base] : 0ull;
-            P[p] = SMALL ? ((v >> L.sh) & L.m) : v;
-        }
-    };
-    load_planes(0, (kLateB && !spr) ? 3 : kPlanes);
-
-    // Sparse variant: a wave all of whose segments are unknown words that
-    // receive nothing live (no live pusher, an all-A t(x), no live pusher of
-    // t(x) ahead of x) and get no injection or external RPC stays all-A, and
-    // its nodes only count empty pushes and empty pulls: it skips phases 1-2
-    // and the transition (a wave-uniform branch: no vector work issued).
-    bool wtriv = false;
-    if (spr && a.n_inj == 0 && a.n_ext == 0 && a.f.churn == 0) {
-        u64 any = 0;
-#pragma unroll
-        for (int p = 0; p < kPlanes; ++p) any |= P[p];
-        bool busy = any != 0;
-        if (DELIVER) {
-#pragma unroll
-            for (uint32_t i = 0; i < kBatchK; ++i) busy |= (q[i].c | q[i].a0 | q[i].a1) != 0;
-#pragma unroll
-            for (uint32_t i = 0; i < kBatchE; ++i) busy |= (e[i].c | e[i].a0 | e[i].a1) != 0;
-            busy |= (qz.c | qz.a0 | qz.a1) != 0;
-            busy |= k > kBatchK || r > kBatchE;
-        }
-        wtriv = __ballot(valid && busy) == 0ull;
+    for (int p = 0; p < kPlanes; ++p) {
+        const u64 v = valid ? stage[L.plane_index(p) - blk_base] : 0ull;
+        P[p] = SMALL ? ((v >> L.sh) & L.m) : v;
     }
+
     // filtered: a skipped t(x) row stays the empty row it was initialised to;
     // skipped pushers and siblings are not absorbed at all (an empty row
     // changes nothing but |P|, which k counts)
@@ -436,7 +284,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     bool seq_gx = false, seq_skip = false;
     uint32_t seq_px = 0, seq_jz = kNone;
     if (DELIVER && valid && k > 30u) atomicOr(&a.flags[2], 1u);
-    if (DELIVER && valid && !wtriv) {
+    if (DELIVER && valid) {
         bool zin = false;
         u64 pv2, pvB, pCl;
         if (DLV) {
@@ -463,10 +311,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             for (uint32_t i = 0; i < kBatchK; ++i)
                 if (i < k) rv.push(q[i], i, k, zs != i);
             for (uint32_t i = kBatchK; i < k; ++i) {
-                const uint32_t ei = a.src[in.x + i];
-                const bool gi = !a.sp.flagrows ||
-                                ((reinterpret_cast<const uint8_t *>(a.recvA)[shard_flag_a(a.sp, ei)] >> L.j) & 1u);
-                rv.push(gi ? L.load_push_row(a.recvA, ei) : Cls{0, 0, 0}, i, k, zs != i);
+                rv.push(L.load_push_row(a.recvA, a.src[in.x + i]), i, k, zs != i);
             }
             // pull row code (b0, b1): 01 counter 1, 10 counter 2, 11 counter 255
             pv2 = qz.a0 & ~qz.c;
@@ -571,14 +416,9 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             }
             for (uint32_t i = kBatchK; i < k; ++i) {  // in-degree > kBatchK (1.9% of nodes)
                 const uint32_t s = i < kInline ? pick_inline(in8.s, i)
-                                               : ((i == kInline && !gchk) ? tail0 : a.src[in8.first() + (i - kInline)]);
+                                               : (i == kInline ? tail0 : a.src[in8.first() + (i - kInline)]);
                 zin |= s == z;
-                const bool gs_ = !gchk || map_bit(a.lb_cur, s);
-                ngath += gs_ ? 1u : 0u;
-                Cls row = {0, 0, 0};
-                if (i == kInline && !gchk) row = t0;
-                else if (gs_) row = L.load_cls(S, s);
-                rv.push(row, i, k, !(pulled && s == z));
+                rv.push(i == kInline ? t0 : L.load_cls(S, s), i, k, !(pulled && s == z));
             }
             // Pull batch from z: z's live set plus what z created from pushers
             // ahead of x.
@@ -592,16 +432,14 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             // deeper can be passed on either)
             if (r > kBatchE && pnot && pulled && (!filt || zneed)) {  // rank > kBatchE (rare)
                 auto sib_row = [&](uint32_t s, bool skip) -> Cls {
-                    if (skip || (gchk && !map_bit(a.lb_cur, s))) return Cls{0, 0, 0};
-                    ++ngath;
+                    if (skip) return Cls{0, 0, 0};
                     return L.load_cls(S, s);
                 };
                 for (uint32_t i = kBatchE; i < min(r, kSibInline); ++i) {
                     const bool sk = ((eskip >> i) & 1u) != 0;
                     Cls row;
-                    if (i == kBatchE && !gchk) {
+                    if (i == kBatchE) {
                         row = s2;
-                        ngath += sk ? 0u : 1u;
                     } else {
                         row = sib_row(pick_sib(sb8.e, i), sk);
                     }
@@ -672,7 +510,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     // ---- node-level statistics of the deliveries
     uint32_t lc = popc(liveX);
     uint32_t part_cw = rv.part_cw, recv = rv.recv, first_create = rv.first_create;
-    if (DELIVER && !SMALL && !wtriv) {
+    if (DELIVER && !SMALL) {
         lc = group_sum(lc, g.W);
         part_cw = group_sum(part_cw, g.W);
         recv = group_sum(recv, g.W);
@@ -707,7 +545,6 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
 
     if (!TRANSITION) {
         // ---------------- observation (post phase 2 of round t) -------------
-        if (kLateB) load_planes(3, kPlanes);
         if (!valid) return;
         if (a.obs_only != 0xFFFFFFFFu || a.obs_list) {  // listed nodes' state codes only
             uint32_t slot = 0;
@@ -762,6 +599,22 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             }
             if (a.obs_psize) a.obs_psize[x] = psize;
         }
+        if (a.obs_dpart) {
+            // rumor slice: this lane's word sum, split over the network words
+            // it covers (its first rumor is the network's rumor dp_lo + 64 jw)
+            const uint32_t jw = SMALL ? 0u : L.j;
+            if (64u * jw < g.R) {
+                u64 pl[20];
+                digest_planes(L.m, B, C, D, crB, crC, a0, a1, &P[3], anyC, rv.c1, rv.c2, pl);
+                const uint32_t gb = a.dp_lo + 64u * jw, gw = gb >> 6, sh = gb & 63u;
+                u64 *dp = a.obs_dpart + (u64)x * a.dp_words;
+                atomicAdd(&dp[gw], digest_sum(pl, sh));
+                if (sh && gw + 1u < a.dp_words) {
+                    for (int p = 0; p < 20; ++p) pl[p] >>= 64u - sh;
+                    atomicAdd(&dp[gw + 1u], digest_sum(pl));
+                }
+            }
+        }
         if (a.obs_digest) {
             // this lane's word (words past ceil(R/64) hold no rumor: no term);
             // the node's lanes add their terms (W adjacent lanes), the leader
@@ -808,10 +661,10 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     }
 
     // ---------------- phase 0 of round t+1 at x ----------------------------
-    u64 N[kPlanes] = {0, 0, 0, 0, 0, 0, 0, 0};  // a trivial wave stays all-A
+    u64 N[kPlanes];
     u64 Bn = 0, Cn = 0;
     bool on_next = true;
-    if (!wtriv) {
+    {
         // Gossip::new_message (insert = replace with MessageState::new, records
         // dropped) for the rumors injected at x this round.
         u64 inj = 0;
@@ -823,7 +676,6 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         const bool pending = off_t && valid;
         const u64 pb = pending ? a.pend[pidx] : 0ull, pa = pending ? a.pend[pidx + g.W] : 0ull;
         NextOut o;
-        if (kLateB && !spr) load_planes(3, kPlanes);
         next_round_seg(P, rv, inj, psize, pending, pb, pa, on_next, a.cmax, a.maxc, a.maxr, o);
 #pragma unroll
         for (int p = 0; p < kPlanes; ++p) N[p] = o.N[p];
@@ -892,61 +744,12 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         if (MODE == 1 && a.acct && a.rows_cnt && bid == 0 && threadIdx.x == 0) atomicAdd(a.acct, *a.rows_cnt);
     }
 
-    // ---- sparse records of the round-(t+1) planes: zero-word bits (one u64
-    // per wave), node live / all-A bits (64/W per wave, W <= 8: whole bytes);
-    // the group and packing work is on wave-uniform ballots (scalar ALU)
-    if (spr) {
-        const u64 any = N[0] | N[1] | N[2] | N[3] | N[4] | N[5] | N[6] | N[7];
-        const bool wz = valid && any == 0;
-        const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        const u64 seg0 = seg - lane;
-        const u64 vC = N[0] & ~(N[1] & N[2]), vB = ~N[0] & (N[1] | N[2]);
-        const u64 bz = __ballot(wz), blive = __ballot(valid && (vB | vC) != 0);
-        const u64 cl = compress_stride(group_or_bits(blive, logw), logw);
-        const u64 ca = compress_stride(group_and_bits(bz, logw), logw);
-        if (lane == 0 && seg0 < g.nseg) {
-            a.zb_nxt[seg0 >> 6] = bz;
-            atomicAdd(&zero_blk, popc(bz));
-            const uint32_t per = 64u >> logw;  // nodes per wave
-            const u64 byte0 = (seg0 >> logw) >> 3;  // first node of the wave / 8
-            if (per == 64u) {
-                *reinterpret_cast<u64 *>(a.lb_nxt + byte0) = cl;
-                *reinterpret_cast<u64 *>(a.ab_nxt + byte0) = ca;
-            } else if (per == 32u) {
-                *reinterpret_cast<uint32_t *>(a.lb_nxt + byte0) = (uint32_t)cl;
-                *reinterpret_cast<uint32_t *>(a.ab_nxt + byte0) = (uint32_t)ca;
-            } else if (per == 16u) {
-                *reinterpret_cast<uint16_t *>(a.lb_nxt + byte0) = (uint16_t)cl;
-                *reinterpret_cast<uint16_t *>(a.ab_nxt + byte0) = (uint16_t)ca;
-            } else {
-                a.lb_nxt[byte0] = (uint8_t)cl;
-                a.ab_nxt[byte0] = (uint8_t)ca;
-            }
-        }
-        if (MODE == 1 && a.acct) {
-            // algorithmic plane segments moved: read unless known zero, written
-            // unless zero over zero; class rows gathered 
-            const bool zcl = ((zc.word(wv) >> lane) & 1ull) != 0, znl = ((zn.word(wv) >> lane) & 1ull) != 0;
-            const bool rd = valid && !(skip_planes && zcl);
-            const bool wr = valid && !(skip_planes && wz && znl);
-            uint32_t ng = 0;  // ngath <= 3 + 1 + (kMaxIn - 3) < 32: five bit ballots
-#pragma unroll
-            for (uint32_t b = 0; b < 5u; ++b) ng += popc(__ballot((ngath >> b) & 1u)) << b;
-            const u64 v = (u64)(popc(__ballot(rd)) + popc(__ballot(wr))) | ((u64)ng << 32);
-            if (lane == 0) atomicAdd(&acc_blk, v);
-        }
-    }
-
     // ---- write round-(t+1) planes (through LDS, 16-byte coalesced stores)
     uint32_t live_new = (valid && on_next) ? popc(Bn | Cn) : 0u;
     if (!SMALL) live_new = group_sum(live_new, g.W);
     if (__ballot(live_new != 0u) != 0ull && (threadIdx.x & 63u) == 0u) blk_any = 1u;
     __syncthreads();  // also: every lane is done reading stage
     const bool blk_live = blk_any != 0u;
-    if (spr && threadIdx.x == 0) {
-        if (MODE == 1 && a.acct) atomicAdd(&a.acct[bid & (kAcctSlots - 1u)], acc_blk);
-        if (a.dens) atomicAdd(&a.dens[bid & (kDensSlots - 1u)], (u64)zero_blk);
-    }
     if (SMALL) {
         const uint32_t npu = 1u << g.lognpu;
 #pragma unroll
@@ -965,19 +768,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         uint4 *dst4 = reinterpret_cast<uint4 *>(a.Snext + blk_base);
         // streaming (nontemporal) stores: 3.11 -> 3.01 ms per round kernel at
         // config 4 (nontemporal plane loads measured slower: 3.27 ms).
-        // Sparse records: zero over known zero is not rewritten.
-        if (skip_planes) {
-#pragma unroll
-            for (uint32_t it = 0; it < 4u; ++it) {
-                const uint32_t i = threadIdx.x + 256u * it;
-                if (i >= blk_v4) break;
-                const uint4 v = src4[i];
-                if ((v.x | v.y | v.z | v.w) == 0u && chunk_zero(zn.word(it), cbit, logw)) continue;
-                nt_store4(v, &dst4[i]);
-            }
-        } else {
-            for (uint32_t i = threadIdx.x; i < blk_v4; i += blockDim.x) nt_store4(src4[i], &dst4[i]);
-        }
+        for (uint32_t i = threadIdx.x; i < blk_v4; i += blockDim.x) nt_store4(src4[i], &dst4[i]);
     }
     if (SHARD) {
         // push row of round t+1: the push batch's class code, to owner(t_{t+1}(x))
@@ -990,26 +781,14 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             a.sendA[L.row_index(sp, 2, 0)] = c0;
             a.sendA[L.row_index(sp, 2, 1)] = c1;
         }
-        if (a.sp.flagrows) {  // the row's flag byte: bit j = word j nonzero (x's W lanes are adjacent)
-            const u64 bal = __ballot(sp != 0xFFFFFFFFu && (c0 | c1) != 0ull);
-            if (sp != 0xFFFFFFFFu && L.j == 0) {
-                const uint32_t bits = (uint32_t)(bal >> (threadIdx.x & 63u)) & ((1u << a.sp.W) - 1u);
-                reinterpret_cast<uint8_t *>(a.sendA)[shard_flag_a(a.sp, sp)] = (uint8_t)bits;
-            }
-        }
     }
 
     // ---- push list + Statistics (src/gossip.rs:80,103-111)
     mark_any_live(a.live, a.round_new, bid, blk_live);
     if (leader) {
-#ifndef GS_EXP_NO_STATS
         // rounds is the engine's round count (every node runs every round);
         // the other four are u32 deltas folded into u64 before they can wrap.
-#ifdef GS_STATS_LATE
-        uint4 v = load_stats(a.st32, a.st16, x);
-#else
         uint4 v = stv;
-#endif
         if (a.st16 && (ext_full | ext_empty | ext_recv)) {
             // u16 deltas hold internal deliveries only (bounded per round):
             // external RPCs, as many as the caller sends, go to the totals
@@ -1034,7 +813,6 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         v.w += d_recv;                             // full_message_received
         store_stats(a.st32, a.st16, x, v);
         if (!on_next) atomicAdd(&a.offc[x], 1u);  // (no return: nothing waits for it)
-#endif
     }
 }
 
@@ -1044,17 +822,6 @@ static hipError_t launch_mode(const RoundArgs &a, int mode, hipStream_t s) {
     const u64 grid = a.blk_count ? a.blk_count : (a.g.nseg + block - 1) / block;
     if (grid == 0) return hipSuccess;
     if (a.blk_list && (mode == 0 || mode == 1)) return hipErrorInvalidValue;  // (observation launches only)
-    if constexpr (!SMALL && !SHARD && !SEQ && !DLV) {
-        if (a.zb_nxt && (mode == 0 || mode == 1)) {  // sparse records
-            if (mode == 0)
-                hipLaunchKernelGGL((round_kernel<false, 0, false, false, false, true>), dim3((uint32_t)grid),
-                                   dim3(block), 0, s, a);
-            else
-                hipLaunchKernelGGL((round_kernel<false, 1, false, false, false, true>), dim3((uint32_t)grid),
-                                   dim3(block), 0, s, a);
-            return hipGetLastError();
-        }
-    }
     switch (mode) {
     case 0: hipLaunchKernelGGL((round_kernel<SMALL, 0, SHARD, SEQ, DLV>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
     case 1: hipLaunchKernelGGL((round_kernel<SMALL, 1, SHARD, SEQ, DLV>), dim3((uint32_t)grid), dim3(block), 0, s, a); break;
@@ -1185,6 +952,26 @@ hipError_t launch_obs_pending(const u64 *pairs, uint32_t m, uint32_t R, u64 *kno
                               uint16_t *rec, hipStream_t s) {
     if (m == 0) return hipSuccess;
     hipLaunchKernelGGL(obs_pending, dim3((m + 255) / 256), dim3(256), 0, s, pairs, m, R, known, state, rec);
+    return hipGetLastError();
+}
+
+// Digests of a sliced network from the summed word parts (gs_digest_finish).
+__global__ __launch_bounds__(256) void digest_finish(const u64 *__restrict__ dpart, uint32_t n, uint32_t words,
+                                                     const uint32_t *__restrict__ psize, const u64 *__restrict__ stats,
+                                                     u64 *out) {
+    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= n) return;
+    u64 st[5];
+    for (int i = 0; i < 5; ++i) st[i] = stats[(u64)x * 5 + i];
+    u64 h = digest_node(psize[x], st);
+    for (uint32_t j = 0; j < words; ++j) h += digest_fin(j, dpart[(u64)x * words + j]);
+    out[x] = h;
+}
+
+hipError_t launch_digest_finish(const u64 *dpart, uint32_t n, uint32_t words, const uint32_t *psize,
+                                const u64 *stats, u64 *out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(digest_finish, dim3((n + 255u) / 256u), dim3(256), 0, s, dpart, n, words, psize, stats, out);
     return hipGetLastError();
 }
 

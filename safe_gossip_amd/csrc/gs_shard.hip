@@ -54,13 +54,13 @@ GS_DEV uint32_t dest_rank(const ShardPlan &P, uint32_t t) {
 }
 
 // Id slots of block d inside an exchange-A buffer: the idrows rows after the
-// capP row slots and the flag rows of d's sub-block of the last part (P*capP ids; the id of
+// capP row slots of d's sub-block of the last part (P*capP ids; the id of
 // next round's source (part h, index i) at h*capP + i).
 GS_DEV uint32_t *id_slots(const ShardPlan &P, u64 *bufA, uint32_t d) {
-    return reinterpret_cast<uint32_t *>(bufA) + (u64)shard_a_slot(P, d, P.P - 1u, P.blk) * P.rw;
+    return reinterpret_cast<uint32_t *>(bufA) + (u64)shard_a_slot(P, d, P.P - 1u, P.capP) * P.rw;
 }
 GS_DEV const uint32_t *id_slots(const ShardPlan &P, const u64 *bufA, uint32_t d) {
-    return reinterpret_cast<const uint32_t *>(bufA) + (u64)shard_a_slot(P, d, P.P - 1u, P.blk) * P.rw;
+    return reinterpret_cast<const uint32_t *>(bufA) + (u64)shard_a_slot(P, d, P.P - 1u, P.capP) * P.rw;
 }
 
 __global__ __launch_bounds__(kPlanBlock) void plan_count(ShardPlan P, uint64_t seed, uint32_t epoch,
@@ -337,8 +337,7 @@ __global__ __launch_bounds__(256) void edge_bin_sort(const u64 *__restrict__ pai
     }
 }
 
-ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t parts, bool row_flags,
-                     bool codes) {
+ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t parts, bool codes) {
     ShardPlan P{};
     P.codes = codes ? 1u : 0u;
     P.rw = codes ? 2u : 4u * W;   // A: (push code, target word) / class code
@@ -360,6 +359,10 @@ ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t pa
     // kernel's blocks at <= 4 nodes per lane)
     const u64 align = codes ? 1024u : kPlanBlock;
     const u64 mp = ((chunk + P.P - 1) / P.P + align - 1) / align * align;
+    // parts are whole aligned blocks, so a small rank range holds fewer than
+    // asked: the trailing ones would be empty (no overlap, an idle exchange
+    // each); P is the number that holds nodes (the same on every rank)
+    P.P = (uint32_t)std::max<u64>(1, (chunk + mp - 1) / mp);
     P.mP = (uint32_t)mp;
     P.bP = (uint32_t)(mp / kPlanBlock);
     // rows from one part of one rank to one rank: ~Binomial(mP, chunk/(n-1));
@@ -369,9 +372,6 @@ ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t pa
     const u64 q = std::max<u64>(64, P.rw);  // P*capP u32 ids fill whole rows of rw u32 words
     P.capP = (uint32_t)(((u64)std::ceil(capd) + q - 1) / q * q);
     P.idrows = codes ? 0u : P.P * P.capP / P.rw;  // (code rows carry their targets: no ids)
-    // a flag byte per row slot (bit j: row word j), capP bytes in rows of 16W
-    P.flagrows = (row_flags && !codes && W <= 8u) ? (P.capP + 16u * W - 1u) / (16u * W) : 0u;
-    P.blk = P.capP + P.flagrows;
     // counting sort of the receive slots of A over the m local targets
     CsrPlan &c = P.edges;
     c.n = std::max<uint32_t>(shard_slotsA(P), 1);
@@ -491,9 +491,6 @@ __global__ __launch_bounds__(256) void pull_kernel(PullArgs a) {
     const uint4 in = a.IN[z];
     const uint32_t e2 = a.IN2[z];
     const uint32_t k = in.y & 0xFFFFu;
-    const bool fl = a.P.flagrows != 0;
-    const uint8_t *fa = reinterpret_cast<const uint8_t *>(a.recvA);
-    uint8_t *fb = reinterpret_cast<uint8_t *>(a.sendB);
     for (uint32_t i = 0; i < k; ++i) {
         const uint32_t e = i == 0 ? in.z : (i == 1 ? in.w : (i == 2 ? e2 : a.EP[in.x + i]));
         const SlotPos q = shard_a_decode(a.P, e);            // slot e of exchange A
@@ -502,18 +499,9 @@ __global__ __launch_bounds__(256) void pull_kernel(PullArgs a) {
         const u64 c0 = zB1 | pB | pcl, c1 = zB2 | pcl;
         a.sendB[L.row_index(eb, 2, 0)] = c0;  // code bit 0: counter 1 or 255
         a.sendB[L.row_index(eb, 2, 1)] = c1;  // code bit 1: counter 2 or 255
-        if (fl) {
-            // the row's flag byte (z's W lanes are adjacent and run the same
-            // k iterations, so the ballot sees all of them)
-            const u64 bal = __ballot((c0 | c1) != 0ull);
-            if (L.j == 0)
-                fb[(u64)(eb - q.i + a.P.capP) * (16u * a.P.W) + q.i] =
-                    (uint8_t)((uint32_t)(bal >> (threadIdx.x & 63u)) & ((1u << a.P.W) - 1u));
-        }
         // a pusher's row matters to the later pull rows only while z lacks
         // rumors (and only if it carries something for this word)
-        if (i + 1 < k && pnot && (!fl || ((fa[(u64)(e - q.i + a.P.capP) * (16u * a.P.W) + q.i] >> L.j) & 1u)))
-            sibling(L.load_push_row(a.recvA, e), pnot, pB, pC);
+        if (i + 1 < k && pnot) sibling(L.load_push_row(a.recvA, e), pnot, pB, pC);
     }
 }
 

@@ -341,7 +341,7 @@ __global__ __launch_bounds__(kW32Threads, GS_W32_MINW) void round_kernel_w32(Rou
 bool w32_eligible(const RoundArgs &a, int mode) {
     const bool geom = a.g.small ? (a.g.rpad == 32u && a.g.lognpu == 1u) : (a.g.logr >= 6u && a.g.logr <= 8u);
     return a.w32 && (mode == 0 || mode == 1) && geom && !a.recvA &&
-           !a.Wb && !a.DR && !a.zb_nxt && a.zlm && a.lvm && a.cpm && a.n_ext == 0 && a.blk_off == 0 &&
+           !a.Wb && !a.DR && a.zlm && a.lvm && a.cpm && a.n_ext == 0 && a.blk_off == 0 &&
            a.blk_count == 0;
 }
 

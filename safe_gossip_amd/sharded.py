@@ -66,13 +66,13 @@ def plan_info(n_nodes: int, n_rumors: int, world: int, rank: int = 0, parts: int
     cfg.n_nodes, cfg.n_rumors, cfg.schedule = n_nodes, n_rumors, schedule
     info = (ctypes.c_uint32 * 14)()
     _check(_lib().gs_shard_plan_info(ctypes.byref(cfg), rank, world, parts, info))
-    keys = ("lo", "m", "blk", "idrows", "row_words", "world", "rank", "chunk", "parts", "mP", "rowsA", "rowsB",
+    keys = ("lo", "m", "capP", "idrows", "row_words", "world", "rank", "chunk", "parts", "mP", "rowsA", "rowsB",
             "row_words_b", "codes")
     d = dict(zip(keys, list(info)))
     ra, rb = d["row_words"] * 4, d["row_words_b"] * 4
     d["row_bytes"], d["row_bytes_b"] = ra, rb
-    # part h of A: world sub-blocks of blk rows (+ idrows for the last part); B: blk rows
-    d["max_collective_bytes"] = max(world * (d["blk"] + d["idrows"]) * ra, world * d["blk"] * rb)
+    # part h of A: world sub-blocks of capP rows (+ idrows for the last part); B: capP rows
+    d["max_collective_bytes"] = max(world * (d["capP"] + d["idrows"]) * ra, world * d["capP"] * rb)
     d["bytes_per_round"] = d["rowsA"] * ra + d["rowsB"] * rb  # A + B sent per rank (self block included)
     return d
 
@@ -107,7 +107,6 @@ class _Shard:
     def region(self, which: str, h: int):
         """Part h of an exchange buffer: (first u32 word, u32 words per rank
         sub-block); the part's world sub-blocks are contiguous."""
-        # (info[2] "capP" here = rows per sub-block: row slots + flag rows)
         rows = self.capP + (self.idrows if which == "A" and h == self.parts - 1 else 0)
         w = self.wa if which == "A" else self.wb
         return h * self.world * self.capP * w, rows * w
@@ -177,6 +176,9 @@ class ShardedNetwork:
                                  f"RCCL all_to_all limit; use more pipeline parts (parts={self.parts})")
         else:
             raise ValueError(transport)
+        # parts that hold nodes (a small rank range holds fewer whole blocks
+        # than asked: gs_shard_info reports the effective count)
+        self.parts = self.shards[0].parts
         self.round = 0
         self._delivered = True
         self._pendA = []   # async works of exchange A of the current round

@@ -39,7 +39,7 @@ from typing import List, Optional
 
 import numpy as np
 
-from . import GossipError, Network, NoPeers, RoundReport, Statistics, _check
+from . import _U64P, GossipError, Network, NoPeers, RoundReport, Statistics, _check
 
 
 def merge_known(per, bounds, n: int, kw: int) -> np.ndarray:
@@ -308,6 +308,32 @@ class SlicedNetwork:
         both = [s.net.dump_records() for s in self.slices]
         recs = self._gather([b[0] for b in both])
         return np.concatenate(recs, axis=1), both[0][1]
+
+    def state_digest(self) -> np.ndarray:
+        """Per-node digest of the whole network (what gs_state_digest of one
+        engine holding every rumor gives): each slice adds its word sums into
+        one device buffer (gs_state_digest_part; dist: an all_reduce SUM),
+        then gs_digest_finish mixes them with |P| and the network Statistics."""
+        st = self.statistics_all()
+        words = self.kw
+        s0 = self.slices[0]
+        dp = self.torch.zeros(self.n * words, dtype=self.torch.int64, device=f"cuda:{self.device}")
+        self.torch.cuda.synchronize(self.device)  # (zeroed on torch's stream; the engines add on theirs)
+        for s in self.slices:
+            _check(s.lib.gs_state_digest_part(s.h, s.lo, words, dp.data_ptr()))
+        if self.transport == "dist":
+            if self.host_staged:
+                h = dp.cpu()
+                self.dist.all_reduce(h, group=self.group)
+                dp.copy_(h.to(dp.device))
+            else:
+                self.dist.all_reduce(dp, group=self.group)
+            self.torch.cuda.synchronize(self.device)
+        out = np.zeros(self.n, dtype=np.uint64)
+        stc = np.ascontiguousarray(st, dtype=np.uint64)
+        _check(s0.lib.gs_digest_finish(s0.h, dp.data_ptr(), words, stc.ctypes.data_as(_U64P),
+                                       out.ctypes.data_as(_U64P)))
+        return out
 
     def known_all(self) -> np.ndarray:
         self._flush()

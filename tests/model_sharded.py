@@ -72,6 +72,13 @@ def decode_code(code):
     return b0 & b1, b0 & ~b1, b1 & ~b0
 
 
+def part_count(n, G, parts, codes=False):
+    """Parts that hold nodes (shard_plan): whole aligned blocks of mP nodes
+    over the rank's chunk, at most `parts`."""
+    chunk = shard_range(n, G, 0)[2]
+    return max(1, -(-chunk // part_nodes(n, G, parts, codes)))
+
+
 def shard_cap(n, G, W=1, parts=1, codes=False):
     """Row slots per (source rank, destination rank, part) sub-block (shard_plan)."""
     import math
@@ -89,8 +96,8 @@ class ShardModel(Model):
         assert R <= 62
         self.rank, self.world, self.a2a = rank, world, a2a
         self.lo, self.m, self.chunk = shard_range(n, world, rank)
-        self.parts = parts
         self.codes = uses_codes(R)
+        self.parts = part_count(n, world, parts, self.codes)
         self.mP = part_nodes(n, world, parts, self.codes)
         self.cap = shard_cap(n, world, parts=parts, codes=self.codes)
         self.tg, self.fl = {}, {}

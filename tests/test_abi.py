@@ -39,6 +39,26 @@ def test_exported_symbols_nm(engine):
     assert set(declared_symbols()) <= exported
 
 
+def test_build_provenance(engine, tmp_path):
+    # the library carries the hash of the sources it was built from and the
+    # ABI version; load_library refuses a library built from other sources
+    from safe_gossip_amd import build
+    lib = engine.load_library()
+    assert lib.gs_abi_version() == engine.ABI_VERSION == 2
+    assert engine.build_id() == build.source_hash()
+    assert open(build.LIB_PATH + ".buildid").read().strip() == build.source_hash()
+    # a tree whose sources differ by one byte has another id
+    root = tmp_path / "tree"
+    for f in build.SOURCES + build.HEADERS:
+        rel = os.path.relpath(f, REPO)
+        (root / rel).parent.mkdir(parents=True, exist_ok=True)
+        (root / rel).write_bytes(open(f, "rb").read())
+    assert build.source_hash(str(root)) == build.source_hash()
+    hdr = root / "include" / "safe_gossip.h"
+    hdr.write_bytes(hdr.read_bytes() + b" ")
+    assert build.source_hash(str(root)) != build.source_hash()
+
+
 def test_derive_params_equal_oracle(engine, oracle):
     for n in list(range(1, 100)) + [1618, 1619, 2000, 5000, 10**4, 10**6, 2**24, 10**8,
                                     528491311, 2**32 - 2]:

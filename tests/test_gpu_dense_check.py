@@ -129,3 +129,40 @@ def test_config5_faults_rounds(engine):
     finally:
         shards.close()
         single.close()
+
+
+@pytest.mark.parametrize("n,R,world,faults", [
+    (5000, 256, 8, None),                    # 32-rumor slices: R_pad 32 (32-bit lane kernel)
+    (3000, 100, 3, (0.05, 0.05, 0.05)),      # ragged slices (33/33/34): words straddle slices
+    (4000, 40, 5, None),                     # 8-rumor slices: delivery records
+])
+def test_sliced_digest_small(engine, n, R, world, faults):
+    # the digest of a rumor-sliced network (each slice's word sums added on the
+    # device, then mixed with |P| and the network Statistics) is the digest of
+    # one engine holding every rumor: against the dense program every round
+    from safe_gossip_amd.sliced import SlicedNetwork
+    net = SlicedNetwork(n, R, world, seed=SEED, transport="local", **_fk(faults))
+    try:
+        _run(engine, [net], n, R, faults, 60)
+    finally:
+        net.close()
+
+
+def test_config4_multi_gpu_shapes_to_termination(engine):
+    # config 4 in the two 8-GPU layouts, on one GPU, to termination against the
+    # dense program (every 4th round and the last): 8 rumor slices of 32 rumors
+    # (round_kernel_w32 per slice, the empty counts MIN-combined on the
+    # device, bench.py --gpus 8's slice mode) and 8 class-row node shards of
+    # 2^21 nodes (device-copy exchanges, 2 pipeline parts each: --mode nodes)
+    from safe_gossip_amd.sharded import ShardedNetwork
+    from safe_gossip_amd.sliced import SlicedNetwork
+    n, R = 1 << 24, 256
+    slices = SlicedNetwork(n, R, 8, seed=SEED, epoch=1, transport="local")
+    shards = ShardedNetwork(n, R, 8, seed=SEED, epoch=1, transport="local", parts=2)
+    try:
+        assert "w32" in slices.round_kernel_name()
+        assert _run(engine, [slices, shards], n, R, None, 60, every=4, epoch=1,
+                    spread=SPREAD[(n, R)]) == SPREAD[(n, R)][0]
+    finally:
+        shards.close()
+        slices.close()

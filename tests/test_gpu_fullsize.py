@@ -110,7 +110,8 @@ def test_dlv_partition_build_matches_gather_path(engine, monkeypatch, n):
 
 
 def test_w32_lane_kernel_matches_w64(engine, monkeypatch):
-    # round_kernel_w32 (32-bit lanes, the default at R_pad 64..256) against
+    # round_kernel_w32 (32-bit lanes, forced at R_pad 256; the default only at
+    # R_pad 32, where a lane holds one node) against
     # the 64-bit lane round_kernel on a network larger than any oracle run:
     # 2^21 + 1234 nodes x 256 rumors with faults, a partial last block, every
     # state code, Statistics row and known set of 8 rounds

@@ -351,60 +351,14 @@ def test_parity_delivery_records_larger(engine):
     run_parity(engine, 20000, 16, "reinject", check_every=3, faults=(0.02, 0.05, 0.05))
 
 
-@pytest.mark.parametrize("mode", ["on", "auto"])
-@pytest.mark.parametrize("n,R,kind,faults", [
-    (300, 64, "trickle", None),
-    (130, 256, "reinject", None),
-    (77, 100, "origins", None),
-    (33, 512, "origins", None),                 # W = 8: one map byte per wave
-    (400, 64, "reinject", (0.3, 0.1, 0.1)),     # frozen nodes, injections into them
-    (130, 256, "origins", (0.1, 0.1, 0.2)),
-])
-def test_parity_sparse_records(engine, monkeypatch, mode, n, R, kind, faults):
-    # sparse records (wide 2P engine, opt-in): "on" runs the sparse variant
-    # every round, "auto" while a quarter of the words are unknown; every
-    # other wide 2P test runs the dense variant (the default)
-    monkeypatch.setenv("SAFE_GOSSIP_AMD_SPARSE", mode)
-    run_parity(engine, n, R, kind, faults=faults)
-
-
-def test_parity_sparse_records_after_clear(engine, monkeypatch):
-    # the maps are reset with the planes: a second dissemination after clear
-    monkeypatch.setenv("SAFE_GOSSIP_AMD_SPARSE", "on")
-    n, R = 500, 128
-    net = engine.Network(n, R, seed=SEED)
-    orc = OracleNet(n, R, seed=SEED)
-    try:
-        for epoch in (0, 4):
-            if epoch:
-                net.clear(epoch)
-                orc.clear(epoch)
-            for r in range(0, R, 3):
-                x = engine.origin_of(SEED, epoch, r, n)
-                net.send_new(x, r)
-                orc.send_new(x, r)
-            for rnd in range(1, 40):
-                rep = net.next_round()
-                _, olive = orc.next_round(SCHED_2P)
-                np.testing.assert_array_equal(net.dump_state(), orc.dump_state())
-                np.testing.assert_array_equal(net.statistics_all(), orc.statistics())
-                if not olive:
-                    break
-    finally:
-        net.close()
-        orc.close()
-
-
-def test_sparse_records_full_dissemination(engine, monkeypatch):
+def test_filtered_full_dissemination(engine, monkeypatch):
     # 2^20 nodes x 256 rumors, all injected in round 1 (the config-4 workload
     # at 1/16 size) through 24 rounds: the live-filtered gathers (the default)
-    # and the sparse path (auto, then every block checking) end bit-identical
-    # to the unfiltered dense kernel, and the traffic counted by the kernels
-    # stays below the dense model and above the streamed floor
+    # end bit-identical to the unfiltered kernel, and the traffic counted by
+    # the kernels stays below the dense model and above the streamed floor
     n, R = 1 << 20, 256
     out = {}
-    for mode, filt in (("dense", "0"), ("dense", "1"), ("auto", "1"), ("on", "1")):
-        monkeypatch.setenv("SAFE_GOSSIP_AMD_SPARSE", mode)
+    for filt in ("0", "1"):
         monkeypatch.setenv("SAFE_GOSSIP_AMD_FILTER", filt)
         net = engine.Network(n, R, seed=SEED)
         for r in range(R):
@@ -416,23 +370,20 @@ def test_sparse_records_full_dissemination(engine, monkeypatch):
         b, launches = net.round_traffic()
         dense = net.round_kernel_bytes()
         name = net.round_kernel_name()
-        if mode == "dense" and filt == "0":  # no maps: the static model
+        if filt == "0":  # no maps: the static model
             assert launches == 0 and b == dense
             assert "filtered" not in name
-        else:                # every deliver launch counted by the kernels
+        else:            # every deliver launch counted by the kernels
             assert launches == 23
             # (the filtered count includes t(x)'s earlier pushers' rows, which
             # the static model leaves out)
-            assert n * 68 < b < (0.9 if mode != "dense" else 1.0) * dense, (b, dense)
-            assert mode != "dense" or "live-filtered" in name
-        out[(mode, filt)] = (net.known_all(), net.statistics_all(),
-                             [net.push_batch(x) for x in range(0, n, 4099)])
+            assert n * 68 < b < dense, (b, dense)
+            assert "live-filtered" in name
+        out[filt] = (net.known_all(), net.statistics_all(), [net.push_batch(x) for x in range(0, n, 4099)])
         net.close()
-    ref = out[("dense", "0")]
-    for key, got in out.items():
-        np.testing.assert_array_equal(got[0], ref[0])
-        np.testing.assert_array_equal(got[1], ref[1])
-        assert got[2] == ref[2], key
+    np.testing.assert_array_equal(out["1"][0], out["0"][0])
+    np.testing.assert_array_equal(out["1"][1], out["0"][1])
+    assert out["1"][2] == out["0"][2]
 
 
 @pytest.mark.parametrize("n,R,kind,faults", [

@@ -102,18 +102,6 @@ def test_sharded_clear(engine):
     orc.close()
 
 
-@pytest.mark.parametrize("n,R,kind,faults", [
-    (1000, 256, "origins", None),
-    (700, 3, "trickle", (0.1, 0.1, 0.1)),
-    (520, 100, "reinject", None),
-])
-def test_sharded_parity_row_flags(engine, monkeypatch, n, R, kind, faults):
-    # SAFE_GOSSIP_AMD_SHARD_FLAGS=1 (opt-in A/B): a flag byte per row slot,
-    # receivers and the pull kernel skip rows flagged empty
-    monkeypatch.setenv("SAFE_GOSSIP_AMD_SHARD_FLAGS", "1")
-    run_parity(engine, n, R, kind, make_net=_maker(3, 2), faults=faults)
-
-
 # Code rows (R_pad <= 16, 2P): one u32 push / pull code per
 # exchange row, the pull kernel writes delivery records, and the packed DLV
 # round kernel (gs_dlv4.hip) runs each part; every R <= 16 case above runs them.

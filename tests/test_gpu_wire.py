@@ -100,12 +100,6 @@ def test_handle_received_seq(engine, n, R, faults):
     _handle_received_case(engine, n, R, faults, schedule="SEQ")
 
 
-def test_handle_received_sparse_records(engine, monkeypatch):
-    # the sparse-record variant of the round kernel applies external RPCs too
-    monkeypatch.setenv("SAFE_GOSSIP_AMD_SPARSE", "on")
-    _handle_received_case(engine, 250, 128, None)
-
-
 def _handle_received_case(engine, n, R, faults, schedule="2P"):
     from oracle_lib import fault_threshold
     fk = dict(churn=faults[0], drop_push=faults[1], drop_pull=faults[2]) if faults else {}

@@ -7,7 +7,7 @@ library's layout is the one the CPU protocol model (tests/model_sharded.py)
 runs."""
 import pytest
 
-from model_sharded import part_nodes, shard_cap, shard_range, uses_codes
+from model_sharded import part_count, part_nodes, shard_cap, shard_range, uses_codes
 
 CONFIGS = {"cfg4": (1 << 24, 256), "cfg5": (100_000_000, 16)}
 
@@ -28,7 +28,7 @@ def test_exchanges_below_rccl_limit(engine, cfg, world):
 
 
 @pytest.mark.parametrize("n,R,world,parts", [
-    (600, 16, 2, 1), (5000, 16, 2, 2), (1600, 8, 3, 3), (600, 40, 2, 1), (1100, 33, 2, 2),
+    (600, 16, 2, 1), (5000, 16, 2, 2), (1600, 8, 3, 3), (600, 40, 2, 1), (1100, 33, 2, 2), (5000, 16, 2, 4),
     (1 << 24, 256, 8, 4), (100_000_000, 16, 8, 4),
 ])
 def test_layout_matches_protocol_model(engine, n, R, world, parts):
@@ -40,7 +40,10 @@ def test_layout_matches_protocol_model(engine, n, R, world, parts):
         lo, m, chunk = shard_range(n, world, rank)
         assert (d["lo"], d["m"], d["chunk"]) == (lo, m, chunk)
         assert d["mP"] == part_nodes(n, world, parts, codes)
-        assert d["blk"] == shard_cap(n, world, W=W, parts=parts, codes=codes)
+        assert d["capP"] == shard_cap(n, world, W=W, parts=parts, codes=codes)
+        # parts are whole blocks: a small range holds fewer than asked, never an empty one
+        assert d["parts"] == part_count(n, world, parts, codes) <= parts
+        assert (d["parts"] - 1) * d["mP"] < chunk <= d["parts"] * d["mP"]
 
 
 def test_rccl_one_rank_default_config5(engine):

@@ -110,7 +110,7 @@ def _worker(rank, world, port, n, R, params, kind, q, faults=None, parts=1):
     (2, 600, 16, None, "origins", (0.1, 0.1, 0.1), 1),    # config 5 faults
     (3, 600, 8, None, "reinject", (0.3, 0.2, 0.2), 1),
     (2, 5000, 16, None, "origins", None, 2),     # code rows: pipeline parts of 2048 / 512 nodes
-    (3, 1600, 8, None, "reinject", (0.1, 0.1, 0.1), 3),  # parts of 1024 / 0 nodes
+    (3, 1600, 8, None, "reinject", (0.1, 0.1, 0.1), 3),  # 3 parts asked, 1 of 1024 nodes holds the range
     (2, 600, 40, None, "origins", None, 1),      # class rows (R_pad 64)
     (2, 1100, 33, None, "origins", None, 2),     # class rows: pipeline parts of 256 nodes
     (3, 1600, 20, None, "reinject", (0.1, 0.1, 0.1), 3),
