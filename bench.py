@@ -72,7 +72,7 @@ def parse():
     p.add_argument("--drop-push", type=float, default=None, help="P(push batch dropped)")
     p.add_argument("--drop-pull", type=float, default=None, help="P(pull batch dropped)")
     p.add_argument("--schedule", default="2P", choices=["2P", "SEQ"],
-                   help="2P (default) or SEQ (the reference harness's literal order; 1 GPU)")
+                   help="2P (default) or SEQ (the reference harness's literal order; N>1: rumor slices)")
     p.add_argument("--seed", type=lambda s: int(s, 0), default=0x5AFE6055)
     p.add_argument("--cpu-seconds", type=float, default=15.0,
                    help="budget of the CPU-oracle sample")
@@ -396,6 +396,8 @@ def main():
         modes = ["slices", "nodes"]
     if R < world:  # fewer rumors than ranks: no rumor slices
         modes = [m for m in modes if m != "slices"] or ["nodes"]
+    if args.schedule == "SEQ" and dist is not None:  # SEQ's pull chains cross node ranges: slices only
+        modes = ["slices"]
     runs = [run_mode(args, m, world, rank, local, dist, sg, np, torch, with_spread=(i == 0 and not args.no_spread))
             for i, m in enumerate(modes)]
     best = min(runs, key=lambda r: r["elapsed"])

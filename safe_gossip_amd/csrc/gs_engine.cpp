@@ -661,9 +661,13 @@ gs_status check_config(const gs_config *cfg, uint32_t rank, uint32_t world, uint
     if (nglob >= 2 && (p[0] > 3 || p[1] > 3 || p[2] > 32 || !p[0] || !p[1] || !p[2]))
         return GS_ERR_UNSUPPORTED;
     if (world && cfg->schedule == GS_SCHED_SEQ) return GS_ERR_UNSUPPORTED;  // chains cross ranks
-    // rumor slices: the 2P single-engine path (SEQ's empty pulls are not a MIN
-    // over slices of a per-slice count, and node shards slice nodes instead)
-    if (cfg->rumor_slice && (world || cfg->schedule == GS_SCHED_SEQ)) return GS_ERR_UNSUPPORTED;
+    // rumor slices are single engines (node shards slice nodes instead); both
+    // schedules: which pushes a node answers, and when, depends on the peer
+    // schedule only, and "has a live entry" only turns on within a round, so
+    // its empty pulls are a nondecreasing function of the first time it is
+    // live and the network's count is the MIN over the slices under SEQ too
+    // (tests/test_sliced_gloo.py: the oracle per slice against one oracle)
+    if (cfg->rumor_slice && world) return GS_ERR_UNSUPPORTED;
     *sp = gs::ShardPlan{};
     if (world) {
         *sp = plan_of(cfg, rank, world, parts);
@@ -804,7 +808,8 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
     for (int i = 0; i < 2 && ok && e->shard && !e->dlv; ++i) {  // (code rows need no in-lists ahead)
         const size_t words = gs::shard_edge_words(e->sp, &e->sel);
         ok = hipEventCreateWithFlags(&e->ev_edges[i], hipEventDisableTiming) == hipSuccess &&
-             dalloc(&e->edgew[i], words) == hipSuccess;
+             dalloc(&e->edgew[i], words) == hipSuccess &&
+             hipMemset(e->edgew[i], 0, words * sizeof(uint32_t)) == hipSuccess;  // (counters zero between builds)
     }
     if (ok && e->shard) ok = hipEventCreateWithFlags(&e->ev_main, hipEventDisableTiming) == hipSuccess;
     if (ok && e->shard && e->dlv) {  // one build set: built and read on the engine stream, in order

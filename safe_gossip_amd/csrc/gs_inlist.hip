@@ -532,9 +532,17 @@ struct PEnt {
 // The bin (part) regions: [nb * kBinCap] part entries at the region base.
 __host__ __device__ inline PEnt *part_entries(uint32_t *region) { return reinterpret_cast<PEnt *>(region); }
 constexpr size_t kDlvRegionWords = 3;  // u32 words per part slot
+// The single engine's entries are 8 bytes, (source, push code): a consumer
+// draws the source's target again (one Philox draw, peer_of) instead of
+// reading it -- the target is a counter-based function of (round, source).
+// Code-row shards keep 12-byte entries (their targets come with the rows).
+__host__ __device__ inline uint2 *part_entries8(uint32_t *region) { return reinterpret_cast<uint2 *>(region); }
 // Coarse-bucket entries inside the region buffer, after the bin regions.
 __host__ __device__ inline PEnt *coarse_entries(uint32_t *region, uint32_t nb) {
     return reinterpret_cast<PEnt *>(region + (size_t)nb * kBinCap * kDlvRegionWords);
+}
+__host__ __device__ inline uint2 *coarse_entries8(uint32_t *region, uint32_t nb) {
+    return reinterpret_cast<uint2 *>(region + (size_t)nb * kBinCap * kDlvRegionWords);
 }
 
 // Pull pass-back arrays, after the coarse buckets: per coarse source bucket
@@ -621,7 +629,8 @@ __global__ __launch_bounds__(NT) void dl_coarse(InListArgs a) {
         const uint32_t slot = res[b] + (i - off[b]);
         if (slot < kShardCap) {
             const u64 o = (u64)(b * kCoarseShards + shard) * kShardCap + slot;
-            ce[o] = PEnt{sx[i], st[i], sc[i]};
+            if constexpr (SH) ce[o] = PEnt{sx[i], st[i], sc[i]};
+            else coarse_entries8(a.region, p.nb)[o] = make_uint2(sx[i], sc[i]);
         }
     }
 }
@@ -637,7 +646,7 @@ constexpr uint32_t kFineThreads = GS_FINE_THREADS;
 constexpr uint32_t kFineChunk = GS_FINE_CHUNK;
 constexpr uint32_t kFineParts = kCoarseBins << kMaxFineSub;  // parts per coarse bucket (sub <= 2)
 // NT threads per block (GS_FINE_THREADS): 512 lets three blocks share a CU
-template <uint32_t NT>
+template <uint32_t NT, bool SH = false>
 __global__ __launch_bounds__(NT) void dl_fine(InListArgs a) {
     constexpr uint32_t kPer = kFineChunk / NT;
     static_assert(kFineChunk % NT == 0 && kFineParts <= NT, "dl_fine: whole entries, a scan slot per part");
@@ -668,10 +677,18 @@ __global__ __launch_bounds__(NT) void dl_fine(InListArgs a) {
     for (uint32_t q = 0; q < kPer; ++q) {
         const uint32_t i = lo + threadIdx.x + q * NT;
         const bool ok = i < hi;
-        const PEnt en = ce[(u64)cs * kShardCap + (ok ? i : lo)];
-        xv[q] = en.a;
-        tv[q] = ok ? en.b : kNone;
-        cv[q] = en.c;
+        const u64 o = (u64)cs * kShardCap + (ok ? i : lo);
+        if constexpr (SH) {
+            const PEnt en = ce[o];
+            xv[q] = en.a;
+            tv[q] = ok ? en.b : kNone;
+            cv[q] = en.c;
+        } else {  // (source, push code): the target drawn again
+            const uint2 en = coarse_entries8(const_cast<uint32_t *>(a.region), p.nb)[o];
+            xv[q] = en.x;
+            cv[q] = en.y;
+            tv[q] = ok ? peer_of(a.seed, a.epoch, a.round, en.x, p.n) : kNone;
+        }
         if (ok) atomicAdd(&cnt[(tv[q] >> plog) & (fp - 1u)], 1u);
     }
     __syncthreads();
@@ -709,7 +726,8 @@ __global__ __launch_bounds__(NT) void dl_fine(InListArgs a) {
         const uint32_t slot = res[lo_b] + (i - off[lo_b]);
         if (slot < pcap) {
             const u64 o = (u64)(cb * fp + lo_b) * pcap + slot;
-            pe[o] = PEnt{sx[i], sc[i], slt[i]};
+            if constexpr (SH) pe[o] = PEnt{sx[i], sc[i], slt[i]};
+            else part_entries8(a.region)[o] = make_uint2(sx[i], sc[i]);
         }
     }
 }
@@ -779,7 +797,8 @@ __global__ __launch_bounds__(kInlThreads) void dl_direct(InListArgs a) {
         const uint32_t b = sb[i];
         const uint32_t slot = res[b] + (i - off[b]);
         if (slot < pcap) {
-            part_entries(a.region)[(u64)b * pcap + slot] = PEnt{sx[i], sc[i], slt[i]};
+            if constexpr (SH) part_entries(a.region)[(u64)b * pcap + slot] = PEnt{sx[i], sc[i], slt[i]};
+            else part_entries8(a.region)[(u64)b * pcap + slot] = make_uint2(sx[i], sc[i]);
         }
     }
 }
@@ -804,31 +823,14 @@ constexpr uint32_t kSplitLog = GS_DLV_SPLIT_LOG;
 #define GS_DLV_SMALL_LOG (kSplitLog + 1u)  // below 128 bins (one coarse bucket, cache-resident)
 #endif
 constexpr uint32_t kDlvSmallLog = GS_DLV_SMALL_LOG;
-#ifndef GS_DLV_EARLY_TARGETS
-#define GS_DLV_EARLY_TARGETS 0  // A/B: 1 = small parts issue their target loads with the region loads (slower)
-#endif
-#ifndef GS_DLV_PP
-#define GS_DLV_PP 0  // 1: inl_sort_dlv as a persistent walk with the next part's loads in flight
-#endif
 // Small networks (few bins) sort with more blocks per bin, so the chip fills;
 // their bin regions stay in L2 (config 2: 64 bins).
-inline uint32_t dlv_split_log(uint32_t nb) {
-#ifdef GS_DLV_SPLIT_FIXED
-    return (void)nb, kSplitLog;  // A/B: the large-n split everywhere
-#endif
-    return nb >= 128u ? kSplitLog : kDlvSmallLog;
-}
+inline uint32_t dlv_split_log(uint32_t nb) { return nb >= 128u ? kSplitLog : kDlvSmallLog; }
 
-// PP (persistent, own regions, several coarse buckets): a resident grid walks
-// the parts in order, and each block issues the region loads of its NEXT part
-// while the current one's records and pulls are computed (one block per CU
-// holds the LDS of a half bin, so without this a CU's loads and its LDS work
-// take turns).
-template <uint32_t SL, bool OWN, bool PP = false, bool SH = false>
+template <uint32_t SL, bool OWN, bool SH = false>
 // (own quarter-bin regions: two blocks per CU, 48 KiB of LDS and
 // <= 64 VGPRs each; the second bound is waves per SIMD)
 __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sort_dlv(InListArgs a) {
-    static_assert(!PP || OWN, "the persistent walk reads own part regions");
     constexpr uint32_t kHalfLog = kBinLog - SL;  // (a "half": one of the 2^SL parts of a bin)
     constexpr uint32_t kHalf = 1u << kHalfLog;
     constexpr uint32_t kHalfCap = kBinCap >> SL;
@@ -850,14 +852,11 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
     // networks (one coarse bucket) write every pull straight to PULL (no
     // pass-back partition)
     constexpr bool own = OWN;
-    const bool direct = !PP && nc == 1u;
+    const bool direct = nc == 1u;
     uint32_t *pcfill = a.scratch + pcfill_off(p.nb);
     const PullArrays pa = pull_arrays(a.region, p.nb);
-    // part w = (bin b, half hh) = w >> SL, w & (2^SL - 1); PP: the parts
-    // holding nodes, blockIdx.x, + gridDim.x, ...
-    const uint32_t items = PP ? (p.n + kHalf - 1u) / kHalf : 0u;
-    uint32_t w = PP ? blockIdx.x : (blockIdx.x << SL) + blockIdx.y;
-    if (PP && w >= items) return;  // (uniform per block)
+    // part w = (bin b, half hh) = w >> SL, w & (2^SL - 1)
+    const uint32_t w = (blockIdx.x << SL) + blockIdx.y;
     uint32_t ex[kPer], ec[kPer], el[kPer];
     auto load_part = [&](uint32_t wp) {
         const uint32_t bp = wp >> SL, hp = wp & ((1u << SL) - 1u);
@@ -867,10 +866,19 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
         for (uint32_t q = 0; q < kPer; ++q) {
             const uint32_t i = threadIdx.x + q * kInlThreads;
             const bool ok = i < cnt;
-            const PEnt en = part_entries(a.region)[rb + (ok ? i : 0u)];
-            const uint32_t lt = ok ? en.c : kNone;
-            ex[q] = en.a;
-            ec[q] = en.b;
+            uint32_t lt;
+            if constexpr (SH) {
+                const PEnt en = part_entries(a.region)[rb + (ok ? i : 0u)];
+                lt = en.c;
+                ex[q] = en.a;
+                ec[q] = en.b;
+            } else {  // (source, push code): the target is the source's Philox draw again
+                const uint2 en = part_entries8(a.region)[rb + (ok ? i : 0u)];
+                ex[q] = en.x;
+                ec[q] = en.y;
+                lt = peer_of(a.seed, a.epoch, a.round, en.x, p.n) & (kBin - 1u);
+            }
+            if (!ok) lt = kNone;
             el[q] = (ok && (lt >> kHalfLog) == hp) ? (lt & (kHalf - 1u)) : kNone;
         }
     };
@@ -908,15 +916,10 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
             }
         }
     };
-    // (small parts only: at SL = 2 the registers they hold across the LDS
-    // sort spill under the two-blocks-per-CU bound)
-    constexpr bool kEarly = GS_DLV_EARLY_TARGETS && !PP && SL >= 3;
     load_part(w);
-    if (kEarly) load_targets(w);
-    for (;;) {
     const uint32_t t0 = w << kHalfLog;
     const uint32_t nodes = t0 < p.n ? min(kHalf, p.n - t0) : 0u;
-    if (nodes == 0) return;  // a half past the last node (uniform per block; not PP)
+    if (nodes == 0) return;  // a half past the last node (uniform per block)
     for (uint32_t i = threadIdx.x; i < kHalf / 2; i += kInlThreads) h[i] = 0u;
     if (threadIdx.x < kMaxCoarse) pcnt[threadIdx.x] = 0u;
     __syncthreads();
@@ -950,7 +953,7 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
         }
     }
     __syncthreads();
-    if (!kEarly) load_targets(w);
+    load_targets(w);
     uint32_t mine = 0;
     for (uint32_t lt = threadIdx.x; lt < nodes; lt += kInlThreads)
         mine += tail_len<kDlvInline>(min(half_of(h, lt), kHalfCap) - (lt ? min(half_of(h, lt - 1), kHalfCap) : 0u));
@@ -963,11 +966,6 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
     } else {
         cur = reserve_tails<kInlThreads>(a, mine, &a.scratch[p.nb], lds_scan);
     }
-    // PP: the next part's region loads, issued after every load and returning
-    // atomic this part still waits for (vmcnt counts in issue order), so
-    // they stay in flight through the record and pull work below
-    const uint32_t wnext = w + gridDim.x;
-    if (PP && wnext < items) load_part(wnext);
     const uint32_t m = (uint32_t)((1ull << a.g.rpad) - 1ull);
 #pragma unroll
     for (uint32_t q = 0; q < kHalfPer; ++q) {
@@ -1069,10 +1067,6 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
         const u64 o = ((u64)cb << kCoarseLog) + slot;
         pa.x[o] = x;
         pa.v[o] = scd[j];
-    }
-    if (!PP || wnext >= items) return;
-    w = wnext;
-    __syncthreads();  // every thread is done with this part's LDS (h, sid, scd, pcnt, pres)
     }
 }
 
@@ -1340,9 +1334,6 @@ CsrPlan dlv_plan(uint32_t n) {
     // dl_direct; dl_fine: at most two parts per bin)
     const uint32_t nc = n_coarse(p.nb);
     p.sub = dlv_split_log(p.nb);
-#ifdef GS_DLV_BIN_REGIONS  // (A/B: whole-bin regions, each sort block filters by part)
-    if (nc > 1u) p.sub = 0u;
-#endif
     if (nc > 1u && p.sub > kMaxFineSub) p.sub = 0u;  // (kFineParts)
     p.fill_off = p.sub ? dlv_head_words(p.nb) : 0u;  // after fill[nb], tailcnt, pull fills
     // own parts: a fixed tail region per part (dlv_part_tails), no shared counter
@@ -1439,11 +1430,8 @@ hipError_t launch_dlv_build(const InListArgs &a, hipStream_t s) {
     // (DlvRec::mf): whole-bin regions and a shared tail counter (A/B
     // variants) would need global tail indices
     if (!own || !GS_DLV_OWN_TAILS) return hipErrorInvalidValue;
-    const void *kd = dsl == kSplitLog
-                         ? (own ? (const void *)inl_sort_dlv<kSplitLog, true, false, SH>
-                                : (const void *)inl_sort_dlv<kSplitLog, false, false, SH>)
-                         : (own ? (const void *)inl_sort_dlv<kDlvSmallLog, true, false, SH>
-                                : (const void *)inl_sort_dlv<kDlvSmallLog, false, false, SH>);
+    const void *kd = dsl == kSplitLog ? (const void *)inl_sort_dlv<kSplitLog, true, SH>
+                                      : (const void *)inl_sort_dlv<kDlvSmallLog, true, SH>;
     hipError_t e = hipFuncSetAttribute(kd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dlv);
     if (e != hipSuccess) return e;
     if (a.lvm || a.zl) return hipErrorInvalidValue;  // DLV records gather nothing
@@ -1460,7 +1448,7 @@ hipError_t launch_dlv_build(const InListArgs &a, hipStream_t s) {
         e = hipFuncSetAttribute((const void *)dl_coarse<kCoarseThreads, SH>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds_c);
     if (e == hipSuccess)
-        e = hipFuncSetAttribute((const void *)dl_fine<kFineThreads>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        e = hipFuncSetAttribute((const void *)dl_fine<kFineThreads, SH>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds_f);
     if (e != hipSuccess) return e;
     const bool direct = nc == 1u;  // small n: one pass into the parts, pulls written directly
@@ -1474,25 +1462,11 @@ hipError_t launch_dlv_build(const InListArgs &a, hipStream_t s) {
         hipLaunchKernelGGL(dl_direct<SH>, dim3(p.ba), dim3(kInlThreads), lds_d, s, ab);
     } else {
         hipLaunchKernelGGL((dl_coarse<kCoarseThreads, SH>), dim3(p.ba), dim3(kCoarseThreads), lds_c, s, ab);
-        hipLaunchKernelGGL(dl_fine<kFineThreads>, dim3((kShardCap + kFineChunk - 1) / kFineChunk, nc * kCoarseShards),
+        hipLaunchKernelGGL((dl_fine<kFineThreads, SH>), dim3((kShardCap + kFineChunk - 1) / kFineChunk, nc * kCoarseShards),
                            dim3(kFineThreads), lds_f, s, ab);
     }
     void *kargs[] = {&ab};
-    if (GS_DLV_PP && own && !direct && !SH) {  // persistent walk over the parts (A/B)
-        const void *kp = dsl == kSplitLog ? (const void *)inl_sort_dlv<kSplitLog, true, true>
-                                          : (const void *)inl_sort_dlv<kDlvSmallLog, true, true>;
-        e = hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dlv);
-        int dev = 0, cus = 0, per_cu = 0;
-        if (e == hipSuccess) e = hipGetDevice(&dev);
-        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, kInlThreads, lds_dlv);
-        if (e != hipSuccess) return e;
-        const u64 items = ((u64)p.n + (kBin >> dsl) - 1) >> (kBinLog - dsl);
-        const uint32_t grid = (uint32_t)std::min<u64>(items, (u64)std::max(1, per_cu) * std::max(1, cus));
-        e = hipLaunchKernel(kp, dim3(grid), dim3(kInlThreads), kargs, lds_dlv, s);
-    } else {
-        e = hipLaunchKernel(kd, dim3(p.nb, 1u << dsl), dim3(kInlThreads), kargs, lds_dlv, s);
-    }
+    e = hipLaunchKernel(kd, dim3(p.nb, 1u << dsl), dim3(kInlThreads), kargs, lds_dlv, s);
     if (e != hipSuccess) return e;
     const size_t lds_pb = ((size_t)kPartChunk + kPartChunk / 2 + kPartChunk / 4) * sizeof(uint32_t);
     e = hipFuncSetAttribute((const void *)pb_fine, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_pb);

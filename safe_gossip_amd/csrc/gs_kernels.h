@@ -311,7 +311,6 @@ struct ShardPlan {
     // 0xFFFFFFFF), rw = 2; a B row is the pull code, rwb = 1; no id rows (the
     // receiver needs no in-lists ahead: its build sorts the arrived rows).
     uint32_t rw, rwb, codes;
-    CsrPlan edges;      // counting sort of the A receive slots over the m targets
 };
 constexpr uint32_t kRowMutual = 1u << 31;
 // Row slot of (rank block s, part h, index i) in an exchange-A / -B buffer.
@@ -368,7 +367,7 @@ struct ShardPlanLayout {
     size_t tg, SPOSA, SPOSB, bc_d, cnt;
 };
 struct ShardEdgeLayout {
-    size_t E_id, E_key, M, tot, base, EP, IN, IN2, pairs;
+    size_t cnt, inl, head, ovf, ovfn, EP, IN, IN2;
 };
 // codes: one u32 code per row (delivery-record shards; no row flags), and
 // parts of whole 1024-node blocks (the packed DLV round kernel's blocks)

@@ -31,10 +31,10 @@
 // sources only; a receiver recomputes the targets of the ids it receives.
 //   plan_count / plan_scan / plan_emit / plan_idle : targets, send slots
 //       (SPOSA in exchange A, SPOSB in exchange B) and the id blocks of round r
-//   edge_keys / edge_bin_* : counting sort of the received ids of round r by
-//       local target -> per-node in-lists of receive slots
-//       IN[z] = {first, k | zi << 16, e0, e1}, IN2[z] = e2, EP[]; zi = index of
-//       t(z) among z's pushers (the mutual pair) or 0xFFFF.
+//   edge_fill / edge_lists : the received ids of round r by local target ->
+//       per-node in-lists of receive slots IN[z] = {first, k | zi << 16, e0,
+//       e1}, IN2[z] = e2, EP[first + i] = pusher i >= 3; zi = index of t(z)
+//       among z's pushers (the mutual pair) or 0xFFFF.
 #include <algorithm>
 #include <cmath>
 
@@ -183,158 +183,120 @@ __global__ __launch_bounds__(256) void plan_idle(ShardPlan P, const uint32_t *__
 }
 
 // ------------------------------------------------ in-lists of receive slots
-// Receive slot e = (source rank s, part h, index i) of exchange A: its id, and
-// the local target of that source (recomputed from the Philox stream), or
-// kNoId for an empty slot (and for the id rows themselves).
-__global__ __launch_bounds__(256) void edge_keys(ShardPlan P, const u64 *__restrict__ recvA, uint64_t seed,
-                                                 uint32_t epoch, uint32_t round, Faults f, uint32_t *E_id,
-                                                 uint32_t *E_key, uint32_t *flags) {
-    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= shard_slotsA(P)) return;
-    const SlotPos q = shard_a_decode(P, e);
-    uint32_t id = kNoId, key = kNoId;
-    if (q.i < P.capP) {
-        id = id_slots(P, recvA, q.s)[q.h * P.capP + q.i];
-        if (id != kNoId) {
-            const uint32_t tw = target_word(seed, epoch, round, id, P.n, f);
-            const uint32_t t = tw & kTgMask;
-            if (id >= P.n || (tw & kTgDead) || t < P.lo || t - P.lo >= P.m) {
-                atomicOr(&flags[2], 1u);  // inconsistent exchange
-                id = kNoId;
-            } else {
-                key = t - P.lo;
-            }
+// The ids exchange A of round r-1 delivered (id slot j = (source rank s,
+// part h, index i) at id_slots(s)[h*capP + i]: j = (s*P + h)*capP + i is
+// also the slot key, ascending = ascending source id) become, per owned node
+// z, its pushers of round r in ascending order as receive slots of exchange A
+// of round r.  Two launches, both O(m) and coalesced but for one atomic per
+// edge on an L2-resident counter:
+//   edge_fill  : per id slot: the source's Philox target z (recomputed), its
+//                mutual bit (t(z) is the source: the receiver's pull copy
+//                supersedes that push copy, src/message_state.rs:79), and the
+//                key stored at z's next position -- four inline positions per
+//                node, the rare rest (in-degree > 4: 0.4 % of nodes) on a
+//                per-node list of overflow entries
+//   edge_lists : per node: its keys sorted (insertion sort, in-degree is
+//                Poisson(1)), the index of the mutual pusher, IN/IN2 and the
+//                tails of in-degree > 3 in the block's own tail region; the
+//                counters are left zeroed for the set's next build
+// (round 4 and before: a global counting sort through 6 launches, 0.20 ms
+// per 2^21-node shard against 0.04, DESIGN.md section 7 "Round 5").
+constexpr uint32_t kEdgeInline = 4;     // inline positions per node
+constexpr uint32_t kEdgeBlock = 256;    // edge_lists nodes per block
+constexpr uint32_t kEdgeTails = 96;     // tail slots per edge_lists block (mean ~6)
+constexpr uint32_t kMutual = 1u << 31;  // key bit: the pusher is the node's own target
+__host__ __device__ inline uint32_t edge_ovf_cap(uint32_t m) { return m / 16u + 256u; }
+
+__global__ __launch_bounds__(256) void edge_fill(ShardPlan P, const u64 *__restrict__ recvA,
+                                                 const uint32_t *__restrict__ tg, uint64_t seed, uint32_t epoch,
+                                                 uint32_t round, Faults f, uint32_t *cnt, uint32_t *inl,
+                                                 uint32_t *head, uint2 *ovf, uint32_t *ovfn, uint32_t *flags) {
+    const uint32_t per = P.P * P.capP;
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= P.G * per) return;
+    const uint32_t src = j / per;
+    const uint32_t id = id_slots(P, recvA, src)[j - src * per];
+    if (id == kNoId) return;
+    const uint32_t tw = target_word(seed, epoch, round, id, P.n, f);
+    const uint32_t t = tw & kTgMask;
+    if (id >= P.n || (tw & kTgDead) || t < P.lo || t - P.lo >= P.m) {
+        atomicOr(&flags[2], 1u);  // inconsistent exchange
+        return;
+    }
+    const uint32_t z = t - P.lo;
+    const uint32_t key = j | ((tg[z] & kTgMask) == id ? kMutual : 0u);
+    const uint32_t pos = atomicAdd(&cnt[z], 1u);
+    if (pos < kEdgeInline) {
+        inl[(u64)z * kEdgeInline + pos] = key;
+    } else {
+        const uint32_t o = atomicAdd(ovfn, 1u);
+        if (o < edge_ovf_cap(P.m)) ovf[o] = make_uint2(key, atomicExch(&head[z], o + 1u));  // (list: o + 1, 0 ends)
+        else atomicOr(&flags[2], 1u);
+    }
+}
+
+__global__ __launch_bounds__(kEdgeBlock) void edge_lists(ShardPlan P, uint32_t *cnt, const uint32_t *__restrict__ inl,
+                                                         uint32_t *head, const uint2 *__restrict__ ovf, uint32_t *ovfn,
+                                                         uint32_t *EP, uint4 *IN, uint32_t *IN2, uint32_t *flags) {
+    __shared__ uint32_t lds_scan[kEdgeBlock / 64];
+    const uint32_t z = blockIdx.x * kEdgeBlock + threadIdx.x;
+    const bool own = z < P.m;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *ovfn = 0u;  // (every edge_fill of this set has finished)
+    uint32_t c = 0;
+    uint4 q = make_uint4(0u, 0u, 0u, 0u);
+    if (own) {
+        c = cnt[z];
+        q = reinterpret_cast<const uint4 *>(inl)[z];
+    }
+    uint32_t k = c;
+    if (k > kMaxIn) {
+        // in-degree above the limit (probability ~1e-34 per node, or a
+        // corrupted exchange): a device limit, reported by gs_sync
+        atomicOr(&flags[2], 1u);
+        k = kMaxIn;
+    }
+    uint32_t ks[kMaxIn];
+    ks[0] = q.x;
+    ks[1] = q.y;
+    ks[2] = q.z;
+    ks[3] = q.w;
+    if (c > kEdgeInline) {  // (0.4 % of nodes) the overflow list, in any order
+        uint32_t o = head[z], i = kEdgeInline;
+        while (o && i < kMaxIn) {
+            const uint2 en = ovf[o - 1u];
+            ks[i++] = en.x;
+            o = en.y;
         }
+        head[z] = 0u;
     }
-    E_id[e] = id;
-    E_key[e] = key;
-}
-
-__global__ __launch_bounds__(256) void edge_bin_count(CsrPlan p, const uint32_t *__restrict__ E_key,
-                                                      uint32_t *M) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
-    for (uint32_t i = threadIdx.x; i < p.nb; i += blockDim.x) hist[i] = 0;
-    __syncthreads();
-    const u64 lo = (u64)blockIdx.x * p.chunk;
-    const u64 hi = min((u64)p.n, lo + p.chunk);
-    for (u64 e = lo + threadIdx.x; e < hi; e += blockDim.x) {
-        const uint32_t k = E_key[e];
-        if (k != kNoId) atomicAdd(&hist[k >> p.logbin], 1u);
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < p.nb; i += blockDim.x) M[(u64)blockIdx.x * p.nb + i] = hist[i];
-}
-
-// One block per bin b: exclusive scan of column b of M[ba][nb] (ba <= 256
-// chunks, one per thread), tot[b] = the bin's edge count.
-__global__ __launch_bounds__(256) void edge_col_scan(uint32_t *M, CsrPlan p, uint32_t *tot) {
-    __shared__ uint32_t lds[kScanBlock / 64];
-    const uint32_t b = blockIdx.x, c = threadIdx.x;
-    const uint32_t v = c < p.ba ? M[(u64)c * p.nb + b] : 0u;
-    uint32_t total;
-    const uint32_t ex = block_exclusive_scan(v, lds, total);
-    if (c < p.ba) M[(u64)c * p.nb + b] = ex;
-    if (c == 0) tot[b] = total;
-}
-
-__global__ __launch_bounds__(kScanBlock) void edge_scan_small(const uint32_t *in, uint32_t *out, uint32_t m) {
-    __shared__ uint32_t lds[kScanBlock / 64];
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < m; base += kScanBlock) {
-        const uint32_t i = base + threadIdx.x;
-        const uint32_t v = i < m ? in[i] : 0u;
-        uint32_t tot;
-        const uint32_t ex = block_exclusive_scan(v, lds, tot);
-        if (i < m) out[i] = carry + ex;
-        carry += tot;
-    }
-}
-
-// pairs = (target within the bin, source-order key of the slot)
-__global__ __launch_bounds__(256) void edge_bin_scatter(CsrPlan p, ShardPlan P, const uint32_t *__restrict__ E_key,
-                                                        const uint32_t *__restrict__ M,
-                                                        const uint32_t *__restrict__ base, u64 *pairs) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
-    for (uint32_t i = threadIdx.x; i < p.nb; i += blockDim.x)
-        cur[i] = base[i] + M[(u64)blockIdx.x * p.nb + i];
-    __syncthreads();
-    const u64 lo = (u64)blockIdx.x * p.chunk;
-    const u64 hi = min((u64)p.n, lo + p.chunk);
-    const uint32_t lm = p.bin - 1u;
-    for (u64 e = lo + threadIdx.x; e < hi; e += blockDim.x) {
-        const uint32_t t = E_key[e];
-        if (t == kNoId) continue;
-        const uint32_t pos = atomicAdd(&cur[t >> p.logbin], 1u);
-        pairs[pos] = ((u64)(t & lm) << 32) | shard_slot_key(P, shard_a_decode(P, (uint32_t)e));
-    }
-}
-
-// One block per bin of local targets: counting sort by target, then each
-// node's pushers in ascending source order (by slot key), stored as receive
-// slots.
-__global__ __launch_bounds__(256) void edge_bin_sort(const u64 *__restrict__ pairs, CsrPlan p, ShardPlan P,
-                                                     uint32_t nodes_total,
-                                                     const uint32_t *__restrict__ base,
-                                                     const uint32_t *__restrict__ tot, uint32_t *EP,
-                                                     uint4 *IN, uint32_t *IN2,
-                                                     const uint32_t *__restrict__ E_id,
-                                                     const uint32_t *__restrict__ tg, uint32_t *flags) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t h[];
-    uint32_t *lds_scan = h + p.bin;
-    const uint32_t b = blockIdx.x;
-    const uint32_t start = base[b], cnt = tot[b];
-    const uint32_t nb0 = b << p.logbin;
-    const uint32_t nodes = min(p.bin, nodes_total - nb0);
-    for (uint32_t i = threadIdx.x; i < p.bin; i += blockDim.x) h[i] = 0;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) atomicAdd(&h[pairs[start + i] >> 32], 1u);
-    __syncthreads();
-    const uint32_t per = p.bin / blockDim.x;
-    const uint32_t i0 = threadIdx.x * per;
-    uint32_t sum = 0;
-    for (uint32_t q = 0; q < per; ++q) sum += h[i0 + q];
-    uint32_t total;
-    uint32_t run = block_exclusive_scan(sum, lds_scan, total);
-    for (uint32_t q = 0; q < per; ++q) {
-        const uint32_t v = h[i0 + q];
-        h[i0 + q] = run;
-        run += v;
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-        const u64 pr = pairs[start + i];
-        const uint32_t pos = atomicAdd(&h[(uint32_t)(pr >> 32)], 1u);
-        EP[start + pos] = (uint32_t)pr;
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nodes; i += blockDim.x) {
-        const uint32_t a = start + (i ? h[i - 1] : 0u);
-        uint32_t e = start + h[i];
-        if (e - a > kMaxIn) {
-            // in-degree above the limit (probability ~1e-34 per node, or a
-            // corrupted exchange): a device limit, reported by gs_sync; the
-            // list is cut so that the insertion sort stays O(kMaxIn^2)
-            atomicOr(&flags[2], 1u);
-            e = a + kMaxIn;
+    if (own) cnt[z] = 0u;
+    for (uint32_t i = 1; i < k; ++i) {  // ascending key = ascending source id
+        const uint32_t v = ks[i];
+        uint32_t r = i;
+        while (r > 0 && (ks[r - 1] & ~kMutual) > (v & ~kMutual)) {
+            ks[r] = ks[r - 1];
+            --r;
         }
-        for (uint32_t q = a + 1; q < e; ++q) {  // slot keys ascending = pushers ascending
-            const uint32_t v = EP[q];
-            uint32_t r = q;
-            while (r > a && EP[r - 1] > v) {
-                EP[r] = EP[r - 1];
-                --r;
-            }
-            EP[r] = v;
-        }
-        for (uint32_t q = a; q < e; ++q) EP[q] = shard_key_slot(P, EP[q]);
-        const uint32_t k = e - a;
-        const uint32_t tz = tg[nb0 + i] & kTgMask;  // t(z): did it push to z?
-        uint32_t zi = 0xFFFFu;
-        for (uint32_t q = a; q < e; ++q)
-            if (E_id[EP[q]] == tz) zi = q - a;
-        IN[nb0 + i] = make_uint4(a, k | (zi << 16), k > 0 ? EP[a] : 0u, k > 1 ? EP[a + 1] : 0u);
-        IN2[nb0 + i] = k > 2 ? EP[a + 2] : 0u;
+        ks[r] = v;
     }
+    uint32_t zi = 0xFFFFu;
+    for (uint32_t i = 0; i < k; ++i)
+        if (ks[i] & kMutual) zi = i;
+    const uint32_t nt = k > 3u ? k - 3u : 0u;
+    uint32_t tot;
+    const uint32_t toff = block_exclusive_scan(nt, lds_scan, tot);
+    uint32_t first = blockIdx.x * kEdgeTails + toff;
+    if (tot > kEdgeTails) {
+        if (threadIdx.x == 0) atomicOr(&flags[2], 1u);
+        first = 0u;  // (reported; the tails are not stored)
+    } else {
+        for (uint32_t i = 3; i < k; ++i) EP[first + i - 3u] = shard_key_slot(P, ks[i] & ~kMutual);
+    }
+    if (!own) return;
+    // pushers i >= 3 at EP[in.x + i] (u32 arithmetic: in.x = first - 3)
+    IN[z] = make_uint4(first - 3u, k | (zi << 16), k > 0 ? shard_key_slot(P, ks[0] & ~kMutual) : 0u,
+                       k > 1 ? shard_key_slot(P, ks[1] & ~kMutual) : 0u);
+    IN2[z] = k > 2 ? shard_key_slot(P, ks[2] & ~kMutual) : 0u;
 }
 
 ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t parts, bool codes) {
@@ -372,18 +334,6 @@ ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t pa
     const u64 q = std::max<u64>(64, P.rw);  // P*capP u32 ids fill whole rows of rw u32 words
     P.capP = (uint32_t)(((u64)std::ceil(capd) + q - 1) / q * q);
     P.idrows = codes ? 0u : P.P * P.capP / P.rw;  // (code rows carry their targets: no ids)
-    // counting sort of the receive slots of A over the m local targets
-    CsrPlan &c = P.edges;
-    c.n = std::max<uint32_t>(shard_slotsA(P), 1);
-    uint32_t bin = 4096;
-    while ((u64)bin * 16384u < P.m) bin <<= 1;
-    c.bin = bin;
-    c.logbin = 0;
-    while ((1u << c.logbin) < bin) ++c.logbin;
-    c.nb = std::max<uint32_t>(1, (uint32_t)(((u64)P.m + bin - 1) / bin));
-    const uint32_t ba = (uint32_t)(((u64)c.n + 4095) / 4096);
-    c.ba = ba < 256u ? (ba ? ba : 1u) : 256u;
-    c.chunk = (uint32_t)(((u64)c.n + c.ba - 1) / c.ba);
     return P;
 }
 
@@ -409,16 +359,18 @@ size_t shard_edge_words(const ShardPlan &P, ShardEdgeLayout *L) {
         off += (words + 3) / 4 * 4;
         return o;
     };
-    const size_t slots = shard_slotsA(P);
-    L->E_id = take(slots);
-    L->E_key = take(slots);
-    L->M = take((size_t)P.edges.ba * P.edges.nb);
-    L->tot = take(P.edges.nb);
-    L->base = take(P.edges.nb);
-    L->EP = take(slots);
+    const size_t nb = ((size_t)P.m + kEdgeBlock - 1) / kEdgeBlock;
+    // counters, inline keys, list heads, overflow entries and their count are
+    // zero between builds (edge_lists leaves them so; the engine clears the
+    // set once at creation)
+    L->cnt = take(P.m);
+    L->inl = take((size_t)kEdgeInline * P.m);
+    L->head = take(P.m);
+    L->ovf = take(2 * (size_t)edge_ovf_cap(P.m));
+    L->ovfn = take(1);
+    L->EP = take(nb * kEdgeTails);
     L->IN = take(4 * (size_t)P.m);
     L->IN2 = take(P.m);
-    L->pairs = take(2 * slots);
     return off;
 }
 
@@ -444,27 +396,13 @@ hipError_t launch_shard_edges(const ShardPlan &P, const ShardEdgeLayout &L, uint
                               const uint32_t *tg, uint64_t seed, uint32_t epoch, uint32_t round,
                               const Faults &f, uint32_t *flags, hipStream_t s) {
     if (P.m == 0) return hipSuccess;  // no local targets: nothing is received
-    uint32_t *E_id = w + L.E_id, *E_key = w + L.E_key, *M = w + L.M, *tot = w + L.tot;
-    uint32_t *base = w + L.base, *EP = w + L.EP, *IN2 = w + L.IN2;
-    uint4 *IN = reinterpret_cast<uint4 *>(w + L.IN);
-    u64 *pairs = reinterpret_cast<u64 *>(w + L.pairs);
-    const CsrPlan &c = P.edges;
-    hipLaunchKernelGGL(edge_keys, dim3((shard_slotsA(P) + 255) / 256), dim3(256), 0, s, P, recvA, seed, epoch,
-                       round, f, E_id, E_key, flags);
-    const size_t lds_nb = (size_t)c.nb * sizeof(uint32_t);
-    hipLaunchKernelGGL(edge_bin_count, dim3(c.ba), dim3(256), lds_nb, s, c, E_key, M);
-    static_assert(kScanBlock == 256, "edge_col_scan: one thread per chunk (ba <= 256)");
-    hipLaunchKernelGGL(edge_col_scan, dim3(c.nb), dim3(256), 0, s, M, c, tot);
-    hipLaunchKernelGGL(edge_scan_small, dim3(1), dim3(kScanBlock), 0, s, tot, base, c.nb);
-    hipLaunchKernelGGL(edge_bin_scatter, dim3(c.ba), dim3(256), lds_nb, s, c, P, E_key, M, base, pairs);
-    const size_t lds_sort = ((size_t)c.bin + 16) * sizeof(uint32_t);
-    if (lds_sort > 65536) {
-        hipError_t e = hipFuncSetAttribute((const void *)edge_bin_sort,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sort);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(edge_bin_sort, dim3(c.nb), dim3(256), lds_sort, s, pairs, c, P, P.m, base, tot, EP, IN,
-                       IN2, E_id, tg, flags);
+    const uint32_t slots = P.G * P.P * P.capP;
+    uint2 *ovf = reinterpret_cast<uint2 *>(w + L.ovf);
+    hipLaunchKernelGGL(edge_fill, dim3((slots + 255u) / 256u), dim3(256), 0, s, P, recvA, tg, seed, epoch, round, f,
+                       w + L.cnt, w + L.inl, w + L.head, ovf, w + L.ovfn, flags);
+    hipLaunchKernelGGL(edge_lists, dim3((P.m + kEdgeBlock - 1) / kEdgeBlock), dim3(kEdgeBlock), 0, s, P, w + L.cnt,
+                       w + L.inl, w + L.head, ovf, w + L.ovfn, w + L.EP, reinterpret_cast<uint4 *>(w + L.IN),
+                       w + L.IN2, flags);
     return hipGetLastError();
 }
 

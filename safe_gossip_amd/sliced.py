@@ -60,10 +60,10 @@ def merge_known(per, bounds, n: int, kw: int) -> np.ndarray:
 class _Slice:
     """One rank's engine (rumors [lo, hi)) and its empty-count buffers."""
 
-    def __init__(self, torch, n, lo, hi, seed, epoch, params, device, faults):
+    def __init__(self, torch, n, lo, hi, seed, epoch, params, device, faults, schedule="2P"):
         self.lo, self.hi = lo, hi
         self.net = Network(n, hi - lo, seed=seed, epoch=epoch, params=params, device=device,
-                           churn=faults[0], drop_push=faults[1], drop_pull=faults[2],
+                           churn=faults[0], drop_push=faults[1], drop_pull=faults[2], schedule=schedule,
                            _rumor_slice=True)
         self.lib, self.h = self.net._lib, self.net._h
         dev = torch.device("cuda", device)
@@ -86,13 +86,15 @@ class SlicedNetwork:
     ``dump_state``, ``dump_records``, ``clear`` and the measurement hooks.
     With ``transport="dist"`` every rank makes the same calls (``send_new`` is
     ignored by ranks that do not hold the rumor) and observers return the whole
-    network on every rank.  2P schedule only (``gs_create`` refuses SEQ
-    slices), no external RPCs.
+    network on every rank.  Both schedules (2P and SEQ: the empty counts are
+    the MIN over the slices under either, tests/test_sliced_gloo.py), no
+    external RPCs.
     """
 
     def __init__(self, n_nodes: int, n_rumors: int, world: int, seed: int = 0x5AFE6055,
                  epoch: int = 0, params=None, device: int = 0, transport: str = "local",
-                 group=None, churn: float = 0.0, drop_push: float = 0.0, drop_pull: float = 0.0):
+                 group=None, churn: float = 0.0, drop_push: float = 0.0, drop_pull: float = 0.0,
+                 schedule: str = "2P"):
         import torch
         if world < 1 or n_rumors < world:
             raise ValueError(f"{n_rumors} rumors cannot be sliced over {world} ranks")
@@ -114,8 +116,9 @@ class SlicedNetwork:
         else:
             raise ValueError(transport)
         self.rank = ranks[0]
+        self.schedule = schedule
         self.slices = [_Slice(torch, n_nodes, self.bounds[g], self.bounds[g + 1], seed, epoch, params,
-                              device, faults) for g in ranks]
+                              device, faults, schedule) for g in ranks]
         self.faults = self.slices[0].net.faults
         self.round = 0
         self._pend = []  # (async work, buffer) of all-reduces not applied yet (RCCL)

@@ -69,6 +69,22 @@ def test_sliced_larger(engine, world, R):
     run_parity(engine, 20000, R, "origins", check_every=4, make_net=_maker(world))
 
 
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("n,R,kind,faults", [
+    (8, 4, "example", None),
+    (300, 16, "origins", None),
+    (777, 20, "reinject", (0.05, 0.05, 0.05)),   # ragged slices, faults
+    (130, 256, "origins", None),                 # wide slices (R_g >= 64)
+    (1500, 32, "trickle", (0.1, 0.1, 0.1)),
+])
+def test_sliced_parity_seq(engine, world, n, R, kind, faults):
+    # the SEQ schedule (the harness's literal order, src/gossiper.rs:217-234)
+    # on rumor slices: each slice runs the SEQ kernels over its rumors, the
+    # empty counts are the MIN over the slices (pinned on CPU by
+    # tests/test_sliced_gloo.py::test_sliced_protocol_gloo_seq)
+    run_parity(engine, n, R, kind, make_net=_maker(world), faults=faults, schedule="SEQ")
+
+
 @pytest.mark.parametrize("pack", ["0", "u64", "u32x1", "default"])
 def test_sliced_delivery_records(engine, monkeypatch, pack):
     # slices of R_g <= 16 run the delivery-record kernels (gs_dlv4.hip, and the
@@ -109,8 +125,6 @@ def test_sliced_clear_and_counts(engine):
 
 def test_slice_engine_refusals(engine):
     import safe_gossip_amd as sg
-    with pytest.raises(sg.GossipError):
-        sg.Network(100, 8, schedule="SEQ", _rumor_slice=True)
     from safe_gossip_amd.sliced import SlicedNetwork
     with pytest.raises(ValueError):
         SlicedNetwork(100, 2, 3, transport="local")  # fewer rumors than slices

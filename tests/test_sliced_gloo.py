@@ -8,7 +8,12 @@ peer schedule and faults), reduces each round's empty-RPC counts with
 gathered per-node state, records, |P|, Statistics and known sets against ONE
 oracle over all R rumors, every round (bit-exact).  This pins the two facts
 the sliced engine rests on: rumors evolve independently, and the network's
-empty push / empty pull counts are the MIN over the slices.
+empty push / empty pull counts are the MIN over the slices.  Both hold under
+the SEQ schedule too (the harness's literal order, src/gossiper.rs:217-234):
+which pushes a node answers, and when, depends on the peer schedule only, and
+"has a live entry" only ever turns on within a round, so a node's empty pulls
+are a nondecreasing function of the first time it is live -- the MIN over the
+slices again.
 """
 import os
 import socket
@@ -30,13 +35,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, R, params, kind, q, faults=None):
+def _worker(rank, world, port, n, R, params, kind, q, faults=None, sched="2P"):
     sys.path.insert(0, HERE)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import oracle_lib
-        from oracle_lib import SCHED_2P, OracleNet
+        from oracle_lib import SCHED_2P, SCHED_SEQ, OracleNet
+        S = SCHED_SEQ if sched == "SEQ" else SCHED_2P
         L = oracle_lib.lib()
         thr = [oracle_lib.fault_threshold(p) for p in faults] if faults else None
         lo, hi = rank * R // world, (rank + 1) * R // world
@@ -56,7 +62,7 @@ def _worker(rank, world, port, n, R, params, kind, q, faults=None):
                     sl.send_new(x, r - lo)
                 if orc:
                     orc.send_new(x, r)
-            _, slive = sl.next_round(SCHED_2P)
+            _, slive = sl.next_round(S)
             live = torch.tensor([int(slive)])
             dist.all_reduce(live, op=dist.ReduceOp.MAX)
             st = sl.statistics().astype(np.int64)
@@ -71,7 +77,7 @@ def _worker(rank, world, port, n, R, params, kind, q, faults=None):
             parts = [None] * world
             dist.all_gather_object(parts, part)
             if orc:
-                _, olive = orc.next_round(SCHED_2P)
+                _, olive = orc.next_round(S)
                 assert bool(live.item()) == olive, f"round {rnd}: any_live"
                 np.testing.assert_array_equal(np.concatenate([p[0] for p in parts], axis=1),
                                               orc.dump_state(), err_msg=f"state round {rnd}")
@@ -110,10 +116,26 @@ def _worker(rank, world, port, n, R, params, kind, q, faults=None):
     (2, 300, 2, (1, 1, 4), "reinject", None),      # one rumor per slice, cmax 1
 ])
 def test_sliced_protocol_gloo(oracle, world, n, R, params, kind, faults):
+    _run_world(world, n, R, params, kind, faults, "2P")
+
+
+@pytest.mark.parametrize("world,n,R,params,kind,faults", [
+    (2, 600, 16, None, "origins", None),
+    (3, 500, 7, None, "reinject", None),             # ragged slices 2/2/3
+    (3, 600, 8, None, "reinject", (0.2, 0.1, 0.1)),  # faults
+    (2, 300, 2, (1, 1, 4), "reinject", None),        # one rumor per slice, cmax 1
+])
+def test_sliced_protocol_gloo_seq(oracle, world, n, R, params, kind, faults):
+    # the SEQ schedule sliced: pull chains hop within a round, and the MIN of
+    # the slices' empty counts is still the network's
+    _run_world(world, n, R, params, kind, faults, "SEQ")
+
+
+def _run_world(world, n, R, params, kind, faults, sched):
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, R, params, kind, q, faults))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, R, params, kind, q, faults, sched))
              for r in range(world)]
     for p in procs:
         p.start()
