@@ -367,7 +367,7 @@ struct ShardPlanLayout {
     size_t tg, SPOSA, SPOSB, bc_d, cnt;
 };
 struct ShardEdgeLayout {
-    size_t cnt, inl, head, ovf, ovfn, EP, IN, IN2;
+    size_t fill, region, EP, IN, IN2;
 };
 // codes: one u32 code per row (delivery-record shards; no row flags), and
 // parts of whole 1024-node blocks (the packed DLV round kernel's blocks)

@@ -31,7 +31,7 @@
 // sources only; a receiver recomputes the targets of the ids it receives.
 //   plan_count / plan_scan / plan_emit / plan_idle : targets, send slots
 //       (SPOSA in exchange A, SPOSB in exchange B) and the id blocks of round r
-//   edge_fill / edge_lists : the received ids of round r by local target ->
+//   edge_bin / edge_sort : the received ids of round r by local target ->
 //       per-node in-lists of receive slots IN[z] = {first, k | zi << 16, e0,
 //       e1}, IN2[z] = e2, EP[first + i] = pusher i >= 3; zi = index of t(z)
 //       among z's pushers (the mutual pair) or 0xFFFF.
@@ -187,116 +187,200 @@ __global__ __launch_bounds__(256) void plan_idle(ShardPlan P, const uint32_t *__
 // part h, index i) at id_slots(s)[h*capP + i]: j = (s*P + h)*capP + i is
 // also the slot key, ascending = ascending source id) become, per owned node
 // z, its pushers of round r in ascending order as receive slots of exchange A
-// of round r.  Two launches, both O(m) and coalesced but for one atomic per
-// edge on an L2-resident counter:
-//   edge_fill  : per id slot: the source's Philox target z (recomputed), its
-//                mutual bit (t(z) is the source: the receiver's pull copy
-//                supersedes that push copy, src/message_state.rs:79), and the
-//                key stored at z's next position -- four inline positions per
-//                node, the rare rest (in-degree > 4: 0.4 % of nodes) on a
-//                per-node list of overflow entries
-//   edge_lists : per node: its keys sorted (insertion sort, in-degree is
-//                Poisson(1)), the index of the mutual pusher, IN/IN2 and the
-//                tails of in-degree > 3 in the block's own tail region; the
-//                counters are left zeroed for the set's next build
-// (round 4 and before: a global counting sort through 6 launches, 0.20 ms
-// per 2^21-node shard against 0.04, DESIGN.md section 7 "Round 5").
-constexpr uint32_t kEdgeInline = 4;     // inline positions per node
-constexpr uint32_t kEdgeBlock = 256;    // edge_lists nodes per block
-constexpr uint32_t kEdgeTails = 96;     // tail slots per edge_lists block (mean ~6)
-constexpr uint32_t kMutual = 1u << 31;  // key bit: the pusher is the node's own target
-__host__ __device__ inline uint32_t edge_ovf_cap(uint32_t m) { return m / 16u + 256u; }
+// of round r.  Two launches; no global atomic per edge (one per (chunk, bin)
+// run), no global prefix sum:
+//   edge_bin  : per chunk of kEdgeChunk id slots: the source's Philox target z
+//               (recomputed) and its mutual bit (t(z) is the source: the
+//               receiver's pull copy supersedes that push copy,
+//               src/message_state.rs:79), an LDS counting sort by bin of
+//               kEdgeBin targets, one reservation per non-empty bin in that
+//               bin's fixed-capacity region, coalesced runs of (key | mutual,
+//               z in the bin) entries
+//   edge_sort : per bin: an LDS counting sort by target, per target an
+//               insertion sort of its keys (in-degree is Poisson(1)), the
+//               mutual pusher's index, IN/IN2 (lanes take consecutive
+//               targets: coalesced) and the tails of in-degree > 3 in the
+//               bin's own tail region; the fill count is left zeroed
+// (round 4 and before: a global counting sort through 6 launches, 0.18 ms
+// per 2^21-node shard against 0.074; a per-node fill by one returning global
+// atomic per edge measured 0.18 too; DESIGN.md section 7 "Round 5").
+constexpr uint32_t kEdgeBinLog = 11;
+constexpr uint32_t kEdgeBin = 1u << kEdgeBinLog;           // targets per bin
+constexpr uint32_t kEdgeBinCap = kEdgeBin + kEdgeBin / 4;  // region entries per bin (mean kEdgeBin, sd 45)
+constexpr uint32_t kEdgeChunk = 4096;                      // id slots per edge_bin block
+constexpr uint32_t kEdgeBinThreads = 1024;
+constexpr uint32_t kEdgeSortThreads = 256;
+constexpr uint32_t kEdgeTails = kEdgeBin / 8;              // tail slots per bin (mean ~48)
+constexpr uint32_t kMutual = 1u << 31;                     // key bit: the pusher is the node's own target
+static_assert(kEdgeChunk % kEdgeBinThreads == 0, "edge_bin: whole slots per thread");
 
-__global__ __launch_bounds__(256) void edge_fill(ShardPlan P, const u64 *__restrict__ recvA,
-                                                 const uint32_t *__restrict__ tg, uint64_t seed, uint32_t epoch,
-                                                 uint32_t round, Faults f, uint32_t *cnt, uint32_t *inl,
-                                                 uint32_t *head, uint2 *ovf, uint32_t *ovfn, uint32_t *flags) {
-    const uint32_t per = P.P * P.capP;
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= P.G * per) return;
-    const uint32_t src = j / per;
-    const uint32_t id = id_slots(P, recvA, src)[j - src * per];
-    if (id == kNoId) return;
-    const uint32_t tw = target_word(seed, epoch, round, id, P.n, f);
-    const uint32_t t = tw & kTgMask;
-    if (id >= P.n || (tw & kTgDead) || t < P.lo || t - P.lo >= P.m) {
-        atomicOr(&flags[2], 1u);  // inconsistent exchange
-        return;
+__global__ __launch_bounds__(kEdgeBinThreads) void edge_bin(ShardPlan P, const u64 *__restrict__ recvA,
+                                                            const uint32_t *__restrict__ tg, uint64_t seed,
+                                                            uint32_t epoch, uint32_t round, Faults f, uint32_t nb,
+                                                            uint32_t *fill, uint2 *region, uint32_t *flags) {
+    constexpr uint32_t kPer = kEdgeChunk / kEdgeBinThreads;
+    extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
+    uint32_t *skey = sh;                                           // [kEdgeChunk] keys by bin
+    uint16_t *sz = reinterpret_cast<uint16_t *>(sh + kEdgeChunk);  // [kEdgeChunk] z in the bin
+    uint16_t *sb = sz + kEdgeChunk;                                // [kEdgeChunk] bin of each staged entry
+    uint32_t *cnt = sh + 2 * kEdgeChunk;                           // [nb] counts, then cursors
+    uint32_t *off = cnt + nb;                                      // [nb] chunk-local starts
+    uint32_t *res = off + nb;                                      // [nb] reserved start in the bin's region
+    __shared__ uint32_t lds_scan[kEdgeBinThreads / 64];
+    for (uint32_t i = threadIdx.x; i < nb; i += kEdgeBinThreads) cnt[i] = 0u;
+    __syncthreads();
+    const uint32_t per = P.P * P.capP, slots = P.G * per;
+    uint32_t kv[kPer], zv[kPer];
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; ++q) {
+        const uint32_t j = blockIdx.x * kEdgeChunk + q * kEdgeBinThreads + threadIdx.x;
+        zv[q] = kNoId;
+        kv[q] = j;
+        if (j >= slots) continue;
+        const uint32_t src = j / per;
+        const uint32_t id = id_slots(P, recvA, src)[j - src * per];
+        if (id == kNoId) continue;
+        const uint32_t tw = target_word(seed, epoch, round, id, P.n, f);
+        const uint32_t t = tw & kTgMask;
+        if (id >= P.n || (tw & kTgDead) || t < P.lo || t - P.lo >= P.m) {
+            atomicOr(&flags[2], 1u);  // inconsistent exchange
+            continue;
+        }
+        zv[q] = t - P.lo;
+        if ((tg[zv[q]] & kTgMask) == id) kv[q] |= kMutual;
+        atomicAdd(&cnt[zv[q] >> kEdgeBinLog], 1u);
     }
-    const uint32_t z = t - P.lo;
-    const uint32_t key = j | ((tg[z] & kTgMask) == id ? kMutual : 0u);
-    const uint32_t pos = atomicAdd(&cnt[z], 1u);
-    if (pos < kEdgeInline) {
-        inl[(u64)z * kEdgeInline + pos] = key;
-    } else {
-        const uint32_t o = atomicAdd(ovfn, 1u);
-        if (o < edge_ovf_cap(P.m)) ovf[o] = make_uint2(key, atomicExch(&head[z], o + 1u));  // (list: o + 1, 0 ends)
-        else atomicOr(&flags[2], 1u);
+    __syncthreads();
+    const uint32_t bper = (nb + kEdgeBinThreads - 1) / kEdgeBinThreads, b0 = threadIdx.x * bper;
+    uint32_t sum = 0;
+    for (uint32_t q = 0; q < bper; ++q)
+        if (b0 + q < nb) sum += cnt[b0 + q];
+    uint32_t total;
+    uint32_t run = block_exclusive_scan_t<kEdgeBinThreads>(sum, lds_scan, total);
+    for (uint32_t q = 0; q < bper && b0 + q < nb; ++q) {
+        const uint32_t b = b0 + q, c = cnt[b];
+        off[b] = run;
+        uint32_t r0 = 0;
+        if (c) {
+            r0 = atomicAdd(&fill[b], c);
+            if (r0 + c > kEdgeBinCap) {
+                atomicOr(&flags[2], 1u);
+                r0 = kEdgeBinCap;  // drop this run; the round reports the limit
+            }
+        }
+        res[b] = r0;
+        cnt[b] = run;  // cursor
+        run += c;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; ++q) {
+        if (zv[q] == kNoId) continue;
+        const uint32_t b = zv[q] >> kEdgeBinLog;
+        const uint32_t pos = atomicAdd(&cnt[b], 1u);
+        skey[pos] = kv[q];
+        sz[pos] = (uint16_t)(zv[q] & (kEdgeBin - 1u));
+        sb[pos] = (uint16_t)b;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < total; i += kEdgeBinThreads) {
+        const uint32_t b = sb[i], slot = res[b] + (i - off[b]);
+        if (slot < kEdgeBinCap) region[(u64)b * kEdgeBinCap + slot] = make_uint2(skey[i], sz[i]);
     }
 }
 
-__global__ __launch_bounds__(kEdgeBlock) void edge_lists(ShardPlan P, uint32_t *cnt, const uint32_t *__restrict__ inl,
-                                                         uint32_t *head, const uint2 *__restrict__ ovf, uint32_t *ovfn,
-                                                         uint32_t *EP, uint4 *IN, uint32_t *IN2, uint32_t *flags) {
-    __shared__ uint32_t lds_scan[kEdgeBlock / 64];
-    const uint32_t z = blockIdx.x * kEdgeBlock + threadIdx.x;
-    const bool own = z < P.m;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *ovfn = 0u;  // (every edge_fill of this set has finished)
-    uint32_t c = 0;
-    uint4 q = make_uint4(0u, 0u, 0u, 0u);
-    if (own) {
-        c = cnt[z];
-        q = reinterpret_cast<const uint4 *>(inl)[z];
+__global__ __launch_bounds__(kEdgeSortThreads) void edge_sort(ShardPlan P, uint32_t *fill,
+                                                              const uint2 *__restrict__ region, uint32_t *EP,
+                                                              uint4 *IN, uint32_t *IN2, uint32_t *flags) {
+    constexpr uint32_t kPer = (kEdgeBinCap + kEdgeSortThreads - 1) / kEdgeSortThreads;
+    constexpr uint32_t kTper = kEdgeBin / kEdgeSortThreads;  // targets per thread (scan)
+    __shared__ uint32_t h[kEdgeBin];                           // per-target counts -> ends
+    __shared__ uint32_t sorted[kEdgeBinCap];
+    __shared__ uint32_t lds_scan[kEdgeSortThreads / 64];
+    const uint32_t b = blockIdx.x;
+    const uint32_t z0 = b << kEdgeBinLog;
+    const uint32_t nodes = min(kEdgeBin, P.m - z0);
+    const uint32_t cnt = min(fill[b], kEdgeBinCap);
+    uint32_t ek[kPer], ez[kPer];
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; ++q) {
+        const uint32_t i = threadIdx.x + q * kEdgeSortThreads;
+        const uint2 en = i < cnt ? region[(u64)b * kEdgeBinCap + i] : make_uint2(0u, kNoId);
+        ek[q] = en.x;
+        ez[q] = en.y;
     }
-    uint32_t k = c;
-    if (k > kMaxIn) {
-        // in-degree above the limit (probability ~1e-34 per node, or a
-        // corrupted exchange): a device limit, reported by gs_sync
-        atomicOr(&flags[2], 1u);
-        k = kMaxIn;
+    for (uint32_t i = threadIdx.x; i < kEdgeBin; i += kEdgeSortThreads) h[i] = 0u;
+    __syncthreads();
+    if (threadIdx.x == 0) fill[b] = 0u;  // (read above by every thread; ready for the set's next build)
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; ++q)
+        if (ez[q] != kNoId) atomicAdd(&h[ez[q]], 1u);
+    __syncthreads();
+    const uint32_t i0 = threadIdx.x * kTper;
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kTper; ++q) sum += h[i0 + q];
+    uint32_t total;
+    uint32_t run = block_exclusive_scan_t<kEdgeSortThreads>(sum, lds_scan, total);
+#pragma unroll
+    for (uint32_t q = 0; q < kTper; ++q) {
+        const uint32_t c = h[i0 + q];
+        h[i0 + q] = run;  // start, then (after the scatter) end
+        run += c;
     }
-    uint32_t ks[kMaxIn];
-    ks[0] = q.x;
-    ks[1] = q.y;
-    ks[2] = q.z;
-    ks[3] = q.w;
-    if (c > kEdgeInline) {  // (0.4 % of nodes) the overflow list, in any order
-        uint32_t o = head[z], i = kEdgeInline;
-        while (o && i < kMaxIn) {
-            const uint2 en = ovf[o - 1u];
-            ks[i++] = en.x;
-            o = en.y;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; ++q)
+        if (ez[q] != kNoId) sorted[atomicAdd(&h[ez[q]], 1u)] = ek[q];
+    __syncthreads();
+    // the records: lanes take consecutive targets (coalesced IN / IN2 stores);
+    // tails (pushers >= 3) go to the bin's own region, in any order
+    uint32_t mine = 0;
+    for (uint32_t lt = threadIdx.x; lt < nodes; lt += kEdgeSortThreads) {
+        const uint32_t k = min(h[lt] - (lt ? h[lt - 1] : 0u), kMaxIn);
+        mine += k > 3u ? k - 3u : 0u;
+    }
+    uint32_t ttot;
+    const uint32_t toff = block_exclusive_scan_t<kEdgeSortThreads>(mine, lds_scan, ttot);
+    const bool tails_ok = ttot <= kEdgeTails;
+    if (!tails_ok && threadIdx.x == 0) atomicOr(&flags[2], 1u);
+    uint32_t cur = b * kEdgeTails + toff;
+    for (uint32_t lt = threadIdx.x; lt < nodes; lt += kEdgeSortThreads) {
+        const uint32_t s = lt ? h[lt - 1] : 0u;
+        uint32_t k = h[lt] - s;
+        if (k > kMaxIn) {
+            // in-degree above the limit (probability ~1e-34 per node, or a
+            // corrupted exchange): a device limit, reported by gs_sync
+            atomicOr(&flags[2], 1u);
+            k = kMaxIn;
         }
-        head[z] = 0u;
-    }
-    if (own) cnt[z] = 0u;
-    for (uint32_t i = 1; i < k; ++i) {  // ascending key = ascending source id
-        const uint32_t v = ks[i];
-        uint32_t r = i;
-        while (r > 0 && (ks[r - 1] & ~kMutual) > (v & ~kMutual)) {
-            ks[r] = ks[r - 1];
-            --r;
+        uint32_t *lst = sorted + s;
+        for (uint32_t i = 1; i < k; ++i) {  // ascending key = ascending source id
+            const uint32_t v = lst[i];
+            uint32_t r = i;
+            while (r > 0 && (lst[r - 1] & ~kMutual) > (v & ~kMutual)) {
+                lst[r] = lst[r - 1];
+                --r;
+            }
+            lst[r] = v;
         }
-        ks[r] = v;
+        uint32_t zi = 0xFFFFu;
+        for (uint32_t i = 0; i < k; ++i)
+            if (lst[i] & kMutual) zi = i;
+        const uint32_t first = tails_ok ? cur : 0u;
+        if (tails_ok)
+            for (uint32_t i = 3; i < k; ++i) EP[cur + i - 3u] = shard_key_slot(P, lst[i] & ~kMutual);
+        if (k > 3u) cur += k - 3u;
+        // pushers i >= 3 at EP[in.x + i] (u32 arithmetic: in.x = first - 3)
+        const uint32_t z = z0 + lt;
+        IN[z] = make_uint4(first - 3u, k | (zi << 16), k > 0 ? shard_key_slot(P, lst[0] & ~kMutual) : 0u,
+                           k > 1 ? shard_key_slot(P, lst[1] & ~kMutual) : 0u);
+        IN2[z] = k > 2 ? shard_key_slot(P, lst[2] & ~kMutual) : 0u;
     }
-    uint32_t zi = 0xFFFFu;
-    for (uint32_t i = 0; i < k; ++i)
-        if (ks[i] & kMutual) zi = i;
-    const uint32_t nt = k > 3u ? k - 3u : 0u;
-    uint32_t tot;
-    const uint32_t toff = block_exclusive_scan(nt, lds_scan, tot);
-    uint32_t first = blockIdx.x * kEdgeTails + toff;
-    if (tot > kEdgeTails) {
-        if (threadIdx.x == 0) atomicOr(&flags[2], 1u);
-        first = 0u;  // (reported; the tails are not stored)
-    } else {
-        for (uint32_t i = 3; i < k; ++i) EP[first + i - 3u] = shard_key_slot(P, ks[i] & ~kMutual);
-    }
-    if (!own) return;
-    // pushers i >= 3 at EP[in.x + i] (u32 arithmetic: in.x = first - 3)
-    IN[z] = make_uint4(first - 3u, k | (zi << 16), k > 0 ? shard_key_slot(P, ks[0] & ~kMutual) : 0u,
-                       k > 1 ? shard_key_slot(P, ks[1] & ~kMutual) : 0u);
-    IN2[z] = k > 2 ? shard_key_slot(P, ks[2] & ~kMutual) : 0u;
+}
+
+__host__ __device__ inline uint32_t edge_bins(const ShardPlan &P) {
+    return (uint32_t)(((u64)P.m + kEdgeBin - 1) / kEdgeBin);
 }
 
 ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t parts, bool codes) {
@@ -359,15 +443,9 @@ size_t shard_edge_words(const ShardPlan &P, ShardEdgeLayout *L) {
         off += (words + 3) / 4 * 4;
         return o;
     };
-    const size_t nb = ((size_t)P.m + kEdgeBlock - 1) / kEdgeBlock;
-    // counters, inline keys, list heads, overflow entries and their count are
-    // zero between builds (edge_lists leaves them so; the engine clears the
-    // set once at creation)
-    L->cnt = take(P.m);
-    L->inl = take((size_t)kEdgeInline * P.m);
-    L->head = take(P.m);
-    L->ovf = take(2 * (size_t)edge_ovf_cap(P.m));
-    L->ovfn = take(1);
+    const size_t nb = edge_bins(P);
+    L->fill = take(nb);  // zero between builds (edge_sort leaves it so; cleared at creation)
+    L->region = take(2 * nb * kEdgeBinCap);
     L->EP = take(nb * kEdgeTails);
     L->IN = take(4 * (size_t)P.m);
     L->IN2 = take(P.m);
@@ -396,13 +474,15 @@ hipError_t launch_shard_edges(const ShardPlan &P, const ShardEdgeLayout &L, uint
                               const uint32_t *tg, uint64_t seed, uint32_t epoch, uint32_t round,
                               const Faults &f, uint32_t *flags, hipStream_t s) {
     if (P.m == 0) return hipSuccess;  // no local targets: nothing is received
-    const uint32_t slots = P.G * P.P * P.capP;
-    uint2 *ovf = reinterpret_cast<uint2 *>(w + L.ovf);
-    hipLaunchKernelGGL(edge_fill, dim3((slots + 255u) / 256u), dim3(256), 0, s, P, recvA, tg, seed, epoch, round, f,
-                       w + L.cnt, w + L.inl, w + L.head, ovf, w + L.ovfn, flags);
-    hipLaunchKernelGGL(edge_lists, dim3((P.m + kEdgeBlock - 1) / kEdgeBlock), dim3(kEdgeBlock), 0, s, P, w + L.cnt,
-                       w + L.inl, w + L.head, ovf, w + L.ovfn, w + L.EP, reinterpret_cast<uint4 *>(w + L.IN),
-                       w + L.IN2, flags);
+    const uint32_t nb = edge_bins(P), slots = P.G * P.P * P.capP;
+    uint2 *region = reinterpret_cast<uint2 *>(w + L.region);
+    const size_t lds = (2 * (size_t)kEdgeChunk + 3 * (size_t)nb) * sizeof(uint32_t);
+    hipError_t e = hipFuncSetAttribute((const void *)edge_bin, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(edge_bin, dim3((slots + kEdgeChunk - 1) / kEdgeChunk), dim3(kEdgeBinThreads), lds, s, P, recvA,
+                       tg, seed, epoch, round, f, nb, w + L.fill, region, flags);
+    hipLaunchKernelGGL(edge_sort, dim3(nb), dim3(kEdgeSortThreads), 0, s, P, w + L.fill, region, w + L.EP,
+                       reinterpret_cast<uint4 *>(w + L.IN), w + L.IN2, flags);
     return hipGetLastError();
 }
 
