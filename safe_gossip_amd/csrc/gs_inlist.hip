@@ -522,6 +522,18 @@ __host__ __device__ inline uint32_t dlv_scratch_words(const CsrPlan &p) {
     return cfill_off(p) + n_coarse(p.nb) * kCoarseShards;
 }
 
+#ifndef GS_DLV_SPLIT_LOG
+#define GS_DLV_SPLIT_LOG 2
+#endif
+// sort blocks per bin = 2^kSplitLog (n >= 2^21): quarter bins, whose 48 KiB of
+// LDS let two 1024-thread blocks share a CU (half bins took 96 KiB, so a CU's
+// loads and LDS work took turns: inl_sort_dlv 1.52 -> 1.09 ms, config 5
+// 5.19 -> 4.76 ms/step, profiles/r3/cfg5_build)
+constexpr uint32_t kSplitLog = GS_DLV_SPLIT_LOG;
+#ifndef GS_DLV_SMALL_LOG
+#define GS_DLV_SMALL_LOG (kSplitLog + 1u)  // below 128 bins (one coarse bucket, cache-resident)
+#endif
+constexpr uint32_t kDlvSmallLog = GS_DLV_SMALL_LOG;
 // DLV partition entries are 12-byte records, one store stream per run: a
 // coarse entry (source, target, push code), a part entry (source, push code,
 // target within the bin).  (Three u32 / u16 arrays made three scattered
@@ -536,7 +548,7 @@ constexpr size_t kDlvRegionWords = 3;  // u32 words per part slot
 // draws the source's target again (one Philox draw, peer_of) instead of
 // reading it -- the target is a counter-based function of (round, source).
 // Code-row shards keep 12-byte entries (their targets come with the rows).
-__host__ __device__ inline uint2 *part_entries8(uint32_t *region) { return reinterpret_cast<uint2 *>(region); }
+[[maybe_unused]] __host__ __device__ inline uint2 *part_entries8(uint32_t *region) { return reinterpret_cast<uint2 *>(region); }
 // Coarse-bucket entries inside the region buffer, after the bin regions.
 __host__ __device__ inline PEnt *coarse_entries(uint32_t *region, uint32_t nb) {
     return reinterpret_cast<PEnt *>(region + (size_t)nb * kBinCap * kDlvRegionWords);
@@ -797,7 +809,9 @@ __global__ __launch_bounds__(kInlThreads) void dl_direct(InListArgs a) {
         const uint32_t b = sb[i];
         const uint32_t slot = res[b] + (i - off[b]);
         if (slot < pcap) {
-            if constexpr (SH) part_entries(a.region)[(u64)b * pcap + slot] = PEnt{sx[i], sc[i], slt[i]};
+            // (small networks, eighth-bin parts: 12-byte entries with the
+            // target, so their sort draws no targets; the regions stay in L2)
+            if (SH || p.sub == kDlvSmallLog) part_entries(a.region)[(u64)b * pcap + slot] = PEnt{sx[i], sc[i], slt[i]};
             else part_entries8(a.region)[(u64)b * pcap + slot] = make_uint2(sx[i], sc[i]);
         }
     }
@@ -811,18 +825,6 @@ __global__ __launch_bounds__(kInlThreads) void dl_direct(InListArgs a) {
 // created from the pushers ahead), partitioned by the pusher's coarse source
 // bucket for the pull pass-back (pb_fine, pb_place).  Halving the bin keeps
 // ids and codes in LDS.
-#ifndef GS_DLV_SPLIT_LOG
-#define GS_DLV_SPLIT_LOG 2
-#endif
-// sort blocks per bin = 2^kSplitLog (n >= 2^21): quarter bins, whose 48 KiB of
-// LDS let two 1024-thread blocks share a CU (half bins took 96 KiB, so a CU's
-// loads and LDS work took turns: inl_sort_dlv 1.52 -> 1.09 ms, config 5
-// 5.19 -> 4.76 ms/step, profiles/r3/cfg5_build)
-constexpr uint32_t kSplitLog = GS_DLV_SPLIT_LOG;
-#ifndef GS_DLV_SMALL_LOG
-#define GS_DLV_SMALL_LOG (kSplitLog + 1u)  // below 128 bins (one coarse bucket, cache-resident)
-#endif
-constexpr uint32_t kDlvSmallLog = GS_DLV_SMALL_LOG;
 // Small networks (few bins) sort with more blocks per bin, so the chip fills;
 // their bin regions stay in L2 (config 2: 64 bins).
 inline uint32_t dlv_split_log(uint32_t nb) { return nb >= 128u ? kSplitLog : kDlvSmallLog; }
@@ -867,7 +869,7 @@ __global__ __launch_bounds__(kInlThreads, (SL == 2 && OWN) ? 8 : 1) void inl_sor
             const uint32_t i = threadIdx.x + q * kInlThreads;
             const bool ok = i < cnt;
             uint32_t lt;
-            if constexpr (SH) {
+            if constexpr (SH || SL == kDlvSmallLog) {  // (12-byte entries, dl_direct)
                 const PEnt en = part_entries(a.region)[rb + (ok ? i : 0u)];
                 lt = en.c;
                 ex[q] = en.a;
