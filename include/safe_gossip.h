@@ -83,7 +83,7 @@ typedef struct {
     uint32_t drop_push;      /* push batch not delivered (so never answered) */
     uint32_t drop_pull;      /* pull batch not delivered                     */
     /* Nonzero: this engine holds one rumor slice of a rumor-sliced network
-     * (gs_slice_*; 2P only, no external RPCs).                               */
+     * (gs_slice_*; 2P or SEQ; external RPCs: see gs_handle_received).       */
     uint32_t rumor_slice;
     uint32_t reserved1[3];
 } gs_config;
@@ -327,7 +327,8 @@ gs_status   gs_rumor_key(const gs_engine *e, uint32_t rumor, uint8_t *out, uint3
 /* Gossiper::next_round's return value for `node` in the current round
  * (src/gossiper.rs:70-79, src/gossip.rs:79-113): the Push RPCs as frames
  * (u32 LE length + bincode GossipRpc), key order; one empty Push if none;
- * no frame for a node the harness skipped (churn). */
+ * no frame for a node the harness skipped (churn).  A shard engine takes a
+ * global node id it owns. */
 gs_status   gs_push_batch(gs_engine *e, uint32_t node, uint8_t *out, uint32_t cap, uint32_t *len,
                           uint32_t *count);
 /* Gossiper::handle_received_message(peer, bytes) on `node` for a peer
@@ -336,8 +337,17 @@ gs_status   gs_push_batch(gs_engine *e, uint32_t node, uint8_t *out, uint32_t ca
  * first Push from the peer this round is answered with the node's live
  * entries as Pull frames (or one empty Pull); the copy is absorbed (a new
  * entry is created, or recorded on a B entry); peers_in_this_round and the
- * Statistics count it.  2P or SEQ schedule, one engine (not node shards or
- * rumor slices: GS_ERR_UNSUPPORTED); after a gs_next_round.
+ * Statistics count it.  2P or SEQ schedule; after a gs_next_round.
+ * Shard engine: `node` a global id this rank owns, peer >= the network's
+ * n_nodes, after gs_shard_pull and exchange B of the round (class-row shards;
+ * code-row shards, R_pad <= 16 under 2P, apply none: GS_ERR_UNSUPPORTED).
+ * Rumor slice: the caller hands EVERY slice the RPC -- the slice holding its
+ * message as sent, the others the empty RPC of the same kind -- and merges
+ * the slices' answers in key order, one empty Pull only if every slice's is
+ * empty (safe_gossip_amd/sliced.py); a slice answers at most
+ * min(200, 32 * R_pad) first Pushes per node and round
+ * (GS_ERR_DEVICE_LIMIT past that: its empty answers ride the one-byte
+ * per-round empty count the slices reduce with MIN).
  * Messages whose bytes are no rumor slot's key: GS_ERR_INVALID_ARGUMENT.
  * A node offline this round (churn) drops the RPC: GS_OK, no frames, no
  * effect.  Undecodable bytes: GS_ERR_SERIALISATION, nothing applied; so is a

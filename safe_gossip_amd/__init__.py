@@ -29,6 +29,7 @@ __all__ = [
     "AlreadyStarted", "DeviceError", "derive_params", "peer_of", "origin_of", "coin_of",
     "send_messages", "load_library", "SYMBOLS", "rpc_encode", "rpc_decode", "message_wrap",
     "message_unwrap", "split_frames", "SigFailure", "sha3_512", "ed25519_sign", "ed25519_verify",
+    "default_rumor_key",
 ]
 
 # ----------------------------------------------------------------- errors
@@ -433,6 +434,65 @@ def split_frames(data: bytes) -> List[bytes]:
     return out
 
 
+def engine_push_batch(lib, h, node: int) -> List[bytes]:
+    """gs_push_batch of one engine (a shard: ``node`` a global id it owns)."""
+    n, c = ctypes.c_uint32(), ctypes.c_uint32()
+    lib.gs_push_batch(h, node, None, 0, ctypes.byref(n), ctypes.byref(c))
+    out = (ctypes.c_uint8 * max(1, n.value))()
+    _check(lib.gs_push_batch(h, node, out, n.value, ctypes.byref(n), ctypes.byref(c)))
+    return split_frames(bytes(out)[:n.value])
+
+
+def engine_handle_received(lib, h, node: int, peer: int, message: bytes) -> List[bytes]:
+    """gs_handle_received of one engine, the response buffer grown as needed."""
+    cap = 4096
+    while True:
+        out = (ctypes.c_uint8 * cap)()
+        n, c = ctypes.c_uint32(), ctypes.c_uint32()
+        st = lib.gs_handle_received(h, node, peer, _buf(message), len(message), out, cap,
+                                    ctypes.byref(n), ctypes.byref(c))
+        if st == 5 and n.value > cap:  # responses larger than the buffer: nothing was applied
+            cap = n.value
+            continue
+        _check(st)
+        return split_frames(bytes(out)[:n.value])
+
+
+def engine_handle_received_batch(lib, h, rpcs) -> List[List[bytes]]:
+    """gs_handle_received_batch of one engine: (node, peer, message bytes) in order."""
+    rpcs = list(rpcs)
+    m = len(rpcs)
+    nodes = np.array([r[0] for r in rpcs], dtype=np.uint32)
+    peers = np.array([r[1] for r in rpcs], dtype=np.uint32)
+    lens = np.array([len(r[2]) for r in rpcs], dtype=np.uint32)
+    offs = np.zeros(m, dtype=np.uint32)
+    if m:
+        offs[1:] = np.cumsum(lens)[:-1]
+    msgs = _buf(b"".join(r[2] for r in rpcs))
+    resp = np.zeros(m + 1, dtype=np.uint32)
+    cap = 4096
+    while True:
+        out = (ctypes.c_uint8 * cap)()
+        n = ctypes.c_uint32()
+        st = lib.gs_handle_received_batch(
+            h, m, nodes.ctypes.data_as(_U32P), peers.ctypes.data_as(_U32P), msgs,
+            offs.ctypes.data_as(_U32P), lens.ctypes.data_as(_U32P), out, cap, ctypes.byref(n),
+            resp.ctypes.data_as(_U32P))
+        if st == 5 and n.value > cap:  # responses larger than the buffer: nothing was applied
+            cap = n.value
+            continue
+        _check(st)
+        data = bytes(out)[:n.value]
+        return [split_frames(data[resp[i]:resp[i + 1]]) for i in range(m)]
+
+
+def default_rumor_key(rumor: int) -> bytes:
+    """The message bytes a rumor slot has until ``set_rumor_key``: bincode of
+    a 4-byte ``Vec<u8>`` holding the slot big-endian (so key order is slot
+    order; gs_engine.cpp gs_create)."""
+    return bytes([4, 0, 0, 0, 0, 0, 0, 0]) + int(rumor).to_bytes(4, "big")
+
+
 # ---------------------------------------------------------------- network
 class Network:
     """A simulated full-mesh network of ``n_nodes`` Gossipers on one MI355X.
@@ -572,55 +632,18 @@ class Network:
 
     def push_batch(self, node: int) -> List[bytes]:
         """``Gossiper::next_round``'s Push RPCs of ``node`` this round (bytes)."""
-        n, c = ctypes.c_uint32(), ctypes.c_uint32()
-        self._lib.gs_push_batch(self._h, node, None, 0, ctypes.byref(n), ctypes.byref(c))
-        out = (ctypes.c_uint8 * max(1, n.value))()
-        _check(self._lib.gs_push_batch(self._h, node, out, n.value, ctypes.byref(n), ctypes.byref(c)))
-        return split_frames(bytes(out)[:n.value])
+        return engine_push_batch(self._lib, self._h, node)
 
     def handle_received(self, node: int, peer: int, message: bytes) -> List[bytes]:
         """``Gossiper::handle_received_message(peer, message)`` on ``node`` for a
         peer outside the simulated network (``peer >= n``): the Pull RPCs."""
-        cap = 4096
-        while True:
-            out = (ctypes.c_uint8 * cap)()
-            n, c = ctypes.c_uint32(), ctypes.c_uint32()
-            st = self._lib.gs_handle_received(self._h, node, peer, _buf(message), len(message), out, cap,
-                                              ctypes.byref(n), ctypes.byref(c))
-            if st == 5 and n.value > cap:  # responses larger than the buffer: nothing was applied
-                cap = n.value
-                continue
-            _check(st)
-            return split_frames(bytes(out)[:n.value])
+        return engine_handle_received(self._lib, self._h, node, peer, message)
 
     def handle_received_batch(self, rpcs) -> List[List[bytes]]:
         """``handle_received`` for many (node, peer, message bytes) at once, in
         order (``gs_handle_received_batch``: one observation launch for all
         first Pushes); returns each RPC's Pull responses."""
-        rpcs = list(rpcs)
-        m = len(rpcs)
-        nodes = np.array([r[0] for r in rpcs], dtype=np.uint32)
-        peers = np.array([r[1] for r in rpcs], dtype=np.uint32)
-        lens = np.array([len(r[2]) for r in rpcs], dtype=np.uint32)
-        offs = np.zeros(m, dtype=np.uint32)
-        if m:
-            offs[1:] = np.cumsum(lens)[:-1]
-        msgs = _buf(b"".join(r[2] for r in rpcs))
-        resp = np.zeros(m + 1, dtype=np.uint32)
-        cap = 4096
-        while True:
-            out = (ctypes.c_uint8 * cap)()
-            n = ctypes.c_uint32()
-            st = self._lib.gs_handle_received_batch(
-                self._h, m, nodes.ctypes.data_as(_U32P), peers.ctypes.data_as(_U32P), msgs,
-                offs.ctypes.data_as(_U32P), lens.ctypes.data_as(_U32P), out, cap, ctypes.byref(n),
-                resp.ctypes.data_as(_U32P))
-            if st == 5 and n.value > cap:  # responses larger than the buffer: nothing was applied
-                cap = n.value
-                continue
-            _check(st)
-            data = bytes(out)[:n.value]
-            return [split_frames(data[resp[i]:resp[i + 1]]) for i in range(m)]
+        return engine_handle_received_batch(self._lib, self._h, rpcs)
 
     def handle_received_signed(self, node: int, peer: int, peer_key: bytes, message: bytes,
                                node_seed: Optional[bytes] = None) -> List[bytes]:

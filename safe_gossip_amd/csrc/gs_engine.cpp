@@ -127,6 +127,7 @@ struct gs_engine {
     };
     std::vector<Ext> ext;                   // in call order
     std::set<std::pair<uint32_t, uint32_t>> ext_peers;  // (node, peer) heard from this round
+    std::map<uint32_t, uint32_t> ext_fp;  // rumor slices: answered external first Pushes per node this round
     u64 *ext_dev = nullptr;
     uint32_t ext_cap = 0, ext_uploaded = 0;
     uint16_t *node_state = nullptr;         // one node's observed codes [R]
@@ -261,6 +262,7 @@ gs_status reset_state(gs_engine *e) {
     e->started = false;
     e->ext.clear();
     e->ext_peers.clear();
+    e->ext_fp.clear();
     e->ext_uploaded = 0;
     return GS_OK;
 }
@@ -1232,6 +1234,7 @@ gs_status round_end(gs_engine *e, gs_round_report *report) {
     e->deliver_pending = true;
     e->ext.clear();  // delivered by this round kernel (upload_ext syncs before reuse)
     e->ext_peers.clear();
+    e->ext_fp.clear();
     e->ext_uploaded = 0;
     e->obs_valid = false;
     if (++e->since_fold >= e->fold_every) {
@@ -1630,6 +1633,31 @@ gs_status append_frame(int pull, const std::string &msg, uint8_t counter, uint8_
                          out + at + 4, need, &w);
 }
 
+// External RPCs (gs_handle_received*) are accepted once a round has run and
+// been delivered: a shard after gs_shard_pull, whose pull rows (exchange B)
+// the caller has waited for.  Code-row shards (R_pad <= 16, 2P) run the
+// packed DLV kernel, which applies none.
+gs_status ext_ready(const gs_engine *e) {
+    if (e->shard && e->dlv) return GS_ERR_UNSUPPORTED;
+    if (e->round == 0 || !e->deliver_pending) return GS_ERR_INVALID_ARGUMENT;  // after a next_round
+    if (e->shard && e->pulled_round != e->round) return GS_ERR_INVALID_ARGUMENT;
+    return GS_OK;
+}
+
+// A node of this engine (shards: a global id owned by this rank) and a peer
+// outside the simulated network.
+bool ext_ids(const gs_engine *e, uint32_t node, uint32_t peer) {
+    if (e->shard) return node >= e->sp.lo && node - e->sp.lo < e->sp.m && peer >= e->n_global;
+    return node < e->g.n && peer >= e->g.n;
+}
+
+// Rumor slices: each slice counts an external first Push answered with an
+// empty Pull into the node's per-round empty count, which the slices reduce
+// as one byte (MIN) and the u16 Statistics deltas take between folds (sized
+// for 32 * R_pad + 32 per round, the internal count being at most 30): at
+// most this many first Pushes per node and round (GS_ERR_DEVICE_LIMIT).
+uint32_t slice_ext_limit(const gs_engine *e) { return std::min<uint32_t>(200u, 32u * e->g.rpad); }
+
 // Post-delivery state codes of one node (gs_dump_state's codes), external
 // RPCs queued so far included: the observation kernel over the node's block.
 gs_status observe_node(gs_engine *e, uint32_t node, std::vector<uint16_t> &codes) {
@@ -1643,6 +1671,7 @@ gs_status observe_node(gs_engine *e, uint32_t node, std::vector<uint16_t> &codes
     a.blk_off = (uint32_t)(seg0 / 256);
     a.blk_count = 1;
     if (e->deliver_pending) {
+        if (e->shard) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_edges[e->round % 2], 0));  // its in-lists
         st = seq_prepare(e);  // SEQ: the round's pull batches (no-op for 2P)
         if (st != GS_OK) return st;
     }
@@ -1699,6 +1728,8 @@ gs_status observe_nodes(gs_engine *e, const std::vector<uint32_t> &nodes, std::v
     if (he == hipSuccess)
         he = hipMemcpyAsync(dev + blocks.size(), nodes.data(), m * sizeof(uint32_t), hipMemcpyHostToDevice,
                             e->stream);
+    if (he == hipSuccess && e->deliver_pending && e->shard)  // a shard's in-lists
+        he = hipStreamWaitEvent(e->stream, e->ev_edges[e->round % 2], 0);
     if (he == hipSuccess && e->deliver_pending && seq_prepare(e) != GS_OK)
         he = hipErrorUnknown;  // SEQ: the round's pull batches
     if (he == hipSuccess) he = gs::launch_round(a, e->deliver_pending ? 2 : 3, e->stream);
@@ -1718,8 +1749,8 @@ gs_status gs_handle_received_batch(gs_engine *e, uint32_t count, const uint32_t 
     if (!e || !out_len || (count && (!nodes || !peers || !msgs || !off || !len || !resp_off)))
         return GS_ERR_INVALID_ARGUMENT;
     *out_len = 0;
-    if (e->shard || e->slice) return GS_ERR_UNSUPPORTED;
-    if (e->round == 0 || !e->deliver_pending) return GS_ERR_INVALID_ARGUMENT;  // after a next_round
+    gs_status st = ext_ready(e);
+    if (st != GS_OK) return st;
     // Decode and check every RPC first: the batch is applied whole or not at all.
     struct Item {
         uint32_t node, peer, rumor;
@@ -1728,15 +1759,16 @@ gs_status gs_handle_received_batch(gs_engine *e, uint32_t count, const uint32_t 
     };
     std::vector<Item> it(count);
     std::set<std::pair<uint32_t, uint32_t>> peers_seen(e->ext_peers);
+    std::map<uint32_t, uint32_t> fp;  // slices: first Pushes per node, this batch included
     std::vector<uint32_t> obs;
     for (uint32_t i = 0; i < count; ++i) {
         Item &v = it[i];
-        v.node = nodes[i];
+        if (!ext_ids(e, nodes[i], peers[i])) return GS_ERR_INVALID_ARGUMENT;
+        v.node = nodes[i] - (e->shard ? e->sp.lo : 0u);  // (shards: global ids, owned by this rank)
         v.peer = peers[i];
-        if (v.node >= e->g.n || v.peer < e->g.n) return GS_ERR_INVALID_ARGUMENT;
         int pull = 0;
         uint32_t mo = 0, ml = 0;
-        gs_status st = gs_rpc_decode(msgs + off[i], len[i], &pull, &mo, &ml, &v.counter);
+        st = gs_rpc_decode(msgs + off[i], len[i], &pull, &mo, &ml, &v.counter);
         if (st != GS_OK) return st;  // Message::deserialise failure (src/gossiper.rs:89-94)
         v.pull = pull != 0;
         v.empty = ml == 0 && v.counter == 0;  // src/gossip.rs:153-154
@@ -1747,13 +1779,23 @@ gs_status gs_handle_received_batch(gs_engine *e, uint32_t count, const uint32_t 
             v.rumor = k->second;
         }
         // churn: a node the harness took offline this round drops it
-        v.offline = e->faults.churn && gs::offline_of(e->seed, e->epoch, e->round, v.node, e->faults.churn);
+        v.offline = e->faults.churn && gs::offline_of(e->seed, e->epoch, e->round, nodes[i], e->faults.churn);
         v.is_new = !v.offline && peers_seen.insert({v.node, v.peer}).second;  // src/gossip.rs:125
-        if (v.is_new && !v.pull) obs.push_back(v.node);
+        if (v.is_new && !v.pull) {
+            obs.push_back(v.node);
+            if (e->slice) {  // (see slice_ext_limit)
+                auto f = fp.find(v.node);
+                if (f == fp.end()) {
+                    auto h = e->ext_fp.find(v.node);
+                    f = fp.emplace(v.node, h == e->ext_fp.end() ? 0u : h->second).first;
+                }
+                if (++f->second > slice_ext_limit(e)) return GS_ERR_DEVICE_LIMIT;
+            }
+        }
     }
     std::sort(obs.begin(), obs.end());
     obs.erase(std::unique(obs.begin(), obs.end()), obs.end());
-    gs_status st = set_device(e);
+    st = set_device(e);
     if (st != GS_OK) return st;
     // the answering nodes' state with every RPC queued before this batch (one
     // launch), then this batch's copies applied in call order on the host:
@@ -1820,6 +1862,7 @@ gs_status gs_handle_received_batch(gs_engine *e, uint32_t count, const uint32_t 
     if (!out || need > cap) return GS_ERR_SERIALISATION;  // nothing applied; *out_len holds the size needed
     frames(true);
     // queue every RPC as gs_handle_received does, in call order
+    for (auto &f : fp) e->ext_fp[f.first] = f.second;
     for (uint32_t i = 0; i < count; ++i) {
         const Item &v = it[i];
         if (v.offline) continue;
@@ -1845,27 +1888,35 @@ gs_status gs_handle_received_batch(gs_engine *e, uint32_t count, const uint32_t 
 
 gs_status gs_push_batch(gs_engine *e, uint32_t node, uint8_t *out, uint32_t cap, uint32_t *len,
                         uint32_t *count) {
-    if (!e || !len || !count || node >= e->g.n) return GS_ERR_INVALID_ARGUMENT;
-    if (e->shard) return GS_ERR_UNSUPPORTED;
+    if (!e || !len || !count) return GS_ERR_INVALID_ARGUMENT;
+    const uint32_t gnode = node;  // (shards: a global id, owned by this rank)
+    if (e->shard) {
+        if (node < e->sp.lo || node - e->sp.lo >= e->sp.m) return GS_ERR_INVALID_ARGUMENT;
+        node -= e->sp.lo;
+    }
+    if (node >= e->g.n) return GS_ERR_INVALID_ARGUMENT;
     *len = 0;
     *count = 0;
     if (e->round == 0) return GS_OK;  // no round run yet: no next_round call, no push batch
     gs_status st = set_device(e);
     if (st != GS_OK) return st;
-    if (e->faults.churn && gs::offline_of(e->seed, e->epoch, e->round, node, e->faults.churn))
+    if (e->faults.churn && gs::offline_of(e->seed, e->epoch, e->round, gnode, e->faults.churn))
         return GS_OK;  // the harness skipped this node's next_round
     // the planes of round t after phase 0 = Gossip::next_round's push list
     const gs::Geometry &g = e->g;
     std::vector<u64> w((size_t)gs::kPlanes * g.W);
     uint32_t sh = 0;
+    // (on the engine stream: a non-blocking stream the legacy default stream
+    // does not wait for, and the round kernel that wrote the planes runs there)
     if (g.small) {
-        GS_HIP(hipMemcpy(w.data(), e->S[e->cur] + (u64)(node >> g.lognpu) * gs::kPlanes,
-                         gs::kPlanes * sizeof(u64), hipMemcpyDeviceToHost));
+        GS_HIP(hipMemcpyAsync(w.data(), e->S[e->cur] + (u64)(node >> g.lognpu) * gs::kPlanes,
+                              gs::kPlanes * sizeof(u64), hipMemcpyDeviceToHost, e->stream));
         sh = (node & ((1u << g.lognpu) - 1u)) << g.logr;
     } else {
-        GS_HIP(hipMemcpy(w.data(), e->S[e->cur] + (u64)node * gs::kPlanes * g.W, w.size() * sizeof(u64),
-                         hipMemcpyDeviceToHost));
+        GS_HIP(hipMemcpyAsync(w.data(), e->S[e->cur] + (u64)node * gs::kPlanes * g.W, w.size() * sizeof(u64),
+                              hipMemcpyDeviceToHost, e->stream));
     }
+    GS_HIP(hipStreamSynchronize(e->stream));
     auto bit = [&](int p, uint32_t r) -> uint32_t {
         return g.small ? (uint32_t)((w[p] >> (sh + r)) & 1u) : (uint32_t)((w[(size_t)p * g.W + (r >> 6)] >> (r & 63)) & 1u);
     };
@@ -1889,18 +1940,20 @@ gs_status gs_push_batch(gs_engine *e, uint32_t node, uint8_t *out, uint32_t cap,
 
 gs_status gs_handle_received(gs_engine *e, uint32_t node, uint32_t peer, const uint8_t *msg, uint32_t msg_len,
                              uint8_t *out, uint32_t cap, uint32_t *out_len, uint32_t *out_count) {
-    if (!e || !msg || !out_len || !out_count || node >= e->g.n) return GS_ERR_INVALID_ARGUMENT;
+    if (!e || !msg || !out_len || !out_count) return GS_ERR_INVALID_ARGUMENT;
     *out_len = 0;
     *out_count = 0;
-    if (e->shard || e->slice) return GS_ERR_UNSUPPORTED;
-    if (peer < e->g.n) return GS_ERR_INVALID_ARGUMENT;  // peers outside the simulated network
-    if (e->round == 0 || !e->deliver_pending) return GS_ERR_INVALID_ARGUMENT;  // after a next_round
+    if (!ext_ids(e, node, peer)) return GS_ERR_INVALID_ARGUMENT;
+    gs_status st = ext_ready(e);
+    if (st != GS_OK) return st;
+    const uint32_t gnode = node;  // (shards: a global id, owned by this rank)
+    if (e->shard) node -= e->sp.lo;
     int pull = 0;
     uint32_t off = 0, mlen = 0;
     uint8_t counter = 0;
     // Message::deserialise failure: the reference logs it and returns no RPC
     // (src/gossiper.rs:89-94)
-    gs_status st = gs_rpc_decode(msg, msg_len, &pull, &off, &mlen, &counter);
+    st = gs_rpc_decode(msg, msg_len, &pull, &off, &mlen, &counter);
     if (st != GS_OK) return st;
     const bool empty = mlen == 0 && counter == 0;  // src/gossip.rs:153-154
     uint32_t rumor = 0;
@@ -1911,10 +1964,12 @@ gs_status gs_handle_received(gs_engine *e, uint32_t node, uint32_t peer, const u
     }
     // churn: a node the harness took offline this round receives nothing (its
     // internal RPCs are dropped too); the RPC is dropped without effect
-    if (e->faults.churn && gs::offline_of(e->seed, e->epoch, e->round, node, e->faults.churn)) return GS_OK;
+    if (e->faults.churn && gs::offline_of(e->seed, e->epoch, e->round, gnode, e->faults.churn)) return GS_OK;
     st = set_device(e);
     if (st != GS_OK) return st;
-    const bool is_new = e->ext_peers.insert({node, peer}).second;  // src/gossip.rs:125
+    const bool fresh = !e->ext_peers.count({node, peer});  // src/gossip.rs:125
+    if (fresh && !pull && e->slice && e->ext_fp[node] >= slice_ext_limit(e)) return GS_ERR_DEVICE_LIMIT;
+    const bool is_new = e->ext_peers.insert({node, peer}).second;
     if (is_new && !pull) {
         // Pull responses: the node's live entries now (src/gossip.rs:126-148)
         std::vector<uint16_t> codes;
@@ -1937,6 +1992,7 @@ gs_status gs_handle_received(gs_engine *e, uint32_t node, uint32_t peer, const u
             e->ext_peers.erase({node, peer});
             return res;
         }
+        ++e->ext_fp[node];
     }
     uint32_t info = (pull ? 0u : gs::kExtPush) | (is_new ? gs::kExtNew : 0u);
     if (empty) {

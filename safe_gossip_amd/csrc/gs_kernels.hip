@@ -467,7 +467,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
             rv.create(newc, pCl);
         }
         rv.recv += popc(pl);
-        if (!SHARD && a.n_ext) {
+        if (a.n_ext) {
             // External RPCs to x (gs_handle_received), after every internal
             // delivery of the round, in call order (Gossip::receive,
             // src/gossip.rs:118-163): a first RPC from a peer joins
@@ -791,12 +791,16 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         uint4 v = stv;
         if (a.st16 && (ext_full | ext_empty | ext_recv)) {
             // u16 deltas hold internal deliveries only (bounded per round):
-            // external RPCs, as many as the caller sends, go to the totals
+            // external RPCs, as many as the caller sends, go to the totals --
+            // but a rumor slice's empty pulls go through emin (MIN over the
+            // slices; the engine bounds them, gs_engine.cpp slice_ext_limit)
             u64 *s64 = const_cast<u64 *>(a.st64) + (u64)x * 4u;
-            s64[0] += ext_empty;
+            if (!a.emin) {
+                s64[0] += ext_empty;
+                d_empty_pull -= ext_empty;
+            }
             s64[2] += ext_full;
             s64[3] += ext_recv;
-            d_empty_pull -= ext_empty;
             d_full_sent -= ext_full;
             d_recv -= ext_recv;
         }

@@ -35,12 +35,12 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import Optional
+from typing import List, Optional
 
 import numpy as np
 
-from . import (DeviceError, GossipError, NoPeers, RoundReport, _check, _Config, _Report,
-               fault_threshold, load_library)
+from . import (DeviceError, GossipError, NoPeers, RoundReport, _buf, _check, _Config, _Report,
+               engine_handle_received_batch, engine_push_batch, fault_threshold, load_library, rpc_decode)
 
 # RCCL's all_to_all_single is exact up to 2^30 bytes per rank (DESIGN.md
 # section 7, "The single-part stall").
@@ -362,6 +362,82 @@ class ShardedNetwork:
     def sync(self) -> None:
         self._wait_all()
         self._sync_all()
+
+    # ------------------------------------------------------------ wire format
+    # The byte boundary of src/gossiper.rs:70-99 on a sharded network: every
+    # shard holds the rumor keys; an RPC goes to the shard owning its node (a
+    # global id).  dist: every rank makes the same calls, the owner answers
+    # and the answers are all-gathered.  Code-row shards (R_pad <= 16, 2P)
+    # take no external RPCs (GS_ERR_UNSUPPORTED).
+    def set_rumor_key(self, rumor: int, key: bytes) -> None:
+        for s in self.shards:
+            _check(self.lib.gs_set_rumor_key(s.h, rumor, _buf(key), len(key)))
+
+    def rumor_key(self, rumor: int) -> bytes:
+        h = self.shards[0].h
+        n = ctypes.c_uint32()
+        self.lib.gs_rumor_key(h, rumor, None, 0, ctypes.byref(n))
+        out = (ctypes.c_uint8 * max(1, n.value))()
+        _check(self.lib.gs_rumor_key(h, rumor, out, n.value, ctypes.byref(n)))
+        return bytes(out)[:n.value]
+
+    def _shard_of(self, node: int):
+        for s in self.shards:
+            if s.lo <= node < s.lo + s.m:
+                return s
+        return None
+
+    def _share(self, mine):
+        """dist: every rank's value (rank order); local: [mine]."""
+        if self.transport == "local":
+            return [mine]
+        objs = [None] * self.world
+        self.dist.all_gather_object(objs, mine, group=self.group)
+        return objs
+
+    def push_batch(self, node: int) -> List[bytes]:
+        """``Gossiper::next_round``'s Push RPCs of ``node`` this round."""
+        if not 0 <= node < self.n:
+            _check(-1)
+        self._wait_all()  # (the round kernel wrote the planes on the engine stream)
+        s = self._shard_of(node)
+        mine = engine_push_batch(self.lib, s.h, node) if s is not None else None
+        return next(v for v in self._share(mine) if v is not None)
+
+    def _validate(self, rpcs):
+        """Every RPC checked before any shard applies one (the batch is whole
+        or nothing across shards too): ids, then the frame (GossipError on
+        bad bytes, src/gossiper.rs:89-94) and its rumor key."""
+        keys = {self.rumor_key(r) for r in range(self.R)}
+        for node, peer, msg in rpcs:
+            if not 0 <= node < self.n or peer < self.n:
+                _check(-1)
+            _, m, ctr = rpc_decode(msg)
+            if (m or ctr) and m not in keys:
+                _check(-1)
+
+    def handle_received(self, node: int, peer: int, message: bytes) -> List[bytes]:
+        """``Gossiper::handle_received_message(peer, message)`` on ``node`` for
+        a peer outside the network: the Pull RPCs (after this round's
+        deliveries, like the single engine)."""
+        return self.handle_received_batch([(node, peer, message)])[0]
+
+    def handle_received_batch(self, rpcs) -> List[List[bytes]]:
+        """``handle_received`` for many (node, peer, message) in order; each
+        shard takes its nodes' RPCs in one gs_handle_received_batch."""
+        rpcs = list(rpcs)
+        self._validate(rpcs)
+        self._per_shard(lambda s: None)  # round delivered: pull rows in, exchange B waited for
+        mine = {}
+        for s in self.shards:
+            idx = [i for i, r in enumerate(rpcs) if s.lo <= r[0] < s.lo + s.m]
+            if idx:
+                for i, resp in zip(idx, engine_handle_received_batch(self.lib, s.h, [rpcs[i] for i in idx])):
+                    mine[i] = resp
+        out = {}
+        for d in self._share(mine):
+            out.update(d)
+        return [out[i] for i in range(len(rpcs))]
 
     # measurement hooks (this process's first shard)
     def set_timing(self, on: bool) -> None:

@@ -39,7 +39,8 @@ from typing import List, Optional
 
 import numpy as np
 
-from . import _U64P, GossipError, Network, NoPeers, RoundReport, Statistics, _check
+from . import (_U64P, GossipError, Network, NoPeers, RoundReport, Statistics, _check, default_rumor_key,
+               rpc_decode, rpc_encode)
 
 
 def merge_known(per, bounds, n: int, kw: int) -> np.ndarray:
@@ -87,8 +88,9 @@ class SlicedNetwork:
     With ``transport="dist"`` every rank makes the same calls (``send_new`` is
     ignored by ranks that do not hold the rumor) and observers return the whole
     network on every rank.  Both schedules (2P and SEQ: the empty counts are
-    the MIN over the slices under either, tests/test_sliced_gloo.py), no
-    external RPCs.
+    the MIN over the slices under either, tests/test_sliced_gloo.py), and the
+    wire boundary (``push_batch``, ``handle_received[_batch]``, rumor keys;
+    see ``handle_received_batch``).
     """
 
     def __init__(self, n_nodes: int, n_rumors: int, world: int, seed: int = 0x5AFE6055,
@@ -122,6 +124,10 @@ class SlicedNetwork:
         self.faults = self.slices[0].net.faults
         self.round = 0
         self._pend = []  # (async work, buffer) of all-reduces not applied yet (RCCL)
+        # wire format: keys set by set_rumor_key (every rank tracks them all);
+        # the slices' engines take the network's keys on first use
+        self._key_of, self._rumor_of = {}, {}
+        self._keys_ready = False
 
     # ------------------------------------------------------------ lifecycle
     def close(self):
@@ -243,6 +249,126 @@ class SlicedNetwork:
         self._flush()
         for s in self.slices:
             s.net.sync()
+
+    # ------------------------------------------------------------ wire format
+    # The byte boundary of src/gossiper.rs:70-99 on a sliced network.  A
+    # rumor's Push / Pull RPC carries one message, held by one slice; but
+    # peers_in_this_round and the answers to a first Push are node-level
+    # (src/gossip.rs:125-148).  So every slice takes every RPC -- the owner
+    # as sent, the others as the empty RPC of the same kind (which counts the
+    # peer and asks for the slice's live entries but creates nothing) -- and
+    # the answer is the slices' Pull responses merged in key order (one empty
+    # Pull if no slice has a live entry).  A slice counts an empty answer
+    # into its per-round empty count, so the network's count stays the MIN
+    # over the slices (the first slice with a live entry ends the empty run,
+    # a nondecreasing function of when that happens, as for the internal
+    # pushes); the engine bounds those answers per node and round
+    # (gs_engine.cpp slice_ext_limit).
+    def _ensure_keys(self):
+        """Each slice's engine keys := the network's (rumor lo+r for slot r),
+        in descending slot order so no key is ever held twice."""
+        if self._keys_ready:
+            return
+        for s in self.slices:
+            if s.lo:
+                for r in range(s.hi - s.lo - 1, -1, -1):
+                    s.net.set_rumor_key(r, default_rumor_key(s.lo + r))
+        self._keys_ready = True
+
+    def rumor_key(self, rumor: int) -> bytes:
+        if not 0 <= rumor < self.R:
+            _check(-1)
+        return self._key_of.get(rumor, default_rumor_key(rumor))
+
+    def _rumor_by_key(self, key: bytes) -> Optional[int]:
+        r = self._rumor_of.get(key)
+        if r is not None:
+            return r
+        if len(key) == 12 and key[:8] == default_rumor_key(0)[:8]:
+            q = int.from_bytes(key[8:], "big")
+            if q < self.R and q not in self._key_of:
+                return q
+        return None
+
+    def set_rumor_key(self, rumor: int, key: bytes) -> None:
+        if not 0 <= rumor < self.R:
+            _check(-1)
+        held = self._rumor_by_key(key)
+        if held is not None:
+            if held != rumor:
+                _check(-1)  # keys are distinct (gs_set_rumor_key)
+            return
+        self._ensure_keys()
+        for s in self.slices:
+            if s.lo <= rumor < s.hi:
+                s.net.set_rumor_key(rumor - s.lo, key)
+        old = self._key_of.pop(rumor, None)
+        if old is not None:
+            del self._rumor_of[old]
+        self._key_of[rumor] = key
+        self._rumor_of[key] = rumor
+
+    def _merge(self, per_slice: List[List[bytes]]) -> List[bytes]:
+        """One RPC's answers from every slice: the non-empty frames in key
+        order, or one empty frame (every slice answered empty), or none."""
+        frames = [f for fs in per_slice for f in fs]
+        if not frames:
+            return []
+        full = []
+        for f in frames:
+            pull, m, ctr = rpc_decode(f)
+            if m or ctr:
+                full.append((m, f))
+        if not full:
+            return [frames[0]]
+        full.sort(key=lambda kv: kv[0])
+        return [f for _, f in full]
+
+    def _gather_lists(self, mine: List[List[List[bytes]]]) -> List[List[List[bytes]]]:
+        """Per slice, per RPC answers of every slice (dist: all-gathered)."""
+        if self.transport == "local":
+            return mine
+        objs = [None] * self.world
+        self.dist.all_gather_object(objs, mine[0], group=self.group)
+        return objs
+
+    def push_batch(self, node: int) -> List[bytes]:
+        """``Gossiper::next_round``'s Push RPCs of ``node`` this round, in key
+        order across the slices (one empty Push if none has any)."""
+        self._ensure_keys()
+        per = self._gather_lists([[s.net.push_batch(node)] for s in self.slices])
+        return self._merge([p[0] for p in per])
+
+    def handle_received(self, node: int, peer: int, message: bytes) -> List[bytes]:
+        """``Gossiper::handle_received_message(peer, message)`` on ``node``
+        for a peer outside the network: the Pull RPCs."""
+        return self.handle_received_batch([(node, peer, message)])[0]
+
+    def handle_received_batch(self, rpcs) -> List[List[bytes]]:
+        """``handle_received`` for many (node, peer, message) in order: every
+        slice takes the whole batch (the owner's RPCs as sent, the others'
+        emptied) in one gs_handle_received_batch."""
+        rpcs = list(rpcs)
+        self._ensure_keys()
+        self._flush()
+        split = []  # per RPC: (owning rumor or None, the empty RPC of its kind)
+        for node, peer, msg in rpcs:
+            pull, m, ctr = rpc_decode(msg)  # GossipError on bad bytes (src/gossiper.rs:89-94)
+            if not 0 <= node < self.n or peer < self.n:
+                _check(-1)
+            r = None
+            if m or ctr:
+                r = self._rumor_by_key(m)
+                if r is None:
+                    _check(-1)  # no rumor slot for this message
+            split.append((r, rpc_encode(pull, b"", 0)))
+        mine = []
+        for s in self.slices:
+            batch = [(node, peer, msg if (r is not None and s.lo <= r < s.hi) else empty)
+                     for (node, peer, msg), (r, empty) in zip(rpcs, split)]
+            mine.append(s.net.handle_received_batch(batch))
+        per = self._gather_lists(mine)
+        return [self._merge([p[i] for p in per]) for i in range(len(rpcs))]
 
     # ------------------------------------------------------------ measurement (this rank's slice)
     def set_timing(self, on: bool) -> None:

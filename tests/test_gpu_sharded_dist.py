@@ -40,6 +40,14 @@ def _worker(rank, world, port, cases, q, backend="gloo", parts=None, env=None):
             return ShardedNetwork(n, R, world, seed=seed, epoch=epoch, params=params, device=0,
                                   transport="dist", parts=parts)
         for n, R, kind in cases:
+            if kind == "wire":  # external RPCs (tests/test_gpu_wire.py): the owner answers, all-gathered
+                from test_gpu_wire import _batch_case, _handle_received_case
+
+                def mk(n_, R_, **kw):
+                    return ShardedNetwork(n_, R_, world, device=0, transport="dist", parts=parts, **kw)
+                _handle_received_case(sg, n, R, (0.05, 0.05, 0.05), make=mk)
+                _batch_case(sg, n, R, None, "2P", make=mk)
+                continue
             run_parity(sg, n, R, kind, make_net=make)
         q.put(("ok", rank))
     except BaseException as e:
@@ -53,7 +61,8 @@ def _worker(rank, world, port, cases, q, backend="gloo", parts=None, env=None):
 def test_sharded_dist_gloo_two_ranks(engine, parts):
     import torch.multiprocessing as mp
     world = 2
-    cases = [(600, 48, "origins"), (1000, 3, "trickle"), (700, 256, "reinject"), (5000, 16, "origins")]
+    cases = [(600, 48, "origins"), (1000, 3, "trickle"), (700, 256, "reinject"), (5000, 16, "origins"),
+             (900, 100, "wire")]
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
@@ -79,7 +88,8 @@ def test_sharded_dist_rccl_single_rank(engine, parts):
     # (parts 2: the exchanges of one part overlap the other part's round
     # kernel), no host synchronisation per round
     import torch.multiprocessing as mp
-    cases = [(600, 48, "origins"), (700, 256, "reinject"), (1000, 3, "trickle"), (5000, 16, "origins")]
+    cases = [(600, 48, "origins"), (700, 256, "reinject"), (1000, 3, "trickle"), (5000, 16, "origins"),
+             (900, 100, "wire")]
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     p = ctx.Process(target=_worker, args=(0, 1, _free_port(), cases, q, "nccl", parts))

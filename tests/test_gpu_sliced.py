@@ -173,6 +173,14 @@ def _worker(rank, world, port, cases, q, backend="gloo"):
             return SlicedNetwork(n, R, world, seed=seed, epoch=epoch, params=params, device=0,
                                  transport="dist", **faults)
         for n, R, kind, faults, *every in cases:
+            if kind == "wire":  # external RPCs (tests/test_gpu_wire.py), answers all-gathered
+                from test_gpu_wire import _batch_case, _handle_received_case
+
+                def mk(n_, R_, **kw):
+                    return SlicedNetwork(n_, R_, world, device=0, transport="dist", **kw)
+                _handle_received_case(sg, n, R, faults, make=mk)
+                _batch_case(sg, n, R, faults, "2P", make=mk)
+                continue
             run_parity(sg, n, R, kind, make_net=make, faults=faults, check_every=every[0] if every else 1)
         q.put(("ok", rank))
     except BaseException as e:
@@ -207,10 +215,17 @@ def test_sliced_dist_gloo_two_ranks(engine):
                (130, 256, "reinject", None)], "gloo")
 
 
+def test_sliced_dist_gloo_wire(engine):
+    # the wire boundary on two slice processes: every rank makes the same
+    # calls, the slices' answers are all-gathered and merged in key order
+    _spawn(2, [(300, 16, "wire", None), (400, 64, "wire", (0.05, 0.05, 0.05))], "gloo")
+
+
 def test_sliced_dist_rccl_single_rank(engine):
     # one RCCL rank: the all-reduce runs asynchronously on the process group's
     # stream and is applied on the engine stream a round later
-    _spawn(1, [(300, 64, "trickle", None), (600, 16, "origins", (0.05, 0.05, 0.05))], "nccl")
+    _spawn(1, [(300, 64, "trickle", None), (600, 16, "origins", (0.05, 0.05, 0.05)),
+               (300, 16, "wire", (0.05, 0.05, 0.05))], "nccl")
 
 
 def test_sliced_dist_rccl_deferred(engine):

@@ -54,9 +54,13 @@ def _compare(net, orc, off=None):
     (400, 8, (0.05, 0.05, 0.1), True),
 ])
 def test_push_batches_match_oracle(engine, n, R, faults, custom_keys):
+    _push_batch_case(engine, n, R, faults, custom_keys)
+
+
+def _push_batch_case(engine, n, R, faults, custom_keys, make=None):
     fk = dict(churn=faults[0], drop_push=faults[1], drop_pull=faults[2]) if faults else {}
     from oracle_lib import fault_threshold
-    net = engine.Network(n, R, seed=SEED, **fk)
+    net = (make or engine.Network)(n, R, seed=SEED, **fk)
     orc = OracleNet(n, R, seed=SEED, faults=[fault_threshold(p) for p in faults] if faults else None)
     rng = np.random.default_rng(n + R)
     if custom_keys:
@@ -100,13 +104,13 @@ def test_handle_received_seq(engine, n, R, faults):
     _handle_received_case(engine, n, R, faults, schedule="SEQ")
 
 
-def _handle_received_case(engine, n, R, faults, schedule="2P"):
+def _handle_received_case(engine, n, R, faults, schedule="2P", make=None):
     from oracle_lib import fault_threshold
     fk = dict(churn=faults[0], drop_push=faults[1], drop_pull=faults[2]) if faults else {}
     if schedule != "2P":
         fk["schedule"] = schedule
     osched = SCHED_SEQ if schedule == "SEQ" else SCHED_2P
-    net = engine.Network(n, R, seed=SEED, **fk)
+    net = (make or engine.Network)(n, R, seed=SEED, **fk)
     orc = OracleNet(n, R, seed=SEED, faults=[fault_threshold(p) for p in faults] if faults else None)
     rng = np.random.default_rng(7 * n + R)
     params = net.params
@@ -184,12 +188,16 @@ def test_handle_received_batch_matches_oracle(engine, n, R, faults, schedule):
     # response, then state, records, |P|, Statistics and known sets, and the
     # rounds after -- with repeated peers, repeated nodes (responses that show
     # the batch's earlier creations), empty RPCs and pulls
+    _batch_case(engine, n, R, faults, schedule)
+
+
+def _batch_case(engine, n, R, faults, schedule, make=None):
     from oracle_lib import fault_threshold
     fk = dict(churn=faults[0], drop_push=faults[1], drop_pull=faults[2]) if faults else {}
     if schedule != "2P":
         fk["schedule"] = schedule
     osched = SCHED_SEQ if schedule == "SEQ" else SCHED_2P
-    net = engine.Network(n, R, seed=SEED, **fk)
+    net = (make or engine.Network)(n, R, seed=SEED, **fk)
     orc = OracleNet(n, R, seed=SEED, faults=[fault_threshold(p) for p in faults] if faults else None)
     rng = np.random.default_rng(11 * n + R)
     params = net.params
@@ -240,5 +248,128 @@ def test_handle_received_batch_all_or_nothing(engine):
         # applied once it is well formed: node 0 answers its first Push (knows nothing yet)
         assert net.handle_received_batch([(0, 70, ok), (1, 71, ok)]) == [[engine.rpc_encode(True, b"", 0)]] * 2
         assert net.handle_received_batch([]) == []
+    finally:
+        net.close()
+
+
+# ---------------------------------------------------------------- multi-engine networks
+# The same boundary on a network split over several engines (local transport,
+# one GPU): rumor slices (every slice takes every RPC, the owner's as sent and
+# the others' emptied; answers merged in key order; safe_gossip_amd/sliced.py)
+# and class-row node shards (the RPC goes to the shard owning the node, a
+# global id; safe_gossip_amd/sharded.py).  Same oracle, same checks.
+
+def _sliced(world):
+    from safe_gossip_amd.sliced import SlicedNetwork
+    return lambda n, R, **kw: SlicedNetwork(n, R, world, transport="local", **kw)
+
+
+def _sharded(world, parts):
+    from safe_gossip_amd.sharded import ShardedNetwork
+    return lambda n, R, **kw: ShardedNetwork(n, R, world, transport="local", parts=parts, **kw)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("n,R,faults,schedule", [
+    (300, 16, None, "2P"),                 # slices of R_pad 8 (delivery records)
+    (250, 64, None, "2P"),
+    (120, 200, (0.05, 0.05, 0.05), "2P"),  # ragged wide slices, faults
+    (500, 4, (0.1, 0.1, 0.1), "2P"),
+    (250, 64, None, "SEQ"),
+])
+def test_handle_received_sliced(engine, world, n, R, faults, schedule):
+    _handle_received_case(engine, n, R, faults, schedule, make=_sliced(world))
+
+
+@pytest.mark.parametrize("world,parts", [(2, 1), (3, 2)])
+@pytest.mark.parametrize("n,R,faults", [
+    (250, 64, None),
+    (120, 200, (0.05, 0.05, 0.05)),
+    (900, 100, (0.1, 0.1, 0.1)),           # every rank owns nodes
+])
+def test_handle_received_sharded(engine, world, parts, n, R, faults):
+    _handle_received_case(engine, n, R, faults, make=_sharded(world, parts))
+
+
+def test_handle_received_sharded_class_rows_small_r(engine, monkeypatch):
+    # R_pad <= 16 with SAFE_GOSSIP_AMD_NO_DLV=1: class rows, external RPCs apply
+    monkeypatch.setenv("SAFE_GOSSIP_AMD_NO_DLV", "1")
+    _handle_received_case(engine, 600, 16, (0.05, 0.05, 0.05), make=_sharded(3, 2))
+
+
+@pytest.mark.parametrize("make", [_sliced(3), _sharded(3, 2)], ids=["sliced", "sharded"])
+@pytest.mark.parametrize("n,R,faults,custom_keys", [
+    (300, 16, None, True),
+    (150, 130, (0.1, 0.05, 0.05), True),
+    (600, 64, None, False),
+])
+def test_push_batches_multi_engine(engine, make, n, R, faults, custom_keys):
+    _push_batch_case(engine, n, R, faults, custom_keys, make=make)
+
+
+@pytest.mark.parametrize("make", [_sliced(2), _sharded(2, 2)], ids=["sliced", "sharded"])
+@pytest.mark.parametrize("n,R,faults,schedule", [
+    (1500, 64, (0.05, 0.05, 0.05), "2P"),
+    (800, 200, None, "2P"),
+])
+def test_handle_received_batch_multi_engine(engine, make, n, R, faults, schedule):
+    _batch_case(engine, n, R, faults, schedule, make=make)
+
+
+def test_handle_received_batch_sliced_seq(engine):
+    _batch_case(engine, 1000, 64, None, "SEQ", make=_sliced(3))
+
+
+def test_multi_engine_wire_errors(engine):
+    from safe_gossip_amd.sharded import ShardedNetwork
+    from safe_gossip_amd.sliced import SlicedNetwork
+    for net in (SlicedNetwork(50, 8, 2, transport="local"), ShardedNetwork(600, 40, 2, transport="local")):
+        n = net.n
+        try:
+            msg = engine.rpc_encode(False, net.rumor_key(3), 1)
+            with pytest.raises(engine.DeviceError, match="status -1"):
+                net.handle_received(0, n + 5, msg)        # before the first round
+            net.next_round()
+            with pytest.raises(engine.DeviceError, match="status -1"):
+                net.handle_received(0, 10, msg)           # peer inside the network
+            with pytest.raises(engine.DeviceError, match="status -1"):
+                net.handle_received(0, n + 5, engine.rpc_encode(False, b"no such rumor", 1))
+            with pytest.raises(engine.GossipError, match="status 5"):
+                net.handle_received_batch([(0, n + 5, msg), (1, n + 6, b"\x07\x00")])  # nothing applied
+            assert (int(net.known_all()[0, 0]) >> 3) & 1 == 0
+            assert net.handle_received(0, n + 5, msg) == [engine.rpc_encode(True, b"", 0)]
+            assert (int(net.known_all()[0, 0]) >> 3) & 1 == 1  # the copy created rumor 3 at once
+            with pytest.raises(engine.DeviceError, match="status -1"):
+                net.set_rumor_key(2, net.rumor_key(3))    # keys are distinct
+            net.set_rumor_key(3, b"renamed")
+            assert net.rumor_key(3) == b"renamed"
+            net.set_rumor_key(2, engine.default_rumor_key(3))  # free again
+        finally:
+            net.close()
+    # code-row shards (R_pad <= 16, 2P) take no external RPCs
+    net = ShardedNetwork(5000, 16, 2, transport="local")
+    try:
+        net.next_round()
+        with pytest.raises(engine.DeviceError, match="status -2"):
+            net.handle_received(0, 6000, engine.rpc_encode(False, net.rumor_key(3), 1))
+    finally:
+        net.close()
+
+
+def test_sliced_first_push_limit(engine):
+    # a slice counts empty answers to external first Pushes in its one-byte
+    # per-round count: at most slice_ext_limit per node and round
+    from safe_gossip_amd.sliced import SlicedNetwork
+    net = SlicedNetwork(40, 4, 2, transport="local")  # R_pad 2 per slice: 64 first Pushes
+    try:
+        net.next_round()
+        empty = engine.rpc_encode(False, b"", 0)
+        assert net.handle_received_batch([(0, 100 + i, empty) for i in range(64)])[63] == [engine.rpc_encode(True, b"", 0)]
+        with pytest.raises(engine.DeviceError, match="status -5"):
+            net.handle_received(0, 1000, empty)
+        net.handle_received(1, 1000, empty)  # another node, and pulls, still go through
+        net.handle_received(0, 1001, engine.rpc_encode(True, b"", 0))
+        net.next_round()
+        net.handle_received(0, 1000, empty)  # a new round
     finally:
         net.close()
