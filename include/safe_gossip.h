@@ -339,8 +339,7 @@ gs_status   gs_push_batch(gs_engine *e, uint32_t node, uint8_t *out, uint32_t ca
  * entry is created, or recorded on a B entry); peers_in_this_round and the
  * Statistics count it.  2P or SEQ schedule; after a gs_next_round.
  * Shard engine: `node` a global id this rank owns, peer >= the network's
- * n_nodes, after gs_shard_pull and exchange B of the round (class-row shards;
- * code-row shards, R_pad <= 16 under 2P, apply none: GS_ERR_UNSUPPORTED).
+ * n_nodes, after gs_shard_pull and exchange B of the round.
  * Rumor slice: the caller hands EVERY slice the RPC -- the slice holding its
  * message as sent, the others the empty RPC of the same kind -- and merges
  * the slices' answers in key order, one empty Pull only if every slice's is

@@ -55,7 +55,10 @@ GS_DEV T ge_seg(const T (&x)[NB], const T (&km)[NB]) {
 // PULL[x], and its next push code goes with its target into its exchange-A
 // row (spos_next) instead of PC[x]; blocks [blk_off, blk_off + grid) (a
 // pipeline part).
-template <int MODE, typename T, uint32_t kNpl, bool SH = false>
+// EXT: the round's external RPCs (gs_handle_received) are applied after the
+// internal deliveries, as in round_kernel (gs_kernels.hip, the a.n_ext
+// block); a variant of its own, launched only for a round that has some.
+template <int MODE, typename T, uint32_t kNpl, bool SH = false, bool EXT = false>
 __global__ __launch_bounds__(kDlv4Threads, (kNpl == 2 && sizeof(T) == 4) ? GS_DLV4_MINW_R16 : GS_DLV4_MINW)
 void round_kernel_dlv4(RoundArgs a) {
     constexpr bool DELIVER = MODE == 1;
@@ -278,6 +281,60 @@ void round_kernel_dlv4(RoundArgs a) {
             recv[q] += popcT(pl & M[q]);
             const bool pulled = (pulledM & M[q]) != 0;
             psize[q] = kk[q] + ((pulled && dzi[q] == kDlvNoZ) ? 1u : 0u);  // |peers_in_this_round|
+        }
+    }
+    // External RPCs to the lane's nodes (sorted by node, then call order),
+    // after every internal delivery (Gossip::receive, src/gossip.rs:118-163):
+    // a first RPC from a peer joins peers_in_this_round, a first Push is
+    // answered with the node's live set at that point, a copy creates an
+    // absent entry or is recorded on a B entry (the last copy per peer).
+    uint32_t ext_full[kNpl], ext_empty[kNpl], ext_recv[kNpl];
+#pragma unroll
+    for (uint32_t q = 0; q < kNpl; ++q) ext_full[q] = ext_empty[q] = ext_recv[q] = 0u;
+    if (EXT && DELIVER && a.n_ext && nv) {
+        uint32_t lo = 0, hi = a.n_ext;
+        const u64 key = (u64)x0 << 32;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (a.ext[mid] < key) lo = mid + 1; else hi = mid;
+        }
+        for (uint32_t i = lo; i < a.n_ext; ++i) {
+            const uint32_t qe = (uint32_t)(a.ext[i] >> 32) - x0;
+            if (qe >= nv) break;
+            const uint32_t info = (uint32_t)a.ext[i];
+            const T Mq = m1 << (qe * rp);
+            uint32_t dn = 0, df = 0, de = 0, dr = 0;
+            if (info & kExtNew) dn = 1u;
+            if ((info & kExtPush) && (info & kExtNew)) {
+                const uint32_t cnt = popcT((B | C | crB | crC) & Mq);
+                if (cnt) df = cnt; else de = 1u;
+            }
+            if (!(info & kExtEmpty)) {
+                dr = 1u;
+                const uint32_t r = info & 0xFFFu, c = (info >> 12) & 0xFFu;
+                const T bit = ((T)1 << r) << (qe * rp);
+                // a counter >= counter_max acts as C; 0 creates B and votes "less"
+                const T vC = c >= a.cmax ? bit : (T)0;
+                const T vB = (c >= 1u && c < a.cmax) ? bit : (T)0;
+                const T v2 = (c == 2u && c < a.cmax) ? bit : (T)0;
+                const T newc = notyet & bit;
+                const T rec = recB & bit & ((info & kExtRec) ? (T)~(T)0 : (T)0);
+                anyC |= rec & vC;
+                add5T(cv, rec & vB & (v2 | oc1r));
+                crB |= newc & ~vC;
+                crC |= newc & vC;
+                recB |= newc & ~vC;
+                oc1r |= newc & ~vC;
+                notyet &= ~newc;
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < kNpl; ++q)
+                if (q == qe) {
+                    psize[q] += dn;
+                    ext_full[q] += df;
+                    ext_empty[q] += de;
+                    ext_recv[q] += dr;
+                }
         }
     }
 
@@ -521,6 +578,17 @@ void round_kernel_dlv4(RoundArgs a) {
         if (q >= nv) break;
         const bool on = (onM & M[q]) != 0;
         uint4 v = stv[q];
+        if (EXT) {
+            // u16 deltas hold internal deliveries only (bounded per round):
+            // external RPCs go to the totals -- but a rumor slice's empty
+            // pulls go through emin (MIN over the slices; the engine bounds
+            // them, gs_engine.cpp slice_ext_limit)
+            u64 *s64 = const_cast<u64 *>(a.st64) + (u64)(x0 + q) * 4u;
+            if (a.emin) d_empty_pull[q] += ext_empty[q];
+            else if (ext_empty[q]) s64[0] += ext_empty[q];
+            if (ext_full[q]) s64[2] += ext_full[q];
+            if (ext_recv[q]) s64[3] += ext_recv[q];
+        }
         const uint32_t d_empty_push = (on && live[q] == 0u) ? 1u : 0u;
         if (a.emin) {  // rumor slice: empty only if empty in every slice (MIN per byte, caller)
             reinterpret_cast<uint16_t *>(a.emin)[x0 + q] =
@@ -548,14 +616,19 @@ static hipError_t launch_dlv4_t(const RoundArgs &a, int mode, hipStream_t s) {
     if (grid == 0) return hipSuccess;
     if (a.blk_off + grid > nblk) return hipErrorInvalidValue;
     const dim3 gd((uint32_t)grid), bd(kDlv4Threads);
+    // (external RPCs only ever come with a delivery: mode 1)
+    const bool ext = mode == 1 && a.n_ext > 0;
+    if (ext && !a.ext) return hipErrorInvalidValue;
     if (a.recvA) {  // code-row shard
         if (!a.sp.codes || !a.recvB || !a.sendA || !a.recvA_next || !a.spos_cur || !a.spos_next || !a.tg_next ||
             !a.sp.chunk)
             return hipErrorInvalidValue;
         if (mode == 0) hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL, true>), gd, bd, 0, s, a);
+        else if (ext) hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, true, true>), gd, bd, 0, s, a);
         else hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, true>), gd, bd, 0, s, a);
     } else {
         if (mode == 0) hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL>), gd, bd, 0, s, a);
+        else if (ext) hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, false, true>), gd, bd, 0, s, a);
         else hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL>), gd, bd, 0, s, a);
     }
     return hipGetLastError();

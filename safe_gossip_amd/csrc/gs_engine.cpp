@@ -475,6 +475,21 @@ gs_status seq_prepare(gs_engine *e) {
     return GS_OK;
 }
 
+// Code-row shards: an observation launch runs the per-node DLV kernel over
+// the pull codes unpacked into node order (the delivery records are the pull
+// kernel's, gs_shard_pull).
+hipError_t code_rows_obs(gs_engine *e, gs::RoundArgs &a) {
+    if (!(e->shard && e->dlv)) return hipSuccess;
+    if (e->deliver_pending) {
+        const hipError_t he = gs::launch_shard_pull_unpack(a.spos_cur, reinterpret_cast<const uint32_t *>(e->recvB),
+                                                           e->pc, e->g.n, e->stream);
+        if (he != hipSuccess) return he;
+    }
+    a.recvA = nullptr;
+    a.pull = e->pc;
+    return hipSuccess;
+}
+
 // Fill the observation buffers with the state after the last delivery.
 gs_status observe(gs_engine *e, bool dumps, bool digest = false, u64 *dpart = nullptr, uint32_t dp_lo = 0,
                   uint32_t dp_words = 0) {
@@ -506,16 +521,7 @@ gs_status observe(gs_engine *e, bool dumps, bool digest = false, u64 *dpart = nu
         st = seq_prepare(e);
         if (st != GS_OK) return st;
     }
-    if (e->shard && e->dlv) {
-        // code rows: the observation runs the per-node DLV kernel over the
-        // pull codes unpacked into node order (the delivery records are the
-        // pull kernel's)
-        if (e->deliver_pending)
-            GS_HIP(gs::launch_shard_pull_unpack(a.spos_cur, reinterpret_cast<const uint32_t *>(e->recvB), e->pc,
-                                                e->g.n, e->stream));
-        a.recvA = nullptr;
-        a.pull = e->pc;
-    }
+    GS_HIP(code_rows_obs(e, a));
     GS_HIP(gs::launch_round(a, e->deliver_pending ? 2 : 3, e->stream));
     if (!e->pending.empty()) {
         // Queued send_new calls: Gossip::new_message inserts MessageState::new
@@ -1635,10 +1641,8 @@ gs_status append_frame(int pull, const std::string &msg, uint8_t counter, uint8_
 
 // External RPCs (gs_handle_received*) are accepted once a round has run and
 // been delivered: a shard after gs_shard_pull, whose pull rows (exchange B)
-// the caller has waited for.  Code-row shards (R_pad <= 16, 2P) run the
-// packed DLV kernel, which applies none.
+// the caller has waited for.
 gs_status ext_ready(const gs_engine *e) {
-    if (e->shard && e->dlv) return GS_ERR_UNSUPPORTED;
     if (e->round == 0 || !e->deliver_pending) return GS_ERR_INVALID_ARGUMENT;  // after a next_round
     if (e->shard && e->pulled_round != e->round) return GS_ERR_INVALID_ARGUMENT;
     return GS_OK;
@@ -1671,10 +1675,11 @@ gs_status observe_node(gs_engine *e, uint32_t node, std::vector<uint16_t> &codes
     a.blk_off = (uint32_t)(seg0 / 256);
     a.blk_count = 1;
     if (e->deliver_pending) {
-        if (e->shard) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_edges[e->round % 2], 0));  // its in-lists
+        if (e->shard && !e->dlv) GS_HIP(hipStreamWaitEvent(e->stream, e->ev_edges[e->round % 2], 0));  // its in-lists
         st = seq_prepare(e);  // SEQ: the round's pull batches (no-op for 2P)
         if (st != GS_OK) return st;
     }
+    GS_HIP(code_rows_obs(e, a));
     GS_HIP(gs::launch_round(a, e->deliver_pending ? 2 : 3, e->stream));
     codes.resize(e->g.R);
     GS_HIP(hipMemcpyAsync(codes.data(), e->node_state, e->g.R * sizeof(uint16_t), hipMemcpyDeviceToHost,
@@ -1728,10 +1733,11 @@ gs_status observe_nodes(gs_engine *e, const std::vector<uint32_t> &nodes, std::v
     if (he == hipSuccess)
         he = hipMemcpyAsync(dev + blocks.size(), nodes.data(), m * sizeof(uint32_t), hipMemcpyHostToDevice,
                             e->stream);
-    if (he == hipSuccess && e->deliver_pending && e->shard)  // a shard's in-lists
+    if (he == hipSuccess && e->deliver_pending && e->shard && !e->dlv)  // a class-row shard's in-lists
         he = hipStreamWaitEvent(e->stream, e->ev_edges[e->round % 2], 0);
     if (he == hipSuccess && e->deliver_pending && seq_prepare(e) != GS_OK)
         he = hipErrorUnknown;  // SEQ: the round's pull batches
+    if (he == hipSuccess) he = code_rows_obs(e, a);
     if (he == hipSuccess) he = gs::launch_round(a, e->deliver_pending ? 2 : 3, e->stream);
     if (he == hipSuccess)
         he = hipMemcpyAsync(codes.data(), dcodes, codes.size() * sizeof(uint16_t), hipMemcpyDeviceToHost, e->stream);

@@ -846,7 +846,7 @@ hipError_t launch_round(const RoundArgs &a, int mode, hipStream_t s) {
         return a.g.small ? launch_mode<true, false, true>(a, mode, s) : launch_mode<false, false, true>(a, mode, s);
     if (a.DR) {   // delivery records (2P, R_pad <= 16)
         if (!a.g.small || a.g.rpad > 16) return hipErrorInvalidValue;
-        if (a.dlv_pack && (mode == 0 || mode == 1) && a.n_ext == 0) return launch_round_dlv4(a, mode, s);
+        if (a.dlv_pack && (mode == 0 || mode == 1)) return launch_round_dlv4(a, mode, s);
         return launch_mode<true, false, false, true>(a, mode, s);
     }
     if (w32_eligible(a, mode)) return launch_round_w32(a, mode, s);                   // gs_w32.hip

@@ -62,7 +62,7 @@ def test_sharded_dist_gloo_two_ranks(engine, parts):
     import torch.multiprocessing as mp
     world = 2
     cases = [(600, 48, "origins"), (1000, 3, "trickle"), (700, 256, "reinject"), (5000, 16, "origins"),
-             (900, 100, "wire")]
+             (900, 100, "wire"), (5000, 16, "wire")]
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()

@@ -291,6 +291,16 @@ def test_handle_received_sharded(engine, world, parts, n, R, faults):
     _handle_received_case(engine, n, R, faults, make=_sharded(world, parts))
 
 
+@pytest.mark.parametrize("world,parts,n,R,faults", [
+    (2, 2, 5000, 16, (0.05, 0.05, 0.05)),   # R_pad 16: two nodes per lane
+    (3, 1, 3000, 5, None),                  # R_pad 8: four nodes per lane
+])
+def test_handle_received_sharded_code_rows(engine, world, parts, n, R, faults):
+    # code rows (R_pad <= 16, 2P): the packed DLV round kernel's external-RPC
+    # variant applies the queue (gs_dlv4.hip EXT); observers unpack the pulls
+    _handle_received_case(engine, n, R, faults, make=_sharded(world, parts))
+
+
 def test_handle_received_sharded_class_rows_small_r(engine, monkeypatch):
     # R_pad <= 16 with SAFE_GOSSIP_AMD_NO_DLV=1: class rows, external RPCs apply
     monkeypatch.setenv("SAFE_GOSSIP_AMD_NO_DLV", "1")
@@ -311,6 +321,7 @@ def test_push_batches_multi_engine(engine, make, n, R, faults, custom_keys):
 @pytest.mark.parametrize("n,R,faults,schedule", [
     (1500, 64, (0.05, 0.05, 0.05), "2P"),
     (800, 200, None, "2P"),
+    (3000, 16, (0.05, 0.05, 0.05), "2P"),   # slices of R_pad 8 / code-row shards: the packed DLV kernel
 ])
 def test_handle_received_batch_multi_engine(engine, make, n, R, faults, schedule):
     _batch_case(engine, n, R, faults, schedule, make=make)
@@ -346,14 +357,6 @@ def test_multi_engine_wire_errors(engine):
             net.set_rumor_key(2, engine.default_rumor_key(3))  # free again
         finally:
             net.close()
-    # code-row shards (R_pad <= 16, 2P) take no external RPCs
-    net = ShardedNetwork(5000, 16, 2, transport="local")
-    try:
-        net.next_round()
-        with pytest.raises(engine.DeviceError, match="status -2"):
-            net.handle_received(0, 6000, engine.rpc_encode(False, net.rumor_key(3), 1))
-    finally:
-        net.close()
 
 
 def test_sliced_first_push_limit(engine):
