@@ -443,3 +443,34 @@ def test_parity_long_run_stats_folds(engine, n, R, faults):
     # u64 totals every 60 rounds (R_pad 16), so several folds happen here and
     # every counter must still equal the oracle's
     run_parity(engine, n, R, "steady", max_rounds=200, check_every=7, faults=faults)
+
+
+@pytest.mark.parametrize("faults", [None, (0.1, 0.05, 0.05)])
+def test_parity_two_epochs_wide(engine, faults):
+    # R_pad 256 (W = 4, config 4's lane shape), a few rumors, so most nodes
+    # hold all-zero planes for a while, then some; churn freezes some nodes;
+    # two epochs (clear() zeroes both plane buffers): every round's state and
+    # known sets, and the Statistics, are the oracle's.
+    from oracle_lib import fault_threshold
+    n, R = 3000, 200
+    fk = dict(churn=faults[0], drop_push=faults[1], drop_pull=faults[2]) if faults else {}
+    net = engine.Network(n, R, seed=SEED, **fk)
+    orc = OracleNet(n, R, seed=SEED, faults=[fault_threshold(p) for p in faults] if faults else None)
+    try:
+        for epoch, rounds in ((0, 6), (3, 40)):
+            if epoch:
+                net.clear(epoch=epoch)
+                orc.clear(epoch)
+            for r in range(0, R, 7):  # a few rumors: most nodes stay all-zero for a while
+                x = engine.origin_of(SEED, epoch, r, n)
+                net.send_new(x, r)
+                orc.send_new(x, r)
+            for _ in range(rounds):
+                net.next_round()
+                orc.next_round(SCHED_2P)
+                np.testing.assert_array_equal(net.dump_state(), orc.dump_state())
+                np.testing.assert_array_equal(net.known_all(), orc.known_all())
+            np.testing.assert_array_equal(net.statistics_all(), orc.statistics())
+    finally:
+        net.close()
+        orc.close()
