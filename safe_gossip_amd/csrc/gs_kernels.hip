@@ -32,6 +32,7 @@ namespace gs {
 // Words of planes one 256-lane block owns (its records are contiguous).
 constexpr uint32_t kBlockWords = 256u * kPlanes;
 constexpr uint32_t kStageIters = kBlockWords / 2u / 256u;  // uint4 loads per thread
+constexpr uint32_t kStageWords = kBlockWords + kBlockWords / 4u;  // (padded node strides: <= 10/8)
 
 #ifndef GS_RK_MINW
 #define GS_RK_MINW 1
@@ -76,7 +77,20 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     // (W <= 256), loaded first with 16-byte coalesced loads (clamped, so every
     // load is unconditional) and transposed through LDS below, instead of
     // eight strided 8-byte loads per lane.
-    __shared__ __attribute__((aligned(16))) u64 stage[kBlockWords];
+    // (W lanes per node, W >= 1: a node's 8 W words sit at a padded stride
+    // of 8 W + W words (8 W + 2 at W = 1), so the 32 lanes of a ds_read_b64
+    // / ds_write_b64 group -- 32 / W nodes -- fall on distinct banks; at the
+    // unpadded stride every node started on bank 0: 8-way conflicts at W = 4,
+    // 59 % of the LDS cycles at config 4)
+    __shared__ __attribute__((aligned(16))) u64 stage[kStageWords];
+    const uint32_t wlog = SMALL ? 0u : g.logr - 6u;
+    const uint32_t pst = SMALL ? 0u : (9u << wlog) + (wlog == 0u ? 1u : 0u);  // padded node stride (words)
+    auto sidx = [&](uint32_t li) -> uint32_t {  // the block's word li -> its stage index
+        return SMALL ? li : (li >> (wlog + 3u)) * pst + (li & ((8u << wlog) - 1u));
+    };
+    // uint4 i = the block's words 2i, 2i + 1 (one node's, 16-B aligned at the
+    // padded stride too): the thread's i = tid + 256 m sit s4 + m s4d apart
+    const uint32_t s4 = sidx(2u * threadIdx.x), s4d = SMALL ? 512u : (64u >> wlog) * pst;
     const uint32_t npu_blk = SMALL ? (1u << g.lognpu) : 1u;
     const u64 blk_base = (u64)bid * (kBlockWords / npu_blk);
     const uint32_t blk_v4 = (uint32_t)min((u64)(kBlockWords / npu_blk),
@@ -245,17 +259,18 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         (!filt || zneed) && !((eskip >> kBatchE) & 1u))
         s2 = L.load_cls(S, pick_sib(sb8.e, kBatchE));
     {
-        uint4 *dst4 = reinterpret_cast<uint4 *>(stage);
-        dst4[threadIdx.x] = st0;
-        dst4[threadIdx.x + 256u] = st1;
-        dst4[threadIdx.x + 512u] = st2;
-        dst4[threadIdx.x + 768u] = st3;
+        *reinterpret_cast<uint4 *>(&stage[s4]) = st0;
+        *reinterpret_cast<uint4 *>(&stage[s4 + s4d]) = st1;
+        *reinterpret_cast<uint4 *>(&stage[s4 + 2u * s4d]) = st2;
+        *reinterpret_cast<uint4 *>(&stage[s4 + 3u * s4d]) = st3;
     }
     __syncthreads();
     u64 P[kPlanes];
+    // the lane's plane 0 word in the stage (plane p: + p W; SMALL: its unit's)
+    const uint32_t sb0 = sidx((uint32_t)(L.plane_index(0) - blk_base));
 #pragma unroll
     for (int p = 0; p < kPlanes; ++p) {
-        const u64 v = valid ? stage[L.plane_index(p) - blk_base] : 0ull;
+        const u64 v = valid ? stage[sb0 + ((uint32_t)p << wlog)] : 0ull;
         P[p] = SMALL ? ((v >> L.sh) & L.m) : v;
     }
 
@@ -756,19 +771,19 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         for (int p = 0; p < kPlanes; ++p) {
             u64 v = valid ? ((N[p] & L.m) << L.sh) : 0ull;
             for (uint32_t o = 1; o < npu; o <<= 1) v |= __shfl_xor(v, (int)o, 64);
-            if (valid && (x & (npu - 1u)) == 0) stage[L.plane_index(p) - blk_base] = v;
+            if (valid && (x & (npu - 1u)) == 0) stage[sidx((uint32_t)(L.plane_index(p) - blk_base))] = v;
         }
     } else if (valid) {
 #pragma unroll
-        for (int p = 0; p < kPlanes; ++p) stage[L.plane_index(p) - blk_base] = N[p];
+        for (int p = 0; p < kPlanes; ++p) stage[sb0 + ((uint32_t)p << wlog)] = N[p];
     }
     __syncthreads();
     {
-        const uint4 *src4 = reinterpret_cast<const uint4 *>(stage);
         uint4 *dst4 = reinterpret_cast<uint4 *>(a.Snext + blk_base);
         // streaming (nontemporal) stores: 3.11 -> 3.01 ms per round kernel at
         // config 4 (nontemporal plane loads measured slower: 3.27 ms).
-        for (uint32_t i = threadIdx.x; i < blk_v4; i += blockDim.x) nt_store4(src4[i], &dst4[i]);
+        for (uint32_t i = threadIdx.x, si = s4; i < blk_v4; i += blockDim.x, si += s4d)
+            nt_store4(*reinterpret_cast<const uint4 *>(&stage[si]), &dst4[i]);
     }
     if (SHARD) {
         // push row of round t+1: the push batch's class code, to owner(t_{t+1}(x))
