@@ -1,5 +1,5 @@
 #!/bin/bash
-# Padded LDS stage (bank-conflict-free plane transposition): parity, then A/B of configs 4 and 3 (base tree vs HEAD), and SQ LDS counters
+# Round kernel change: parity, then A/B of configs 4 and 3 (base tree vs HEAD), and SQ LDS counters
 set -e
 T=${1:-a}
 O=gpurun_out/r5pad_$T; mkdir -p $O
