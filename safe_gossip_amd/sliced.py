@@ -58,6 +58,25 @@ def merge_known(per, bounds, n: int, kw: int) -> np.ndarray:
     return out
 
 
+def merge_answers(per_slice: List[List[bytes]]) -> List[bytes]:
+    """One RPC's answers from every slice (frames of bincode GossipRpc): the
+    non-empty frames in key order (the BTreeMap order a single Gossip
+    iterates, src/gossip.rs:126-148), one empty frame if every slice
+    answered empty, none if no slice answered."""
+    frames = [f for fs in per_slice for f in fs]
+    if not frames:
+        return []
+    full = []
+    for f in frames:
+        _, m, ctr = rpc_decode(f)
+        if m or ctr:
+            full.append((m, f))
+    if not full:
+        return [frames[0]]
+    full.sort(key=lambda kv: kv[0])
+    return [f for _, f in full]
+
+
 class _Slice:
     """One rank's engine (rumors [lo, hi)) and its empty-count buffers."""
 
@@ -309,20 +328,7 @@ class SlicedNetwork:
         self._rumor_of[key] = rumor
 
     def _merge(self, per_slice: List[List[bytes]]) -> List[bytes]:
-        """One RPC's answers from every slice: the non-empty frames in key
-        order, or one empty frame (every slice answered empty), or none."""
-        frames = [f for fs in per_slice for f in fs]
-        if not frames:
-            return []
-        full = []
-        for f in frames:
-            pull, m, ctr = rpc_decode(f)
-            if m or ctr:
-                full.append((m, f))
-        if not full:
-            return [frames[0]]
-        full.sort(key=lambda kv: kv[0])
-        return [f for _, f in full]
+        return merge_answers(per_slice)
 
     def _gather_lists(self, mine: List[List[List[bytes]]]) -> List[List[List[bytes]]]:
         """Per slice, per RPC answers of every slice (dist: all-gathered)."""
