@@ -41,12 +41,13 @@ def _worker(rank, world, port, cases, q, backend="gloo", parts=None, env=None):
                                   transport="dist", parts=parts)
         for n, R, kind in cases:
             if kind == "wire":  # external RPCs (tests/test_gpu_wire.py): the owner answers, all-gathered
-                from test_gpu_wire import _batch_case, _handle_received_case
+                from test_gpu_wire import _batch_case, _handle_received_case, _push_batch_case
 
                 def mk(n_, R_, **kw):
                     return ShardedNetwork(n_, R_, world, device=0, transport="dist", parts=parts, **kw)
                 _handle_received_case(sg, n, R, (0.05, 0.05, 0.05), make=mk)
                 _batch_case(sg, n, R, None, "2P", make=mk)
+                _push_batch_case(sg, n, R, (0.05, 0.05, 0.05), True, make=mk)
                 continue
             run_parity(sg, n, R, kind, make_net=make)
         q.put(("ok", rank))

@@ -174,12 +174,13 @@ def _worker(rank, world, port, cases, q, backend="gloo"):
                                  transport="dist", **faults)
         for n, R, kind, faults, *every in cases:
             if kind == "wire":  # external RPCs (tests/test_gpu_wire.py), answers all-gathered
-                from test_gpu_wire import _batch_case, _handle_received_case
+                from test_gpu_wire import _batch_case, _handle_received_case, _push_batch_case
 
                 def mk(n_, R_, **kw):
                     return SlicedNetwork(n_, R_, world, device=0, transport="dist", **kw)
                 _handle_received_case(sg, n, R, faults, make=mk)
                 _batch_case(sg, n, R, faults, "2P", make=mk)
+                _push_batch_case(sg, n, R, faults, True, make=mk)
                 continue
             run_parity(sg, n, R, kind, make_net=make, faults=faults, check_every=every[0] if every else 1)
         q.put(("ok", rank))
