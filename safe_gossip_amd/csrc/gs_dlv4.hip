@@ -84,6 +84,7 @@ void round_kernel_dlv4(RoundArgs a) {
     const uint32_t lpw_log = lognpu - kLogNpl;  // lanes per word = npu / kNpl
     const uint32_t shL = (x0 & ((1u << lognpu) - 1u)) << lr;
 
+    __builtin_amdgcn_s_setprio(2);  // the load-issue phase at raised priority (gs_kernels.hip)
     // ---- own round-t planes, staged through LDS (16-byte coalesced loads)
     __shared__ __attribute__((aligned(16))) u64 stage[kDlv4Threads * kNpl * kPlanes / 4];  // >= 8 words per unit
     const uint32_t units_blk = (kDlv4Threads * kNpl) >> lognpu;
@@ -181,6 +182,7 @@ void round_kernel_dlv4(RoundArgs a) {
         pv0[q] = off ? pe[0] : 0u;
         pv1[q] = off ? pe[2] : 0u;
     }
+    __builtin_amdgcn_s_setprio(0);
     __syncthreads();
     // class planes now; the five b planes only for the transition (still in
     // LDS then: fewer registers live across the deliveries)
@@ -550,6 +552,7 @@ void round_kernel_dlv4(RoundArgs a) {
         any_live |= live[q] != 0u;
     }
     __syncthreads();  // every lane is done reading stage; blk_any is cleared
+    __builtin_amdgcn_s_setprio(1);
     {
         const uint32_t lpw = 1u << lpw_log;
 #pragma unroll

@@ -72,6 +72,9 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
 
     __shared__ uint32_t blk_any;  // some node pushes a live rumor in round t+1
     if (threadIdx.x == 0) blk_any = 0;
+    // the load-issue phase at raised priority: a young wave's requests go out
+    // ahead of older waves' compute (issue is by priority, then age)
+    __builtin_amdgcn_s_setprio(2);
 
     // ---- own round-t planes: the block's records are one contiguous range
     // (W <= 256), loaded first with 16-byte coalesced loads (clamped, so every
@@ -258,6 +261,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     if (DELIVER && !SEQ && !DLV && !SHARD && r > kBatchE && !(tgw & kTgNoPull) &&
         (!filt || zneed) && !((eskip >> kBatchE) & 1u))
         s2 = L.load_cls(S, pick_sib(sb8.e, kBatchE));
+    __builtin_amdgcn_s_setprio(0);
     {
         *reinterpret_cast<uint4 *>(&stage[s4]) = st0;
         *reinterpret_cast<uint4 *>(&stage[s4 + s4d]) = st1;
@@ -765,6 +769,7 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     if (__ballot(live_new != 0u) != 0ull && (threadIdx.x & 63u) == 0u) blk_any = 1u;
     __syncthreads();  // also: every lane is done reading stage
     const bool blk_live = blk_any != 0u;
+    __builtin_amdgcn_s_setprio(1);  // the drain: retire the block, free its slot
     if (SMALL) {
         const uint32_t npu = 1u << g.lognpu;
 #pragma unroll
