@@ -52,7 +52,8 @@ typedef enum {
     GS_ERR_IO = 4,                /* Error::Io (reserved)   */
     GS_ERR_SERIALISATION = 5,     /* Error::Serialisation: undecodable RPC bytes, buffer too small */
     GS_ERR_INVALID_ARGUMENT = -1,
-    GS_ERR_UNSUPPORTED = -2,      /* parameters outside the packed state layout */
+    GS_ERR_UNSUPPORTED = -2,      /* parameters outside the packed state layout,
+                                     or a shard layout the engine cannot hold */
     GS_ERR_HIP = -3,
     GS_ERR_OUT_OF_MEMORY = -4,
     GS_ERR_DEVICE_LIMIT = -5      /* a node's in-degree exceeded the packed
@@ -62,7 +63,9 @@ typedef enum {
 /* Delivery order of a round.  2P: the reference harness
  * with each pull batch delivered after all push batches of the round.  SEQ:
  * the harness's literal order (src/gossiper.rs:217-234), each pull answered
- * from the responder's current state and delivered at once; single-GPU only. */
+ * from the responder's current state and delivered at once.  SEQ runs on one
+ * engine and on rumor slices (cfg.rumor_slice); node
+ * shards refuse it (GS_ERR_UNSUPPORTED: its pull chains cross node ranges). */
 typedef enum { GS_SCHED_2P = 0, GS_SCHED_SEQ = 1 } gs_schedule;
 
 typedef struct {
@@ -301,6 +304,13 @@ gs_status   gs_slice_apply(gs_engine *e, uint32_t which);
  * buffer at a time; a second call adds the first at once).  The buffer must
  * stay unchanged until that kernel ran. */
 gs_status   gs_slice_defer(gs_engine *e, uint32_t which);
+/* External first Pushes a slice answers per node and round (its one-byte
+ * empty count and u16 deltas must not wrap; GS_ERR_DEVICE_LIMIT past it):
+ * by default min(200, 32 R_pad) of the slice's own R_pad, which differs
+ * between slices of uneven size.  Set every slice of a network to the same
+ * bound, min(200, 32 * next_pow2(floor(R / world))) = the smallest slice's,
+ * so a batch is refused by all of them or by none (1..the slice's own). */
+gs_status   gs_slice_set_ext_limit(gs_engine *e, uint32_t limit);
 
 /* ---- Wire format (src/messages.rs) ----------------------------------------
  * GossipRpc as maidsafe_utilities::serialisation (bincode, fixed-width little

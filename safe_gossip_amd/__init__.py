@@ -170,6 +170,7 @@ SYMBOLS = {
     "gs_slice_bind": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "gs_slice_apply": (ctypes.c_int, [_P, ctypes.c_uint32]),
     "gs_slice_defer": (ctypes.c_int, [_P, ctypes.c_uint32]),
+    "gs_slice_set_ext_limit": (ctypes.c_int, [_P, ctypes.c_uint32]),
 }
 
 _LIB = None

@@ -128,6 +128,7 @@ struct gs_engine {
     std::vector<Ext> ext;                   // in call order
     std::set<std::pair<uint32_t, uint32_t>> ext_peers;  // (node, peer) heard from this round
     std::map<uint32_t, uint32_t> ext_fp;  // rumor slices: answered external first Pushes per node this round
+    uint32_t ext_limit = 0;               // rumor slices: the network's bound on them (0: this slice's own)
     u64 *ext_dev = nullptr;
     uint32_t ext_cap = 0, ext_uploaded = 0;
     uint16_t *node_state = nullptr;         // one node's observed codes [R]
@@ -567,7 +568,7 @@ const char *gs_status_string(gs_status s) {
     case GS_ERR_IO: return "I/O error";
     case GS_ERR_SERIALISATION: return "Serialisation error";
     case GS_ERR_INVALID_ARGUMENT: return "invalid argument";
-    case GS_ERR_UNSUPPORTED: return "parameters outside the packed state layout (counter_max<=3, max_c_rounds<=3, max_rounds<=32, R<=4096)";
+    case GS_ERR_UNSUPPORTED: return "parameters outside the packed state layout (counter_max<=3, max_c_rounds<=3, max_rounds<=32, R<=4096), or a shard layout the engine cannot hold (class-row rank above 33.3 M nodes)";
     case GS_ERR_HIP: return "HIP runtime error (no usable MI355X device?)";
     case GS_ERR_OUT_OF_MEMORY: return "out of device memory";
     case GS_ERR_DEVICE_LIMIT: return "device limit hit (in-degree > 30, in-list or receive-row capacity, SEQ depth)";
@@ -682,6 +683,8 @@ gs_status check_config(const gs_config *cfg, uint32_t rank, uint32_t world, uint
         // code rows run the delivery-record build over max(owned nodes, slot
         // keys) sources: only on its binned plan
         if (sp->codes && !gs::dlv_plan(std::max(sp->m, shard_keys(*sp))).binned) return GS_ERR_UNSUPPORTED;
+        // class rows build the next round's in-lists in LDS bins (gs_shard.hip edge_bin)
+        if (!gs::shard_edges_fit(*sp)) return GS_ERR_UNSUPPORTED;
     }
     return GS_OK;
 }
@@ -1660,7 +1663,12 @@ bool ext_ids(const gs_engine *e, uint32_t node, uint32_t peer) {
 // as one byte (MIN) and the u16 Statistics deltas take between folds (sized
 // for 32 * R_pad + 32 per round, the internal count being at most 30): at
 // most this many first Pushes per node and round (GS_ERR_DEVICE_LIMIT).
-uint32_t slice_ext_limit(const gs_engine *e) { return std::min<uint32_t>(200u, 32u * e->g.rpad); }
+// The bound must be the same on every slice of a network (a batch is refused
+// on all of them or applied on all of them, and |peers_in_this_round| stays
+// equal on every slice): the caller sets the network's, the smallest over its
+// slices (gs_slice_set_ext_limit; SlicedNetwork does).
+uint32_t slice_own_ext_limit(const gs_engine *e) { return std::min<uint32_t>(200u, 32u * e->g.rpad); }
+uint32_t slice_ext_limit(const gs_engine *e) { return e->ext_limit ? e->ext_limit : slice_own_ext_limit(e); }
 
 // Post-delivery state codes of one node (gs_dump_state's codes), external
 // RPCs queued so far included: the observation kernel over the node's block.
@@ -1748,6 +1756,12 @@ gs_status observe_nodes(gs_engine *e, const std::vector<uint32_t> &nodes, std::v
 }  // namespace
 
 extern "C" {
+
+gs_status gs_slice_set_ext_limit(gs_engine *e, uint32_t limit) {
+    if (!e || !e->slice || limit == 0 || limit > slice_own_ext_limit(e)) return GS_ERR_INVALID_ARGUMENT;
+    e->ext_limit = limit;
+    return GS_OK;
+}
 
 gs_status gs_handle_received_batch(gs_engine *e, uint32_t count, const uint32_t *nodes, const uint32_t *peers,
                                    const uint8_t *msgs, const uint32_t *off, const uint32_t *len, uint8_t *out,

@@ -374,6 +374,11 @@ struct ShardEdgeLayout {
 ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t parts, bool codes = false);
 size_t shard_plan_words(const ShardPlan &P, ShardPlanLayout *L);
 size_t shard_edge_words(const ShardPlan &P, ShardEdgeLayout *L);
+// A class-row shard's next-round in-list build (edge_bin) keeps 8 B of LDS
+// per 2 K-node bin: ranks of up to 16256 bins (33.3 M nodes) fit gfx950's
+// 160 KiB; check_config refuses larger ones (GS_ERR_UNSUPPORTED).
+constexpr size_t kEdgeBinMaxLds = 159u * 1024u;  // (1 KiB left for its static LDS)
+bool shard_edges_fit(const ShardPlan &P);
 // Plan of `round`: owned targets, send slots, and the ids of every block of
 // the exchange-A buffer bufA (which carries them one round ahead).
 hipError_t launch_shard_plan(const ShardPlan &P, const ShardPlanLayout &L, uint32_t *words, u64 *bufA,

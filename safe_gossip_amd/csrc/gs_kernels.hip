@@ -29,10 +29,14 @@
 
 namespace gs {
 
-// Words of planes one 256-lane block owns (its records are contiguous).
-constexpr uint32_t kBlockWords = 256u * kPlanes;
-constexpr uint32_t kStageIters = kBlockWords / 2u / 256u;  // uint4 loads per thread
-constexpr uint32_t kStageWords = kBlockWords + kBlockWords / 4u;  // (padded node strides: <= 10/8)
+// Lanes of a round-kernel block (BLK): 128 for the single engine's
+// transitions on the gather path with 64 <= R_pad <= 1024 (128 / W nodes;
+// a thread's uint4 steps of 2 BLK words must cover whole nodes), 256
+// otherwise -- the observation launches and the shard parts count their
+// blocks in 256 lanes (gs_engine.cpp).  Two-wave blocks wait at their two
+// barriers for two waves, not four: config 4's round kernel 2.476 -> 2.370
+// ms, 2.816 -> 2.715 ms per step (profiles/r5/ab_blk128/).
+constexpr uint32_t kRkSmallBlk = 128u;
 
 #ifndef GS_RK_MINW
 #define GS_RK_MINW 1
@@ -55,11 +59,19 @@ GS_DEV Cls decode16(uint32_t code) {
 // DLV: delivery records (gs_common.h DlvRec) replace every class-plane
 // gather: a lane's pushers' push codes are in its own record and its pull
 // batch in PULL[x], both read coalesced.
-template <bool SMALL, int MODE, bool SHARD, bool SEQ, bool DLV>
-__global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
+template <bool SMALL, int MODE, bool SHARD, bool SEQ, bool DLV, uint32_t BLK = 256u>
+__global__ __launch_bounds__(BLK, GS_RK_MINW) void round_kernel(RoundArgs a) {
     constexpr bool DELIVER = (MODE == 1 || MODE == 2);
     constexpr bool TRANSITION = (MODE == 0 || MODE == 1);
     const Geometry &g = a.g;
+    // words of planes one block owns (its records are contiguous), uint4
+    // loads per thread, and the stage (padded node strides: <= 10/8)
+    constexpr uint32_t kBlk = BLK;
+    static_assert(BLK == 256u || (!SMALL && !SHARD && !SEQ && !DLV && (MODE == 0 || MODE == 1)),
+                  "smaller blocks: single-engine gather-path transitions only");
+    constexpr uint32_t kBlockWords = kBlk * kPlanes;
+    constexpr uint32_t kStageIters = kBlockWords / 2u / kBlk;
+    constexpr uint32_t kStageWords = kBlockWords + kBlockWords / 4u;
     if (a.zero_buf || a.zero_rows) zero_for_build(a.zero_buf, a.zero_words, a.zero_rows);
     if (a.zero_buf2) zero_for_build(a.zero_buf2, a.zero_words2, nullptr);
     const uint32_t bid = (!TRANSITION && a.blk_list) ? a.blk_list[blockIdx.x] : blockIdx.x + a.blk_off;
@@ -92,8 +104,8 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
         return SMALL ? li : (li >> (wlog + 3u)) * pst + (li & ((8u << wlog) - 1u));
     };
     // uint4 i = the block's words 2i, 2i + 1 (one node's, 16-B aligned at the
-    // padded stride too): the thread's i = tid + 256 m sit s4 + m s4d apart
-    const uint32_t s4 = sidx(2u * threadIdx.x), s4d = SMALL ? 512u : (64u >> wlog) * pst;
+    // padded stride too): the thread's i = tid + kBlk m sit s4 + m s4d apart
+    const uint32_t s4 = sidx(2u * threadIdx.x), s4d = SMALL ? 2u * kBlk : ((kBlk / 4u) >> wlog) * pst;
     const uint32_t npu_blk = SMALL ? (1u << g.lognpu) : 1u;
     const u64 blk_base = (u64)bid * (kBlockWords / npu_blk);
     const uint32_t blk_v4 = (uint32_t)min((u64)(kBlockWords / npu_blk),
@@ -101,9 +113,9 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
     static_assert(kStageIters == 4, "stage loads are unrolled by hand");
     const uint4 *src4 = reinterpret_cast<const uint4 *>(S + blk_base);
     const uint4 st0 = src4[min(threadIdx.x, blk_v4 - 1u)];
-    const uint4 st1 = src4[min(threadIdx.x + 256u, blk_v4 - 1u)];
-    const uint4 st2 = src4[min(threadIdx.x + 512u, blk_v4 - 1u)];
-    const uint4 st3 = src4[min(threadIdx.x + 768u, blk_v4 - 1u)];
+    const uint4 st1 = src4[min(threadIdx.x + kBlk, blk_v4 - 1u)];
+    const uint4 st2 = src4[min(threadIdx.x + 2u * kBlk, blk_v4 - 1u)];
+    const uint4 st3 = src4[min(threadIdx.x + 3u * kBlk, blk_v4 - 1u)];
 
     // ---- coalesced per-node metadata (level 1)
     // Statistics deltas of x, loaded with the other level-1 reads so the
@@ -842,6 +854,20 @@ __global__ __launch_bounds__(256, GS_RK_MINW) void round_kernel(RoundArgs a) {
 
 template <bool SMALL, bool SHARD, bool SEQ, bool DLV = false>
 static hipError_t launch_mode(const RoundArgs &a, int mode, hipStream_t s) {
+    if constexpr (!SMALL && !SHARD && !SEQ && !DLV) {
+        if ((mode == 0 || mode == 1) && a.g.W <= 16u && a.blk_count == 0 && a.blk_off == 0) {
+            const u64 grid = (a.g.nseg + kRkSmallBlk - 1) / kRkSmallBlk;
+            if (grid == 0) return hipSuccess;
+            if (a.blk_list) return hipErrorInvalidValue;
+            if (mode == 0)
+                hipLaunchKernelGGL((round_kernel<false, 0, false, false, false, kRkSmallBlk>), dim3((uint32_t)grid),
+                                   dim3(kRkSmallBlk), 0, s, a);
+            else
+                hipLaunchKernelGGL((round_kernel<false, 1, false, false, false, kRkSmallBlk>), dim3((uint32_t)grid),
+                                   dim3(kRkSmallBlk), 0, s, a);
+            return hipGetLastError();
+        }
+    }
     const uint32_t block = 256;
     const u64 grid = a.blk_count ? a.blk_count : (a.g.nseg + block - 1) / block;
     if (grid == 0) return hipSuccess;

@@ -213,6 +213,7 @@ constexpr uint32_t kEdgeSortThreads = 256;
 constexpr uint32_t kEdgeTails = kEdgeBin / 8;              // tail slots per bin (mean ~48)
 constexpr uint32_t kMutual = 1u << 31;                     // key bit: the pusher is the node's own target
 static_assert(kEdgeChunk % kEdgeBinThreads == 0, "edge_bin: whole slots per thread");
+static_assert(kEdgeChunk <= 0xFFFFu && kEdgeBinCap < 0xFFFFu, "edge_bin: 16-bit offsets and reservations");
 
 __global__ __launch_bounds__(kEdgeBinThreads) void edge_bin(ShardPlan P, const u64 *__restrict__ recvA,
                                                             const uint32_t *__restrict__ tg, uint64_t seed,
@@ -224,8 +225,9 @@ __global__ __launch_bounds__(kEdgeBinThreads) void edge_bin(ShardPlan P, const u
     uint16_t *sz = reinterpret_cast<uint16_t *>(sh + kEdgeChunk);  // [kEdgeChunk] z in the bin
     uint16_t *sb = sz + kEdgeChunk;                                // [kEdgeChunk] bin of each staged entry
     uint32_t *cnt = sh + 2 * kEdgeChunk;                           // [nb] counts, then cursors
-    uint32_t *off = cnt + nb;                                      // [nb] chunk-local starts
-    uint32_t *res = off + nb;                                      // [nb] reserved start in the bin's region
+    // [nb] chunk-local start (low 16 bits, < kEdgeChunk) | reserved start in
+    // the bin's region << 16 (<= kEdgeBinCap): 8 B of LDS per bin in all
+    uint32_t *offres = cnt + nb;
     __shared__ uint32_t lds_scan[kEdgeBinThreads / 64];
     for (uint32_t i = threadIdx.x; i < nb; i += kEdgeBinThreads) cnt[i] = 0u;
     __syncthreads();
@@ -259,7 +261,6 @@ __global__ __launch_bounds__(kEdgeBinThreads) void edge_bin(ShardPlan P, const u
     uint32_t run = block_exclusive_scan_t<kEdgeBinThreads>(sum, lds_scan, total);
     for (uint32_t q = 0; q < bper && b0 + q < nb; ++q) {
         const uint32_t b = b0 + q, c = cnt[b];
-        off[b] = run;
         uint32_t r0 = 0;
         if (c) {
             r0 = atomicAdd(&fill[b], c);
@@ -268,7 +269,7 @@ __global__ __launch_bounds__(kEdgeBinThreads) void edge_bin(ShardPlan P, const u
                 r0 = kEdgeBinCap;  // drop this run; the round reports the limit
             }
         }
-        res[b] = r0;
+        offres[b] = run | (r0 << 16);
         cnt[b] = run;  // cursor
         run += c;
     }
@@ -284,7 +285,7 @@ __global__ __launch_bounds__(kEdgeBinThreads) void edge_bin(ShardPlan P, const u
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < total; i += kEdgeBinThreads) {
-        const uint32_t b = sb[i], slot = res[b] + (i - off[b]);
+        const uint32_t b = sb[i], orb = offres[b], slot = (orb >> 16) + (i - (orb & 0xFFFFu));
         if (slot < kEdgeBinCap) region[(u64)b * kEdgeBinCap + slot] = make_uint2(skey[i], sz[i]);
     }
 }
@@ -383,6 +384,15 @@ __host__ __device__ inline uint32_t edge_bins(const ShardPlan &P) {
     return (uint32_t)(((u64)P.m + kEdgeBin - 1) / kEdgeBin);
 }
 
+// Dynamic LDS of edge_bin: the staged chunk (key, z, bin) and 8 B per bin.
+static size_t edge_bin_lds(uint32_t nb) { return (2 * (size_t)kEdgeChunk + 2 * (size_t)nb) * sizeof(uint32_t); }
+
+bool shard_edges_fit(const ShardPlan &P) {
+    // class-row shards only (code rows build no in-lists ahead); the bin of a
+    // staged entry is a u16 as well
+    return P.codes || (edge_bin_lds(edge_bins(P)) <= kEdgeBinMaxLds && edge_bins(P) <= 0xFFFFu);
+}
+
 ShardPlan shard_plan(uint32_t n, uint32_t G, uint32_t g, uint32_t W, uint32_t parts, bool codes) {
     ShardPlan P{};
     P.codes = codes ? 1u : 0u;
@@ -476,7 +486,8 @@ hipError_t launch_shard_edges(const ShardPlan &P, const ShardEdgeLayout &L, uint
     if (P.m == 0) return hipSuccess;  // no local targets: nothing is received
     const uint32_t nb = edge_bins(P), slots = P.G * P.P * P.capP;
     uint2 *region = reinterpret_cast<uint2 *>(w + L.region);
-    const size_t lds = (2 * (size_t)kEdgeChunk + 3 * (size_t)nb) * sizeof(uint32_t);
+    if (!shard_edges_fit(P)) return hipErrorInvalidValue;  // (check_config refuses such a rank)
+    const size_t lds = edge_bin_lds(nb);
     hipError_t e = hipFuncSetAttribute((const void *)edge_bin, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(edge_bin, dim3((slots + kEdgeChunk - 1) / kEdgeChunk), dim3(kEdgeBinThreads), lds, s, P, recvA,

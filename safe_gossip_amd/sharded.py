@@ -368,8 +368,10 @@ class ShardedNetwork:
     # shard holds the rumor keys; an RPC goes to the shard owning its node (a
     # global id).  dist: every rank makes the same calls, the owner answers
     # and the answers are all-gathered.  Code-row shards (R_pad <= 16, 2P)
-    # take no external RPCs (GS_ERR_UNSUPPORTED).
+    # apply them through the EXT variant of the packed DLV kernel
+    # (gs_dlv4.hip), class-row shards in their round kernel's n_ext block.
     def set_rumor_key(self, rumor: int, key: bytes) -> None:
+        self._keys = None  # the key set _validate checks against, rebuilt on next use
         for s in self.shards:
             _check(self.lib.gs_set_rumor_key(s.h, rumor, _buf(key), len(key)))
 
@@ -408,7 +410,9 @@ class ShardedNetwork:
         """Every RPC checked before any shard applies one (the batch is whole
         or nothing across shards too): ids, then the frame (GossipError on
         bad bytes, src/gossiper.rs:89-94) and its rumor key."""
-        keys = {self.rumor_key(r) for r in range(self.R)}
+        if getattr(self, "_keys", None) is None:  # (2 FFI calls per rumor: built once per key change)
+            self._keys = {self.rumor_key(r) for r in range(self.R)}
+        keys = self._keys
         for node, peer, msg in rpcs:
             if not 0 <= node < self.n or peer < self.n:
                 _check(-1)

@@ -77,6 +77,13 @@ def merge_answers(per_slice: List[List[bytes]]) -> List[bytes]:
     return [f for _, f in full]
 
 
+def slice_ext_limit(n_rumors: int, world: int) -> int:
+    """The network's bound on external first Pushes answered per node and
+    round: min(200, 32 R_pad) of its smallest slice (gs_engine.cpp)."""
+    r = n_rumors // world
+    return min(200, 32 * (1 << (r - 1).bit_length()))
+
+
 class _Slice:
     """One rank's engine (rumors [lo, hi)) and its empty-count buffers."""
 
@@ -141,6 +148,12 @@ class SlicedNetwork:
         self.slices = [_Slice(torch, n_nodes, self.bounds[g], self.bounds[g + 1], seed, epoch, params,
                               device, faults, schedule) for g in ranks]
         self.faults = self.slices[0].net.faults
+        # one bound on external first Pushes per node and round for the whole
+        # network: the smallest slice's (floor(R / world) rumors), so every
+        # slice refuses the same batches (gs_slice_set_ext_limit)
+        self.ext_limit = slice_ext_limit(n_rumors, world)
+        for s in self.slices:
+            _check(s.lib.gs_slice_set_ext_limit(s.h, self.ext_limit))
         self.round = 0
         self._pend = []  # (async work, buffer) of all-reduces not applied yet (RCCL)
         # wire format: keys set by set_rumor_key (every rank tracks them all);

@@ -32,7 +32,7 @@ def _first_bad(a, b):
 SPREAD = {(1 << 20, 64): (22, 16), (1 << 24, 256): (34, 18)}
 
 
-def _run(engine, nets, n, R, faults, max_rounds, every=1, epoch=0, dumps=False, spread=None):
+def _run(engine, nets, n, R, faults, max_rounds, every=1, epoch=0, dumps=False, spread=None, complete=None):
     """Inject every rumor at its Philox origin into every engine of `nets`
     (one network each) and into the dense program, then run them round by
     round; returns the rounds run.  An engine's digest after round t is
@@ -75,7 +75,12 @@ def _run(engine, nets, n, R, faults, max_rounds, every=1, epoch=0, dumps=False, 
             if not live or rnd == max_rounds:
                 check(prev, dn.digest(), rnd)
                 if spread is not None:
-                    assert nets[0].known_counts() == (n * R, n), "full dissemination at termination"
+                    full = n if complete is None else complete
+                    for i, net in enumerate(nets):
+                        kc = net.known_counts()
+                        assert kc[1] == full, f"net {i}: {kc[1]} nodes complete at termination, not {full}"
+                        if complete is None:
+                            assert kc == (n * R, n), "full dissemination at termination"
                     assert (rnd, r_full) == spread, f"spread record {(rnd, r_full)}"
                 return rnd
         return max_rounds
@@ -114,18 +119,24 @@ def test_to_termination(engine, n, R):
         net.close()
 
 
-def test_config5_faults_rounds(engine):
-    # config 5: 10^8 x 16 with 1 % churn / push drop / pull drop, 8 rounds, on
-    # the single engine (the DLV build and the packed round kernel) and on 4
-    # code-row node shards of the same network (one GPU, device-copy
-    # exchanges, 2 pipeline parts each: the multi-GPU layout at full size)
+def test_config5_faults_to_termination(engine):
+    # config 5: 10^8 x 16 with 1 % churn / push drop / pull drop, at the
+    # bench's epoch, to termination (every 3rd round and the last) on the
+    # single engine (the DLV build and the packed round kernel) and on the
+    # layout `bench.py --gpus 8` runs: 8 code-row node shards of 12.5 M nodes
+    # with 4 pipeline parts each (one GPU, device-copy exchanges).  The late
+    # rounds are where churned nodes return (their frozen votes) and C / D
+    # transitions dominate.  The spread record is the bench's: 42 rounds, two
+    # nodes kept from some rumor by churn, never a full spread.
     from safe_gossip_amd.sharded import ShardedNetwork
     n, R = 100_000_000, 16
     faults = (0.01, 0.01, 0.01)
-    single = engine.Network(n, R, seed=SEED, **_fk(faults))
-    shards = ShardedNetwork(n, R, 4, seed=SEED, transport="local", parts=2, **_fk(faults))
+    single = engine.Network(n, R, seed=SEED, epoch=1, **_fk(faults))
+    shards = ShardedNetwork(n, R, 8, seed=SEED, epoch=1, transport="local", parts=4, **_fk(faults))
     try:
-        _run(engine, [single, shards], n, R, faults, 8, every=2)
+        assert shards.parts == 4 and shards.shards[0].codes
+        assert _run(engine, [single, shards], n, R, faults, 80, every=3, epoch=1, spread=(42, 0),
+                    complete=99_999_998) == 42
     finally:
         shards.close()
         single.close()

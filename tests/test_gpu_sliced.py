@@ -182,6 +182,10 @@ def _worker(rank, world, port, cases, q, backend="gloo"):
                 _batch_case(sg, n, R, faults, "2P", make=mk)
                 _push_batch_case(sg, n, R, faults, True, make=mk)
                 continue
+            if kind == "wire_limit":  # uneven slices: one network-wide first-Push bound
+                from test_gpu_wire import _uneven_limit_case
+                _uneven_limit_case(sg, lambda n_, R_: SlicedNetwork(n_, R_, world, device=0, transport="dist"))
+                continue
             run_parity(sg, n, R, kind, make_net=make, faults=faults, check_every=every[0] if every else 1)
         q.put(("ok", rank))
     except BaseException as e:
@@ -219,7 +223,8 @@ def test_sliced_dist_gloo_two_ranks(engine):
 def test_sliced_dist_gloo_wire(engine):
     # the wire boundary on two slice processes: every rank makes the same
     # calls, the slices' answers are all-gathered and merged in key order
-    _spawn(2, [(300, 16, "wire", None), (400, 64, "wire", (0.05, 0.05, 0.05))], "gloo")
+    _spawn(2, [(300, 16, "wire", None), (400, 64, "wire", (0.05, 0.05, 0.05)), (60, 9, "wire_limit", None)],
+           "gloo")
 
 
 def test_sliced_dist_rccl_single_rank(engine):

@@ -376,3 +376,43 @@ def test_sliced_first_push_limit(engine):
         net.handle_received(0, 1000, empty)  # a new round
     finally:
         net.close()
+
+
+def _uneven_limit_case(sg, make):
+    """R = 9 over 2 slices (4 + 5 rumors, R_pad 4 and 8: own bounds 128 and
+    200): every slice takes the network's bound, 128, so the 129th first Push
+    to a node is refused whole by both slices, which stay equal."""
+    from safe_gossip_amd.sliced import slice_ext_limit
+    assert slice_ext_limit(9, 2) == 128 and slice_ext_limit(3, 2) == 32
+    net = make(60, 9)
+    try:
+        assert net.ext_limit == 128
+        net.next_round()
+        st0 = net.statistics_all().astype(np.int64)
+        empty = sg.rpc_encode(False, b"", 0)
+        pull_empty = sg.rpc_encode(True, b"", 0)
+        out = net.handle_received_batch([(5, 100 + i, empty) for i in range(128)])
+        assert out[127] == [pull_empty]
+        with pytest.raises(sg.DeviceError, match="status -5"):
+            net.handle_received_batch([(5, 1000, empty), (6, 1000, empty)])
+        # nothing of the refused batch was applied: node 6 still answers
+        assert net.handle_received(6, 1000, empty) == [pull_empty]
+        st = net.statistics_all().astype(np.int64) - st0
+        assert st[5][1] == 128 and st[6][1] == 1  # empty pulls sent (the MIN over the slices)
+        net.next_round()
+        net.handle_received(5, 1000, empty)  # a new round
+    finally:
+        net.close()
+
+
+def test_sliced_uneven_first_push_limit(engine):
+    from safe_gossip_amd.sliced import SlicedNetwork
+    _uneven_limit_case(engine, lambda n, R: SlicedNetwork(n, R, 2, transport="local"))
+    with pytest.raises(engine.DeviceError, match="status -1"):  # above a slice's own bound
+        net = SlicedNetwork(40, 4, 2, transport="local")
+        try:
+            s = net.slices[0]
+            from safe_gossip_amd import _check
+            _check(s.lib.gs_slice_set_ext_limit(s.h, 65))
+        finally:
+            net.close()

@@ -52,3 +52,23 @@ def test_rccl_one_rank_default_config5(engine):
     from safe_gossip_amd.sharded import RCCL_MAX_BYTES, plan_info
     d = plan_info(100_000_000, 16, 1, 0, parts=4)
     assert d["max_collective_bytes"] <= RCCL_MAX_BYTES
+
+
+@pytest.mark.parametrize("n,R,world,fits", [
+    # class-row shards build the next round's in-lists in LDS bins of 2 K
+    # nodes (gs_shard.hip edge_bin, 8 B of LDS per bin): up to 16256 bins per
+    # rank; a larger rank is refused up front, by plan_info and create alike
+    ((1 << 24), 256, 1, True), (16256 * 2048, 32, 1, True), (16256 * 2048 + 1, 32, 1, False),
+    ((1 << 25) + 4096, 64, 1, False), (100_000_000, 32, 4, True), (100_000_000, 32, 2, False),
+    # code rows (R_pad <= 16, 2P) build no in-lists ahead: no such limit
+    (100_000_000, 16, 1, True),
+])
+def test_class_row_rank_size_limit(engine, n, R, world, fits):
+    import safe_gossip_amd as sg
+    from safe_gossip_amd.sharded import plan_info
+    for rank in range(world):
+        if fits:
+            plan_info(n, R, world, rank, parts=4)
+        else:
+            with pytest.raises(sg.DeviceError, match="status -2"):
+                plan_info(n, R, world, rank, parts=4)
