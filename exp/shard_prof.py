@@ -5,7 +5,7 @@ import sys
 import time
 
 import os
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.environ.get("GS_TREE") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 import safe_gossip_amd as sg  # noqa: E402
 from safe_gossip_amd.sharded import ShardedNetwork  # noqa: E402

@@ -312,6 +312,51 @@ gs_status   gs_slice_defer(gs_engine *e, uint32_t which);
  * so a batch is refused by all of them or by none (1..the slice's own). */
 gs_status   gs_slice_set_ext_limit(gs_engine *e, uint32_t limit);
 
+/* ---- A whole multi-GPU network through this ABI alone (DESIGN.md section
+ * 7d): the per-round loop of the two sections above -- exchanges, pipeline
+ * parts, the slices' MIN reductions -- run by the library, so a host without
+ * Python drives node shards or rumor slices over several GPUs with gs_net_*
+ * calls only (safe_gossip_amd/sharded.py and sliced.py are the Python
+ * drivers of the same engines).
+ *
+ * gs_net_create: one rank per process (one GPU each: cfg->device), joined
+ * through RCCL (loaded at run time; GS_ERR_UNSUPPORTED without it): rank 0
+ * makes an id with gs_net_unique_id and hands it to every rank out of band.
+ * The collectives run on a stream of the rank's, ordered against the engine
+ * stream with events, so gs_net_next_round(net, NULL) enqueues a round without
+ * a host synchronisation.  Every rank makes the same calls in the same order
+ * (gs_net_send_new is ignored by ranks that do not hold the node / rumor;
+ * the observers are collective and return the WHOLE network on every rank).
+ * gs_net_create_local: all `world` ranks in this process on cfg->device,
+ * exchanged by device copies with host synchronisation (a test transport for
+ * the same loop on one GPU).  `parts`: node shards' pipeline parts (1..4;
+ * ignored by slices).  SEQ runs on slices only (node shards:
+ * GS_ERR_UNSUPPORTED).  The wire calls (gs_push_batch, gs_handle_received*)
+ * go to the engines themselves (gs_net_engine), as the sections above say. */
+#define GS_NET_ID_BYTES 128
+typedef struct gs_net gs_net;
+typedef enum { GS_NET_SLICES = 0, GS_NET_SHARDS = 1 } gs_net_mode;
+gs_status   gs_net_unique_id(uint8_t id[GS_NET_ID_BYTES]);
+gs_status   gs_net_create(const gs_config *cfg, gs_net_mode mode, uint32_t rank, uint32_t world, uint32_t parts,
+                          const uint8_t id[GS_NET_ID_BYTES], gs_net **out);
+gs_status   gs_net_create_local(const gs_config *cfg, gs_net_mode mode, uint32_t world, uint32_t parts,
+                                gs_net **out);
+void        gs_net_destroy(gs_net *net);
+/* Gossiper::send_new on a node of the network (global ids). */
+gs_status   gs_net_send_new(gs_net *net, uint32_t node, uint32_t rumor);
+/* One round of the whole network; with a report, any_live is the network's
+ * (a host synchronisation, as gs_next_round's report). */
+gs_status   gs_net_next_round(gs_net *net, gs_round_report *report);
+gs_status   gs_net_sync(gs_net *net);
+gs_status   gs_net_clear(gs_net *net, uint32_t epoch);
+/* Observers of the whole network (collective with RCCL). */
+gs_status   gs_net_known_counts(gs_net *net, uint64_t *known_total, uint64_t *nodes_complete);
+gs_status   gs_net_statistics_all(gs_net *net, uint64_t *out /* n*5 */);
+gs_status   gs_net_dump_state(gs_net *net, uint16_t *out /* n*R, gs_dump_state's codes */);
+/* The engines this process holds (1 with RCCL, `world` local ones). */
+uint32_t    gs_net_local_engines(const gs_net *net);
+gs_engine  *gs_net_engine(gs_net *net, uint32_t i);
+
 /* ---- Wire format (src/messages.rs) ----------------------------------------
  * GossipRpc as maidsafe_utilities::serialisation (bincode, fixed-width little
  * endian) writes it: u32 variant (0 Push, 1 Pull) | u64 msg length | msg |

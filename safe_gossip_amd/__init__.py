@@ -171,6 +171,21 @@ SYMBOLS = {
     "gs_slice_apply": (ctypes.c_int, [_P, ctypes.c_uint32]),
     "gs_slice_defer": (ctypes.c_int, [_P, ctypes.c_uint32]),
     "gs_slice_set_ext_limit": (ctypes.c_int, [_P, ctypes.c_uint32]),
+    # the whole multi-GPU network behind the ABI (gs_net.cpp; C / C++ hosts)
+    "gs_net_unique_id": (ctypes.c_int, [_U8P]),
+    "gs_net_create": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _U8P,
+                                     ctypes.POINTER(_P)]),
+    "gs_net_create_local": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(_P)]),
+    "gs_net_destroy": (None, [_P]),
+    "gs_net_send_new": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_uint32]),
+    "gs_net_next_round": (ctypes.c_int, [_P, _P]),
+    "gs_net_sync": (ctypes.c_int, [_P]),
+    "gs_net_clear": (ctypes.c_int, [_P, ctypes.c_uint32]),
+    "gs_net_known_counts": (ctypes.c_int, [_P, _U64P, _U64P]),
+    "gs_net_statistics_all": (ctypes.c_int, [_P, _U64P]),
+    "gs_net_dump_state": (ctypes.c_int, [_P, _U16P]),
+    "gs_net_local_engines": (ctypes.c_uint32, [_P]),
+    "gs_net_engine": (_P, [_P, ctypes.c_uint32]),
 }
 
 _LIB = None

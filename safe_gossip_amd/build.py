@@ -16,7 +16,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libsafe_gossip_amd.so")
 SOURCES = [os.path.join(CSRC, "gs_kernels.hip"), os.path.join(CSRC, "gs_inlist.hip"),
            os.path.join(CSRC, "gs_shard.hip"), os.path.join(CSRC, "gs_seq.hip"), os.path.join(CSRC, "gs_dlv4.hip"), os.path.join(CSRC, "gs_w32.hip"), os.path.join(CSRC, "gs_verify.hip"),
-           os.path.join(CSRC, "gs_engine.cpp"), os.path.join(CSRC, "gs_wire.cpp"),
+           os.path.join(CSRC, "gs_engine.cpp"), os.path.join(CSRC, "gs_net.cpp"), os.path.join(CSRC, "gs_wire.cpp"),
            os.path.join(CSRC, "gs_sign.cpp")]
 HEADERS = [os.path.join(CSRC, f) for f in ("gs_common.h", "gs_kernels.h", "gs_device.h", "gs_recv.h")] + [
     os.path.join(REPO_DIR, "include", "safe_gossip.h")
@@ -96,7 +96,7 @@ def build_engine(force: bool = False, verbose: bool = False, defines=(), out: st
         if x_:
             with open(o_ + ".buildid", "w") as f:
                 f.write(bid)
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", target + ".tmp"] + objs
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", target + ".tmp"] + objs + ["-ldl"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -29,14 +29,19 @@
 
 namespace gs {
 
-// Lanes of a round-kernel block (BLK): 128 for the single engine's
-// transitions on the gather path with 64 <= R_pad <= 1024 (128 / W nodes;
-// a thread's uint4 steps of 2 BLK words must cover whole nodes), 256
-// otherwise -- the observation launches and the shard parts count their
-// blocks in 256 lanes (gs_engine.cpp).  Two-wave blocks wait at their two
-// barriers for two waves, not four: config 4's round kernel 2.476 -> 2.370
-// ms, 2.816 -> 2.715 ms per step (profiles/r5/ab_blk128/).
-constexpr uint32_t kRkSmallBlk = 128u;
+// Lanes of a round-kernel block (BLK): 128 for the transitions of the
+// gather path and of class-row shards with 64 <= R_pad <= 1024 (128 / W
+// nodes; a thread's uint4 steps of 2 BLK words must cover whole nodes), 256
+// otherwise.  The observation launches and the shard parts count their
+// blocks in 256 lanes (gs_engine.cpp); launch_mode converts.  Two-wave
+// blocks wait at their two barriers for two waves, not four: config 4's
+// round kernel 2.470 -> 2.343 ms, 2.810 -> 2.693 ms per step
+// (profiles/r6/ab_blk128/).
+#ifndef GS_RK_SMALL_BLK
+#define GS_RK_SMALL_BLK 128u  // (A/B builds: 64)
+#endif
+constexpr uint32_t kRkSmallBlk = GS_RK_SMALL_BLK;
+static_assert(kRkSmallBlk == 64u || kRkSmallBlk == 128u, "a thread's stage step must cover whole nodes at W <= 16");
 
 #ifndef GS_RK_MINW
 #define GS_RK_MINW 1
@@ -67,8 +72,8 @@ __global__ __launch_bounds__(BLK, GS_RK_MINW) void round_kernel(RoundArgs a) {
     // words of planes one block owns (its records are contiguous), uint4
     // loads per thread, and the stage (padded node strides: <= 10/8)
     constexpr uint32_t kBlk = BLK;
-    static_assert(BLK == 256u || (!SMALL && !SHARD && !SEQ && !DLV && (MODE == 0 || MODE == 1)),
-                  "smaller blocks: single-engine gather-path transitions only");
+    static_assert(BLK == 256u || (!SMALL && !SEQ && !DLV && (MODE == 0 || MODE == 1)),
+                  "smaller blocks: gather-path and class-row shard transitions only");
     constexpr uint32_t kBlockWords = kBlk * kPlanes;
     constexpr uint32_t kStageIters = kBlockWords / 2u / kBlk;
     constexpr uint32_t kStageWords = kBlockWords + kBlockWords / 4u;
@@ -854,17 +859,25 @@ __global__ __launch_bounds__(BLK, GS_RK_MINW) void round_kernel(RoundArgs a) {
 
 template <bool SMALL, bool SHARD, bool SEQ, bool DLV = false>
 static hipError_t launch_mode(const RoundArgs &a, int mode, hipStream_t s) {
-    if constexpr (!SMALL && !SHARD && !SEQ && !DLV) {
-        if ((mode == 0 || mode == 1) && a.g.W <= 16u && a.blk_count == 0 && a.blk_off == 0) {
-            const u64 grid = (a.g.nseg + kRkSmallBlk - 1) / kRkSmallBlk;
-            if (grid == 0) return hipSuccess;
-            if (a.blk_list) return hipErrorInvalidValue;
+    if constexpr (!SMALL && !SEQ && !DLV) {
+        if ((mode == 0 || mode == 1) && a.g.W <= 16u) {
+            if (a.blk_list) return hipErrorInvalidValue;  // (observation launches only)
+            // a part's 256-lane blocks [blk_off, blk_off + blk_count) as
+            // 128-lane blocks, none past the last segment (a block wholly
+            // past it would compute a stage range below zero)
+            constexpr u64 f = 256u / kRkSmallBlk;
+            const u64 nblk = (a.g.nseg + kRkSmallBlk - 1) / kRkSmallBlk;
+            const u64 b0 = std::min<u64>((u64)a.blk_off * f, nblk);
+            const u64 b1 = a.blk_count ? std::min<u64>(((u64)a.blk_off + a.blk_count) * f, nblk) : nblk;
+            if (b1 <= b0) return hipSuccess;
+            RoundArgs b = a;
+            b.blk_off = (uint32_t)b0;
             if (mode == 0)
-                hipLaunchKernelGGL((round_kernel<false, 0, false, false, false, kRkSmallBlk>), dim3((uint32_t)grid),
-                                   dim3(kRkSmallBlk), 0, s, a);
+                hipLaunchKernelGGL((round_kernel<false, 0, SHARD, false, false, kRkSmallBlk>), dim3((uint32_t)(b1 - b0)),
+                                   dim3(kRkSmallBlk), 0, s, b);
             else
-                hipLaunchKernelGGL((round_kernel<false, 1, false, false, false, kRkSmallBlk>), dim3((uint32_t)grid),
-                                   dim3(kRkSmallBlk), 0, s, a);
+                hipLaunchKernelGGL((round_kernel<false, 1, SHARD, false, false, kRkSmallBlk>), dim3((uint32_t)(b1 - b0)),
+                                   dim3(kRkSmallBlk), 0, s, b);
             return hipGetLastError();
         }
     }

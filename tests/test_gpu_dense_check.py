@@ -119,24 +119,77 @@ def test_to_termination(engine, n, R):
         net.close()
 
 
-def test_config5_faults_to_termination(engine):
-    # config 5: 10^8 x 16 with 1 % churn / push drop / pull drop, at the
-    # bench's epoch, to termination (every 3rd round and the last) on the
-    # single engine (the DLV build and the packed round kernel) and on the
-    # layout `bench.py --gpus 8` runs: 8 code-row node shards of 12.5 M nodes
-    # with 4 pipeline parts each (one GPU, device-copy exchanges).  The late
-    # rounds are where churned nodes return (their frozen votes) and C / D
-    # transitions dominate.  The spread record is the bench's: 42 rounds, two
-    # nodes kept from some rumor by churn, never a full spread.
+def test_config5_faults_rounds(engine):
+    # config 5: 10^8 x 16 with 1 % churn / push drop / pull drop, 8 rounds
+    # against the dense program, on the single engine (the DLV build and the
+    # packed round kernel) and on the layout `bench.py --gpus 8` runs: 8
+    # code-row node shards of 12.5 M nodes with 4 pipeline parts each (one
+    # GPU, device-copy exchanges)
     from safe_gossip_amd.sharded import ShardedNetwork
     n, R = 100_000_000, 16
+    faults = (0.01, 0.01, 0.01)
+    single = engine.Network(n, R, seed=SEED, **_fk(faults))
+    shards = ShardedNetwork(n, R, 8, seed=SEED, transport="local", parts=4, **_fk(faults))
+    try:
+        assert shards.parts == 4 and shards.shards[0].codes
+        _run(engine, [single, shards], n, R, faults, 8, every=2)
+    finally:
+        shards.close()
+        single.close()
+
+
+# config 5's spread record at the bench's epoch (bench.py prints it): 42
+# rounds, churn keeps two nodes from some rumor, never a full spread
+SPREAD5 = (42, 0, 99_999_998)
+
+
+def test_config5_eight_shards_to_termination(engine):
+    # config 5 to termination at full size in its 8-GPU layout: 8 code-row
+    # shards (4 parts) against the single engine, node by node through the
+    # state digest every 3rd round and the last, and the spread record on
+    # both.  The late rounds are where churned nodes return with their frozen
+    # votes and C / D transitions dominate.  (The dense program takes ~4.5 s
+    # per round at this size; it checks rounds 1-8 above and a quarter-size
+    # network to termination below.)
+    from safe_gossip_amd.sharded import ShardedNetwork
+    n, R = 100_000_000, 16
+    fk = _fk((0.01, 0.01, 0.01))
+    single = engine.Network(n, R, seed=SEED, epoch=1, **fk)
+    shards = ShardedNetwork(n, R, 8, seed=SEED, epoch=1, transport="local", parts=4, **fk)
+    try:
+        for r in range(R):
+            x = engine.origin_of(SEED, 1, r, n)
+            single.send_new(x, r)
+            shards.send_new(x, r)
+        rnd = 0
+        for rnd in range(1, 81):
+            a, b = single.next_round(), shards.next_round()
+            assert a.any_live == b.any_live, f"round {rnd}: any_live"
+            if rnd % 3 == 0 or not a.any_live:
+                bad = _first_bad(single.state_digest(), shards.state_digest())
+                assert bad is None, f"round {rnd}: {bad[1]} nodes differ, first {bad[0]}"
+            if not a.any_live:
+                break
+        assert rnd == SPREAD5[0], f"{rnd} rounds"
+        for net in (single, shards):
+            known, complete = net.known_counts()
+            assert complete == SPREAD5[2] and known < n * R
+    finally:
+        shards.close()
+        single.close()
+
+
+def test_config5_quarter_to_termination(engine):
+    # config 5's network at a quarter of its size (2.5 * 10^7 x 16, the same
+    # faults) to termination against the dense program, every 3rd round and
+    # the last, on the single engine and on 8 code-row shards with 4 parts
+    from safe_gossip_amd.sharded import ShardedNetwork
+    n, R = 25_000_000, 16
     faults = (0.01, 0.01, 0.01)
     single = engine.Network(n, R, seed=SEED, epoch=1, **_fk(faults))
     shards = ShardedNetwork(n, R, 8, seed=SEED, epoch=1, transport="local", parts=4, **_fk(faults))
     try:
-        assert shards.parts == 4 and shards.shards[0].codes
-        assert _run(engine, [single, shards], n, R, faults, 80, every=3, epoch=1, spread=(42, 0),
-                    complete=99_999_998) == 42
+        assert _run(engine, [single, shards], n, R, faults, 80, every=3, epoch=1) < 80
     finally:
         shards.close()
         single.close()
