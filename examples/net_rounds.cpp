@@ -9,13 +9,15 @@
 //              [--rank g --id-file F] [--parts P] [--nodes n] [--rumors R]
 //              [--seed S] [--epoch E] [--churn p] [--drop-push p]
 //              [--drop-pull p] [--schedule 2P|SEQ] [--rounds K] [--device d]
-//              [--dump FILE]
+//              [--dump FILE] [--time K]
 //
 // RCCL ranks (one process per GPU): rank 0 writes the RCCL id to --id-file,
 // the others read it.  --dump writes, after every round, the round number,
 // the network's any-live flag, every node's state codes (n*R u16,
 // gs_dump_state's) and Statistics (n*5 u64) -- the whole network, from rank
 // 0 -- so a checker can compare each round with another implementation.
+// --time K: instead, after 3 unreported rounds, time K unreported rounds
+// (nothing waits on the host between them) and print ms per round.
 #include <safe_gossip.h>
 
 #include <chrono>
@@ -38,7 +40,7 @@ static uint32_t threshold(double p) {
 
 int main(int argc, char **argv) {
     std::string mode = "slices", transport = "rccl", id_file, dump, sched = "2P";
-    uint32_t world = 1, rank = 0, parts = 4, n = 4096, R = 16, epoch = 0, rounds = 200;
+    uint32_t world = 1, rank = 0, parts = 4, n = 4096, R = 16, epoch = 0, rounds = 200, timed = 0;
     uint64_t seed = 0x5AFE6055ull;
     double churn = 0, dpush = 0, dpull = 0;
     int device = 0;
@@ -61,6 +63,7 @@ int main(int argc, char **argv) {
         else if (k == "--rounds") rounds = (uint32_t)std::stoul(v);
         else if (k == "--device") device = std::stoi(v);
         else if (k == "--dump") dump = v;
+        else if (k == "--time") timed = (uint32_t)std::stoul(v);
         else {
             std::fprintf(stderr, "net_rounds: unknown option %s\n", k.c_str());
             return 2;
@@ -111,6 +114,22 @@ int main(int argc, char **argv) {
     for (uint32_t r = 0; r < R; ++r) {
         st = gs_net_send_new(net, gs_origin(seed, epoch, r, n), r);
         if (st != GS_OK) die("gs_net_send_new", st);
+    }
+    if (timed) {  // throughput: unreported rounds, one host wait at the end
+        for (int w = 0; w < 3; ++w)
+            if ((st = gs_net_next_round(net, nullptr)) != GS_OK) die("gs_net_next_round", st);
+        if ((st = gs_net_sync(net)) != GS_OK) die("gs_net_sync", st);
+        const auto a = std::chrono::steady_clock::now();
+        for (uint32_t k = 0; k < timed; ++k)
+            if ((st = gs_net_next_round(net, nullptr)) != GS_OK) die("gs_net_next_round", st);
+        if ((st = gs_net_sync(net)) != GS_OK) die("gs_net_sync", st);
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+        if (rank == 0)
+            std::printf("{\"mode\": \"%s\", \"transport\": \"%s\", \"world\": %u, \"nodes\": %u, \"rumors\": %u, "
+                        "\"parts\": %u, \"rounds\": %u, \"ms_per_round\": %.4f}\n",
+                        mode.c_str(), transport.c_str(), world, n, R, parts, timed, ms / timed);
+        gs_net_destroy(net);
+        return 0;
     }
     FILE *df = nullptr;
     if (!dump.empty() && rank == 0 && !(df = std::fopen(dump.c_str(), "wb"))) return 1;

@@ -29,16 +29,16 @@
 
 namespace gs {
 
-// Lanes of a round-kernel block (BLK): 128 for the transitions of the
-// gather path and of class-row shards with 64 <= R_pad <= 1024 (128 / W
-// nodes; a thread's uint4 steps of 2 BLK words must cover whole nodes), 256
-// otherwise.  The observation launches and the shard parts count their
-// blocks in 256 lanes (gs_engine.cpp); launch_mode converts.  Two-wave
-// blocks wait at their two barriers for two waves, not four: config 4's
-// round kernel 2.470 -> 2.343 ms, 2.810 -> 2.693 ms per step
-// (profiles/r6/ab_blk128/).
+// Lanes of a round-kernel block (BLK): one wave (64 lanes) for the
+// transitions of the gather path and of class-row shards with 64 <= R_pad <=
+// 1024 (64 / W nodes; a thread's uint4 steps of 2 BLK words must cover whole
+// nodes), 256 otherwise.  The observation launches and the shard parts count
+// their blocks in 256 lanes (gs_engine.cpp); launch_mode converts.  A block's
+// two barriers wait for no other wave: config 4's round kernel 2.470 ->
+// 2.343 ms with two-wave blocks, 2.321 -> 2.222 ms with one-wave blocks
+// (2.810 -> 2.693 -> 2.582 ms per step; profiles/r6/ab_blk128/, ab_blk64/).
 #ifndef GS_RK_SMALL_BLK
-#define GS_RK_SMALL_BLK 128u  // (A/B builds: 64)
+#define GS_RK_SMALL_BLK 64u  // (A/B builds: 128)
 #endif
 constexpr uint32_t kRkSmallBlk = GS_RK_SMALL_BLK;
 static_assert(kRkSmallBlk == 64u || kRkSmallBlk == 128u, "a thread's stage step must cover whole nodes at W <= 16");
