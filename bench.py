@@ -28,15 +28,21 @@ cfg4, the configuration the metric is quoted on that fits one GPU.
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N, or plain
 `python bench.py --gpus N`, which starts that launcher itself): ONE network
 of the same n x R over the N ranks, measured in both multi-GPU modes one after
-the other, and the faster is the headline (the other under "alternative"):
-rumor slices (every rank holds all n nodes and R/N of the rumors,
-safe_gossip_amd.sliced; rumors evolve independently, so
-a round's only exchange is one RCCL all_reduce(MIN) of 2 bytes per node, the
-empty-RPC Statistics, overlapped with the next round) and node-range shards
-(safe_gossip_amd.sharded, DESIGN.md section 7: push and pull rows exchanged
-with RCCL all_to_all_single every round).  --mode slices|nodes measures one.
-Total work is fixed, so "scaling" is "strong".  Barrier + synchronize around
-the timed region, time = max over ranks.  The roofline line describes rank 0's round kernel.
+the other, and the faster is the headline (the others under "alternative"):
+rumor slices (every rank holds all n nodes and R/N of the rumors, DESIGN.md
+section 7b; rumors evolve independently, so a round's only exchange is one
+RCCL all_reduce(MIN) of 2 bytes per node, the empty-RPC Statistics,
+overlapped with the next round) and node-range shards (DESIGN.md section 7:
+push and pull rows exchanged by RCCL all-to-all every round).  Each mode runs
+twice: with the round loop in the library (gs_net, safe_gossip_amd.net,
+DESIGN.md section 7d: the C++ loop issues its own RCCL collectives; one RCCL
+rank measured it 0.35-0.77 ms per round where the Python drivers took
+0.36-1.19) and with the Python drivers (safe_gossip_amd.sliced / .sharded,
+torch.distributed collectives).  --mode slices|nodes|slices-lib|nodes-lib
+measures one.  Total work is fixed, so "scaling" is "strong".  Barrier +
+synchronize around the timed region, time = max over ranks.  The roofline
+line describes rank 0's round kernel.  A watchdog prints the line of the
+modes finished so far and ends every rank if a mode overruns --deadline.
 """
 import argparse
 import json
@@ -81,10 +87,13 @@ def parse():
     p.add_argument("--parts", type=int, default=None,
                    help="pipeline parts per rank (N>1; default 4 with RCCL: the exchanges of one "
                         "part overlap the round kernel of another)")
-    p.add_argument("--mode", default="both", choices=["both", "slices", "nodes"],
-                   help="N>1: measure both multi-GPU modes and report the faster (default), or only "
-                        "rumor slices per rank / node-range shards; with --sharded at N=1 the "
-                        "default is node shards")
+    p.add_argument("--mode", default="both", choices=["both", "slices", "nodes", "slices-lib", "nodes-lib"],
+                   help="N>1: measure both multi-GPU modes, each with the library's round loop (-lib) "
+                        "and the Python drivers, and report the fastest (default), or only one; with "
+                        "--sharded at N=1 the default is node shards")
+    p.add_argument("--deadline", type=float, default=420.0,
+                   help="N>1: seconds after which a watchdog reports the modes finished so far and "
+                        "ends every rank")
     p.add_argument("--sharded", action="store_true",
                    help="run a multi-GPU mode even at N=1 (one RCCL rank: node-shard exchanges are "
                         "self-copies, the slice all-reduce a no-op; measures that path's overhead)")
@@ -280,7 +289,11 @@ def run_mode(args, mode, world, rank, local, dist, sg, np, torch, with_spread):
     fk = dict(churn=args.faults[0], drop_push=args.faults[1], drop_pull=args.faults[2])
     if args.schedule != "2P":
         fk["schedule"] = args.schedule
-    if mode == "slices":
+    if mode in ("slices-lib", "nodes-lib"):
+        from safe_gossip_amd.net import Net
+        net = Net(n, R, world, mode="slices" if mode == "slices-lib" else "shards", seed=args.seed, epoch=0,
+                  device=local, transport="dist", parts=args.parts or 4, **fk)
+    elif mode == "slices":
         from safe_gossip_amd.sliced import SlicedNetwork
         net = SlicedNetwork(n, R, world, seed=args.seed, epoch=0, device=local, transport="dist", **fk)
     elif mode == "nodes":
@@ -338,6 +351,13 @@ def run_mode(args, mode, world, rank, local, dist, sg, np, torch, with_spread):
 def parallelism(args, mode, world, parts):
     backend = "RCCL" if args.dist_backend == "nccl" else args.dist_backend
     n, R = args.nodes, args.rumors
+    if mode == "slices-lib":
+        return (f"rumor slices x{world} (all {n} nodes, {R // world}-{-(-R // world)} rumors per rank), "
+                "library round loop (gs_net): RCCL ncclAllReduce(MIN) of 2 B/node empty-RPC counts per round, "
+                "overlapped with the next round")
+    if mode == "nodes-lib":
+        return (f"node-range shards x{world}, library round loop (gs_net): RCCL ncclAllToAll push/pull rows, "
+                f"{parts} pipeline part(s) per rank")
     if mode == "slices":
         return (f"rumor slices x{world} (all {n} nodes, {R // world}-{-(-R // world)} rumors per rank), "
                 + backend + " all_reduce(MIN) of 2 B/node empty-RPC counts per round"
@@ -393,13 +413,57 @@ def main():
     elif world == 1:
         modes = ["nodes"]
     else:
-        modes = ["slices", "nodes"]
+        # the Python drivers first (rehearsed with 8 ranks), then
+        # the library's loop (RCCL only: gs_net joins RCCL itself)
+        modes = ["slices", "nodes"] + (["slices-lib", "nodes-lib"] if args.dist_backend == "nccl" else [])
     if R < world:  # fewer rumors than ranks: no rumor slices
-        modes = [m for m in modes if m != "slices"] or ["nodes"]
+        modes = [m for m in modes if not m.startswith("slices")] or ["nodes"]
     if args.schedule == "SEQ" and dist is not None:  # SEQ's pull chains cross node ranges: slices only
-        modes = ["slices"]
-    runs = [run_mode(args, m, world, rank, local, dist, sg, np, torch, with_spread=(i == 0 and not args.no_spread))
-            for i, m in enumerate(modes)]
+        modes = [m for m in modes if m.startswith("slices")] or ["slices"]
+    runs, failed = [], []
+    if dist is not None and world > 1:
+        start_watchdog(args, runs, failed, world, rank, np, sg)
+    for i, m in enumerate(modes):
+        try:
+            runs.append(run_mode(args, m, world, rank, local, dist, sg, np, torch,
+                                 with_spread=(not runs and not args.no_spread)))
+        except Exception as e:  # a later mode that cannot run here (e.g. no RCCL for gs_net)
+            if not (runs and m.endswith("-lib")):
+                raise
+            failed.append(f"{m}: {type(e).__name__}: {e}")
+            print(f"bench.py: mode {m} failed: {e}", file=sys.stderr)
+    if rank == 0:
+        report(args, runs, failed, world, rank, np, sg, None, dist is not None)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+_REPORTED = []
+
+
+def start_watchdog(args, runs, failed, world, rank, np, sg):
+    """A mode that overruns --deadline (a stuck collective) must not cost the
+    modes already measured: print their line (rank 0) and end this rank."""
+    import threading
+
+    def fire():
+        if _REPORTED:
+            return
+        if rank == 0 and runs:
+            report(args, list(runs), failed, world, rank, np, sg,
+                   f"watchdog: a later mode overran the {args.deadline:.0f} s deadline", True)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0 if runs else 1)
+    t = threading.Timer(args.deadline, fire)
+    t.daemon = True
+    t.start()
+
+
+def report(args, runs, failed, world, rank, np, sg, note, dist_on):
+    """Rank 0: the JSON line of the fastest of `runs`."""
+    _REPORTED.append(True)
+    n, R = args.nodes, args.rumors
     best = min(runs, key=lambda r: r["elapsed"])
     spread = runs[0]["spread"]
 
@@ -440,7 +504,7 @@ def main():
                 traffic = None
 
     cpu = cpu_best_line = None
-    if rank == 0 and world == 1 and dist is None and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not dist_on and not args.no_cpu_baseline:
         cpu = cpu_baseline(R, args.seed, args.cpu_seconds, args.faults, args.schedule)
         if args.schedule == "2P" and not any(args.faults):
             cpu_best_line = cpu_best(R, args.seed, args.cpu_seconds)
@@ -500,9 +564,11 @@ def main():
                 "value": total_updates / r["elapsed"], "ms_per_step": r["elapsed"] / args.steps * 1e3,
                 "kernel": r["name"], "kernel_ms": float(np.mean(r["kt"])) if len(r["kt"]) else None,
             } for r in runs if r is not best]
+        if failed:
+            line["failed_modes"] = failed
+        if note:
+            line["note"] = note
         print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -90,3 +90,85 @@ def test_net_later_epoch(engine, tmp_path):
     # a later epoch (the bench times epoch 1) through the same C++ host
     rounds, _ = _run(tmp_path, "shards", "local", 2, 2, 1500, 32, None, "2P", epoch=3)
     _check(rounds, 1500, 32, None, "2P", epoch=3)
+
+
+def _net_vs_oracle(sg, net, n, R, faults=None, schedule="2P"):
+    thr = [sg.fault_threshold(p) for p in faults] if faults else None
+    orc = OracleNet(n, R, seed=SEED, faults=thr)
+    try:
+        for r in range(R):
+            x = sg.origin_of(SEED, 0, r, n)
+            net.send_new(x, r)
+            orc.send_new(x, r)
+        for _ in range(80):
+            rep = net.next_round()
+            _, live = orc.next_round(SCHED_SEQ if schedule == "SEQ" else SCHED_2P)
+            assert rep.any_live == bool(live)
+            np.testing.assert_array_equal(net.dump_state(), orc.dump_state())
+            np.testing.assert_array_equal(net.statistics_all(), orc.statistics())
+            if not live:
+                break
+        assert net.known_counts()[0] == orc.known_total()
+    finally:
+        orc.close()
+
+
+@pytest.mark.parametrize("mode,world,n,R,faults,schedule", [
+    ("shards", 3, 900, 16, (0.05, 0.05, 0.05), "2P"),
+    ("shards", 2, 800, 100, None, "2P"),
+    ("slices", 3, 700, 30, (0.05, 0.05, 0.05), "SEQ"),
+])
+def test_python_net_local(engine, mode, world, n, R, faults, schedule):
+    # the same library loop bound from Python (safe_gossip_amd.net.Net)
+    from safe_gossip_amd.net import Net
+    fk = dict(churn=faults[0], drop_push=faults[1], drop_pull=faults[2]) if faults else {}
+    net = Net(n, R, world, mode=mode, seed=SEED, transport="local", parts=2, schedule=schedule, **fk)
+    try:
+        _net_vs_oracle(engine, net, n, R, faults, schedule)
+    finally:
+        net.close()
+
+
+def _rccl_worker(port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        import safe_gossip_amd as sg
+        from safe_gossip_amd.net import Net
+        for mode, n, R in (("shards", 1500, 70), ("slices", 1200, 16)):
+            net = Net(n, R, 1, mode=mode, seed=SEED, transport="dist", parts=3)
+            try:
+                _net_vs_oracle(sg, net, n, R)
+            finally:
+                net.close()
+        q.put("ok")
+    except BaseException as e:
+        q.put(f"fail: {type(e).__name__}: {e}")
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_python_net_rccl_one_rank(engine):
+    # one RCCL rank in a torch.distributed process: the library's RCCL (the
+    # one torch loaded) joined through an id broadcast over the process group
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    p = ctx.Process(target=_rccl_worker, args=(port, q))
+    p.start()
+    p.join(timeout=200)
+    if p.is_alive():
+        p.kill()
+    assert not q.empty() and q.get() == "ok"
+    assert p.exitcode == 0
