@@ -16,12 +16,18 @@
 // The algebra is the per-node kernel's (gs_kernels.hip, round_kernel DLV
 // path), term by term; observation launches and rounds with external RPCs
 // still run that kernel.
+#include <algorithm>
+
 #include "gs_device.h"
 #include "gs_kernels.h"
 
 namespace gs {
 
-constexpr uint32_t kDlv4Threads = 256;
+#ifndef GS_DLV4_THREADS
+#define GS_DLV4_THREADS 256u  // lanes per block (A/B builds: 64, 128)
+#endif
+constexpr uint32_t kDlv4Threads = GS_DLV4_THREADS;
+static_assert(kDlv4Threads == 64u || kDlv4Threads == 128u || kDlv4Threads == 256u, "whole waves, <= 256");
 // 4 waves per SIMD (128 VGPRs): 2.63 -> 2.36 ms at config 5 against the
 // unconstrained 134-VGPR build (3 waves)
 #ifndef GS_DLV4_MINW
@@ -615,9 +621,14 @@ template <typename T, uint32_t NPL>
 static hipError_t launch_dlv4_t(const RoundArgs &a, int mode, hipStream_t s) {
     const u64 lanes = ((u64)a.g.n + NPL - 1) / NPL;
     const u64 nblk = (lanes + kDlv4Threads - 1) / kDlv4Threads;
-    const u64 grid = a.blk_count ? a.blk_count : nblk;
-    if (grid == 0) return hipSuccess;
-    if (a.blk_off + grid > nblk) return hipErrorInvalidValue;
+    // a shard part's blocks come in 256-lane units (gs_engine.cpp launch_part)
+    constexpr u64 f = 256u / kDlv4Threads;
+    const u64 b0 = (u64)a.blk_off * f;
+    const u64 b1 = a.blk_count ? std::min<u64>(((u64)a.blk_off + a.blk_count) * f, nblk) : nblk;
+    if (b1 <= b0) return hipSuccess;
+    const u64 grid = b1 - b0;
+    RoundArgs b = a;
+    b.blk_off = (uint32_t)b0;
     const dim3 gd((uint32_t)grid), bd(kDlv4Threads);
     // (external RPCs only ever come with a delivery: mode 1)
     const bool ext = mode == 1 && a.n_ext > 0;
@@ -626,13 +637,13 @@ static hipError_t launch_dlv4_t(const RoundArgs &a, int mode, hipStream_t s) {
         if (!a.sp.codes || !a.recvB || !a.sendA || !a.recvA_next || !a.spos_cur || !a.spos_next || !a.tg_next ||
             !a.sp.chunk)
             return hipErrorInvalidValue;
-        if (mode == 0) hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL, true>), gd, bd, 0, s, a);
-        else if (ext) hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, true, true>), gd, bd, 0, s, a);
-        else hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, true>), gd, bd, 0, s, a);
+        if (mode == 0) hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL, true>), gd, bd, 0, s, b);
+        else if (ext) hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, true, true>), gd, bd, 0, s, b);
+        else hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, true>), gd, bd, 0, s, b);
     } else {
-        if (mode == 0) hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL>), gd, bd, 0, s, a);
-        else if (ext) hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, false, true>), gd, bd, 0, s, a);
-        else hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL>), gd, bd, 0, s, a);
+        if (mode == 0) hipLaunchKernelGGL((round_kernel_dlv4<0, T, NPL>), gd, bd, 0, s, b);
+        else if (ext) hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL, false, true>), gd, bd, 0, s, b);
+        else hipLaunchKernelGGL((round_kernel_dlv4<1, T, NPL>), gd, bd, 0, s, b);
     }
     return hipGetLastError();
 }

@@ -30,7 +30,10 @@
 
 namespace gs {
 
-constexpr uint32_t kW32Threads = 256;
+#ifndef GS_W32_THREADS
+#define GS_W32_THREADS 128u  // lanes per block: 2^24 x 32 1.051 -> 1.037 ms/step against 256 (64: 1.051)
+#endif
+constexpr uint32_t kW32Threads = GS_W32_THREADS;
 #ifndef GS_W32_MINW
 #define GS_W32_MINW 1
 #endif
