@@ -106,3 +106,35 @@ def test_node_ids_beyond_target_word_rejected(engine):
         engine.Network((1 << 29) + 1, 1, params=(3, 3, 21))
     with pytest.raises(engine.DeviceError, match="status -2"):
         engine.Network(0xFFFFFFFE, 1, params=(3, 3, 21))
+
+
+@pytest.mark.skipif(_has_gpu(), reason="checks the no-GPU failure mode")
+def test_net_fails_loudly_without_gpu(engine):
+    # the library's multi-GPU loop has no CPU path either
+    from safe_gossip_amd.net import Net
+    with pytest.raises(engine.DeviceError):
+        Net(64, 8, 2, mode="shards", transport="local")
+    with pytest.raises(engine.DeviceError):
+        Net(64, 8, 2, mode="slices", transport="local")
+
+
+def test_net_invalid_arguments(engine):
+    # argument checks run before any device call
+    lib = engine.load_library()
+    from safe_gossip_amd import _Config
+    cfg = _Config()
+    cfg.n_nodes, cfg.n_rumors = 100, 4
+    h = ctypes.c_void_p()
+    assert lib.gs_net_create_local(ctypes.byref(cfg), 0, 0, 1, ctypes.byref(h)) == -1   # no ranks
+    assert lib.gs_net_create_local(ctypes.byref(cfg), 0, 5, 1, ctypes.byref(h)) == -1   # 4 rumors, 5 slices
+    assert lib.gs_net_create_local(ctypes.byref(cfg), 7, 2, 1, ctypes.byref(h)) == -1   # no such mode
+    cfg.schedule = 1
+    assert lib.gs_net_create_local(ctypes.byref(cfg), 1, 2, 1, ctypes.byref(h)) == -2   # SEQ: slices only
+    cfg.schedule, cfg.rumor_slice = 0, 1
+    assert lib.gs_net_create_local(ctypes.byref(cfg), 1, 2, 1, ctypes.byref(h)) == -1   # a slice is not a network
+    ident = (ctypes.c_uint8 * 128)()
+    cfg.rumor_slice = 0
+    assert lib.gs_net_create(ctypes.byref(cfg), 1, 2, 2, 1, ident, ctypes.byref(h)) == -1  # rank >= world
+    assert lib.gs_net_send_new(None, 0, 0) == -1
+    assert lib.gs_net_next_round(None, None) == -1
+    assert lib.gs_net_local_engines(None) == 0
