@@ -91,7 +91,7 @@ def parse():
                    help="N>1: measure both multi-GPU modes, each with the library's round loop (-lib) "
                         "and the Python drivers, and report the fastest (default), or only one; with "
                         "--sharded at N=1 the default is node shards")
-    p.add_argument("--deadline", type=float, default=420.0,
+    p.add_argument("--deadline", type=float, default=240.0,
                    help="N>1: seconds after which a watchdog reports the modes finished so far and "
                         "ends every rank")
     p.add_argument("--sharded", action="store_true",
