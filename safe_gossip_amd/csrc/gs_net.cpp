@@ -332,19 +332,17 @@ gs_status slice_apply_pending(gs_net *net, size_t keep) {
     return GS_OK;
 }
 
-// MIN over the local slices' device byte buffers, into each (host-staged).
-gs_status local_min_u8(gs_net *net, uint8_t *NetRank::*field, int which, size_t bytes) {
+// MIN over the local slices' device byte buffers buf_of(rank), into each
+// (host-staged: the in-process test transport).
+template <typename BufOf>
+gs_status local_min_u8(gs_net *net, BufOf buf_of, size_t bytes) {
     NET_ST(sync_all(net));
     std::vector<uint8_t> m(bytes, 0xFF), v(bytes);
     for (auto &r : net->ranks) {
-        uint8_t *p = which >= 0 ? r.buf[which] : (r.*field);
-        NET_HIP(hipMemcpy(v.data(), p, bytes, hipMemcpyDeviceToHost));
+        NET_HIP(hipMemcpy(v.data(), buf_of(r), bytes, hipMemcpyDeviceToHost));
         for (size_t i = 0; i < bytes; ++i) m[i] = std::min(m[i], v[i]);
     }
-    for (auto &r : net->ranks) {
-        uint8_t *p = which >= 0 ? r.buf[which] : (r.*field);
-        NET_HIP(hipMemcpy(p, m.data(), bytes, hipMemcpyHostToDevice));
-    }
+    for (auto &r : net->ranks) NET_HIP(hipMemcpy(buf_of(r), m.data(), bytes, hipMemcpyHostToDevice));
     return GS_OK;
 }
 
@@ -357,7 +355,7 @@ gs_status slice_round(gs_net *net, bool report, bool *live) {
     }
     const uint32_t b = (net->round + 1) % 3;  // the round just run wrote buf[t % 3]
     if (!net->dist) {
-        NET_ST(local_min_u8(net, nullptr, (int)b, 2 * (size_t)net->n));
+        NET_ST(local_min_u8(net, [b](NetRank &r) { return r.buf[b]; }, 2 * (size_t)net->n));
         for (auto &r : net->ranks) NET_ST(gs_slice_defer(r.e, b));  // added by the next round kernel
         return GS_OK;
     }
@@ -723,7 +721,7 @@ gs_status gs_net_statistics_all(gs_net *net, uint64_t *out) {
     }
     std::vector<uint8_t> pend(n);
     if (!net->dist) {
-        NET_ST(local_min_u8(net, &NetRank::obs, -1, n));
+        NET_ST(local_min_u8(net, [](NetRank &r) { return r.obs; }, n));
     } else if (net->world > 1) {
         NetRank &r = net->ranks[0];
         NET_HIP(hipSetDevice(r.device));
