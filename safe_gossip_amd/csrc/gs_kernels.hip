@@ -46,6 +46,12 @@ static_assert(kRkSmallBlk == 64u || kRkSmallBlk == 128u, "a thread's stage step 
 #ifndef GS_RK_MINW
 #define GS_RK_MINW 1
 #endif
+#ifndef GS_RK_MINW_SMALL
+#define GS_RK_MINW_SMALL 1  // waves per SIMD asked of the small-block transitions (A/B builds)
+#endif
+#ifndef GS_RK_TAILPRE
+#define GS_RK_TAILPRE 1  // rows of pusher #3 and of t(x)'s sibling #2 issued with the batch (A/B: 0)
+#endif
 
 // MODE: 0 transition only (first round), 1 deliver round t + transition to
 // t+1, 2 deliver round t + observe, 3 observe only.
@@ -65,7 +71,7 @@ GS_DEV Cls decode16(uint32_t code) {
 // gather: a lane's pushers' push codes are in its own record and its pull
 // batch in PULL[x], both read coalesced.
 template <bool SMALL, int MODE, bool SHARD, bool SEQ, bool DLV, uint32_t BLK = 256u>
-__global__ __launch_bounds__(BLK, GS_RK_MINW) void round_kernel(RoundArgs a) {
+__global__ __launch_bounds__(BLK, BLK == 256u ? GS_RK_MINW : GS_RK_MINW_SMALL) void round_kernel(RoundArgs a) {
     constexpr bool DELIVER = (MODE == 1 || MODE == 2);
     constexpr bool TRANSITION = (MODE == 0 || MODE == 1);
     const Geometry &g = a.g;
@@ -271,11 +277,11 @@ __global__ __launch_bounds__(BLK, GS_RK_MINW) void round_kernel(RoundArgs a) {
     // ... and that pusher's row, issued as soon as the id is in (the batch's
     // rows, issued after it, stay in flight)
     Cls t0 = {0, 0, 0};
-    if (DELIVER && !SEQ && !DLV && !SHARD && k > kInline) t0 = L.load_cls(S, tail0);
+    if (GS_RK_TAILPRE && DELIVER && !SEQ && !DLV && !SHARD && k > kInline) t0 = L.load_cls(S, tail0);
     // likewise the row of t(x)'s pusher #kBatchE ahead of x (its id is inline)
     static_assert(kBatchE < kSibInline, "sibling #kBatchE is inline");
     Cls s2 = {0, 0, 0};
-    if (DELIVER && !SEQ && !DLV && !SHARD && r > kBatchE && !(tgw & kTgNoPull) &&
+    if (GS_RK_TAILPRE && DELIVER && !SEQ && !DLV && !SHARD && r > kBatchE && !(tgw & kTgNoPull) &&
         (!filt || zneed) && !((eskip >> kBatchE) & 1u))
         s2 = L.load_cls(S, pick_sib(sb8.e, kBatchE));
     __builtin_amdgcn_s_setprio(0);
@@ -454,7 +460,7 @@ __global__ __launch_bounds__(BLK, GS_RK_MINW) void round_kernel(RoundArgs a) {
                 const uint32_t s = i < kInline ? pick_inline(in8.s, i)
                                                : (i == kInline ? tail0 : a.src[in8.first() + (i - kInline)]);
                 zin |= s == z;
-                rv.push(i == kInline ? t0 : L.load_cls(S, s), i, k, !(pulled && s == z));
+                rv.push((GS_RK_TAILPRE && i == kInline) ? t0 : L.load_cls(S, s), i, k, !(pulled && s == z));
             }
             // Pull batch from z: z's live set plus what z created from pushers
             // ahead of x.
@@ -474,7 +480,7 @@ __global__ __launch_bounds__(BLK, GS_RK_MINW) void round_kernel(RoundArgs a) {
                 for (uint32_t i = kBatchE; i < min(r, kSibInline); ++i) {
                     const bool sk = ((eskip >> i) & 1u) != 0;
                     Cls row;
-                    if (i == kBatchE) {
+                    if (GS_RK_TAILPRE && i == kBatchE) {
                         row = s2;
                     } else {
                         row = sib_row(pick_sib(sb8.e, i), sk);
