@@ -291,8 +291,10 @@ def run_mode(args, mode, world, rank, local, dist, sg, np, torch, with_spread):
         fk["schedule"] = args.schedule
     if mode in ("slices-lib", "nodes-lib"):
         from safe_gossip_amd.net import Net
+        # RCCL, or (gloo rehearsal) the library calling back into the process group
         net = Net(n, R, world, mode="slices" if mode == "slices-lib" else "shards", seed=args.seed, epoch=0,
-                  device=local, transport="dist", parts=args.parts or 4, **fk)
+                  device=local, transport="dist" if args.dist_backend == "nccl" else "host",
+                  parts=args.parts or 4, **fk)
     elif mode == "slices":
         from safe_gossip_amd.sliced import SlicedNetwork
         net = SlicedNetwork(n, R, world, seed=args.seed, epoch=0, device=local, transport="dist", **fk)
@@ -414,8 +416,8 @@ def main():
         modes = ["nodes"]
     else:
         # the Python drivers first (rehearsed with 8 ranks), then
-        # the library's loop (RCCL only: gs_net joins RCCL itself)
-        modes = ["slices", "nodes"] + (["slices-lib", "nodes-lib"] if args.dist_backend == "nccl" else [])
+        # the library's loop (over RCCL; with gloo, over the host collectives)
+        modes = ["slices", "nodes", "slices-lib", "nodes-lib"]
     if R < world:  # fewer rumors than ranks: no rumor slices
         modes = [m for m in modes if not m.startswith("slices")] or ["nodes"]
     if args.schedule == "SEQ" and dist is not None:  # SEQ's pull chains cross node ranges: slices only

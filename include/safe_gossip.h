@@ -342,6 +342,24 @@ gs_status   gs_net_create(const gs_config *cfg, gs_net_mode mode, uint32_t rank,
 gs_status   gs_net_create_local(const gs_config *cfg, gs_net_mode mode, uint32_t world, uint32_t parts,
                                 gs_net **out);
 void        gs_net_destroy(gs_net *net);
+/* Collectives a host brings instead of RCCL (gs_net_create_with): the
+ * library calls them on HOST buffers it staged -- after synchronising the
+ * rank's device work, copying the results back after they return -- in the
+ * same order on every rank; 0 = success (else GS_ERR_IO).  alltoall: block i
+ * of `send` (bytes_per_rank each) to rank i, block j of `recv` from rank j;
+ * allgather: `send` of every rank into `recv` in rank order; allreduce: in
+ * place over `count` elements of `dtype` with `op`.  Any transport (MPI,
+ * sockets, gloo) serves; several ranks may share a GPU. */
+enum { GS_NET_U8 = 0, GS_NET_U32 = 1, GS_NET_U64 = 2 };
+enum { GS_NET_SUM = 0, GS_NET_MIN = 1, GS_NET_MAX = 2 };
+typedef struct {
+    void *ctx;
+    int (*alltoall)(void *ctx, const void *send, void *recv, uint64_t bytes_per_rank);
+    int (*allreduce)(void *ctx, void *buf, uint64_t count, int dtype, int op);
+    int (*allgather)(void *ctx, const void *send, void *recv, uint64_t bytes_per_rank);
+} gs_net_collectives;
+gs_status   gs_net_create_with(const gs_config *cfg, gs_net_mode mode, uint32_t rank, uint32_t world, uint32_t parts,
+                               const gs_net_collectives *coll, gs_net **out);
 /* Gossiper::send_new on a node of the network (global ids). */
 gs_status   gs_net_send_new(gs_net *net, uint32_t node, uint32_t rumor);
 /* One round of the whole network; with a report, any_live is the network's

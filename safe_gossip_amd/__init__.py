@@ -176,6 +176,8 @@ SYMBOLS = {
     "gs_net_create": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _U8P,
                                      ctypes.POINTER(_P)]),
     "gs_net_create_local": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(_P)]),
+    "gs_net_create_with": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _P,
+                                          ctypes.POINTER(_P)]),
     "gs_net_destroy": (None, [_P]),
     "gs_net_send_new": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_uint32]),
     "gs_net_next_round": (ctypes.c_int, [_P, _P]),

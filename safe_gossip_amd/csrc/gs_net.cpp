@@ -20,7 +20,10 @@
 // gs_net_create_local runs every rank in this process on one device and
 // exchanges by device copies with host synchronisation (the "local" transport
 // of the Python wrappers): a test transport for the same loop at world > 1 on
-// one GPU.
+// one GPU.  gs_net_create_with takes the collectives from the caller (any
+// transport: MPI, sockets, gloo) and runs them on host-staged buffers after a
+// synchronisation of the rank -- no RCCL needed, several ranks may share a
+// GPU (the rehearsal of the multi-process loop on one box).
 #include "../../include/safe_gossip.h"
 
 #include <dlfcn.h>
@@ -141,7 +144,9 @@ struct NetRank {
 
 struct gs_net {
     gs_net_mode mode = GS_NET_SLICES;
-    bool dist = false;  // RCCL, one rank per process; else every rank here
+    bool dist = false;  // one rank per process (RCCL or the host's collectives); else every rank here
+    bool host = false;  // dist over collectives the caller brings (gs_net_create_with), on host buffers
+    gs_net_collectives coll{};
     uint32_t world = 1, rank = 0;
     uint32_t n = 0, R = 0, parts = 1;
     bool codes = false;  // node shards: code rows (R_pad <= 16, 2P)
@@ -205,6 +210,34 @@ gs_status sync_all(gs_net *net) {
     return GS_OK;
 }
 
+// ------------------------------------------------------------ host collectives
+// gs_net_create_with: the caller's collectives on host buffers the library
+// stages; every call follows a synchronisation of this rank's engine (its
+// engine and side streams), so the exchanged bytes are final and nothing
+// still reads the buffers a result lands in.
+gs_status host_call(int rc) { return rc == 0 ? GS_OK : GS_ERR_IO; }
+
+gs_status host_alltoall_dev(gs_net *net, NetRank &r, const void *send, void *recv, size_t bytes_per_rank) {
+    NET_ST(gs_sync(r.e));
+    NET_HIP(hipSetDevice(r.device));
+    std::vector<uint8_t> hs(bytes_per_rank * net->world), hr(bytes_per_rank * net->world);
+    NET_HIP(hipMemcpy(hs.data(), send, hs.size(), hipMemcpyDeviceToHost));
+    NET_ST(host_call(net->coll.alltoall(net->coll.ctx, hs.data(), hr.data(), bytes_per_rank)));
+    NET_HIP(hipMemcpy(recv, hr.data(), hr.size(), hipMemcpyHostToDevice));
+    return GS_OK;
+}
+
+// MIN over the ranks of `bytes` device bytes, in place (host collectives).
+gs_status host_min_u8_dev(gs_net *net, NetRank &r, uint8_t *buf, size_t bytes) {
+    NET_ST(gs_sync(r.e));
+    NET_HIP(hipSetDevice(r.device));
+    std::vector<uint8_t> h(bytes);
+    NET_HIP(hipMemcpy(h.data(), buf, bytes, hipMemcpyDeviceToHost));
+    NET_ST(host_call(net->coll.allreduce(net->coll.ctx, h.data(), bytes, GS_NET_U8, GS_NET_MIN)));
+    NET_HIP(hipMemcpy(buf, h.data(), bytes, hipMemcpyHostToDevice));
+    return GS_OK;
+}
+
 // ------------------------------------------------------------ node shards
 // Part h of exchange A (buffer set k) or B: (first u32 word, u32 words per
 // rank sub-block); the part's `world` sub-blocks are contiguous.
@@ -242,6 +275,7 @@ gs_status exchange(gs_net *net, bool A, uint32_t h, uint32_t k, hipEvent_t *ev) 
     const auto rg = region(r, A, h);
     const uint32_t *sb = (A ? r.sendA[k] : r.sendB) + rg.first;
     uint32_t *rb = (A ? r.recvA[k] : r.recvB) + rg.first;
+    if (net->host) return host_alltoall_dev(net, r, sb, rb, rg.second * sizeof(uint32_t));
     NET_HIP(hipSetDevice(r.device));
     NET_ST(comm_after_engine(net, r));
     const size_t limit = rccl_max_bytes() / sizeof(uint32_t);
@@ -360,6 +394,10 @@ gs_status slice_round(gs_net *net, bool report, bool *live) {
         return GS_OK;
     }
     NetRank &r = net->ranks[0];
+    if (net->host) {  // reduced now, added by the next round kernel
+        NET_ST(host_min_u8_dev(net, r, r.buf[b], 2 * (size_t)net->n));
+        return gs_slice_defer(r.e, b);
+    }
     NET_HIP(hipSetDevice(r.device));
     NET_ST(comm_after_engine(net, r));
     NET_NCCL(rccl().allReduce(r.buf[b], r.buf[b], 2 * (size_t)net->n, ncclUint8, ncclMin, net->comm, r.cs));
@@ -400,6 +438,11 @@ gs_status grow_scratch(NetRank &r, size_t bytes) {
 // In-place all-reduce of host data over the ranks (RCCL; synchronous).
 gs_status host_allreduce(gs_net *net, void *data, size_t count, ncclDataType_t dt, size_t elem, ncclRedOp_t op) {
     if (!net->dist || net->world == 1) return GS_OK;
+    if (net->host) {
+        const int hdt = dt == ncclUint8 ? GS_NET_U8 : (dt == ncclUint32 ? GS_NET_U32 : GS_NET_U64);
+        const int hop = op == ncclSum ? GS_NET_SUM : (op == ncclMin ? GS_NET_MIN : GS_NET_MAX);
+        return host_call(net->coll.allreduce(net->coll.ctx, data, count, hdt, hop));
+    }
     NetRank &r = net->ranks[0];
     NET_ST(grow_scratch(r, count * elem));
     NET_HIP(hipSetDevice(r.device));
@@ -416,6 +459,7 @@ gs_status host_allgather(gs_net *net, const void *mine, size_t bytes, void *out)
         std::memcpy(out, mine, bytes);
         return GS_OK;
     }
+    if (net->host) return host_call(net->coll.allgather(net->coll.ctx, mine, out, bytes));
     NetRank &r = net->ranks[0];
     NET_ST(grow_scratch(r, bytes * (net->world + 1)));
     uint8_t *s = static_cast<uint8_t *>(r.scratch), *g = s + bytes;
@@ -496,7 +540,7 @@ gs_status make_rank(gs_net *net, const gs_config *cfg, uint32_t g, NetRank &r) {
         NET_ST(gs_slice_set_ext_limit(r.e, std::min<uint32_t>(200u, 32u * rp)));
     }
     r.stream = reinterpret_cast<hipStream_t>(gs_stream(r.e));
-    if (net->dist) NET_HIP(hipStreamCreateWithFlags(&r.cs, hipStreamNonBlocking));
+    if (net->dist && !net->host) NET_HIP(hipStreamCreateWithFlags(&r.cs, hipStreamNonBlocking));
     return GS_OK;
 }
 
@@ -517,7 +561,7 @@ gs_status finish_create(gs_net *net, const gs_config *cfg) {
         const NetRank &r = net->ranks[0];
         net->parts = r.info[8];  // parts that hold nodes (gs_shard_info)
         net->codes = r.info[13] != 0;
-        if (net->dist && net->world > 1) {  // every exchange within RCCL's exact range
+        if (net->dist && !net->host && net->world > 1) {  // every exchange within RCCL's exact range
             size_t biggest = 0;
             for (uint32_t h = 0; h < net->parts; ++h)
                 for (bool A : {true, false}) biggest = std::max(biggest, net->world * region(r, A, h).second * 4);
@@ -587,6 +631,31 @@ gs_status gs_net_create_local(const gs_config *cfg, gs_net_mode mode, uint32_t w
     gs_net *net = new gs_net();
     net->mode = mode;
     net->world = world;
+    net->n = cfg->n_nodes;
+    net->R = cfg->n_rumors;
+    net->parts = parts ? parts : 1u;
+    const gs_status st = finish_create(net, cfg);
+    if (st != GS_OK) {
+        release(net);
+        return st;
+    }
+    *out = net;
+    return GS_OK;
+}
+
+gs_status gs_net_create_with(const gs_config *cfg, gs_net_mode mode, uint32_t rank, uint32_t world, uint32_t parts,
+                             const gs_net_collectives *coll, gs_net **out) {
+    if (!out || !coll || !coll->alltoall || !coll->allreduce || !coll->allgather || rank >= world)
+        return GS_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    NET_ST(check_net_args(cfg, mode, world, parts));
+    gs_net *net = new gs_net();
+    net->mode = mode;
+    net->dist = true;
+    net->host = true;
+    net->coll = *coll;
+    net->world = world;
+    net->rank = rank;
     net->n = cfg->n_nodes;
     net->R = cfg->n_rumors;
     net->parts = parts ? parts : 1u;
@@ -722,6 +791,8 @@ gs_status gs_net_statistics_all(gs_net *net, uint64_t *out) {
     std::vector<uint8_t> pend(n);
     if (!net->dist) {
         NET_ST(local_min_u8(net, [](NetRank &r) { return r.obs; }, n));
+    } else if (net->world > 1 && net->host) {
+        NET_ST(host_min_u8_dev(net, net->ranks[0], net->ranks[0].obs, n));
     } else if (net->world > 1) {
         NetRank &r = net->ranks[0];
         NET_HIP(hipSetDevice(r.device));

@@ -7,6 +7,10 @@ With ``transport="dist"`` every process of a ``torch.distributed`` group is
 one rank (one GPU each): rank 0's RCCL id is broadcast over the group, then
 the library joins its own RCCL communicator and issues every exchange on a
 stream of its own, ordered against the engine stream with events.
+``transport="host"``: the same, but the library calls back into this module
+for every collective, on host buffers it staged (``gs_net_create_with``),
+which runs them over the group's own backend (gloo: several ranks may share
+one GPU -- the rehearsal of the multi-process loop on one box).
 ``transport="local"`` holds every rank in this process on one device.
 """
 from __future__ import annotations
@@ -22,6 +26,62 @@ _U64P = ctypes.POINTER(ctypes.c_uint64)
 _U16P = ctypes.POINTER(ctypes.c_uint16)
 _U32P = ctypes.POINTER(ctypes.c_uint32)
 MODES = {"slices": 0, "shards": 1}
+
+_A2A = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
+_ARED = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int)
+
+
+class _Collectives(ctypes.Structure):
+    """include/safe_gossip.h gs_net_collectives."""
+    _fields_ = [("ctx", ctypes.c_void_p), ("alltoall", _A2A), ("allreduce", _ARED), ("allgather", _A2A)]
+
+
+def _host_bytes(ptr: int, n: int) -> np.ndarray:
+    return np.ctypeslib.as_array((ctypes.c_uint8 * max(n, 1)).from_address(ptr))[:n]
+
+
+def _group_collectives(group, world: int):
+    """gs_net_collectives over a torch.distributed group, on CPU tensors (any
+    backend that takes CPU tensors: gloo).  Exceptions become a nonzero
+    status (GS_ERR_IO in the library)."""
+    import torch
+    import torch.distributed as dist
+    dts = {0: (np.uint8, torch.int32), 1: (np.uint32, torch.int64), 2: (np.uint64, torch.int64)}
+    ops = {0: dist.ReduceOp.SUM, 1: dist.ReduceOp.MIN, 2: dist.ReduceOp.MAX}
+
+    def alltoall(_ctx, send, recv, nb):
+        try:
+            inp = torch.from_numpy(_host_bytes(send, nb * world).copy())
+            out = torch.empty(nb * world, dtype=torch.uint8)
+            dist.all_to_all_single(out, inp, group=group)
+            _host_bytes(recv, nb * world)[:] = out.numpy()
+            return 0
+        except Exception:  # noqa: BLE001 -- reported as a status
+            return 1
+
+    def allreduce(_ctx, buf, count, dtype, op):
+        try:
+            npt, tt = dts[dtype]
+            view = np.ctypeslib.as_array((ctypes.c_uint8 * max(count * np.dtype(npt).itemsize, 1))
+                                         .from_address(buf)).view(npt)[:count]
+            t = torch.from_numpy(view.astype(np.int64)).to(tt)
+            dist.all_reduce(t, op=ops[op], group=group)
+            view[:] = t.numpy().astype(npt)
+            return 0
+        except Exception:  # noqa: BLE001
+            return 1
+
+    def allgather(_ctx, send, recv, nb):
+        try:
+            inp = torch.from_numpy(_host_bytes(send, nb).copy())
+            outs = [torch.empty(nb, dtype=torch.uint8) for _ in range(world)]
+            dist.all_gather(outs, inp, group=group)
+            _host_bytes(recv, nb * world)[:] = torch.cat(outs).numpy()
+            return 0
+        except Exception:  # noqa: BLE001
+            return 1
+    fns = (_A2A(alltoall), _ARED(allreduce), _A2A(allgather))
+    return _Collectives(None, *fns), fns
 
 
 class Net:
@@ -61,6 +121,14 @@ class Net:
             ident = (ctypes.c_uint8 * 128).from_buffer_copy(box[0])
             _check(self.lib.gs_net_create(ctypes.byref(cfg), MODES[mode], rank, world, parts, ident,
                                           ctypes.byref(h)))
+        elif transport == "host":
+            import torch.distributed as dist
+            rank = dist.get_rank(group)
+            assert dist.get_world_size(group) == world
+            # (the callbacks must outlive the network: kept on self)
+            self._coll, self._fns = _group_collectives(group, world)
+            _check(self.lib.gs_net_create_with(ctypes.byref(cfg), MODES[mode], rank, world, parts,
+                                               ctypes.byref(self._coll), ctypes.byref(h)))
         else:
             raise ValueError(transport)
         self.h = h

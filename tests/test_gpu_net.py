@@ -172,3 +172,63 @@ def test_python_net_rccl_one_rank(engine):
         p.kill()
     assert not q.empty() and q.get() == "ok"
     assert p.exitcode == 0
+
+
+def _host_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import safe_gossip_amd as sg
+        from safe_gossip_amd.net import Net
+        for mode, n, R, parts, faults, schedule in (
+                ("shards", 1500, 70, 2, None, "2P"),                 # class rows, ids a round ahead
+                ("shards", 2000, 16, 2, (0.05, 0.05, 0.05), "2P"),   # code rows, faults
+                ("slices", 900, 9, 1, (0.05, 0.05, 0.05), "2P"),     # uneven slices
+                ("slices", 700, 20, 1, None, "SEQ")):
+            fk = dict(churn=faults[0], drop_push=faults[1], drop_pull=faults[2]) if faults else {}
+            net = Net(n, R, world, mode=mode, seed=SEED, transport="host", parts=parts, schedule=schedule, **fk)
+            try:
+                _net_vs_oracle(sg, net, n, R, faults, schedule)
+            finally:
+                net.close()
+        q.put("ok")
+    except BaseException as e:
+        q.put(f"fail: rank {rank}: {type(e).__name__}: {e}")
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_net_multi_process_host_collectives(engine, world):
+    # the library's loop in `world` processes sharing the one GPU, joined by
+    # the host's collectives (gs_net_create_with over gloo): the multi-rank
+    # paths of gs_net -- exchange regions of every part, the slices' MIN
+    # reduction, the any-live reduction, observers gathered over the ranks --
+    # each rank checked against the oracle every round
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    procs = [ctx.Process(target=_host_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    msgs = []
+    while not q.empty():
+        msgs.append(q.get())
+    assert len(msgs) == world and all(m == "ok" for m in msgs), msgs
+    assert all(p.exitcode == 0 for p in procs)
