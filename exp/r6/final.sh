@@ -1,8 +1,8 @@
 #!/bin/bash
 # Round-6 HEAD validation: the whole -m gpu suite, smoke, bench lines of
 # configs 4 (live PMC, CPU baselines), 5, 2 and 3, rocprofv3 kernel-trace +
-# PMC passes of configs 4 and 5, and bench.py --gpus 8 rehearsed with 8 gloo
-# ranks on the one GPU.  Usage: final.sh <tag>
+# PMC passes of configs 4 and 5.  Usage: final.sh <tag>
+# (bench.py --gpus 8 rehearsed with 8 gloo ranks: exp/r6/rehearse8.sh)
 set -e
 T=${1:-f}
 O=gpurun_out/r6final_$T; mkdir -p $O
@@ -15,4 +15,3 @@ timeout -k 10 300 python bench.py --config cfg5 --no-cpu-baseline > $O/bench_cfg
 for c in cfg2 cfg3; do timeout -k 10 200 python bench.py --config $c --no-cpu-baseline --pmc off > $O/bench_$c.json 2>> $O/bench.err; done
 bash profiles/rocprof_r2.sh ${T}_cfg4
 bash profiles/rocprof_r2.sh ${T}_cfg5 --config cfg5
-timeout -k 10 400 python bench.py --gpus 8 --dist-backend gloo > $O/rehearsal8_cfg4.json 2> $O/rehearsal8.err
