@@ -49,6 +49,10 @@ static_assert(kRkSmallBlk == 64u || kRkSmallBlk == 128u, "a thread's stage step 
 #ifndef GS_RK_MINW_SMALL
 #define GS_RK_MINW_SMALL 1  // waves per SIMD asked of the small-block transitions (A/B builds)
 #endif
+#ifndef GS_RK_ZSKIP
+#define GS_RK_ZSKIP 1  // one-wave blocks: no plane stores for a wave whose new planes are all A
+#endif
+
 #ifndef GS_RK_TAILPRE
 #define GS_RK_TAILPRE 1  // rows of pusher #3 and of t(x)'s sibling #2 issued with the batch (A/B: 0)
 #endif
@@ -793,7 +797,13 @@ __global__ __launch_bounds__(BLK, BLK == 256u ? GS_RK_MINW : GS_RK_MINW_SMALL) v
     __syncthreads();  // also: every lane is done reading stage
     const bool blk_live = blk_any != 0u;
     __builtin_amdgcn_s_setprio(1);  // the drain: retire the block, free its slot
-    if (SMALL) {
+    // A wave (= block) whose nodes are all-A in round t+1 were all-A in
+    // round t-1 as well (no entry ever returns to A; clear zeroes both
+    // buffers), and Snext holds round t-1: its zero planes are there already.
+    const bool zskip = GS_RK_ZSKIP && kBlk == 64u && __ballot(valid && (N[0] | N[1] | N[2]) != 0ull) == 0ull;
+    if (zskip) {
+        // nothing to store
+    } else if (SMALL) {
         const uint32_t npu = 1u << g.lognpu;
 #pragma unroll
         for (int p = 0; p < kPlanes; ++p) {
@@ -805,8 +815,8 @@ __global__ __launch_bounds__(BLK, BLK == 256u ? GS_RK_MINW : GS_RK_MINW_SMALL) v
 #pragma unroll
         for (int p = 0; p < kPlanes; ++p) stage[sb0 + ((uint32_t)p << wlog)] = N[p];
     }
-    __syncthreads();
-    {
+    if (!zskip) __syncthreads();  // (zskip is uniform over the block's one wave)
+    if (!zskip) {
         uint4 *dst4 = reinterpret_cast<uint4 *>(a.Snext + blk_base);
         // streaming (nontemporal) stores: 3.11 -> 3.01 ms per round kernel at
         // config 4 (nontemporal plane loads measured slower: 3.27 ms).
