@@ -26,6 +26,9 @@ namespace gs {
 #ifndef GS_DLV4_THREADS
 #define GS_DLV4_THREADS 256u  // lanes per block (A/B builds: 64, 128)
 #endif
+#ifndef GS_DLV4_ZSKIP
+#define GS_DLV4_ZSKIP 1  // no plane stores for a block whose new planes are all A
+#endif
 constexpr uint32_t kDlv4Threads = GS_DLV4_THREADS;
 static_assert(kDlv4Threads == 64u || kDlv4Threads == 128u || kDlv4Threads == 256u, "whole waves, <= 256");
 // 4 waves per SIMD (128 VGPRs): 2.63 -> 2.36 ms at config 5 against the
@@ -548,8 +551,9 @@ void round_kernel_dlv4(RoundArgs a) {
 
     // ---- write round-(t+1) planes (lanes of one word OR their fields; LDS
     // stage, 16-byte coalesced nontemporal stores)
-    __shared__ uint32_t blk_any;
+    __shared__ uint32_t blk_any, blk_nz;  // (blk_nz: some node not all-A in round t+1, GS_DLV4_ZSKIP)
     if (threadIdx.x == 0) blk_any = 0;
+    if (threadIdx.x == 0) blk_nz = 0;
     uint32_t live[kNpl];
     bool any_live = false;
 #pragma unroll
@@ -569,8 +573,13 @@ void round_kernel_dlv4(RoundArgs a) {
         }
     }
     if (__ballot(any_live) != 0ull && (threadIdx.x & 63u) == 0u) blk_any = 1u;
+    if (GS_DLV4_ZSKIP && __ballot(((N[0] | N[1] | N[2]) & mV) != (T)0) != 0ull && (threadIdx.x & 63u) == 0u)
+        blk_nz = 1u;
     __syncthreads();
-    {
+    // a block whose nodes are all-A in round t+1 were all-A in round t-1
+    // (no entry returns to A; clear zeroes both buffers): Snext, which holds
+    // round t-1, has its zero planes already
+    if (!GS_DLV4_ZSKIP || blk_nz != 0u) {
         const uint4 *src4 = reinterpret_cast<const uint4 *>(stage);
         uint4 *dst4 = reinterpret_cast<uint4 *>(a.Snext + unit0 * kPlanes);
 #pragma unroll

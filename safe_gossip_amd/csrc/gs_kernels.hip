@@ -52,6 +52,9 @@ static_assert(kRkSmallBlk == 64u || kRkSmallBlk == 128u, "a thread's stage step 
 #ifndef GS_RK_ZSKIP
 #define GS_RK_ZSKIP 1  // one-wave blocks: no plane stores for a wave whose new planes are all A
 #endif
+#ifndef GS_RK_ZSKIP_BLK
+#define GS_RK_ZSKIP_BLK 1  // the same for a whole 256-lane transition block
+#endif
 
 #ifndef GS_RK_TAILPRE
 #define GS_RK_TAILPRE 1  // rows of pusher #3 and of t(x)'s sibling #2 issued with the batch (A/B: 0)
@@ -98,7 +101,9 @@ __global__ __launch_bounds__(BLK, BLK == 256u ? GS_RK_MINW : GS_RK_MINW_SMALL) v
     const u64 *__restrict__ S = a.Scur;
 
     __shared__ uint32_t blk_any;  // some node pushes a live rumor in round t+1
+    __shared__ uint32_t blk_nz;   // some node is not all-A in round t+1 (256-lane zero skip)
     if (threadIdx.x == 0) blk_any = 0;
+    if (threadIdx.x == 0) blk_nz = 0;
     // the load-issue phase at raised priority: a young wave's requests go out
     // ahead of older waves' compute (issue is by priority, then age)
     __builtin_amdgcn_s_setprio(2);
@@ -794,13 +799,19 @@ __global__ __launch_bounds__(BLK, BLK == 256u ? GS_RK_MINW : GS_RK_MINW_SMALL) v
     uint32_t live_new = (valid && on_next) ? popc(Bn | Cn) : 0u;
     if (!SMALL) live_new = group_sum(live_new, g.W);
     if (__ballot(live_new != 0u) != 0ull && (threadIdx.x & 63u) == 0u) blk_any = 1u;
+    constexpr bool kZBlk = GS_RK_ZSKIP_BLK && TRANSITION && kBlk != 64u;
+    const u64 nz_mask = SMALL ? L.m : ~0ull;
+    if (kZBlk && __ballot(valid && ((N[0] | N[1] | N[2]) & nz_mask) != 0ull) != 0ull && (threadIdx.x & 63u) == 0u)
+        blk_nz = 1u;
     __syncthreads();  // also: every lane is done reading stage
     const bool blk_live = blk_any != 0u;
     __builtin_amdgcn_s_setprio(1);  // the drain: retire the block, free its slot
     // A wave (= block) whose nodes are all-A in round t+1 were all-A in
     // round t-1 as well (no entry ever returns to A; clear zeroes both
     // buffers), and Snext holds round t-1: its zero planes are there already.
-    const bool zskip = GS_RK_ZSKIP && kBlk == 64u && __ballot(valid && (N[0] | N[1] | N[2]) != 0ull) == 0ull;
+    // (a 256-lane block: the same over its four waves, from blk_nz)
+    const bool zskip = kZBlk ? blk_nz == 0u
+                             : GS_RK_ZSKIP && kBlk == 64u && __ballot(valid && (N[0] | N[1] | N[2]) != 0ull) == 0ull;
     if (zskip) {
         // nothing to store
     } else if (SMALL) {
@@ -815,7 +826,7 @@ __global__ __launch_bounds__(BLK, BLK == 256u ? GS_RK_MINW : GS_RK_MINW_SMALL) v
 #pragma unroll
         for (int p = 0; p < kPlanes; ++p) stage[sb0 + ((uint32_t)p << wlog)] = N[p];
     }
-    if (!zskip) __syncthreads();  // (zskip is uniform over the block's one wave)
+    if (!zskip) __syncthreads();  // (zskip is uniform over the block)
     if (!zskip) {
         uint4 *dst4 = reinterpret_cast<uint4 *>(a.Snext + blk_base);
         // streaming (nontemporal) stores: 3.11 -> 3.01 ms per round kernel at

@@ -33,6 +33,9 @@ namespace gs {
 #ifndef GS_W32_THREADS
 #define GS_W32_THREADS 128u  // lanes per block: 2^24 x 32 1.051 -> 1.037 ms/step against 256 (64: 1.051)
 #endif
+#ifndef GS_W32_ZSKIP
+#define GS_W32_ZSKIP 1  // no plane stores for a block whose new planes are all A
+#endif
 constexpr uint32_t kW32Threads = GS_W32_THREADS;
 #ifndef GS_W32_MINW
 #define GS_W32_MINW 1
@@ -89,7 +92,9 @@ __global__ __launch_bounds__(kW32Threads, GS_W32_MINW) void round_kernel_w32(Rou
     const uint32_t j = (uint32_t)seg & (W32 - 1u);
     const u32 *__restrict__ S = reinterpret_cast<const u32 *>(a.Scur);
     __shared__ uint32_t blk_any;  // some node pushes a live rumor in round t+1
+    __shared__ uint32_t blk_nz;   // some node is not all-A in round t+1 (GS_W32_ZSKIP)
     if (threadIdx.x == 0) blk_any = 0;
+    if (threadIdx.x == 0) blk_nz = 0;
 
     // ---- own round-t planes: the block's records (kW32Threads / W32 nodes,
     // 8 KiB) with 16-byte coalesced loads, transposed through LDS below
@@ -305,14 +310,20 @@ __global__ __launch_bounds__(kW32Threads, GS_W32_MINW) void round_kernel_w32(Rou
     uint32_t live_new = (valid && on_next) ? popcT(o.Bn | o.Cn) : 0u;
     live_new = group_sum(live_new, W32);
     if (__ballot(live_new != 0u) != 0ull && (threadIdx.x & 63u) == 0u) blk_any = 1u;
+    if (GS_W32_ZSKIP && __ballot(valid && (o.N[0] | o.N[1] | o.N[2]) != 0u) != 0ull && (threadIdx.x & 63u) == 0u)
+        blk_nz = 1u;
     __syncthreads();  // also: every lane is done reading stage
     const bool blk_live = blk_any != 0u;
-    if (valid) {
+    // a block whose nodes are all-A in round t+1 were all-A in round t-1 (no
+    // entry returns to A; clear zeroes both buffers): Snext, which holds round
+    // t-1, has its zero planes already
+    const bool zskip = GS_W32_ZSKIP && blk_nz == 0u;
+    if (valid && !zskip) {
 #pragma unroll
         for (int p = 0; p < kPlanes; ++p) stage[pbase + (uint32_t)p * pstr] = o.N[p];
     }
-    __syncthreads();
-    {
+    if (!zskip) __syncthreads();  // (uniform over the block)
+    if (!zskip) {
         const uint4 *s4 = reinterpret_cast<const uint4 *>(stage);
         uint4 *dst4 = reinterpret_cast<uint4 *>(reinterpret_cast<u32 *>(a.Snext) + blk_base);
         if (threadIdx.x < blk_v4) nt_store4(s4[threadIdx.x], &dst4[threadIdx.x]);
