@@ -53,7 +53,8 @@ static_assert(kRkSmallBlk == 64u || kRkSmallBlk == 128u, "a thread's stage step 
 #define GS_RK_ZSKIP 1  // one-wave blocks: no plane stores for a wave whose new planes are all A
 #endif
 #ifndef GS_RK_ZSKIP_BLK
-#define GS_RK_ZSKIP_BLK 1  // the same for a whole 256-lane transition block
+#define GS_RK_ZSKIP_BLK 0  // the same for a whole 256-lane transition block (off: no bench configuration
+                           // runs these blocks, and one SEQ harness mismatch, not reproduced, followed it)
 #endif
 
 #ifndef GS_RK_TAILPRE
