@@ -288,7 +288,10 @@ gs_status upload_ext(gs_engine *e) {
     std::vector<u64> keys(m);
     for (uint32_t i = 0; i < m; ++i) keys[i] = ((u64)v[i].node << 32) | v[i].info;
     GS_HIP(hipStreamSynchronize(e->stream));  // the previous upload may still be read
-    GS_HIP(hipMemcpy(e->ext_dev, keys.data(), m * sizeof(u64), hipMemcpyHostToDevice));
+    // on the engine stream, waited for (keys is a host temporary; a hipMemcpy
+    // on the null stream is not ordered before the non-blocking engine stream)
+    GS_HIP(hipMemcpyAsync(e->ext_dev, keys.data(), m * sizeof(u64), hipMemcpyHostToDevice, e->stream));
+    GS_HIP(hipStreamSynchronize(e->stream));
     e->ext_uploaded = m;
     return GS_OK;
 }
@@ -820,7 +823,7 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         const size_t words = gs::shard_edge_words(e->sp, &e->sel);
         ok = hipEventCreateWithFlags(&e->ev_edges[i], hipEventDisableTiming) == hipSuccess &&
              dalloc(&e->edgew[i], words) == hipSuccess &&
-             hipMemset(e->edgew[i], 0, words * sizeof(uint32_t)) == hipSuccess;  // (counters zero between builds)
+             hipMemsetAsync(e->edgew[i], 0, words * sizeof(uint32_t), e->stream) == hipSuccess;  // (counters zero between builds)
     }
     if (ok && e->shard) ok = hipEventCreateWithFlags(&e->ev_main, hipEventDisableTiming) == hipSuccess;
     if (ok && e->shard && e->dlv) {  // one build set: built and read on the engine stream, in order
@@ -838,12 +841,12 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         ok = dalloc(&c.src, isz.src_words) == hipSuccess && dalloc(&c.tg, npad) == hipSuccess &&
              dalloc(&c.region, isz.region_words) == hipSuccess &&
              dalloc(&c.scratch, isz.scratch_words) == hipSuccess &&
-             hipMemset(c.scratch, 0, std::max<size_t>(isz.scratch_words, 1) * sizeof(uint32_t)) == hipSuccess;
+             hipMemsetAsync(c.scratch, 0, std::max<size_t>(isz.scratch_words, 1) * sizeof(uint32_t), e->stream) == hipSuccess;
         if (ok && e->dlv) {
             ok = dalloc(&c.DR, n) == hipSuccess && dalloc(&c.pull, n) == hipSuccess;
         } else if (ok) {
             ok = dalloc(&c.IN8, npad) == hipSuccess && dalloc(&c.SIB8, npad) == hipSuccess &&
-                 hipMemset(c.SIB8, 0, std::max<size_t>(n, 1) * sizeof(gs::SibRec)) == hipSuccess;
+                 hipMemsetAsync(c.SIB8, 0, std::max<size_t>(n, 1) * sizeof(gs::SibRec), e->stream) == hipSuccess;
             if (ok && e->filt) ok = dalloc(&c.zl, gs::node_map_words(n)) == hipSuccess;
         }
     }
@@ -855,7 +858,7 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         ok = dalloc(&e->lvm, gs::node_map_words(n)) == hipSuccess &&
              dalloc(&e->cpm, gs::node_map_words(n)) == hipSuccess &&
              dalloc(&e->rows_dev, 2) == hipSuccess &&
-             dalloc(&e->acct, 1) == hipSuccess && hipMemset(e->acct, 0, sizeof(u64)) == hipSuccess;
+             dalloc(&e->acct, 1) == hipSuccess && hipMemsetAsync(e->acct, 0, sizeof(u64), e->stream) == hipSuccess;
     if (ok && e->seq)
         ok = dalloc(&e->Wb, (size_t)n * 2 * g.W) == hipSuccess && dalloc(&e->sinfo, n) == hipSuccess &&
              dalloc(&e->seqw, (size_t)gs::seq_blocks(n) * gs::kSeqLists + gs::kSeqLists + n) == hipSuccess;
@@ -866,6 +869,9 @@ gs_status create_engine(const gs_config *cfg, uint32_t rank, uint32_t world, uin
         release(e);
         return le == hipErrorOutOfMemory ? GS_ERR_OUT_OF_MEMORY : GS_ERR_HIP;
     }
+    // (the zeroing above and reset_state's run on the engine stream: a plain
+    // hipMemset goes to the null stream, which non-blocking streams do not
+    // wait for; every buffer is zero once this synchronisation returns)
     if (reset_state(e) != GS_OK || hipStreamSynchronize(e->stream) != hipSuccess) {
         release(e);
         return GS_ERR_HIP;

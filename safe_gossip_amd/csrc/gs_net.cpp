@@ -217,14 +217,24 @@ gs_status sync_all(gs_net *net) {
 // still reads the buffers a result lands in.
 gs_status host_call(int rc) { return rc == 0 ? GS_OK : GS_ERR_IO; }
 
+// Host bytes into a device buffer the engine's kernels read next: on the
+// engine stream, waited for before the host buffer goes.  (A plain hipMemcpy
+// runs on the null stream, which a non-blocking engine stream does not wait
+// for, and a pageable upload may return before its data lands.)
+gs_status upload_to_engine(NetRank &r, void *dst, const void *src, size_t bytes) {
+    NET_HIP(hipSetDevice(r.device));
+    NET_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, r.stream));
+    NET_HIP(hipStreamSynchronize(r.stream));
+    return GS_OK;
+}
+
 gs_status host_alltoall_dev(gs_net *net, NetRank &r, const void *send, void *recv, size_t bytes_per_rank) {
     NET_ST(gs_sync(r.e));
     NET_HIP(hipSetDevice(r.device));
     std::vector<uint8_t> hs(bytes_per_rank * net->world), hr(bytes_per_rank * net->world);
     NET_HIP(hipMemcpy(hs.data(), send, hs.size(), hipMemcpyDeviceToHost));
     NET_ST(host_call(net->coll.alltoall(net->coll.ctx, hs.data(), hr.data(), bytes_per_rank)));
-    NET_HIP(hipMemcpy(recv, hr.data(), hr.size(), hipMemcpyHostToDevice));
-    return GS_OK;
+    return upload_to_engine(r, recv, hr.data(), hr.size());
 }
 
 // MIN over the ranks of `bytes` device bytes, in place (host collectives).
@@ -234,8 +244,7 @@ gs_status host_min_u8_dev(gs_net *net, NetRank &r, uint8_t *buf, size_t bytes) {
     std::vector<uint8_t> h(bytes);
     NET_HIP(hipMemcpy(h.data(), buf, bytes, hipMemcpyDeviceToHost));
     NET_ST(host_call(net->coll.allreduce(net->coll.ctx, h.data(), bytes, GS_NET_U8, GS_NET_MIN)));
-    NET_HIP(hipMemcpy(buf, h.data(), bytes, hipMemcpyHostToDevice));
-    return GS_OK;
+    return upload_to_engine(r, buf, h.data(), bytes);
 }
 
 // ------------------------------------------------------------ node shards
@@ -257,6 +266,9 @@ gs_status exchange(gs_net *net, bool A, uint32_t h, uint32_t k, hipEvent_t *ev) 
     *ev = nullptr;
     const bool own = net->codes && net->world == 1;  // one code-row rank: rows written in place
     if (!net->dist) {
+        // (every engine idle: the sources are final and no reader of the
+        // receive buffers is left; each copy runs on its destination's engine
+        // stream, ahead of the kernels that read it)
         NET_ST(sync_all(net));
         for (uint32_t d = 0; d < net->world; ++d)
             for (uint32_t s = 0; s < net->world; ++s) {
@@ -265,8 +277,9 @@ gs_status exchange(gs_net *net, bool A, uint32_t h, uint32_t k, hipEvent_t *ev) 
                 const auto rg = region(src, A, h);
                 const uint32_t *sb = A ? src.sendA[k] : src.sendB;
                 uint32_t *rb = A ? dst.recvA[k] : dst.recvB;
-                NET_HIP(hipMemcpy(rb + rg.first + s * rg.second, sb + rg.first + d * rg.second,
-                                  rg.second * sizeof(uint32_t), hipMemcpyDeviceToDevice));
+                NET_HIP(hipSetDevice(dst.device));
+                NET_HIP(hipMemcpyAsync(rb + rg.first + s * rg.second, sb + rg.first + d * rg.second,
+                                       rg.second * sizeof(uint32_t), hipMemcpyDeviceToDevice, dst.stream));
             }
         return GS_OK;
     }
@@ -376,7 +389,7 @@ gs_status local_min_u8(gs_net *net, BufOf buf_of, size_t bytes) {
         NET_HIP(hipMemcpy(v.data(), buf_of(r), bytes, hipMemcpyDeviceToHost));
         for (size_t i = 0; i < bytes; ++i) m[i] = std::min(m[i], v[i]);
     }
-    for (auto &r : net->ranks) NET_HIP(hipMemcpy(buf_of(r), m.data(), bytes, hipMemcpyHostToDevice));
+    for (auto &r : net->ranks) NET_ST(upload_to_engine(r, buf_of(r), m.data(), bytes));
     return GS_OK;
 }
 
@@ -502,6 +515,9 @@ template <typename T>
 gs_status zalloc(T **p, size_t count) {
     NET_HIP(hipMalloc((void **)p, std::max<size_t>(count, 1) * sizeof(T)));
     NET_HIP(hipMemset(*p, 0, std::max<size_t>(count, 1) * sizeof(T)));
+    // (the null stream's memset done before any engine or comm stream --
+    // non-blocking, not ordered after it -- touches the buffer)
+    NET_HIP(hipDeviceSynchronize());
     return GS_OK;
 }
 

@@ -99,6 +99,9 @@ class _Shard:
         self.recvA = [torch.zeros(self.rowsA * self.wa, dtype=i32, device=dev) for _ in range(2)]
         self.sendB = torch.zeros(self.rowsB * self.wb, dtype=i32, device=dev)
         self.recvB = torch.zeros(self.rowsB * self.wb, dtype=i32, device=dev)
+        # (zeroed on torch's stream: done before the engine's non-blocking
+        # streams, which do not wait for it, touch the buffers)
+        torch.cuda.synchronize(dev)
         _check(lib.gs_shard_bind(h, self.sendA[0].data_ptr(), self.sendA[1].data_ptr(),
                                  self.recvA[0].data_ptr(), self.recvA[1].data_ptr(),
                                  self.sendB.data_ptr(), self.recvB.data_ptr()))
