@@ -549,7 +549,7 @@ def report(args, runs, failed, world, rank, np, sg, note, dist_on):
                 # its kernels is smaller than the round kernel at every config) and
                 # the launch gaps
                 "rest_of_step_ms": ms_per_step - kernel_ms,
-                "bytes_counted_by": ("kernels (rows actually gathered + planes moved), %d launches"
+                "bytes_counted_by": ("kernels (rows actually gathered + every node's planes read and written, the stores all-A waves skip included), %d launches"
                                      % best["launches"]) if best["launches"] else "static model",
                 "dense_model_bytes_per_launch": best["bytes_dense"],
                 "kernel_ms_per_round": [round(float(v), 4) for v in kt],
